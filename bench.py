@@ -1,0 +1,230 @@
+"""Benchmark: LoMPC QP solves/sec on MI355X (BASELINE.json metric, config 3/4).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode path|direct]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+One step = one batched price iteration of a whole charging-station time step on
+this rank's EV shard: for each EV type (small, large) load P = 12 fresh
+partition price vectors (lambda ~ theta U[0,1]^{3N}, test_lompc.py:34) and
+solve every EV's LoMPC QP (gamma_i = y_max - y0_i, y0 ~ U[0.3, 0.5],
+settings.py:27-28) with full outputs (w, cost) plus the fused per-partition
+reductions of price_solver.py:203-214; with N > 1 ranks the per-partition
+reductions are combined by one RCCL sum + one max all-reduce.  Weak scaling:
+262 144 EVs per GPU (config 3; at 8 GPUs this is config 4's 2 097 152).
+
+Rank 0 prints ONE JSON line.  ``roofline`` prices the dominant kernel
+(k_eval) by its algorithmic bytes per QP (gamma in 8 B, w out 8N B, cost out
+8 B) over its HIP-event-timed launch duration; ``cpu_baseline`` times the C
+oracle (oracle/, dense active set) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "incentive-design-mpc_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP64_VALU_PEAK_TFLOPS = 78.6  # vendor datasheet (not in the container guide)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--evs-per-gpu", type=int, default=262144)
+    ap.add_argument("--horizon", type=int, default=24)
+    ap.add_argument("--partitions", type=int, default=12)
+    ap.add_argument("--mode", choices=["path", "direct"], default="path")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from lompc_amd import LoMPC, LoMPCConstants, _lib
+    from lompc_amd.dist import allreduce_set_results
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device(f"cuda:{torch.cuda.current_device()}")
+
+    N, P = args.horizon, args.partitions
+    B = args.evs_per_gpu
+    types = [("small", LoMPCConstants(0.05, 10.0, 0.9, 0.25, "small")),
+             ("large", LoMPCConstants(0.025, 50.0, 0.9, 0.15, "large"))]  # real_time_price_control.py:26-39
+    rng = np.random.default_rng(args.seed * 1000 + rank)
+    per_type = [B // 2, B - B // 2]
+    nsteps = args.steps + args.warmup
+    eng = []
+    for (name, c), M in zip(types, per_type):
+        lompc = LoMPC(N, c, device=dev.index, mode=args.mode)
+        off = np.array([(M * p) // P for p in range(P + 1)], dtype=np.int64)  # P partitions
+        y0 = 0.3 + 0.2 * rng.random(M)
+        gamma = torch.as_tensor(c.y_max - y0, device=dev)
+        lm = torch.as_tensor(c.theta * rng.random((nsteps, P, 3 * N)), device=dev)
+        lr = torch.zeros(P, dtype=torch.float64, device=dev)
+        wr = torch.as_tensor(c.w_max * rng.random((P, N)), device=dev)
+        gref = torch.as_tensor(c.y_max - 0.4 * np.ones(P), device=dev)
+        eng.append(dict(name=name, c=c, lompc=lompc, off=off, gamma=gamma, lm=lm, lr=lr, wr=wr, gref=gref,
+                        out={}, M=M))
+
+    def step(k):
+        for e in eng:
+            lo = e["lompc"]
+            lo.set_params(e["lm"][k], e["lr"], w_ref=e["wr"], gamma_ref=e["gref"], validate=False)
+            r = lo.solve_batch(e["gamma"], e["off"], want_w=True, want_cost=True, want_set=True,
+                               out=e["out"], check=False)
+            if world > 1:
+                allreduce_set_results(r["set_sum_w"], r["set_stats"])
+
+    # warmup (and correctness gate: every QP certified)
+    for k in range(args.warmup):
+        step(k)
+    for e in eng:
+        rep, fail, inv = e["lompc"].check_last()
+        assert fail == 0 and inv == 0, (e["name"], fail, inv)
+    for e in eng:
+        e["lompc"].profile(enable=True)
+        e["lompc"].profile(read=True, reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, nsteps):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    repaired = 0
+    for e in eng:
+        rep, fail, inv = e["lompc"].check_last()
+        assert fail == 0 and inv == 0
+        repaired += rep
+    # dominant kernel (k_eval) timing from HIP events on the launch stream
+    k_ms, k_n, k_qps = 0.0, 0, 0
+    for e in eng:
+        ms, n = e["lompc"].profile(read=True)
+        k_ms += ms
+        k_n += n
+        k_qps += e["M"] * n
+    avg_launch_s = (k_ms / 1e3) / max(k_n, 1)
+    qp_per_launch = k_qps / max(k_n, 1)
+    bytes_per_qp = 8 * (N + 2)
+    achieved_gbs = bytes_per_qp * qp_per_launch / avg_launch_s / 1e9
+
+    total_qp = world * B * args.steps
+    value = total_qp / dt
+    line = {
+        "metric": "LoMPC QP solves/sec",
+        "value": value,
+        "unit": "QP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded EV populations and price vectors; reference ships no data for this path)",
+        "config": {
+            "workload": (f"config3/4: {B} EVs per GPU, horizon {N}, 50% small / 50% large EVs, "
+                         f"{P} partitions per type ({2 * P} parameter sets), fresh prices every step, "
+                         "full outputs (w, cost) + fused per-partition reductions"),
+            "evs_per_gpu": B,
+            "horizon": N,
+            "parameter_sets": 2 * P,
+            "mode": args.mode,
+            "parallelism": f"dp{world} (EV shards, RCCL all-reduce of per-set reductions)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "k_eval" if args.mode == "path" else "k_direct",
+            "bytes_per_qp": bytes_per_qp,
+            "qp_per_launch": qp_per_launch,
+            "avg_launch_us": avg_launch_s * 1e6,
+        },
+        "repaired_qps": repaired,
+    }
+    traffic_file = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(traffic_file):
+        try:
+            tr = json.load(open(traffic_file))
+            if tr.get("mode") == args.mode and tr.get("horizon") == N and tr.get("qp_per_launch") == qp_per_launch:
+                line["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
+                line["roofline"]["traffic_source"] = tr.get("source")
+        except Exception:
+            pass
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(eng, N, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(eng, N, seconds):
+    """C oracle (dense primal active set, oracle/lompc_oracle.c) on this host's
+    cores over a bounded sample of the same workload (both EV types, the
+    last step's partition prices)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_c  # checker / baseline only
+
+    oracle_c.build()
+    threads = oracle_c.max_threads()
+    # calibrate, then size the sample to ~`seconds` of CPU work
+    samples = []
+    for e in eng:
+        g = e["gamma"].cpu().numpy()
+        lm = e["lm"][-1, 0].cpu().numpy()
+        samples.append((e["c"], lm, g))
+    t0 = time.perf_counter()
+    n_cal = 256 * threads
+    for c, lm, g in samples:
+        oracle_c.solve_batch(N, c, lm, 0.0, g[:n_cal], nthreads=threads)
+    rate = 2 * n_cal / (time.perf_counter() - t0)
+    n = int(min(len(samples[0][2]), max(n_cal, rate * seconds / 2)))
+    t0 = time.perf_counter()
+    done = 0
+    for c, lm, g in samples:
+        _, _, nf = oracle_c.solve_batch(N, c, lm, 0.0, g[:n], nthreads=threads)
+        assert nf == 0
+        done += n
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "QP/s", "cores": threads, "kind": "port",
+            "sample": f"{done} QPs ({n} small + {n} large EVs, horizon {N}, partition-0 prices) "
+                      f"in {dt:.1f} s, C oracle dense active set, OpenMP {threads} threads"}
+
+
+if __name__ == "__main__":
+    main()

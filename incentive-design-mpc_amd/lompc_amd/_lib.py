@@ -1,0 +1,97 @@
+"""ctypes binding of the C-ABI in ``include/lompc_amd.h``.
+
+The shared library ``liblompc_amd.so`` is built in-tree (``lompc_amd.build``)
+from ``csrc/lompc_kernels.hip`` with ``hipcc --offload-arch=gfx950``.  There is
+no CPU fallback: if the library is missing or no HIP device is visible, every
+entry point raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblompc_amd.so")
+
+# status codes (include/lompc_amd.h)
+LOMPC_OK = 0
+LOMPC_ERR_INVALID_ARG = 1
+LOMPC_ERR_NOT_CONVERGED = 2
+LOMPC_ERR_HIP = 3
+LOMPC_ERR_UNSUPPORTED = 4
+
+LOMPC_EV_SMALL = 0
+LOMPC_EV_LARGE = 1
+LOMPC_MODE_PATH = 0
+LOMPC_MODE_DIRECT = 1
+
+LOMPC_QP_OK = 0
+LOMPC_QP_REPAIRED = 1
+LOMPC_QP_FAILED = 2
+LOMPC_QP_INVALID = 3
+
+LOMPC_STAT_COUNT = 0
+LOMPC_STAT_SUM_W0 = 1
+LOMPC_STAT_SUM_PRICE0 = 2
+LOMPC_STAT_MAX_ERR = 3
+LOMPC_STAT_SUM_COST = 4
+LOMPC_STAT_N_REPAIRED = 5
+LOMPC_STAT_N_FAILED = 6
+LOMPC_STAT_N_INVALID = 7
+LOMPC_SET_STATS = 8
+LOMPC_MAX_N = 64
+
+# (name, restype, argtypes) — must match include/lompc_amd.h exactly.
+_P = ctypes.c_void_p
+_D = ctypes.c_double
+_I = ctypes.c_int
+_L = ctypes.c_int64
+SIGNATURES = [
+    ("lompc_create", _I, [_I, _D, _D, _D, _D, _I, _I, ctypes.POINTER(_P)]),
+    ("lompc_destroy", _I, [_P]),
+    ("lompc_set_mode", _I, [_P, _I]),
+    ("lompc_set_params", _I, [_P, _L, _P, _P, _P, _P, _P]),
+    ("lompc_solve_batch", _I, [_P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    ("lompc_solve_host", _I, [_P, _P, _D, _D, _P, _P]),
+    ("lompc_last_status", _I, [_P, _P, _P, _P, _P]),
+    ("lompc_profile_enable", _I, [_P, _I]),
+    ("lompc_profile_read", _I, [_P, _P, _P, _I]),
+    ("lompc_get_info", _I, [_P, _P, _P]),
+    ("lompc_status_string", ctypes.c_char_p, [_I]),
+    ("lompc_last_error", ctypes.c_char_p, [_P]),
+    ("lompc_abi_version", _I, []),
+]
+ABI_VERSION = 1
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load (once) and type the C-ABI library. Raises RuntimeError if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RuntimeError(
+                f"lompc_amd: HIP extension not built ({p} missing); run "
+                "`python -c 'import __graft_entry__ as g; g.build()'` — there is no CPU fallback")
+        lib = ctypes.CDLL(p)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.lompc_abi_version() != ABI_VERSION:
+            raise RuntimeError("lompc_amd: ABI version mismatch; rebuild the extension")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def status_text(lib, ctx, rc: int) -> str:
+    msg = lib.lompc_last_error(ctx) if ctx else b""
+    base = lib.lompc_status_string(rc).decode()
+    return f"{base}: {msg.decode()}" if msg else base

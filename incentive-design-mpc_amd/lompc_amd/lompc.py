@@ -1,0 +1,317 @@
+"""Drop-in ``LoMPC`` for the reference's CVXPY/Clarabel path.
+
+Mirrors ``chargingstation/lompc.py`` (AkshayThiru/incentive-design-mpc):
+same ``LoMPCConstants`` dataclass (lompc.py:12-26), same constructor checks
+(lompc.py:36-38), same attributes (``N, delta, theta, y_max, w_max, ev_type,
+q_scale, A, m`` — lompc.py:59-71) and the same methods ``solve_lompc``,
+``get_sc_modulus``, ``get_input_mat``, ``get_price0``, ``phi``, ``Dphi``
+(lompc.py:137-187).  ``solve_lompc`` returns a fresh ``(N,)`` ndarray and the
+optimal cost including its constant, exactly what ``self.w.value`` /
+``self.cost.value`` give at lompc.py:154-156.
+
+Added for the batched hot path: ``set_params`` (S parameter sets at once) and
+``solve_batch`` (B QPs in one device call with fused per-set reductions).
+
+All numerics run in the HIP extension (``liblompc_amd.so``); this module only
+moves buffers and maps status codes to the reference's exception types:
+AssertionError (gamma > y_max, lompc.py:87), ValueError (negative
+parameters: cvxpy nonneg Parameters, lompc.py:78-82) and ``SolverError``
+(cvxpy.error.SolverError).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .settings import MAX_BAT_CHARGE_RATE, MAX_MAX_BAT_SOC, MIN_MAX_BAT_SOC, LOMPC_MODE
+
+
+class SolverError(Exception):
+    """Counterpart of ``cvxpy.error.SolverError``: no certified optimum."""
+
+
+@dataclass
+class LoMPCConstants:
+    """
+    delta:      Relative weight of charging cost.
+    theta:      Battery capacity [kWh].
+    y_max:      Maximum allowed state of charge (SoC) as a fraction of capacity.
+    w_max:      Maximum fraction of charge replenished per time step (normalized charging rate).
+    ev_type:    EV type, either "small" or "large".
+    """
+
+    delta: float
+    theta: float
+    y_max: float
+    w_max: float
+    ev_type: str
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+class LoMPC:
+    def __init__(self, N: int, consts: LoMPCConstants, device: int | None = None,
+                 mode: str | None = None) -> None:
+        """
+        Inputs:
+            N:      LoMPC horizon length.
+            consts: LoMPC constants.
+            device: HIP device index (default: torch's current device).
+            mode:   "path" (default) or "direct" — engine algorithm, see DESIGN.md.
+        """
+        # lompc.py:36-38
+        assert (consts.y_max >= MIN_MAX_BAT_SOC) and (consts.y_max <= MAX_MAX_BAT_SOC)
+        assert (consts.w_max >= 0) and (consts.w_max <= MAX_BAT_CHARGE_RATE)
+        assert (consts.ev_type == "small") or (consts.ev_type == "large")
+        self._ctx = None
+        self._set_constants(N, consts)
+        torch = _torch()
+        self._lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise RuntimeError("lompc_amd: no HIP device visible (the engine has no CPU path)")
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        ctx = ctypes.c_void_p()
+        ev = _lib.LOMPC_EV_SMALL if self.ev_type == "small" else _lib.LOMPC_EV_LARGE
+        rc = self._lib.lompc_create(int(N), float(self.delta), float(self.theta), float(self.y_max),
+                                    float(self.w_max), ev, self.device, ctypes.byref(ctx))
+        if rc == _lib.LOMPC_ERR_UNSUPPORTED:
+            raise ValueError(f"lompc_amd supports horizons N <= {_lib.LOMPC_MAX_N}")
+        if rc == _lib.LOMPC_ERR_INVALID_ARG:
+            raise AssertionError("invalid LoMPC constants (delta > 0, theta > 0 required)")
+        if rc != _lib.LOMPC_OK:
+            raise RuntimeError("lompc_create failed: " + _lib.status_text(self._lib, None, rc))
+        self._ctx = ctx
+        self._keep = ()
+        self.S = 0
+        self.set_mode(mode or LOMPC_MODE)
+
+    def __del__(self):
+        if getattr(self, "_ctx", None) is not None:
+            try:
+                self._lib.lompc_destroy(self._ctx)
+            except Exception:
+                pass
+            self._ctx = None
+
+    # ------------------------------------------------------------ lompc.py
+    def _set_constants(self, N: int, consts: LoMPCConstants) -> None:
+        # lompc.py:59-71
+        self.N = N
+        self.delta = consts.delta
+        self.theta = consts.theta
+        self.y_max = consts.y_max
+        self.w_max = consts.w_max
+        self.ev_type = consts.ev_type
+        # Scaling factor for the quadratic electricity cost.
+        self.q_scale = 3 * self.theta / (4 * self.w_max)
+        # LoMPC input matrix, y = A w.
+        self.A = np.tril(np.ones((self.N, self.N)))
+        # Strong convexity modulus.
+        self.m = 2 * self.delta * self.theta ** 2
+
+    def _check_rc(self, rc: int) -> None:
+        if rc == _lib.LOMPC_OK:
+            return
+        text = _lib.status_text(self._lib, self._ctx, rc)
+        if rc == _lib.LOMPC_ERR_INVALID_ARG:
+            raise ValueError(text)
+        if rc == _lib.LOMPC_ERR_NOT_CONVERGED:
+            raise SolverError(text)
+        raise RuntimeError(text)
+
+    def _validate_params(self, lmbd, lmbd_r, gamma) -> None:
+        # lompc.py:87 and cvxpy's nonneg Parameter checks (lompc.py:78-82)
+        assert gamma <= self.y_max
+        lmbd = np.asarray(lmbd, dtype=np.float64)
+        if lmbd.shape != (3 * self.N,):
+            raise ValueError(f"Invalid dimensions {lmbd.shape} for Parameter value.")
+        if gamma < 0 or lmbd_r < 0 or np.any(lmbd < 0):
+            raise ValueError("Parameter value must be nonnegative.")
+
+    def solve_lompc(self, lmbd: np.ndarray, lmbd_r: float, gamma: float) -> tuple[np.ndarray, float]:
+        """
+        Inputs:
+            lmbd:   Unit price (incentive) vector.
+            lmbd_r: Robustness price parameter.
+            gamma:  Fraction of battery capacity remaining to be charged.
+        Outputs:
+            w_opt:      Optimal w vector.
+            cost_opt:   Optimal cost.
+        """
+        self._validate_params(lmbd, lmbd_r, gamma)
+        lm = np.ascontiguousarray(np.asarray(lmbd, dtype=np.float64))
+        w = np.empty(self.N, dtype=np.float64)
+        cost = ctypes.c_double(0.0)
+        rc = self._lib.lompc_solve_host(self._ctx, lm.ctypes.data, float(lmbd_r), float(gamma),
+                                        w.ctypes.data, ctypes.addressof(cost))
+        self._check_rc(rc)
+        self.S = 0  # the single-QP call reloads the context's parameter sets
+        return w, float(cost.value)
+
+    def get_sc_modulus(self) -> float:
+        return self.m
+
+    def get_input_mat(self) -> np.ndarray:
+        return self.A
+
+    def get_price0(self, w: np.ndarray, lmbd: np.ndarray, lmbd_r: float) -> float:
+        # lompc.py:164-170
+        price0 = (
+            self.theta * (w[0] * lmbd[0] + (self.w_max - w[0]) * lmbd[self.N])
+            + self.q_scale * w[0] ** 2 * lmbd[2 * self.N]
+            + self.theta ** 2 * w[0] ** 2 * lmbd_r
+        )
+        return price0
+
+    def phi(self, w: np.ndarray) -> np.ndarray:
+        # lompc.py:172-177
+        assert w.shape == (self.N,)
+        return np.hstack((self.theta * w, self.theta * (self.w_max - w), self.q_scale * (w * w)))
+
+    def Dphi(self, w: np.ndarray) -> np.ndarray:
+        # lompc.py:179-187
+        assert w.shape == (self.N,)
+        return np.block([[self.theta * np.eye(self.N)], [-self.theta * np.eye(self.N)],
+                         [2 * self.q_scale * np.diag(w)]])
+
+    # ------------------------------------------------------------ batch API
+    def set_mode(self, mode: str) -> None:
+        m = {"path": _lib.LOMPC_MODE_PATH, "direct": _lib.LOMPC_MODE_DIRECT}[mode]
+        self._check_rc(self._lib.lompc_set_mode(self._ctx, m))
+        self.mode = mode
+
+    def _dev(self, x, dtype=None):
+        torch = _torch()
+        dtype = dtype or torch.float64
+        if isinstance(x, torch.Tensor):
+            t = x.to(device=f"cuda:{self.device}", dtype=dtype)
+        else:
+            t = torch.as_tensor(np.asarray(x), dtype=dtype, device=f"cuda:{self.device}")
+        return t.contiguous()
+
+    def _stream(self) -> int:
+        return _torch().cuda.current_stream(self.device).cuda_stream
+
+    def set_params(self, lmbd, lmbd_r, w_ref=None, gamma_ref=None, validate: bool = True) -> None:
+        """Load S parameter sets (one per (EV type, partition) price vector).
+
+        lmbd: (S, 3N) or (3N,); lmbd_r: (S,) or scalar; w_ref: (S, N) or (N,)
+        (needed for the A_bar error reduction); gamma_ref: (S,) central gamma
+        (DIRECT mode warm start).  Device tensors are used in place.
+        """
+        torch = _torch()
+        lm = self._dev(lmbd)
+        if lm.dim() == 1:
+            lm = lm.unsqueeze(0)
+        S = lm.shape[0]
+        if lm.shape[1] != 3 * self.N:
+            raise ValueError(f"lmbd must have 3N = {3 * self.N} columns")
+        lr = self._dev(lmbd_r).reshape(-1)
+        if lr.numel() == 1 and S > 1:
+            lr = lr.expand(S).contiguous()
+        if lr.numel() != S:
+            raise ValueError("lmbd_r must have one entry per parameter set")
+        wr = None
+        if w_ref is not None:
+            wr = self._dev(w_ref).reshape(S, self.N)
+        gr = None
+        if gamma_ref is not None:
+            gr = self._dev(gamma_ref).reshape(S)
+        if validate:
+            bad = torch.logical_not(lm >= 0).any() | torch.logical_not(lr >= 0).any()
+            if bool(bad):
+                raise ValueError("Parameter value must be nonnegative.")
+        rc = self._lib.lompc_set_params(self._ctx, S, _ptr(lm), _ptr(lr), _ptr(wr), _ptr(gr), self._stream())
+        self._check_rc(rc)
+        self._keep = (lm, lr, wr, gr)
+        self.S = S
+
+    def solve_batch(self, gamma, set_offsets=None, *, want_w: bool = True, want_cost: bool = True,
+                    want_w0: bool = False, want_status: bool = False, want_set: bool = True,
+                    out: dict | None = None, check: bool = True) -> dict:
+        """Solve B QPs against the loaded parameter sets.
+
+        gamma: (B,) gamma_i = y_max - y0_i (device tensor or array-like).
+        set_offsets: host int64 (S+1,) — EVs of set s are
+            [set_offsets[s], set_offsets[s+1]); default: all EVs in set 0 (S must be 1).
+        Returns a dict of device tensors: "w" (B, N), "cost" (B,), "w0" (B,),
+        "status" (B,) int8, "set_sum_w" (S, N), "set_stats" (S, 8).
+        ``check`` synchronises and raises on invalid input / uncertified QPs.
+        """
+        torch = _torch()
+        if self.S < 1:
+            raise RuntimeError("solve_batch: call set_params first")
+        g = self._dev(gamma).reshape(-1)
+        B = g.numel()
+        if set_offsets is None:
+            if self.S != 1:
+                raise ValueError("set_offsets required when more than one parameter set is loaded")
+            set_offsets = np.array([0, B], dtype=np.int64)
+        off = np.ascontiguousarray(np.asarray(set_offsets, dtype=np.int64))
+        if off.shape != (self.S + 1,):
+            raise ValueError(f"set_offsets must have S+1 = {self.S + 1} entries")
+        if check:
+            # lompc.py:87 (assert gamma <= y_max); nonneg Parameter (lompc.py:82)
+            if bool((g > self.y_max).any()):
+                raise AssertionError("gamma <= y_max required")
+            if bool(torch.logical_not(g >= 0).any()):
+                raise ValueError("Parameter value must be nonnegative.")
+        dev = f"cuda:{self.device}"
+        res = {} if out is None else out
+
+        def buf(name, shape, dtype=torch.float64, want=True):
+            if not want:
+                return None
+            t = res.get(name)
+            if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+                t = torch.empty(shape, dtype=dtype, device=dev)
+                res[name] = t
+            return t
+
+        w = buf("w", (B, self.N), want=want_w)
+        cost = buf("cost", (B,), want=want_cost)
+        w0 = buf("w0", (B,), want=want_w0)
+        status = buf("status", (B,), torch.int8, want=want_status)
+        ssw = buf("set_sum_w", (self.S, self.N), want=want_set)
+        sst = buf("set_stats", (self.S, _lib.LOMPC_SET_STATS), want=want_set)
+        rc = self._lib.lompc_solve_batch(self._ctx, B, _ptr(g), off.ctypes.data, _ptr(w), _ptr(cost),
+                                         _ptr(w0), _ptr(status), _ptr(ssw), _ptr(sst), self._stream())
+        self._check_rc(rc)
+        res["_gamma"] = g
+        if check:
+            self.check_last()
+        return res
+
+    def check_last(self) -> tuple[int, int, int]:
+        """Synchronise and raise on uncertified QPs; returns (repaired, failed, invalid)."""
+        rep, fail, inv = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        rc = self._lib.lompc_last_status(self._ctx, self._stream(), ctypes.byref(rep), ctypes.byref(fail),
+                                         ctypes.byref(inv))
+        self._check_rc(rc)
+        if inv.value:
+            raise AssertionError(f"{inv.value} EVs with gamma outside [0, y_max]")
+        if fail.value:
+            raise SolverError(f"{fail.value} LoMPC QPs without a certified optimum")
+        return rep.value, fail.value, inv.value
+
+    def profile(self, enable: bool | None = None, read: bool = False, reset: bool = False):
+        """Kernel-time profiling of the per-EV evaluation kernel (HIP events)."""
+        if enable is not None:
+            self._check_rc(self._lib.lompc_profile_enable(self._ctx, int(bool(enable))))
+        if read:
+            ms, n = ctypes.c_double(0.0), ctypes.c_int64(0)
+            self._check_rc(self._lib.lompc_profile_read(self._ctx, ctypes.byref(ms), ctypes.byref(n),
+                                                        int(bool(reset))))
+            return ms.value, n.value
+        return None

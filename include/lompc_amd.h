@@ -1,0 +1,146 @@
+/*
+ * lompc_amd.h — C-ABI of the MI355X-native batched LoMPC QP engine.
+ *
+ * Drop-in boundary for the reference's per-EV LoMPC solve
+ * (AkshayThiru/incentive-design-mpc, chargingstation/lompc.py).  The reference
+ * has no FFI layer: its boundary is the Python class ``LoMPC``
+ * (lompc.py:29-187) whose ``solve_lompc`` (lompc.py:137-156) is called once
+ * per EV from the loops in price_solver.py:203-209 and :280-283.  Every
+ * entry point below names the reference interface it replaces.
+ *
+ * Conventions
+ *   - Plain C types only (no torch / HIP types in signatures).  ``stream`` is
+ *     a ``hipStream_t`` passed as ``void*`` (NULL = the legacy default stream).
+ *   - "dev" pointers are device pointers owned by the caller (e.g. the
+ *     data_ptr() of a PyTorch-ROCm tensor); "host" pointers are host memory.
+ *   - All device work is asynchronous on ``stream`` unless stated otherwise.
+ *   - Counts are int64.  Every function returns an int status (LOMPC_OK = 0).
+ *   - A context is bound to one device; it is not re-entrant (the reference's
+ *     ``LoMPC`` holds mutable cvx.Parameters and is not re-entrant either).
+ */
+#ifndef LOMPC_AMD_H
+#define LOMPC_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (mapped to the reference's Python exceptions by the shim) */
+#define LOMPC_OK                0  /* success                                        */
+#define LOMPC_ERR_INVALID_ARG   1  /* AssertionError / ValueError in the reference    */
+#define LOMPC_ERR_NOT_CONVERGED 2  /* cvxpy SolverError                               */
+#define LOMPC_ERR_HIP           3  /* HIP runtime failure                             */
+#define LOMPC_ERR_UNSUPPORTED   4  /* e.g. horizon N > LOMPC_MAX_N                    */
+
+/* ---- EV types (LoMPCConstants.ev_type, lompc.py:26) */
+#define LOMPC_EV_SMALL 0
+#define LOMPC_EV_LARGE 1
+
+/* ---- solve modes */
+#define LOMPC_MODE_PATH   0  /* exact solution path in gamma per set + per-EV evaluation,
+                                KKT certificate and active-set repair (default)        */
+#define LOMPC_MODE_DIRECT 1  /* independent per-EV active-set solve, warm-started from the
+                                set's central solution                                  */
+
+/* ---- per-EV status values written to ``status[B]`` */
+#define LOMPC_QP_OK        0 /* certified optimal (KKT residual <= tol)                 */
+#define LOMPC_QP_REPAIRED  1 /* certified optimal after the per-EV active-set repair    */
+#define LOMPC_QP_FAILED    2 /* no certified solution (would be SolverError)            */
+#define LOMPC_QP_INVALID   3 /* gamma outside [0, y_max] or NaN (AssertionError)        */
+
+/* ---- layout of one row of ``set_stats[S][LOMPC_SET_STATS]`` */
+#define LOMPC_STAT_COUNT      0 /* number of EVs in the set                          */
+#define LOMPC_STAT_SUM_W0     1 /* sum_i w_i[0]            (charging_station.py:359) */
+#define LOMPC_STAT_SUM_PRICE0 2 /* sum_i get_price0(w_i)   (price_solver.py:283)     */
+#define LOMPC_STAT_MAX_ERR    3 /* max_i ||w_i - w_ref||_{A_bar} (price_solver.py:207-209) */
+#define LOMPC_STAT_SUM_COST   4 /* sum_i cost_i                                      */
+#define LOMPC_STAT_N_REPAIRED 5 /* EVs that needed the active-set repair             */
+#define LOMPC_STAT_N_FAILED   6 /* EVs without a certified solution                  */
+#define LOMPC_STAT_N_INVALID  7 /* EVs with invalid gamma                            */
+#define LOMPC_SET_STATS       8
+
+#define LOMPC_MAX_N 64
+
+typedef struct lompc_ctx lompc_ctx;
+
+/* Create a context for one EV type and horizon on ``device``.
+ * Replaces LoMPC.__init__ / _set_constants (lompc.py:30-71): validates
+ * y_max in [0.75, 0.9] and w_max in (0, 0.25] (lompc.py:36-37; settings.py:7-9),
+ * ev_type (lompc.py:38) and requires delta > 0 (strict convexity). */
+int lompc_create(int N, double delta, double theta, double y_max, double w_max,
+                 int ev_type, int device, lompc_ctx** out);
+
+/* Release every device/host resource of the context. */
+int lompc_destroy(lompc_ctx* ctx);
+
+/* Select LOMPC_MODE_PATH (default) or LOMPC_MODE_DIRECT. */
+int lompc_set_mode(lompc_ctx* ctx, int mode);
+
+/* Load S parameter sets and prepare them on device.
+ * Replaces LoMPC._update_cvx_parameters (lompc.py:84-90) for S sets at once
+ * (one set = one (EV type, partition) price vector in price_solver.py).
+ *   lmbd   dev  [S, 3N]  unit prices lambda >= 0        (lompc.py:78)
+ *   lmbd_r dev  [S]      robustness price >= 0           (lompc.py:80)
+ *   w_ref  dev  [S, N]   reference w for the A_bar error (price_solver.py:196), or NULL
+ *   gamma_ref dev [S]    central gamma per set (gamma_sc, price_solver.py:76), or NULL
+ *                        (NULL = y_max / 2); only used by LOMPC_MODE_DIRECT
+ * Launches the per-set preparation kernel (derived data + exact solution
+ * path in gamma, or the central solution in DIRECT mode). */
+int lompc_set_params(lompc_ctx* ctx, int64_t S, const double* lmbd,
+                     const double* lmbd_r, const double* w_ref,
+                     const double* gamma_ref, void* stream);
+
+/* Solve B LoMPC QPs against the loaded parameter sets.
+ * Replaces the per-EV loops of PriceSolver._get_w_err (price_solver.py:196-214)
+ * and PriceSolver.get_w0_price0 (price_solver.py:272-285), each iteration of
+ * which is one LoMPC.solve_lompc (lompc.py:137-156).
+ *   gamma        dev  [B]      gamma_i = y_max - y0_i (price_solver.py:202)
+ *   set_offsets  host [S+1]    EVs of set s are [set_offsets[s], set_offsets[s+1])
+ *   w            dev  [B, N]   optimal w_i (row-major), or NULL
+ *   cost         dev  [B]      optimal cost incl. constant (lompc.py:155), or NULL
+ *   w0           dev  [B]      w_i[0] (price_solver.py:282), or NULL
+ *   status       dev  [B]      int8 LOMPC_QP_* per EV, or NULL
+ *   set_sum_w    dev  [S, N]   sum_i w_i per set (price_solver.py:205), or NULL
+ *   set_stats    dev  [S, LOMPC_SET_STATS] fused per-set reductions, or NULL
+ * Errors detected on device are reported through ``status``/``set_stats`` and
+ * ``lompc_last_status``. */
+int lompc_solve_batch(lompc_ctx* ctx, int64_t B, const double* gamma,
+                      const int64_t* set_offsets, double* w, double* cost,
+                      double* w0, int8_t* status, double* set_sum_w,
+                      double* set_stats, void* stream);
+
+/* Synchronous single-QP convenience entry with host buffers.
+ * Replaces LoMPC.solve_lompc (lompc.py:137-156) one-for-one:
+ *   lmbd host [3N], lmbd_r, gamma -> w host [N], *cost. */
+int lompc_solve_host(lompc_ctx* ctx, const double* lmbd, double lmbd_r,
+                     double gamma, double* w, double* cost);
+
+/* Synchronise ``stream`` and report the device-side counters of the last
+ * lompc_solve_batch: EVs repaired, failed, invalid (any may be NULL). */
+int lompc_last_status(lompc_ctx* ctx, void* stream, int64_t* n_repaired,
+                      int64_t* n_failed, int64_t* n_invalid);
+
+/* Profiling: when enabled, every lompc_solve_batch brackets its per-EV
+ * evaluation kernel with HIP events on ``stream``; lompc_profile_read
+ * synchronises and returns the summed milliseconds and launch count since
+ * the last reset. */
+int lompc_profile_enable(lompc_ctx* ctx, int enable);
+int lompc_profile_read(lompc_ctx* ctx, double* total_ms, int64_t* launches,
+                       int reset);
+
+/* Horizon N and EV type of a context. */
+int lompc_get_info(const lompc_ctx* ctx, int* N, int* ev_type);
+
+/* Human-readable text of a status code or of the context's last error. */
+const char* lompc_status_string(int status);
+const char* lompc_last_error(const lompc_ctx* ctx);
+
+/* ABI version (bumped on any signature change). */
+int lompc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LOMPC_AMD_H */

@@ -4,21 +4,20 @@
 // per EV from PriceSolver._get_w_err (price_solver.py:203-209) and
 // PriceSolver.get_w0_price0 (price_solver.py:280-283).
 //
-// Kernels (one batched call = K1 at set_params time, K2 -> K2b -> K3 per solve):
-//   K1 k_prepare   one wave per parameter set. Derived data (d, e, c0, ...) and, in
-//                  PATH mode, the exact piecewise-affine solution path w*(gamma) over
-//                  [0, y_max]: lane l solves the QP at gamma_l = l*y_max/64 (PDAS with
-//                  primal active-set fallback) and tracks the active-set changes up to
-//                  gamma_{l+1} (parametric-QP homotopy). In DIRECT mode: the central
-//                  solution's working set.
-//   K2 k_eval      one EV per lane, 256 EVs of one set per workgroup. Looks up its
-//                  piece, w = a + b*gamma, certifies it by the KKT residual, computes
-//                  cost / w0 / price0 / A_bar error, writes outputs and per-workgroup
-//                  partial reductions. Uncertified EVs go to a per-workgroup list.
-//   K2b k_direct   per-EV active-set solve (PDAS from a warm start, primal active set
-//                  as last resort), certified; repairs K2's list (PATH) or solves every
-//                  EV (DIRECT).
-//   K3 k_finalize  deterministic per-set reduction of the workgroup partials.
+// Kernels (K1 at set_params time, K2 (or K2d) -> K3 per solve):
+//   K1  k_path      one wave per (parameter set, gamma cell). PATH mode: the exact
+//                   piecewise-affine solution path w*(gamma) on the cell [l h, (l+1) h]:
+//                   wave-parallel PDAS at the cell start, then parametric active-set
+//                   tracking (homotopy) to the cell end, pieces w = a + b gamma stored
+//                   with their working sets.  DIRECT mode: the central solution.
+//   K2  k_eval      one EV per lane, one wave per workgroup (64 EVs of one set).
+//                   w = a + b gamma from the EV's piece, KKT certificate, cost / w0 /
+//                   price0 / A_bar error.  Uncertified EVs are re-solved in place by the
+//                   whole wave (wave_solve).  Epilogue through an LDS tile: coalesced w
+//                   stores and deterministic per-workgroup column sums.
+//   K2d k_direct    DIRECT mode: every EV solved by its own lane (PDAS warm-started
+//                   from the central working set), same certificate/repair/epilogue.
+//   K3  k_finalize  deterministic per-set reduction of the workgroup partials.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -29,20 +28,20 @@
 #include <vector>
 
 #include "lompc_qp.hpp"
+#include "lompc_wave.hpp"
 #include "../../include/lompc_amd.h"
 
-#define EVAL_BLOCK 256
-#define NPART_EXTRA 8  // partial record: [0,N) sum_w, then 8 scalars
+#define EVAL_BLOCK 64  // one wave per workgroup
+#define NPX 7          // partial record: [0,N) sum_w, then NPX scalars
 
-enum {
-  PT_SUM_W0 = 0,
-  PT_SUM_PRICE0 = 1,
-  PT_MAX_ERR = 2,
-  PT_SUM_COST = 3,
-  PT_N_OK = 4,
-  PT_N_REPAIRED = 5,
-  PT_N_FAILED = 6,
-  PT_N_INVALID = 7
+enum {  // partial columns after the N sums
+  PX_COST = 0,
+  PX_PRICE0 = 1,
+  PX_MAX_ERR = 2,
+  PX_N_OK = 3,
+  PX_N_REPAIRED = 4,
+  PX_N_FAILED = 5,
+  PX_N_INVALID = 6
 };
 
 struct KArgs {
@@ -56,27 +55,13 @@ struct KArgs {
   const int64_t* set_off;  // [S+1]
   const double* setdata;   // [S][SD]
   PathTable tab;
-  const uint32_t* central; // [S][LQ_NW_MAX]
+  const uint8_t* central;  // [S][LQ_STB]
   double* w;
   double* cost;
   double* w0;
   int8_t* status;
-  double* partial;  // [nblk][N+8]
-  int* fail_cnt;    // [nblk]
-  int* fail_idx;    // [nblk][EVAL_BLOCK]
+  double* partial;  // [nblk][N+NPX]
 };
-
-// ------------------------------------------------------------------ helpers
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
-  return v;
-}
 
 // block -> (set, first EV) for set-contiguous batches
 __device__ __forceinline__ void block_set(const KArgs& a, int b, int& s, int64_t& start, int64_t& end) {
@@ -91,246 +76,258 @@ __device__ __forceinline__ void block_set(const KArgs& a, int b, int& s, int64_t
   end = a.set_off[s + 1];
 }
 
-// Block reduction of the per-EV contributions into partial[b] (deterministic).
-// mode_add = 1: add into the existing record (repair pass).
-template <int NMAX>
-__device__ __forceinline__ void block_partials(const QPConst& q, const double (&w)[NMAX], bool ok, const EVOut& o,
-                               int n_rep, int n_fail, int n_inv, double* __restrict__ part, bool mode_add) {
-  __shared__ double red[EVAL_BLOCK / 64][NMAX + NPART_EXTRA];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int N = q.N;
+__device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
-  for (int t = 0; t < NMAX; ++t) {
-    if (t < N) {
-      const double v = wave_sum(ok ? w[t] : 0.0);
-      if (lane == 0) red[wv][t] = v;
-    }
-  }
-  double s0 = wave_sum(ok ? w[0] : 0.0);
-  double s1 = wave_sum(ok ? o.price0 : 0.0);
-  double s2 = wave_max(ok ? o.err : 0.0);
-  double s3 = wave_sum(ok ? o.cost : 0.0);
-  double s4 = wave_sum(ok ? 1.0 : 0.0);
-  double s5 = wave_sum((double)n_rep);
-  double s6 = wave_sum((double)n_fail);
-  double s7 = wave_sum((double)n_inv);
-  if (lane == 0) {
-    red[wv][NMAX + 0] = s0;
-    red[wv][NMAX + 1] = s1;
-    red[wv][NMAX + 2] = s2;
-    red[wv][NMAX + 3] = s3;
-    red[wv][NMAX + 4] = s4;
-    red[wv][NMAX + 5] = s5;
-    red[wv][NMAX + 6] = s6;
-    red[wv][NMAX + 7] = s7;
-  }
-  __syncthreads();
-  const int tid = threadIdx.x;
-  if (tid < N + NPART_EXTRA) {
-    const int src = tid < N ? tid : NMAX + (tid - N);
-    const bool is_max = (tid == N + PT_MAX_ERR);
-    double acc = red[0][src];
-#pragma unroll
-    for (int k = 1; k < EVAL_BLOCK / 64; ++k) acc = is_max ? fmax(acc, red[k][src]) : acc + red[k][src];
-    if (mode_add) {
-      const double old = part[tid];
-      acc = is_max ? fmax(old, acc) : old + acc;
-    }
-    part[tid] = acc;
-  }
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
 }
 
+// Cost / A_bar error / price0 of the QP solved by the whole wave (lane t = w_t),
+// the wave form of lq_outputs.  Result valid on every lane.
+__device__ __forceinline__ EVOut wave_outputs(const QPConst& q, const double* __restrict__ sd, double gamma,
+                                              int lane, double w, bool want_err) {
+  const int N = q.N;
+  const bool act = lane < N;
+  lqw::Aff<2> h = lqw::Aff<2>::identity();  // prefix sums of w and of (w - w_ref)
+  const double wr = act ? sd[2 * N + lane] : 0.0;
+  if (act) {
+    h.B[0] = w;
+    h.B[1] = w - wr;
+  }
+  const lqw::Aff<2> Y = lqw::wave_scan(h);
+  const double y = Y.B[0], ey = Y.B[1];
+  double term = 0.0, eyy = 0.0, edd = 0.0, pwl = 0.0;
+  if (act) {
+    const double d = sd[lane], e = sd[N + lane];
+    term = 0.5 * q.c * y * y - q.c * gamma * y + w * fma(0.5 * d, w, e);
+    if (!q.ev_small) pwl = lq_pwl(w * q.inv_wmax);
+    eyy = ey * ey;
+    edd = (w - wr) * (w - wr);
+  }
+  const double tw = q.theta * q.w_max;
+  EVOut o;
+  o.cost = wave_sum(term) + sd[3 * N + 0] + (q.ev_small ? 0.0 : tw * tw * wave_sum(pwl));
+  o.err = want_err ? sqrt(wave_sum(eyy) + sd[3 * N + 5] * wave_sum(edd)) : 0.0;
+  const double w0 = __shfl(w, 0, 64);
+  o.price0 = lq_price0(q, sd, w0);
+  return o;
+}
+
+// Shared epilogue of K2 / K2d for one wave of EVs [start, start+64) of set s.
+// ok lanes carry a certified w[] and outputs; failed lanes are re-solved by the
+// whole wave starting from `st_fail` (per-lane working-set bytes, or nullptr).
 template <int NMAX>
-__device__ __forceinline__ void load_states(States<NMAX>& st, const uint32_t* __restrict__ src) {
+__device__ __forceinline__ void ev_epilogue(const QPConst& q, const KArgs& a, int b, int s, int64_t start,
+                                            int64_t end, double g, bool valid, bool ok, const double (&w)[NMAX],
+                                            const EVOut& o, const uint8_t* st_fail, int8_t ok_code) {
+  __shared__ double tile[EVAL_BLOCK * (NMAX + 3)];
+  const int N = q.N;
+  const int TS = N + 3;  // odd for even N: conflict-free row-per-lane ds_write_b64
+  const int lane = threadIdx.x;
+  const int64_t i = start + lane;
+  const bool active = i < end;
+  const double* __restrict__ sd = a.setdata + (size_t)s * lq_sd(N);
+  const bool fail = valid && !ok;
+  int8_t stat = !active ? 0 : (!valid ? LOMPC_QP_INVALID : (ok ? ok_code : LOMPC_QP_FAILED));
+  // rows: w, cost, price0, err
+  const double fill = valid ? 0.0 : NAN;
 #pragma unroll
-  for (int i = 0; i < States<NMAX>::NW; ++i) st.w[i] = src[i];
+  for (int t = 0; t < NMAX; ++t)
+    if (t < N) tile[lane * TS + t] = ok ? w[t] : fill;
+  tile[lane * TS + N] = ok ? o.cost : fill;
+  tile[lane * TS + N + 1] = ok ? o.price0 : 0.0;
+  tile[lane * TS + N + 2] = ok ? o.err : 0.0;
+  // in-place repair of uncertified EVs: the whole wave solves each one
+  unsigned long long fm = __ballot(fail);
+  int n_rep = 0, n_fail = 0;
+  if (fm) {
+    lqw::WaveSet ws;
+    ws.load(sd, N);
+    while (fm) {
+      const int k = __ffsll((long long)fm) - 1;
+      fm &= fm - 1;
+      const double gk = __shfl(g, k, 64);
+      const uint8_t* sk = reinterpret_cast<const uint8_t*>(__shfl((long long)(uintptr_t)st_fail, k, 64));
+      int sl = lane < N ? (sk ? (int)sk[lane] : 1) : 0;
+      double wl = 0.0, rl = 0.0;
+      const bool okk = lqw::wave_solve(q, ws, gk, sl, wl, rl);
+      const EVOut ok_out = wave_outputs(q, sd, gk, lane, wl, a.want_err != 0);
+      if (lane < N) tile[k * TS + lane] = wl;
+      if (lane == 0) {
+        tile[k * TS + N] = ok_out.cost;
+        tile[k * TS + N + 1] = ok_out.price0;
+        tile[k * TS + N + 2] = ok_out.err;
+      }
+      if (lane == k) stat = okk ? LOMPC_QP_REPAIRED : LOMPC_QP_FAILED;
+      n_rep += okk ? 1 : 0;
+      n_fail += okk ? 0 : 1;
+    }
+  }
+  __syncthreads();
+  // coalesced stores (row-major w[B][N])
+  const int nrow = (int)min((int64_t)EVAL_BLOCK, end - start);
+  if (a.w && nrow > 0) {
+    double* wo = a.w + (size_t)start * N;
+    const int tot = nrow * N;
+    const int q64 = EVAL_BLOCK / N, r64 = EVAL_BLOCK % N;
+    int row = lane / N, col = lane % N;
+    for (int e = lane; e < tot; e += EVAL_BLOCK) {
+      wo[e] = tile[row * TS + col];
+      row += q64;
+      col += r64;
+      if (col >= N) {
+        col -= N;
+        row += 1;
+      }
+    }
+  }
+  if (active) {
+    if (a.cost) a.cost[i] = tile[lane * TS + N];
+    if (a.w0) a.w0[i] = tile[lane * TS + 0];
+    if (a.status) a.status[i] = stat;
+  }
+  // per-workgroup partials: column sums over the valid rows (max for the error)
+  const unsigned long long vm = __ballot(valid);
+  const unsigned long long okm = __ballot(ok);
+  const unsigned long long im = __ballot(active && !valid);
+  double* part = a.partial + (size_t)b * (N + NPX);
+  for (int c = lane; c < TS; c += EVAL_BLOCK) {
+    const bool is_max = (c == N + PX_MAX_ERR);
+    double acc0 = 0.0, acc1 = 0.0;
+    for (int r = 0; r < EVAL_BLOCK; r += 2) {
+      const double v0 = ((vm >> r) & 1ull) ? tile[r * TS + c] : 0.0;
+      const double v1 = ((vm >> (r + 1)) & 1ull) ? tile[(r + 1) * TS + c] : 0.0;
+      acc0 = is_max ? fmax(acc0, v0) : acc0 + v0;
+      acc1 = is_max ? fmax(acc1, v1) : acc1 + v1;
+    }
+    part[c] = is_max ? fmax(acc0, acc1) : acc0 + acc1;
+  }
+  if (lane == 0) {
+    const int nok = __popcll(okm);
+    part[N + PX_N_OK] = (double)(nok + n_rep);
+    part[N + PX_N_REPAIRED] = (double)n_rep;
+    part[N + PX_N_FAILED] = (double)n_fail;
+    part[N + PX_N_INVALID] = (double)__popcll(im);
+  }
 }
 
 // ------------------------------------------------------------------- K1
-// Piecewise-affine tracking of w*(gamma) from (st optimal at g_lo) up to g_hi.
-template <int NMAX>
-__device__ __forceinline__ int lq_track(const QPConst& q, const double* __restrict__ d, const double* __restrict__ e,
-                        States<NMAX>& st, double g_lo, double g_hi, const PathTable& tab, size_t cb) {
+__global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __restrict__ lmbd,
+                                             const double* __restrict__ lmbd_r, const double* __restrict__ w_ref,
+                                             const double* __restrict__ gamma_ref, double* __restrict__ setdata,
+                                             int mode, PathTable tab, uint8_t* __restrict__ central,
+                                             int* __restrict__ errflag) {
+  lq_tab_init(q);
+  const int lane = threadIdx.x;
   const int N = q.N;
-  double gcur = g_lo;
+  const int s = (mode == LOMPC_MODE_PATH) ? (int)(blockIdx.x / LQ_G) : (int)blockIdx.x;
+  const int cell = (mode == LOMPC_MODE_PATH) ? (int)(blockIdx.x % LQ_G) : 0;
+  const double* L = lmbd + (size_t)s * 3 * N;
+  const double lr = lmbd_r[s];
+  const double tt = q.theta * q.theta;
+  // per-stage data, natural (stage = lane) and reversed (stage = N-1-lane) layouts
+  lqw::WaveSet ws;
+  ws.N = N;
+  ws.lane = lane;
+  ws.rsrc = lane < N ? N - 1 - lane : lane;
+  double l2 = 0.0;
+  if (lane < N) {
+    const double l1 = L[lane], l3 = L[2 * N + lane];
+    l2 = L[N + lane];
+    if (!(l1 >= 0.0 && l2 >= 0.0 && l3 >= 0.0)) atomicOr(errflag, 1);
+    ws.d_nat = 2.0 * lr * tt + 2.0 * q.q_scale * l3 + q.dsmall;
+    ws.e_nat = q.theta * (l1 - l2);
+    const int tr = ws.rsrc;
+    ws.d_rev = 2.0 * lr * tt + 2.0 * q.q_scale * L[2 * N + tr] + q.dsmall;
+    ws.e_rev = q.theta * (L[tr] - L[N + tr]);
+  } else {
+    ws.d_nat = ws.e_nat = ws.d_rev = ws.e_rev = 0.0;
+  }
+  if (cell == 0) {  // one block per set writes the derived set record
+    const int SD = lq_sd(N);
+    double* out = setdata + (size_t)s * SD;
+    if (lane < N) {
+      out[lane] = ws.d_nat;
+      out[N + lane] = ws.e_nat;
+      out[2 * N + lane] = w_ref ? w_ref[(size_t)s * N + lane] : 0.0;
+    }
+    const double s2 = wave_sum(l2);
+    if (lane == 0) {
+      if (!(lr >= 0.0)) atomicOr(errflag, 1);
+      out[3 * N + 0] = q.theta * q.w_max * s2;  // c0, lompc.py:128
+      out[3 * N + 1] = L[0];
+      out[3 * N + 2] = L[N];
+      out[3 * N + 3] = L[2 * N];
+      out[3 * N + 4] = lr;
+      out[3 * N + 5] = lr / q.delta;  // kappa, price_solver.py:191
+      out[3 * N + 6] = gamma_ref ? gamma_ref[s] : 0.5 * q.y_max;
+      out[3 * N + 7] = w_ref ? 1.0 : 0.0;
+    }
+  }
+  if (mode != LOMPC_MODE_PATH) {
+    const double g = gamma_ref ? gamma_ref[s] : 0.5 * q.y_max;
+    int sl = lane < N ? 1 : 0;
+    double w = 0.0, r = 0.0;
+    if (!lqw::wave_solve(q, ws, g, sl, w, r)) sl = lane < N ? 1 : 0;
+    central[(size_t)s * LQ_STB + lane] = (uint8_t)(lane < N ? sl : 0);
+    return;
+  }
+  const double h = q.y_max / (double)LQ_G;
+  const double glo = (double)cell * h;
+  const double ghi = (cell == LQ_G - 1) ? q.y_max : (double)(cell + 1) * h;
+  const size_t cb = (size_t)s * LQ_G + cell;
+  int sl = lane < N ? 1 : 0;
+  double w = 0.0, r = 0.0;
+  if (!lqw::wave_solve(q, ws, glo, sl, w, r)) {
+    if (lane == 0) tab.cnt[cb] = 0;  // EVs of this cell are solved in K2 by wave_solve
+    return;
+  }
+  // parametric active-set tracking of w*(gamma) on [glo, ghi]
+  double gcur = glo;
   int last = -1, npc = 0;
   const int max_iter = 4 * LQ_PPL + 16;
   for (int it = 0; it < max_iter && npc < LQ_PPL; ++it) {
-    double K[NMAX], a[NMAX], b[NMAX];
-    {
-      double P = 0.0, p0 = 0.0, p1 = 0.0;
-#pragma unroll
-      for (int t = NMAX - 1; t >= 0; --t) {
-        if (t < N) {
-          const double Q = q.c + P;
-          const double q0 = p0, q1 = p1 - q.c;
-          const int s = st.get(t);
-          const bool fr = (s & 1) != 0;
-          const double dt = d[t];
-          const double et = e[t] + lq_slope(q, (s - 1) >> 1);
-          const double inv = 1.0 / (Q + dt);
-          const double wb = lq_knot(q, s >> 1);
-          K[t] = fr ? -Q * inv : 0.0;
-          a[t] = fr ? -(q0 + et) * inv : wb;
-          b[t] = fr ? -q1 * inv : 0.0;
-          P = fr ? Q * dt * inv : Q;
-          p0 = fr ? (q0 * dt - et * Q) * inv : fma(Q, wb, q0);
-          p1 = fr ? q1 * dt * inv : q1;
-        }
+    const lqw::StageSol<2> sol = lqw::solve_stage<2>(q, ws, 0.0, sl);
+    const double av = sol.w[0], bv = sol.w[1], r0 = sol.r[0], r1 = sol.r[1];
+    double gc = INFINITY;
+    int ns = sl;
+    if (lane < N) {
+      const Box bx = lq_box(sl);
+      if (sl & 1) {  // free: w(gamma) = a + b gamma leaves [lo, hi]
+        if (bv > 0.0) { gc = (bx.hi - av) / bv; ns = sl + 1; }
+        else if (bv < 0.0) { gc = (bx.lo - av) / bv; ns = sl - 1; }
+      } else {       // fixed: v(gamma) = -r0 - r1 gamma leaves [slo, shi]
+        if (r1 < 0.0) { gc = -(bx.shi + r0) / r1; ns = sl + 1; }
+        else if (r1 > 0.0) { gc = -(bx.slo + r0) / r1; ns = sl - 1; }
       }
-      double y0 = 0.0, y1 = 0.0;
-#pragma unroll
-      for (int t = 0; t < NMAX; ++t) {
-        if (t < N) {
-          a[t] = fma(K[t], y0, a[t]);
-          b[t] = fma(K[t], y1, b[t]);
-          y0 += a[t];
-          y1 += b[t];
-        }
-      }
+      if (!(gc == gc)) gc = INFINITY;  // NaN guard
+      if (lane == last && gc <= gcur) gc = INFINITY;
+      gc = fmax(gc, gcur);
     }
-    // totals of the cumulative sums (gradient r = r0 + gamma r1 by the prefix trick)
-    double Z0t = 0.0, Z1t = 0.0;
-    {
-      double y0 = 0.0, y1 = 0.0;
-#pragma unroll
-      for (int t = 0; t < NMAX; ++t)
-        if (t < N) {
-          y0 += a[t];
-          y1 += b[t];
-          Z0t += y0;
-          Z1t += y1;
-        }
+    double best = gc;
+    int bj = lane;
+    lqw::wave_argmin(best, bj);
+    if (!(best < ghi)) {
+      best = ghi;
+      bj = -1;
     }
-    double best = g_hi;
-    int bj = -1, bns = 0;
-    {
-      double y0 = 0.0, y1 = 0.0, Z0 = 0.0, Z1 = 0.0;
-#pragma unroll
-      for (int t = 0; t < NMAX; ++t) {
-        if (t < N) {
-          y0 += a[t];
-          y1 += b[t];
-          const double r0 = q.c * (Z0t - Z0) + d[t] * a[t] + e[t];
-          const double r1 = q.c * (Z1t - Z1 - (double)(N - t)) + d[t] * b[t];
-          Z0 += y0;
-          Z1 += y1;
-          const int s = st.get(t);
-          double gc = INFINITY;
-          int ns = s;
-          if (s & 1) {
-            const int kk = (s - 1) >> 1;
-            if (b[t] > 0.0) {
-              gc = (lq_knot(q, kk + 1) - a[t]) / b[t];
-              ns = 2 * (kk + 1);
-            } else if (b[t] < 0.0) {
-              gc = (lq_knot(q, kk) - a[t]) / b[t];
-              ns = 2 * kk;
-            }
-          } else {
-            const int kk = s >> 1;
-            if (r1 < 0.0 && kk < q.m) {
-              gc = -(lq_slope(q, kk) + r0) / r1;
-              ns = 2 * kk + 1;
-            } else if (r1 > 0.0 && kk > 0) {
-              gc = -(lq_slope(q, kk - 1) + r0) / r1;
-              ns = 2 * kk - 1;
-            }
-          }
-          if (t == last && gc <= gcur) gc = INFINITY;
-          gc = fmax(gc, gcur);
-          if (gc < best) {
-            best = gc;
-            bj = t;
-            bns = ns;
-          }
-        }
-      }
-    }
-    // record piece [gcur, best] unless it has zero length (simultaneous events)
     const bool final_piece = (bj < 0) || (npc == LQ_PPL - 1);
-    if (best > gcur || bj < 0 || final_piece) {
+    if (best > gcur || final_piece) {
       const size_t pidx = cb * LQ_PPL + npc;
-      tab.gend[pidx] = (bj < 0) ? g_hi : best;
-      double2* row = reinterpret_cast<double2*>(tab.ab + pidx * (size_t)N * 2);
-#pragma unroll
-      for (int t = 0; t < NMAX; ++t)
-        if (t < N) row[t] = make_double2(a[t], b[t]);
-#pragma unroll
-      for (int i = 0; i < States<NMAX>::NW; ++i) tab.st[pidx * LQ_NW_MAX + i] = st.w[i];
+      if (lane < N) {
+        reinterpret_cast<double2*>(tab.ab + pidx * (size_t)N * 2)[lane] = make_double2(av, bv);
+        tab.st[pidx * LQ_STB + lane] = (uint8_t)sl;
+      }
+      if (lane == 0) tab.gend[pidx] = best;
       ++npc;
     }
     if (bj < 0) break;
-    st.set_rt(bj, bns);
+    const int bns = __shfl(ns, bj, 64);
+    if (lane == bj) sl = bns;
     gcur = best;
     last = bj;
   }
-  tab.cnt[cb] = npc;
-  return npc;
-}
-
-template <int NMAX>
-__global__ __launch_bounds__(64) void k_prepare(QPConst q, int S, const double* __restrict__ lmbd,
-                                                const double* __restrict__ lmbd_r,
-                                                const double* __restrict__ w_ref,
-                                                const double* __restrict__ gamma_ref,
-                                                double* __restrict__ setdata, int mode, PathTable tab,
-                                                uint32_t* __restrict__ central, int* __restrict__ errflag) {
-  lq_tab_init(q);
-  const int s = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int N = q.N;
-  const int SD = lq_sd(N);
-  __shared__ double sd[3 * NMAX + 8];
-  const double* L = lmbd + (size_t)s * 3 * N;
-  const double lr = lmbd_r[s];
-  for (int t = lane; t < N; t += 64) {
-    const double l1 = L[t], l2 = L[N + t], l3 = L[2 * N + t];
-    if (!(l1 >= 0.0 && l2 >= 0.0 && l3 >= 0.0)) atomicOr(errflag, 1);
-    sd[t] = 2.0 * lr * q.theta * q.theta + 2.0 * q.q_scale * l3 + q.dsmall;
-    sd[N + t] = q.theta * (l1 - l2);
-    sd[2 * N + t] = w_ref ? w_ref[(size_t)s * N + t] : 0.0;
-  }
-  if (lane == 0) {
-    double s2 = 0.0;
-    for (int t = 0; t < N; ++t) s2 += L[N + t];
-    if (!(lr >= 0.0)) atomicOr(errflag, 1);
-    sd[3 * N + 0] = q.theta * q.w_max * s2;
-    sd[3 * N + 1] = L[0];
-    sd[3 * N + 2] = L[N];
-    sd[3 * N + 3] = L[2 * N];
-    sd[3 * N + 4] = lr;
-    sd[3 * N + 5] = lr / q.delta;
-    sd[3 * N + 6] = gamma_ref ? gamma_ref[s] : 0.5 * q.y_max;
-    sd[3 * N + 7] = w_ref ? 1.0 : 0.0;
-  }
-  __syncthreads();
-  for (int i = lane; i < SD; i += 64) setdata[(size_t)s * SD + i] = sd[i];
-  const double* d = sd;
-  const double* e = sd + N;
-  if (mode == LOMPC_MODE_PATH) {
-    const double h = q.y_max / (double)LQ_G;
-    const double glo = (double)lane * h;
-    const double ghi = (lane == LQ_G - 1) ? q.y_max : (double)(lane + 1) * h;
-    States<NMAX> st;
-    st.fill(1);
-    double w[NMAX];
-    bool ok = lq_pdas<NMAX>(q, d, e, glo, st, w, 4 * N + 8);
-    if (!ok) ok = lq_primal_as<NMAX>(q, d, e, glo, st, w, 16 * N + 16);
-    const size_t cb = (size_t)s * LQ_G + lane;
-    if (ok) lq_track<NMAX>(q, d, e, st, glo, ghi, tab, cb);
-    else tab.cnt[cb] = 0;
-  } else if (lane == 0) {
-    const double g = sd[3 * N + 6];
-    States<NMAX> st;
-    st.fill(1);
-    double w[NMAX];
-    bool ok = lq_pdas<NMAX>(q, d, e, g, st, w, 4 * N + 8);
-    if (!ok) ok = lq_primal_as<NMAX>(q, d, e, g, st, w, 16 * N + 16);
-    if (!ok) st.fill(1);
-#pragma unroll
-    for (int i = 0; i < LQ_NW_MAX; ++i) central[(size_t)s * LQ_NW_MAX + i] = (i < States<NMAX>::NW) ? st.w[i] : 0u;
-  }
+  if (lane == 0) tab.cnt[cb] = npc;
 }
 
 // ------------------------------------------------------------------- K2
@@ -342,19 +339,17 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a) {
   int64_t start, end;
   block_set(a, b, s, start, end);
   const int N = q.N;
-  const int tid = threadIdx.x;
-  const int64_t i = start + tid;
+  const int lane = threadIdx.x;
+  const int64_t i = start + lane;
   const bool active = i < end;
   const double* __restrict__ sd = a.setdata + (size_t)s * lq_sd(N);
-  const double* d = sd;
-  const double* e = sd + N;
   const double g = active ? a.gamma[i] : 0.0;
   const bool valid = active && (g >= 0.0) && (g <= q.y_max);
   double w[NMAX];
-  States<NMAX> st;
-  bool ok = false;
 #pragma unroll
   for (int t = 0; t < NMAX; ++t) w[t] = 0.0;
+  bool ok = false;
+  const uint8_t* stp = nullptr;
   if (valid) {
     const double invh = (double)LQ_G / q.y_max;
     const int cell = min(LQ_G - 1, (int)(g * invh));
@@ -367,183 +362,112 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a) {
         if (pp < cnt && g <= a.tab.gend[cb * LQ_PPL + pp]) p = pp;
       const size_t pidx = cb * LQ_PPL + p;
       const double2* row = reinterpret_cast<const double2*>(a.tab.ab + pidx * (size_t)N * 2);
+      stp = a.tab.st + pidx * LQ_STB;
+      States<NMAX> st;
+      st.load_bytes(stp);
 #pragma unroll
       for (int t = 0; t < NMAX; ++t)
         if (t < N) {
           const double2 ab = row[t];
-          w[t] = fma(ab.y, g, ab.x);
+          const Box bx = lq_box(st.get(t));
+          w[t] = fmin(fmax(fma(ab.y, g, ab.x), bx.lo), bx.hi);
         }
-      load_states<NMAX>(st, a.tab.st + pidx * LQ_NW_MAX);
-      lq_snap<NMAX>(q, st, w);
-      ok = lq_kkt<NMAX>(q, d, e, g, st, w) <= q.tol_cert;
+      ok = lq_kkt<NMAX>(q, sd, sd + N, g, st, w) <= q.tol_cert;
     }
   }
-  const bool fail = valid && !ok;
   EVOut o{0.0, 0.0, 0.0};
-  if (ok) {
-    o = lq_outputs<NMAX>(q, sd, g, w, a.want_err != 0);
-    if (a.w) {
-      double* wo = a.w + (size_t)i * N;
-#pragma unroll
-      for (int t = 0; t < NMAX; ++t)
-        if (t < N) wo[t] = w[t];
-    }
-    if (a.cost) a.cost[i] = o.cost;
-    if (a.w0) a.w0[i] = w[0];
-  } else if (active && !valid) {
-    if (a.w) {
-      double* wo = a.w + (size_t)i * N;
-      for (int t = 0; t < N; ++t) wo[t] = NAN;
-    }
-    if (a.cost) a.cost[i] = NAN;
-    if (a.w0) a.w0[i] = NAN;
-  }
-  if (a.status && active) a.status[i] = valid ? (ok ? LOMPC_QP_OK : LOMPC_QP_FAILED) : LOMPC_QP_INVALID;
-  // deterministic compaction of the uncertified EVs (ballot order)
-  {
-    __shared__ int wcnt[EVAL_BLOCK / 64];
-    const int lane = tid & 63, wv = tid >> 6;
-    const unsigned long long m = __ballot(fail);
-    if (lane == 0) wcnt[wv] = __popcll(m);
-    __syncthreads();
-    int base = 0;
-    for (int k = 0; k < wv; ++k) base += wcnt[k];
-    if (fail) {
-      const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-      a.fail_idx[(size_t)b * EVAL_BLOCK + pos] = (int)(i - start);
-    }
-    if (tid == 0) {
-      int tot = 0;
-      for (int k = 0; k < EVAL_BLOCK / 64; ++k) tot += wcnt[k];
-      a.fail_cnt[b] = tot;
-    }
-  }
-  block_partials<NMAX>(q, w, ok, o, 0, 0, (active && !valid) ? 1 : 0,
-                       a.partial + (size_t)b * (N + NPART_EXTRA), false);
+  if (ok) o = lq_outputs<NMAX>(q, sd, g, w, a.want_err != 0);
+  ev_epilogue<NMAX>(q, a, b, s, start, end, g, valid, ok, w, o, stp, (int8_t)LOMPC_QP_OK);
 }
 
-// ------------------------------------------------------------------- K2b
+// ------------------------------------------------------------------- K2d
 template <int NMAX>
-__global__ __launch_bounds__(EVAL_BLOCK) void k_direct(QPConst q, KArgs a, int repair) {
-  const int b = blockIdx.x;
-  if (repair) {
-    const int nf = a.fail_cnt[b];
-    if (nf == 0) return;  // uniform exit: nothing to repair in this workgroup
-  }
+__global__ __launch_bounds__(EVAL_BLOCK) void k_direct(QPConst q, KArgs a) {
   lq_tab_init(q);
+  const int b = blockIdx.x;
   int s;
   int64_t start, end;
   block_set(a, b, s, start, end);
   const int N = q.N;
-  const int tid = threadIdx.x;
-  int64_t i;
-  bool active;
-  if (repair) {
-    const int nf = a.fail_cnt[b];
-    active = tid < nf;
-    i = active ? start + a.fail_idx[(size_t)b * EVAL_BLOCK + tid] : start;
-  } else {
-    i = start + tid;
-    active = i < end;
-  }
+  const int lane = threadIdx.x;
+  const int64_t i = start + lane;
+  const bool active = i < end;
   const double* __restrict__ sd = a.setdata + (size_t)s * lq_sd(N);
-  const double* d = sd;
-  const double* e = sd + N;
   const double g = active ? a.gamma[i] : 0.0;
   const bool valid = active && (g >= 0.0) && (g <= q.y_max);
   double w[NMAX];
-  States<NMAX> st;
 #pragma unroll
   for (int t = 0; t < NMAX; ++t) w[t] = 0.0;
   bool ok = false;
+  const uint8_t* cst = a.central + (size_t)s * LQ_STB;
   if (valid) {
-    if (repair) {
-      const double invh = (double)LQ_G / q.y_max;
-      const int cell = min(LQ_G - 1, (int)(g * invh));
-      const size_t cb = (size_t)s * LQ_G + cell;
-      if (a.tab.cnt[cb] > 0) load_states<NMAX>(st, a.tab.st + cb * LQ_PPL * LQ_NW_MAX);
-      else st.fill(1);
-    } else {
-      load_states<NMAX>(st, a.central + (size_t)s * LQ_NW_MAX);
-    }
-    ok = lq_pdas<NMAX>(q, d, e, g, st, w, 4 * N + 8);
+    States<NMAX> st;
+    st.load_bytes(cst);
+    ok = lq_pdas<NMAX>(q, sd, sd + N, g, st, w, 4 * N + 8);
     if (ok) {
       lq_snap<NMAX>(q, st, w);
-      ok = lq_kkt<NMAX>(q, d, e, g, st, w) <= q.tol_cert;
-    }
-    if (!ok) {
-      ok = lq_primal_as<NMAX>(q, d, e, g, st, w, 16 * N + 16);
-      if (ok) {
-        lq_snap<NMAX>(q, st, w);
-        ok = lq_kkt<NMAX>(q, d, e, g, st, w) <= q.tol_cert;
-      }
+      ok = lq_kkt<NMAX>(q, sd, sd + N, g, st, w) <= q.tol_cert;
     }
   }
   EVOut o{0.0, 0.0, 0.0};
-  if (valid) {
-    o = lq_outputs<NMAX>(q, sd, g, w, a.want_err != 0);
-    if (a.w) {
-      double* wo = a.w + (size_t)i * N;
-#pragma unroll
-      for (int t = 0; t < NMAX; ++t)
-        if (t < N) wo[t] = w[t];
-    }
-    if (a.cost) a.cost[i] = o.cost;
-    if (a.w0) a.w0[i] = w[0];
-  } else if (active) {
-    if (a.w) {
-      double* wo = a.w + (size_t)i * N;
-      for (int t = 0; t < N; ++t) wo[t] = NAN;
-    }
-    if (a.cost) a.cost[i] = NAN;
-    if (a.w0) a.w0[i] = NAN;
-  }
-  if (a.status && active)
-    a.status[i] = !valid ? LOMPC_QP_INVALID : (ok ? (repair ? LOMPC_QP_REPAIRED : LOMPC_QP_OK) : LOMPC_QP_FAILED);
-  // failed EVs still contribute their best-effort w (the status says so)
-  const bool contrib = valid;
-  block_partials<NMAX>(q, w, contrib, o, (repair && valid && ok) ? 1 : 0, (valid && !ok) ? 1 : 0,
-                       (!repair && active && !valid) ? 1 : 0, a.partial + (size_t)b * (N + NPART_EXTRA),
-                       repair != 0);
+  if (ok) o = lq_outputs<NMAX>(q, sd, g, w, a.want_err != 0);
+  ev_epilogue<NMAX>(q, a, b, s, start, end, g, valid, ok, w, o, cst, (int8_t)LOMPC_QP_OK);
 }
 
 // ------------------------------------------------------------------- K3
-__global__ __launch_bounds__(128) void k_finalize(int N, int S, const int* __restrict__ blk_prefix,
-                                                  const int64_t* __restrict__ set_off,
-                                                  const double* __restrict__ partial,
-                                                  double* __restrict__ set_sum_w, double* __restrict__ set_stats,
-                                                  unsigned long long* __restrict__ counters) {
+// One workgroup of 1024 threads per set: wave wv sums rows wv, wv+16, ... of
+// the set's partial records (lane = column), then the 16 waves combine in LDS.
+__global__ __launch_bounds__(1024) void k_finalize(int N, int S, const int* __restrict__ blk_prefix,
+                                                   const int64_t* __restrict__ set_off,
+                                                   const double* __restrict__ partial, double* __restrict__ set_sum_w,
+                                                   double* __restrict__ set_stats, double* __restrict__ stats_int) {
+  __shared__ double red[16][LOMPC_MAX_N + NPX + 1];
   const int s = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int W = N + NPART_EXTRA;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int W = N + NPX;
   const int b0 = blk_prefix[s], b1 = blk_prefix[s + 1];
-  for (int col = tid; col < W; col += blockDim.x) {
-    const bool is_max = (col == N + PT_MAX_ERR);
-    double acc = 0.0;
-    for (int b = b0; b < b1; ++b) {
-      const double v = partial[(size_t)b * W + col];
-      acc = is_max ? fmax(acc, v) : acc + v;
-    }
-    if (col < N) {
-      if (set_sum_w) set_sum_w[(size_t)s * N + col] = acc;
-    } else {
-      const int k = col - N;
-      if (set_stats) {
-        double* row = set_stats + (size_t)s * LOMPC_SET_STATS;
-        switch (k) {
-          case PT_SUM_W0: row[LOMPC_STAT_SUM_W0] = acc; break;
-          case PT_SUM_PRICE0: row[LOMPC_STAT_SUM_PRICE0] = acc; break;
-          case PT_MAX_ERR: row[LOMPC_STAT_MAX_ERR] = acc; break;
-          case PT_SUM_COST: row[LOMPC_STAT_SUM_COST] = acc; break;
-          case PT_N_OK: row[LOMPC_STAT_COUNT] = (double)(set_off[s + 1] - set_off[s]); break;
-          case PT_N_REPAIRED: row[LOMPC_STAT_N_REPAIRED] = acc; break;
-          case PT_N_FAILED: row[LOMPC_STAT_N_FAILED] = acc; break;
-          case PT_N_INVALID: row[LOMPC_STAT_N_INVALID] = acc; break;
-        }
+  for (int c = lane; c < W; c += 64) {
+    const bool is_max = (c == N + PX_MAX_ERR);
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    int b = b0 + wv;
+    for (; b + 48 < b1; b += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double v = partial[(size_t)(b + 16 * u) * W + c];
+        acc[u] = is_max ? fmax(acc[u], v) : acc[u] + v;
       }
-      if (k == PT_N_REPAIRED && acc > 0) atomicAdd(&counters[0], (unsigned long long)acc);
-      if (k == PT_N_FAILED && acc > 0) atomicAdd(&counters[1], (unsigned long long)acc);
-      if (k == PT_N_INVALID && acc > 0) atomicAdd(&counters[2], (unsigned long long)acc);
+    }
+    for (; b < b1; b += 16) {
+      const double v = partial[(size_t)b * W + c];
+      acc[0] = is_max ? fmax(acc[0], v) : acc[0] + v;
+    }
+    red[wv][c] = is_max ? fmax(fmax(acc[0], acc[1]), fmax(acc[2], acc[3])) : (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  }
+  __syncthreads();
+  if (threadIdx.x < W) {
+    const int c = threadIdx.x;
+    const bool is_max = (c == N + PX_MAX_ERR);
+    double acc = red[0][c];
+    for (int k = 1; k < 16; ++k) acc = is_max ? fmax(acc, red[k][c]) : acc + red[k][c];
+    red[0][c] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < N) {
+    if (set_sum_w) set_sum_w[(size_t)s * N + threadIdx.x] = red[0][threadIdx.x];
+  }
+  if (threadIdx.x == 0) {
+    double row[LOMPC_SET_STATS];
+    row[LOMPC_STAT_COUNT] = (double)(set_off[s + 1] - set_off[s]);
+    row[LOMPC_STAT_SUM_W0] = red[0][0];
+    row[LOMPC_STAT_SUM_PRICE0] = red[0][N + PX_PRICE0];
+    row[LOMPC_STAT_MAX_ERR] = red[0][N + PX_MAX_ERR];
+    row[LOMPC_STAT_SUM_COST] = red[0][N + PX_COST];
+    row[LOMPC_STAT_N_REPAIRED] = red[0][N + PX_N_REPAIRED];
+    row[LOMPC_STAT_N_FAILED] = red[0][N + PX_N_FAILED];
+    row[LOMPC_STAT_N_INVALID] = red[0][N + PX_N_INVALID];
+    for (int k = 0; k < LOMPC_SET_STATS; ++k) {
+      if (set_stats) set_stats[(size_t)s * LOMPC_SET_STATS + k] = row[k];
+      stats_int[(size_t)s * LOMPC_SET_STATS + k] = row[k];
     }
   }
 }
@@ -560,23 +484,22 @@ struct lompc_ctx {
   int64_t S = 0, S_cap = 0;
   double* d_setdata = nullptr;
   PathTable tab{nullptr, nullptr, nullptr, nullptr};
-  uint32_t* d_central = nullptr;
+  uint8_t* d_central = nullptr;
   int* d_errflag = nullptr;
   int params_mode = -1;
   // batch workspaces
-  int64_t nblk_cap = 0, soff_cap = 0;
+  int64_t nblk_cap = 0, soff_cap = 0, stats_cap = 0;
   double* d_partial = nullptr;
-  int* d_fail_cnt = nullptr;
-  int* d_fail_idx = nullptr;
   int* d_blk_prefix = nullptr;
   int64_t* d_set_off = nullptr;
-  unsigned long long* d_counters = nullptr;
+  double* d_stats = nullptr;  // [S][LOMPC_SET_STATS], always written by k_finalize
+  int64_t stats_S = 0;
   int* h_pin_prefix = nullptr;
   int64_t* h_pin_off = nullptr;
   hipEvent_t ev_map = nullptr;
   std::vector<int64_t> last_off;
   void* last_off_stream = nullptr;
-  // single-solve scratch (3N + N + 4 doubles)
+  // single-solve scratch (3N + N + 8 doubles)
   double* d_single = nullptr;
   int8_t* d_single_status = nullptr;
   // profiling
@@ -628,14 +551,14 @@ static int pick_nmax(int N) {
   return 0;
 }
 
-#define DISPATCH_NMAX(nmax, ...) \
-  switch (nmax) {                 \
+#define DISPATCH_NMAX(nmax, ...)                            \
+  switch (nmax) {                                           \
     case 16: { constexpr int NM = 16; __VA_ARGS__; } break; \
     case 24: { constexpr int NM = 24; __VA_ARGS__; } break; \
     case 32: { constexpr int NM = 32; __VA_ARGS__; } break; \
     case 48: { constexpr int NM = 48; __VA_ARGS__; } break; \
     case 64: { constexpr int NM = 64; __VA_ARGS__; } break; \
-    default: break;               \
+    default: break;                                         \
   }
 
 extern "C" {
@@ -681,14 +604,14 @@ int lompc_create(int N, double delta, double theta, double y_max, double w_max, 
   q.theta = theta;
   q.y_max = y_max;
   q.w_max = w_max;
-  q.c = 2.0 * delta * theta * theta;          // lompc.py:71
-  q.q_scale = 3.0 * theta / (4.0 * w_max);    // lompc.py:67
+  q.inv_wmax = 1.0 / w_max;
+  q.c = 2.0 * delta * theta * theta;        // lompc.py:71
+  q.q_scale = 3.0 * theta / (4.0 * w_max);  // lompc.py:67
   q.dsmall = q.ev_small ? 2.0 * theta * theta / (0.9 * 0.9) : 0.0;  // lompc.py:105
   if (q.ev_small) {
     q.m = 1;
     q.knots[0] = 0.0;
-    q.knots[1] = w_max;
-    for (int k = 2; k <= LQ_MAXSEG; ++k) q.knots[k] = w_max;
+    for (int k = 1; k <= LQ_MAXSEG; ++k) q.knots[k] = w_max;
     for (int k = 0; k < LQ_MAXSEG; ++k) q.slopes[k] = 0.0;
   } else {  // lompc.py:108-114
     q.m = 4;
@@ -706,7 +629,6 @@ int lompc_create(int N, double delta, double theta, double y_max, double w_max, 
   q.ktol = 1e-13 * w_max;
   hipError_t e;
   if ((e = hipMalloc((void**)&c->d_errflag, sizeof(int))) != hipSuccess ||
-      (e = hipMalloc((void**)&c->d_counters, 4 * sizeof(unsigned long long))) != hipSuccess ||
       (e = hipMalloc((void**)&c->d_single, (4 * N + 8) * sizeof(double))) != hipSuccess ||
       (e = hipMalloc((void**)&c->d_single_status, 8)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&c->ev_map, hipEventDisableTiming)) != hipSuccess) {
@@ -714,7 +636,6 @@ int lompc_create(int N, double delta, double theta, double y_max, double w_max, 
     return LOMPC_ERR_HIP;
   }
   (void)hipMemset(c->d_errflag, 0, sizeof(int));
-  (void)hipMemset(c->d_counters, 0, 4 * sizeof(unsigned long long));
   *out = c;
   return LOMPC_OK;
 }
@@ -724,8 +645,7 @@ int lompc_destroy(lompc_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   void* ptrs[] = {c->d_setdata, c->tab.cnt, c->tab.gend, c->tab.ab, c->tab.st, c->d_central, c->d_errflag,
-                  c->d_partial, c->d_fail_cnt, c->d_fail_idx, c->d_blk_prefix, c->d_set_off, c->d_counters,
-                  c->d_single, c->d_single_status};
+                  c->d_partial, c->d_blk_prefix, c->d_set_off, c->d_stats, c->d_single, c->d_single_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_pin_prefix) (void)hipHostFree(c->h_pin_prefix);
@@ -754,33 +674,29 @@ int lompc_set_params(lompc_ctx* c, int64_t S, const double* lmbd, const double* 
                      const double* gamma_ref, void* stream) {
   if (!c) return LOMPC_ERR_INVALID_ARG;
   if (S < 1 || !lmbd || !lmbd_r) return fail_arg(c, "set_params: S >= 1 and lmbd, lmbd_r required");
-  if (S > (1 << 24)) return fail_arg(c, "set_params: too many parameter sets");
+  if (S > (1 << 20)) return fail_arg(c, "set_params: too many parameter sets");
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
   const int N = c->N;
   if (S > c->S_cap) {
     int rc;
     const size_t cells = (size_t)S * LQ_G;
-    if ((rc = grow(c, &c->d_setdata, (size_t)S * lq_sd(N))) ||
-        (rc = grow(c, &c->tab.cnt, cells)) || (rc = grow(c, &c->tab.gend, cells * LQ_PPL)) ||
-        (rc = grow(c, &c->tab.ab, cells * LQ_PPL * (size_t)N * 2)) ||
-        (rc = grow(c, &c->tab.st, cells * LQ_PPL * LQ_NW_MAX)) ||
-        (rc = grow(c, &c->d_central, (size_t)S * LQ_NW_MAX)))
+    if ((rc = grow(c, &c->d_setdata, (size_t)S * lq_sd(N))) || (rc = grow(c, &c->tab.cnt, cells)) ||
+        (rc = grow(c, &c->tab.gend, cells * LQ_PPL)) || (rc = grow(c, &c->tab.ab, cells * LQ_PPL * (size_t)N * 2)) ||
+        (rc = grow(c, &c->tab.st, cells * LQ_PPL * LQ_STB)) || (rc = grow(c, &c->d_central, (size_t)S * LQ_STB)))
       return rc;
     c->S_cap = S;
   }
   c->S = S;
   c->params_mode = c->mode;
-  dim3 grid((unsigned)S), block(64);
-  DISPATCH_NMAX(c->nmax, hipLaunchKernelGGL(k_prepare<NM>, grid, block, 0, st, c->q, (int)S, lmbd, lmbd_r, w_ref,
-                                             gamma_ref, c->d_setdata, c->mode, c->tab, c->d_central,
-                                             c->d_errflag));
+  const unsigned grid = (unsigned)(c->mode == LOMPC_MODE_PATH ? S * LQ_G : S);
+  hipLaunchKernelGGL(k_path, dim3(grid), dim3(64), 0, st, c->q, (int)S, lmbd, lmbd_r, w_ref, gamma_ref,
+                     c->d_setdata, c->mode, c->tab, c->d_central, c->d_errflag);
   HIPCHK(c, hipGetLastError());
   return LOMPC_OK;
 }
 
 static int upload_block_map(lompc_ctx* c, const int64_t* set_off, int64_t S, int* nblk_out, hipStream_t st) {
-  // host prefix of workgroups per set
   std::vector<int> pre(S + 1);
   int64_t nb = 0;
   pre[0] = 0;
@@ -792,15 +708,18 @@ static int upload_block_map(lompc_ctx* c, const int64_t* set_off, int64_t S, int
     pre[s + 1] = (int)nb;
   }
   *nblk_out = (int)nb;
-  const bool same = (int64_t)c->last_off.size() == S + 1 && c->last_off_stream == (void*)st &&
-                    memcmp(c->last_off.data(), set_off, (S + 1) * sizeof(int64_t)) == 0;
   if (nb > c->nblk_cap) {
     int rc;
-    if ((rc = grow(c, &c->d_partial, (size_t)nb * (c->N + NPART_EXTRA))) ||
-        (rc = grow(c, &c->d_fail_cnt, (size_t)nb)) || (rc = grow(c, &c->d_fail_idx, (size_t)nb * EVAL_BLOCK)))
-      return rc;
+    if ((rc = grow(c, &c->d_partial, (size_t)nb * (c->N + NPX)))) return rc;
     c->nblk_cap = nb;
   }
+  if (S > c->stats_cap) {
+    int rc;
+    if ((rc = grow(c, &c->d_stats, (size_t)S * LOMPC_SET_STATS))) return rc;
+    c->stats_cap = S;
+  }
+  const bool same = (int64_t)c->last_off.size() == S + 1 && c->last_off_stream == (void*)st &&
+                    memcmp(c->last_off.data(), set_off, (S + 1) * sizeof(int64_t)) == 0;
   if (same && c->d_blk_prefix) return LOMPC_OK;
   if (S + 1 > c->soff_cap) {
     int rc;
@@ -840,7 +759,6 @@ int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_
   int nblk = 0;
   int rc = upload_block_map(c, set_offsets, c->S, &nblk, st);
   if (rc) return rc;
-  HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), st));
   KArgs a{};
   a.B = B;
   a.S = (int)c->S;
@@ -857,8 +775,6 @@ int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_
   a.w0 = w0;
   a.status = status;
   a.partial = c->d_partial;
-  a.fail_cnt = c->d_fail_cnt;
-  a.fail_idx = c->d_fail_idx;
   if (nblk > 0) {
     dim3 grid((unsigned)nblk), block(EVAL_BLOCK);
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -870,38 +786,41 @@ int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_
     if (c->params_mode == LOMPC_MODE_PATH) {
       DISPATCH_NMAX(c->nmax, hipLaunchKernelGGL(k_eval<NM>, grid, block, 0, st, c->q, a));
     } else {
-      DISPATCH_NMAX(c->nmax, hipLaunchKernelGGL(k_direct<NM>, grid, block, 0, st, c->q, a, 0));
+      DISPATCH_NMAX(c->nmax, hipLaunchKernelGGL(k_direct<NM>, grid, block, 0, st, c->q, a));
     }
+    HIPCHK(c, hipGetLastError());
     if (c->prof) {
       HIPCHK(c, hipEventRecord(e1, st));
       c->prof_ev.push_back(e0);
       c->prof_ev.push_back(e1);
     }
-    HIPCHK(c, hipGetLastError());
-    if (c->params_mode == LOMPC_MODE_PATH) {
-      DISPATCH_NMAX(c->nmax, hipLaunchKernelGGL(k_direct<NM>, grid, block, 0, st, c->q, a, 1));
-      HIPCHK(c, hipGetLastError());
-    }
   }
-  if (set_sum_w || set_stats || nblk > 0) {
-    hipLaunchKernelGGL(k_finalize, dim3((unsigned)c->S), dim3(128), 0, st, c->N, (int)c->S, c->d_blk_prefix,
-                       c->d_set_off, c->d_partial, set_sum_w, set_stats, c->d_counters);
-    HIPCHK(c, hipGetLastError());
-  }
+  hipLaunchKernelGGL(k_finalize, dim3((unsigned)c->S), dim3(1024), 0, st, c->N, (int)c->S, c->d_blk_prefix,
+                     c->d_set_off, c->d_partial, set_sum_w, set_stats, c->d_stats);
+  HIPCHK(c, hipGetLastError());
+  c->stats_S = c->S;
   return LOMPC_OK;
 }
 
 int lompc_last_status(lompc_ctx* c, void* stream, int64_t* n_repaired, int64_t* n_failed, int64_t* n_invalid) {
   if (!c) return LOMPC_ERR_INVALID_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  unsigned long long h[4] = {0, 0, 0, 0};
+  std::vector<double> h((size_t)std::max<int64_t>(c->stats_S, 1) * LOMPC_SET_STATS, 0.0);
   int ef = 0;
-  HIPCHK(c, hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  if (c->stats_S > 0)
+    HIPCHK(c, hipMemcpyAsync(h.data(), c->d_stats, c->stats_S * LOMPC_SET_STATS * sizeof(double),
+                             hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(c, hipMemcpyAsync(&ef, c->d_errflag, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
-  if (n_repaired) *n_repaired = (int64_t)h[0];
-  if (n_failed) *n_failed = (int64_t)h[1];
-  if (n_invalid) *n_invalid = (int64_t)h[2];
+  double rep = 0, fail = 0, inv = 0;
+  for (int64_t s = 0; s < c->stats_S; ++s) {
+    rep += h[s * LOMPC_SET_STATS + LOMPC_STAT_N_REPAIRED];
+    fail += h[s * LOMPC_SET_STATS + LOMPC_STAT_N_FAILED];
+    inv += h[s * LOMPC_SET_STATS + LOMPC_STAT_N_INVALID];
+  }
+  if (n_repaired) *n_repaired = (int64_t)rep;
+  if (n_failed) *n_failed = (int64_t)fail;
+  if (n_invalid) *n_invalid = (int64_t)inv;
   if (ef) {
     HIPCHK(c, hipMemsetAsync(c->d_errflag, 0, sizeof(int), (hipStream_t)stream));
     return fail_arg(c, "negative or NaN price parameter (lmbd >= 0, lmbd_r >= 0 required)");

@@ -15,18 +15,24 @@
 // for any working set (each coordinate either fixed at a "knot" — a box bound
 // or a PWL kink — or free inside one PWL segment) the equality-constrained
 // sub-problem is solved EXACTLY by a backward scalar Riccati recursion plus a
-// forward pass: O(N) flops and N divisions, no N x N matrix anywhere.
+// forward pass: O(N) flops, no N x N matrix anywhere.
 //
-// State encoding per coordinate (4 bits): even s = 2k  -> fixed at knot k,
-//                                          odd  s = 2k+1 -> free in segment k.
+// State encoding per coordinate: even s = 2k -> fixed at knot k, odd s = 2k+1 ->
+// free in segment k.  Every state has a "box" (lo, hi, slo, shi):
+//   w in [lo, hi]   and   -r in [slo, shi]      (r = gradient of the smooth part)
+//   free seg k : [knot_k, knot_k+1] x [sigma_k, sigma_k]
+//   knot k     : [knot_k, knot_k]   x [sigma_k-1, sigma_k]   (+-inf at the box ends)
+// so projection, KKT residual and the active-set moves (always s -> s +- 1) are
+// branch-free: KKT(w) = max over t of dist(-r_t, [slo, shi]) with w_t in [lo, hi].
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define LQ_MAXSEG 4     // large EVs: 4 PWL segments (lompc.py:111)
-#define LQ_G 64         // path cells per parameter set (one lane each)
-#define LQ_PPL 8        // max affine pieces stored per cell
-#define LQ_NW_MAX 8     // packed state words per stored piece (64 coords / 8)
+#define LQ_MAXSEG 4                     // large EVs: 4 PWL segments (lompc.py:111)
+#define LQ_NSTATE (2 * LQ_MAXSEG + 1)   // 9 states
+#define LQ_G 64                         // path cells per parameter set (one wave each)
+#define LQ_PPL 8                        // max affine pieces stored per cell
+#define LQ_STB 64                       // state bytes per stored working set (N <= 64)
 
 struct QPConst {
   int N;             // horizon
@@ -35,6 +41,7 @@ struct QPConst {
   int pad0;
   double c;          // 2 delta theta^2
   double delta, theta, y_max, w_max, q_scale;
+  double inv_wmax;   // 1 / w_max
   double dsmall;     // 2 theta^2 / 0.9^2 for small EVs, 0 otherwise
   double knots[LQ_MAXSEG + 1];
   double slopes[LQ_MAXSEG];
@@ -51,32 +58,71 @@ __host__ __device__ inline int lq_sd(int N) { return 3 * N + 8; }
 
 // Path table (device pointers). Cell l of set s covers gamma in [l h, (l+1) h], h = y_max / LQ_G.
 struct PathTable {
-  int* cnt;          // [S][G]          pieces stored in the cell (0 = cell unsolved)
-  double* gend;      // [S][G][PPL]     upper gamma of each piece
-  double* ab;        // [S][G][PPL][N][2]  w_j(gamma) = a_j + b_j gamma
-  uint32_t* st;      // [S][G][PPL][LQ_NW_MAX] packed working set of the piece
+  int* cnt;          // [S][G]              pieces stored in the cell (0 = cell unsolved)
+  double* gend;      // [S][G][PPL]         upper gamma of each piece
+  double* ab;        // [S][G][PPL][N][2]   w_j(gamma) = a_j + b_j gamma
+  uint8_t* st;       // [S][G][PPL][STB]    working set of the piece (one byte per stage)
 };
 
-// Knot / slope tables live in LDS: indexed by a per-lane state, a register
-// select chain is turned into an indexed load by the compiler, and indexing the
-// by-value kernel argument would force a scratch copy of QPConst.
+struct Box {
+  double lo, hi, slo, shi;
+};
+
+// Box table in LDS (per-lane state -> one ds_read_b128 pair; a register select
+// chain over a by-value kernel argument makes hipcc copy it to scratch).
 __device__ __forceinline__ double* lq_tab() {
-  __shared__ double tab[LQ_MAXSEG * 2 + 2];
+  __shared__ __attribute__((aligned(16))) double tab[LQ_NSTATE * 4];
   return tab;
 }
-// Every kernel calls this (all threads) before the first lq_knot / lq_slope.
+// Every kernel calls this (all threads, before anything else).
 __device__ __forceinline__ void lq_tab_init(const QPConst& q) {
   double* tb = lq_tab();
-  const int t = threadIdx.x;
-  if (t <= LQ_MAXSEG) tb[t] = q.knots[t];
-  if (t < LQ_MAXSEG) tb[LQ_MAXSEG + 1 + t] = q.slopes[t];
+  const int s = threadIdx.x;
+  if (s < LQ_NSTATE) {
+    const int k = s >> 1;
+    double lo, hi, slo, shi;
+    if (s & 1) {
+      const int kk = k < q.m ? k : q.m - 1;
+      lo = q.knots[kk];
+      hi = q.knots[kk + 1];
+      slo = shi = q.slopes[kk];
+    } else {
+      const int kk = k <= q.m ? k : q.m;
+      lo = hi = q.knots[kk];
+      slo = kk > 0 ? q.slopes[kk - 1] : -INFINITY;
+      shi = kk < q.m ? q.slopes[kk] : INFINITY;
+    }
+    tb[4 * s + 0] = lo;
+    tb[4 * s + 1] = hi;
+    tb[4 * s + 2] = slo;
+    tb[4 * s + 3] = shi;
+  }
   __syncthreads();
 }
-__device__ __forceinline__ double lq_knot(const QPConst&, int k) { return lq_tab()[k]; }
-// k = -1 is read only on paths whose value is discarded (fixed coordinates).
-__device__ __forceinline__ double lq_slope(const QPConst&, int k) { return lq_tab()[LQ_MAXSEG + 1 + k]; }
+__device__ __forceinline__ Box lq_box(int s) {
+  const double2* tb = reinterpret_cast<const double2*>(lq_tab());
+  const double2 x = tb[2 * s], y = tb[2 * s + 1];
+  return {x.x, x.y, y.x, y.y};
+}
 
-// Packed working set: 4 bits per coordinate, 8 coordinates per word.
+// Active-set move of one coordinate from (w, r): s -> s+1 / s-1 / s.
+//   free : w above hi -> fixed at the upper knot (s+1), below lo -> lower knot (s-1)
+//   fixed: -r above shi -> free in the segment above (s+1), below slo -> below (s-1)
+__device__ __forceinline__ int lq_move(const QPConst& q, int s, const Box& b, double w, double r) {
+  const double v = -r;
+  const bool fr = (s & 1) != 0;
+  const bool up = fr ? (w > b.hi + q.ktol) : (v > b.shi + q.tol_switch);
+  const bool dn = fr ? (w < b.lo - q.ktol) : (v < b.slo - q.tol_switch);
+  return s + (up ? 1 : 0) - (dn ? 1 : 0);
+}
+// distance of (w, -r) from the state's box, in gradient units (w outside -> +inf)
+__device__ __forceinline__ double lq_resid(const QPConst& q, const Box& b, double w, double r) {
+  const double v = -r;
+  const double res = fmax(fmax(b.slo - v, v - b.shi), 0.0);
+  return (w < b.lo - q.ktol || w > b.hi + q.ktol) ? INFINITY : res;
+}
+
+// Packed working set for the lane-per-QP solver: 4 bits per coordinate.
 template <int NMAX>
 struct States {
   static constexpr int NW = (NMAX + 7) / 8;
@@ -88,8 +134,7 @@ struct States {
     const int sh = (t & 7) * 4;
     w[t >> 3] = (w[t >> 3] & ~(15u << sh)) | ((uint32_t)v << sh);
   }
-  // runtime-index set without dynamic register indexing
-  __device__ __forceinline__ void set_rt(int t, int v) {
+  __device__ __forceinline__ void set_rt(int t, int v) {  // runtime index, no dynamic register indexing
     const int wi = t >> 3;
     const int sh = (t & 7) * 4;
 #pragma unroll
@@ -103,7 +148,26 @@ struct States {
 #pragma unroll
     for (int i = 0; i < NW; ++i) w[i] = x;
   }
+  // from one byte per coordinate (16-byte aligned source)
+  __device__ __forceinline__ void load_bytes(const uint8_t* __restrict__ src) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(src);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const uint32_t x0 = p[2 * i], x1 = p[2 * i + 1];
+      const uint32_t n0 = (x0 & 0xfu) | ((x0 >> 4) & 0xf0u) | ((x0 >> 8) & 0xf00u) | ((x0 >> 12) & 0xf000u);
+      const uint32_t n1 = (x1 & 0xfu) | ((x1 >> 4) & 0xf0u) | ((x1 >> 8) & 0xf00u) | ((x1 >> 12) & 0xf000u);
+      w[i] = n0 | (n1 << 16);
+    }
+  }
 };
+
+__device__ __forceinline__ double lq_rcp(double x) {  // v_rcp_f64 + two Newton steps (~0.5 ulp)
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
 
 // ---------------------------------------------------------------------------
 // Exact sub-problem solve for a working set (single right-hand side).
@@ -111,7 +175,7 @@ struct States {
 //   free  : w_t = K y_{t-1} + k,  K = -Q/(Q+d), k = -(q+e~)/(Q+d),
 //           P' = Q d/(Q+d),  p' = (q d - e~ Q)/(Q+d)       (e~ = e_t + slope)
 //   fixed : w_t = wbar,  P' = Q,  p' = Q wbar + q
-// Q >= c > 0, so every division is well defined.
+// Q >= c > 0, so every reciprocal is well defined.
 // ---------------------------------------------------------------------------
 template <int NMAX>
 __device__ __forceinline__ void lq_riccati(const QPConst& q, const double* __restrict__ d,
@@ -126,15 +190,15 @@ __device__ __forceinline__ void lq_riccati(const QPConst& q, const double* __res
       const double Q = q.c + P;
       const double qq = p - cg;
       const int s = st.get(t);
+      const Box b = lq_box(s);
       const double dt = d[t];
       const bool fr = (s & 1) != 0;
-      const double et = e[t] + lq_slope(q, (s - 1) >> 1);
-      const double inv = 1.0 / (Q + dt);
-      const double wb = lq_knot(q, s >> 1);
+      const double et = e[t] + b.slo;
+      const double inv = lq_rcp(Q + dt);
       K[t] = fr ? -Q * inv : 0.0;
-      k[t] = fr ? -(qq + et) * inv : wb;
+      k[t] = fr ? -(qq + et) * inv : b.lo;
       P = fr ? Q * dt * inv : Q;
-      p = fr ? (qq * dt - et * Q) * inv : fma(Q, wb, qq);
+      p = fr ? (qq * dt - et * Q) * inv : fma(Q, b.lo, qq);
     }
   }
   double y = 0.0;
@@ -147,8 +211,8 @@ __device__ __forceinline__ void lq_riccati(const QPConst& q, const double* __res
   }
 }
 
-// Gradient of the smooth part: r_j = c (sum_{i>=j} y_i - (N-j) gamma) + d_j w_j + e_j.
-// Computed on the fly by callers with the prefix trick (two forward passes).
+// Gradient of the smooth part: r_j = c (sum_{i>=j} y_i - (N-j) gamma) + d_j w_j + e_j,
+// computed on the fly with the prefix trick (total of y first, then running prefix).
 template <int NMAX>
 __device__ __forceinline__ double lq_sum_y(const QPConst& q, const double (&w)[NMAX]) {
   double y = 0.0, Z = 0.0;
@@ -161,8 +225,8 @@ __device__ __forceinline__ double lq_sum_y(const QPConst& q, const double (&w)[N
   return Z;
 }
 
-// One PDAS (semismooth-Newton active-set) state update from the current
-// sub-problem solution w.  Returns true if any coordinate changed state.
+// One PDAS (semismooth-Newton active-set) state update from the sub-problem
+// solution w.  Returns true if any coordinate changed state.
 template <int NMAX>
 __device__ __forceinline__ bool lq_pdas_update(const QPConst& q, const double* __restrict__ d,
                                                const double* __restrict__ e, double gamma,
@@ -177,31 +241,18 @@ __device__ __forceinline__ bool lq_pdas_update(const QPConst& q, const double* _
       const double r = q.c * (Zt - Z - (double)(q.N - t) * gamma) + d[t] * w[t] + e[t];
       Z += y;
       const int s = st.get(t);
-      int ns = s;
-      if (s & 1) {
-        const int kk = (s - 1) >> 1;
-        if (w[t] > lq_knot(q, kk + 1) + q.ktol) ns = 2 * (kk + 1);
-        else if (w[t] < lq_knot(q, kk) - q.ktol) ns = 2 * kk;
-      } else {
-        const int kk = s >> 1;
-        const double v = -r;
-        if (kk < q.m && v > lq_slope(q, kk) + q.tol_switch) ns = 2 * kk + 1;
-        else if (kk > 0 && v < lq_slope(q, kk - 1) - q.tol_switch) ns = 2 * kk - 1;
-      }
-      if (ns != s) {
-        st.set(t, ns);
-        changed = true;
-      }
+      const int ns = lq_move(q, s, lq_box(s), w[t], r);
+      changed |= (ns != s);
+      st.set(t, ns);
     }
   }
   return changed;
 }
 
-// PDAS from the given working set. Returns true on convergence (w then solves
-// the sub-problem of the final working set, which satisfies KKT within tol).
 template <int NMAX>
-__device__ __forceinline__ bool lq_pdas(const QPConst& q, const double* __restrict__ d, const double* __restrict__ e,
-                        double gamma, States<NMAX>& st, double (&w)[NMAX], int max_it) {
+__device__ __forceinline__ bool lq_pdas(const QPConst& q, const double* __restrict__ d,
+                                        const double* __restrict__ e, double gamma, States<NMAX>& st,
+                                        double (&w)[NMAX], int max_it) {
   bool done = false;
   for (int it = 0; it < max_it && !done; ++it) {
     lq_riccati<NMAX>(q, d, e, gamma, st, w);
@@ -210,28 +261,23 @@ __device__ __forceinline__ bool lq_pdas(const QPConst& q, const double* __restri
   return done;
 }
 
-// Clamp a free coordinate into its segment; fixed coordinates sit exactly on their knot.
+// Project onto the working set's box (free: clamp into the segment; fixed: the knot).
 template <int NMAX>
 __device__ __forceinline__ void lq_snap(const QPConst& q, const States<NMAX>& st, double (&w)[NMAX]) {
 #pragma unroll
   for (int t = 0; t < NMAX; ++t)
     if (t < q.N) {
-      const int s = st.get(t);
-      if (s & 1) {
-        const int kk = (s - 1) >> 1;
-        w[t] = fmin(fmax(w[t], lq_knot(q, kk)), lq_knot(q, kk + 1));
-      } else {
-        w[t] = lq_knot(q, s >> 1);
-      }
+      const Box b = lq_box(st.get(t));
+      w[t] = fmin(fmax(w[t], b.lo), b.hi);
     }
 }
 
-// Primal active-set method (Nocedal & Wright Alg. 16.3 with PWL kinks as
-// knots) from w = 0 with every coordinate fixed at knot 0.  Slow but
-// monotone; used only when PDAS does not converge.
+// Primal active-set method (Nocedal & Wright Alg. 16.3, PWL kinks as knots)
+// from w = 0 with every coordinate fixed at knot 0.  Monotone; last resort.
 template <int NMAX>
-__device__ __forceinline__ bool lq_primal_as(const QPConst& q, const double* __restrict__ d, const double* __restrict__ e,
-                             double gamma, States<NMAX>& st, double (&w)[NMAX], int max_it) {
+__device__ __forceinline__ bool lq_primal_as(const QPConst& q, const double* __restrict__ d,
+                                             const double* __restrict__ e, double gamma, States<NMAX>& st,
+                                             double (&w)[NMAX], int max_it) {
   st.fill(0);
 #pragma unroll
   for (int t = 0; t < NMAX; ++t) w[t] = 0.0;
@@ -240,20 +286,21 @@ __device__ __forceinline__ bool lq_primal_as(const QPConst& q, const double* __r
     double wh[NMAX];
     lq_riccati<NMAX>(q, d, e, gamma, st, wh);
     double alpha = 1.0;
-    int blk = -1, bknot = 0;
+    int blk = -1, bs = 0;
+    double bval = 0.0;
 #pragma unroll
     for (int t = 0; t < NMAX; ++t) {
       if (t < q.N) {
         const int s = st.get(t);
-        const double pj = wh[t] - w[t];
         if (s & 1) {
-          const int kk = (s - 1) >> 1;
+          const Box b = lq_box(s);
+          const double pj = wh[t] - w[t];
           if (pj > 0.0) {
-            const double a = (lq_knot(q, kk + 1) - w[t]) / pj;
-            if (a < alpha) { alpha = a; blk = t; bknot = kk + 1; }
+            const double a = (b.hi - w[t]) / pj;
+            if (a < alpha) { alpha = a; blk = t; bs = s + 1; bval = b.hi; }
           } else if (pj < 0.0) {
-            const double a = (lq_knot(q, kk) - w[t]) / pj;
-            if (a < alpha) { alpha = a; blk = t; bknot = kk; }
+            const double a = (b.lo - w[t]) / pj;
+            if (a < alpha) { alpha = a; blk = t; bs = s - 1; bval = b.lo; }
           }
         }
       }
@@ -261,10 +308,9 @@ __device__ __forceinline__ bool lq_primal_as(const QPConst& q, const double* __r
     if (blk < 0) {
 #pragma unroll
       for (int t = 0; t < NMAX; ++t) w[t] = wh[t];
-      // most violated fixed coordinate
       const double Zt = lq_sum_y<NMAX>(q, w);
       double y = 0.0, Z = 0.0, best = q.tol_switch;
-      int bj = -1, bs = 0;
+      int bj = -1, bns = 0;
 #pragma unroll
       for (int t = 0; t < NMAX; ++t) {
         if (t < q.N) {
@@ -273,73 +319,64 @@ __device__ __forceinline__ bool lq_primal_as(const QPConst& q, const double* __r
           Z += y;
           const int s = st.get(t);
           if (!(s & 1)) {
-            const int kk = s >> 1;
-            if (kk < q.m) {
-              const double v = -r - lq_slope(q, kk);
-              if (v > best) { best = v; bj = t; bs = 2 * kk + 1; }
-            }
-            if (kk > 0) {
-              const double v = r + lq_slope(q, kk - 1);
-              if (v > best) { best = v; bj = t; bs = 2 * kk - 1; }
-            }
+            const Box b = lq_box(s);
+            const double up = -r - b.shi, dn = b.slo + r;
+            if (up > best) { best = up; bj = t; bns = s + 1; }
+            if (dn > best) { best = dn; bj = t; bns = s - 1; }
           }
         }
       }
       if (bj < 0) done = true;
-      else st.set_rt(bj, bs);
+      else st.set_rt(bj, bns);
     } else {
       alpha = fmax(alpha, 0.0);
-      const double kv = lq_knot(q, bknot);
 #pragma unroll
       for (int t = 0; t < NMAX; ++t) {
         w[t] = fma(alpha, wh[t] - w[t], w[t]);
-        if (t == blk) w[t] = kv;
+        if (t == blk) w[t] = bval;
       }
-      st.set_rt(blk, 2 * bknot);
+      st.set_rt(blk, bs);
     }
   }
   return done;
 }
 
-// KKT certificate of (w, working set): returns the max violation in gradient
-// units (stationarity of free coordinates, multiplier range of fixed ones) or
-// +inf when a free coordinate left its segment by more than ktol.
+// KKT certificate of (w, working set): max distance of -r from the state boxes.
 template <int NMAX>
 __device__ __forceinline__ double lq_kkt(const QPConst& q, const double* __restrict__ d,
-                                         const double* __restrict__ e, double gamma,
-                                         const States<NMAX>& st, const double (&w)[NMAX]) {
+                                         const double* __restrict__ e, double gamma, const States<NMAX>& st,
+                                         const double (&w)[NMAX]) {
   const double Zt = lq_sum_y<NMAX>(q, w);
   double y = 0.0, Z = 0.0, res = 0.0;
-  bool outside = false;
 #pragma unroll
   for (int t = 0; t < NMAX; ++t) {
     if (t < q.N) {
       y += w[t];
       const double r = q.c * (Zt - Z - (double)(q.N - t) * gamma) + d[t] * w[t] + e[t];
       Z += y;
-      const int s = st.get(t);
-      const double v = -r;
-      if (s & 1) {
-        const int kk = (s - 1) >> 1;
-        res = fmax(res, fabs(v - lq_slope(q, kk)));
-        outside |= (w[t] < lq_knot(q, kk) - q.ktol) || (w[t] > lq_knot(q, kk + 1) + q.ktol);
-      } else {
-        const int kk = s >> 1;
-        if (kk > 0) res = fmax(res, lq_slope(q, kk - 1) - v);
-        if (kk < q.m) res = fmax(res, v - lq_slope(q, kk));
-      }
+      res = fmax(res, lq_resid(q, lq_box(st.get(t)), w[t], r));
     }
   }
-  return outside ? INFINITY : res;
+  return res;
 }
 
 // Per-EV scalar outputs from an optimal w:
-//   cost  (lompc.py:155: the full objective incl. c0)
-//   err   = sqrt((w-w_ref)' A_bar (w-w_ref)), A_bar = A'A + kappa I (price_solver.py:191-192, :207)
+//   cost   (lompc.py:155: the full objective incl. c0)
+//   err    = sqrt((w-w_ref)' A_bar (w-w_ref)), A_bar = A'A + kappa I (price_solver.py:191-192, :207)
 //   price0 (lompc.py:164-170)
 struct EVOut {
   double cost, err, price0;
 };
+
+__device__ __forceinline__ double lq_pwl(double u) {  // lompc.py:111
+  return fmax(fmax(0.0 * u, u - 0.125), fmax(1.5 * u - 0.375, 2.0 * u - 0.75));
+}
+
+__device__ __forceinline__ double lq_price0(const QPConst& q, const double* __restrict__ sd, double w0) {
+  const int N = q.N;
+  return q.theta * (w0 * sd[3 * N + 1] + (q.w_max - w0) * sd[3 * N + 2]) + q.q_scale * w0 * w0 * sd[3 * N + 3] +
+         q.theta * q.theta * w0 * w0 * sd[3 * N + 4];
+}
 
 template <int NMAX>
 __device__ __forceinline__ EVOut lq_outputs(const QPConst& q, const double* __restrict__ sd, double gamma,
@@ -358,12 +395,8 @@ __device__ __forceinline__ EVOut lq_outputs(const QPConst& q, const double* __re
       y += wt;
       sy += y;
       syy = fma(y, y, syy);
-      quad += wt * fma(0.5 * d[t], wt, e[t]);
-      if (!q.ev_small) {
-        const double u = wt / q.w_max;
-        const double v = fmax(fmax(0.0 * u, u - 0.125), fmax(1.5 * u - 0.375, 2.0 * u - 0.75));
-        pwl += v;
-      }
+      quad = fma(wt, fma(0.5 * d[t], wt, e[t]), quad);
+      if (!q.ev_small) pwl += lq_pwl(wt * q.inv_wmax);
       if (want_err) {
         const double dv = wt - wr[t];
         ey += dv;
@@ -376,8 +409,6 @@ __device__ __forceinline__ EVOut lq_outputs(const QPConst& q, const double* __re
   const double tw = q.theta * q.w_max;
   o.cost = 0.5 * q.c * syy - q.c * gamma * sy + quad + sd[3 * N + 0] + (q.ev_small ? 0.0 : tw * tw * pwl);
   o.err = want_err ? sqrt(eyy + kappa * edd) : 0.0;
-  const double w0 = w[0];
-  o.price0 = q.theta * (w0 * sd[3 * N + 1] + (q.w_max - w0) * sd[3 * N + 2]) +
-             q.q_scale * w0 * w0 * sd[3 * N + 3] + q.theta * q.theta * w0 * w0 * sd[3 * N + 4];
+  o.price0 = lq_price0(q, sd, w[0]);
   return o;
 }

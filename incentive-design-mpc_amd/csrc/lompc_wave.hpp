@@ -1,0 +1,304 @@
+// lompc_wave.hpp — one LoMPC QP per 64-lane wavefront, lane t = horizon stage t.
+//
+// Used where latency, not throughput, matters: the per-set path kernel (K1) and
+// the rare in-kernel repair of an EV whose path value failed its certificate.
+// A lane-per-QP Riccati recursion is a ~3N-deep dependent fp64 chain, so here
+// the three recursions of one sub-problem solve are wave-parallel scans:
+//
+//   (1) P_t  = F_t(P_{t+1})          Moebius map   free: d(c+P)/(c+P+d)   fixed: c+P
+//   (2) p_t  = al_t p_{t+1} + be_t   affine map    (given P_{t+1})
+//   (3) y_t  = (1+K_t) y_{t-1} + k_t affine map    forward, w_t = K_t y_{t-1} + k_t
+//
+// (1) and (2) run as prefix scans in the REVERSED layout (lane l = stage N-1-l),
+// (3) in the natural layout; one ds_bpermute round moves the per-stage gains
+// between layouts.  Scans use DPP row_shr 1/2/4/8 + row_bcast 15/31 (gfx9-family
+// cross-lane moves at ALU latency).  The multiplier of coordinate t comes from
+// the cost-to-go derivative (envelope theorem), so no fourth scan is needed:
+//   r_t = c (y_t - gamma) + P_{t+1} y_t + p_{t+1} + d_t w_t + e_t .
+#pragma once
+#include "lompc_qp.hpp"
+
+namespace lqw {
+
+// ---- DPP helpers (64-bit values as two 32-bit lanes) -----------------------
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp(double old, double x) {
+  const long long xi = __builtin_bit_cast(long long, x);
+  const long long oi = __builtin_bit_cast(long long, old);
+  const int lo = __builtin_amdgcn_update_dpp((int)oi, (int)xi, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(oi >> 32), (int)(xi >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+// value of lane l-1 (lane 0 gets `old`): DPP wave_shr:1
+__device__ __forceinline__ double shr1(double old, double x) { return dpp<0x138, 0xf>(old, x); }
+
+struct Mob {  // Moebius map P -> (a P + b) / (c P + 1)
+  double a, b, c;
+  __device__ __forceinline__ static Mob identity() { return {1.0, 0.0, 0.0}; }
+  __device__ __forceinline__ static Mob combine(const Mob& L, const Mob& R) {  // R o L (L applied first)
+    const double a = fma(R.a, L.a, R.b * L.c);
+    const double b = fma(R.a, L.b, R.b);
+    const double c = fma(R.c, L.a, L.c);
+    const double inv = lq_rcp(fma(R.c, L.b, 1.0));  // >= 1: entries stay bounded
+    return {a * inv, b * inv, c * inv};
+  }
+  template <int CTRL, int ROW_MASK>
+  __device__ __forceinline__ Mob from() const {  // DPP source, identity where no source lane
+    return {dpp<CTRL, ROW_MASK>(1.0, a), dpp<CTRL, ROW_MASK>(0.0, b), dpp<CTRL, ROW_MASK>(0.0, c)};
+  }
+};
+
+template <int NB>
+struct Aff {  // y -> A y + B[k]
+  double A;
+  double B[NB];
+  __device__ __forceinline__ static Aff identity() {
+    Aff r;
+    r.A = 1.0;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) r.B[k] = 0.0;
+    return r;
+  }
+  __device__ __forceinline__ static Aff combine(const Aff& L, const Aff& R) {
+    Aff r;
+    r.A = R.A * L.A;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) r.B[k] = fma(R.A, L.B[k], R.B[k]);
+    return r;
+  }
+  template <int CTRL, int ROW_MASK>
+  __device__ __forceinline__ Aff from() const {
+    Aff r;
+    r.A = dpp<CTRL, ROW_MASK>(1.0, A);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) r.B[k] = dpp<CTRL, ROW_MASK>(0.0, B[k]);
+    return r;
+  }
+};
+
+// Inclusive prefix scan across the 64 lanes (lane order = application order).
+template <typename T>
+__device__ __forceinline__ T wave_scan(T x) {
+  x = T::combine(x.template from<0x111, 0xf>(), x);  // row_shr:1
+  x = T::combine(x.template from<0x112, 0xf>(), x);  // row_shr:2
+  x = T::combine(x.template from<0x114, 0xf>(), x);  // row_shr:4
+  x = T::combine(x.template from<0x118, 0xf>(), x);  // row_shr:8
+  x = T::combine(x.template from<0x142, 0xa>(), x);  // row_bcast:15 -> rows 1, 3
+  x = T::combine(x.template from<0x143, 0xc>(), x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+__device__ __forceinline__ double bperm(int src_lane, double x) {
+  const long long xi = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)xi);
+  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(xi >> 32));
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+__device__ __forceinline__ int bperm_i(int src_lane, int x) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, x); }
+
+// min over the wave of (value, lane); ties to the lowest index; result on every lane
+__device__ __forceinline__ void wave_argmin(double& v, int& idx) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ov = __shfl_xor(v, off, 64);
+    const int oi = __shfl_xor(idx, off, 64);
+    if (ov < v || (ov == v && oi < idx)) {
+      v = ov;
+      idx = oi;
+    }
+  }
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// Per-set stage data of one wave: lane t holds stage t (natural) and stage N-1-t (reversed).
+struct WaveSet {
+  int N, lane, rsrc;
+  double d_nat, e_nat, d_rev, e_rev;
+  __device__ __forceinline__ void load(const double* __restrict__ sd, int N_) {
+    N = N_;
+    lane = threadIdx.x & 63;
+    rsrc = lane < N ? N - 1 - lane : lane;
+    d_nat = lane < N ? sd[lane] : 0.0;
+    e_nat = lane < N ? sd[N + lane] : 0.0;
+    d_rev = lane < N ? sd[rsrc] : 0.0;
+    e_rev = lane < N ? sd[N + rsrc] : 0.0;
+  }
+};
+
+// Per-lane (natural layout) results of one sub-problem solve; NB = 1 (value at
+// gamma) or 2 (affine in gamma: [0] constant part, [1] gamma coefficient).
+template <int NB>
+struct StageSol {
+  double w[NB];  // w_t
+  double r[NB];  // multiplier r_t = gradient of the smooth part
+};
+
+template <int NB>
+__device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const WaveSet& ws, double gamma, int s_nat) {
+  const double c = q.c;
+  const int N = ws.N;
+  const int lane = ws.lane;
+  const bool act = lane < N;
+  const int s_rev = bperm_i(ws.rsrc, s_nat);
+  const Box br = lq_box(act ? s_rev : 0);
+  const double d_rev = ws.d_rev;
+  // ---- (1) Moebius scan, reversed layout (lane l = stage N-1-l)
+  const bool fr = act && (s_rev & 1);
+  Mob f = Mob::identity();
+  if (fr) {
+    const double iv = lq_rcp(c + d_rev);
+    f = {d_rev * iv, d_rev * c * iv, iv};
+  } else if (act) {
+    f = {1.0, c, 0.0};
+  }
+  const Mob T = wave_scan(f);
+  const double P_next = shr1(0.0, T.b);  // P_{t+1}
+  // ---- (2) affine scan for p
+  const double Q = c + P_next;
+  const double iv = lq_rcp(Q + d_rev);
+  const double et = ws.e_rev + br.slo;
+  Aff<NB> g = Aff<NB>::identity();
+  if (fr) {
+    g.A = d_rev * iv;
+    if (NB == 1) g.B[0] = -(c * gamma * d_rev + et * Q) * iv;
+    else {
+      g.B[0] = -et * Q * iv;
+      g.B[NB - 1] = -c * d_rev * iv;
+    }
+  } else if (act) {
+    if (NB == 1) g.B[0] = fma(Q, br.lo, -c * gamma);
+    else {
+      g.B[0] = Q * br.lo;
+      g.B[NB - 1] = -c;
+    }
+  }
+  const Aff<NB> Gp = wave_scan(g);
+  double p_next[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) p_next[k] = shr1(0.0, Gp.B[k]);
+  const double Kr = fr ? -Q * iv : 0.0;
+  double kr[NB];
+  if (NB == 1) {
+    kr[0] = fr ? -(p_next[0] - c * gamma + et) * iv : br.lo;
+  } else {
+    kr[0] = fr ? -(p_next[0] + et) * iv : br.lo;
+    kr[NB - 1] = fr ? -(p_next[NB - 1] - c) * iv : 0.0;
+  }
+  // ---- reversed -> natural layout (lane t reads lane N-1-t)
+  const double K = bperm(ws.rsrc, Kr);
+  const double Pn = bperm(ws.rsrc, P_next);
+  double kk[NB], pn[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    kk[k] = bperm(ws.rsrc, kr[k]);
+    pn[k] = bperm(ws.rsrc, p_next[k]);
+  }
+  // ---- (3) forward scan y_t = (1+K_t) y_{t-1} + k_t
+  Aff<NB> h = Aff<NB>::identity();
+  if (act) {
+    h.A = 1.0 + K;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) h.B[k] = kk[k];
+  }
+  const Aff<NB> Y = wave_scan(h);
+  StageSol<NB> out;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const double y = Y.B[k];
+    const double yp = shr1(0.0, y);
+    out.w[k] = fma(K, yp, kk[k]);
+    const double base = (NB == 1) ? ws.e_nat - c * gamma : (k == 0 ? ws.e_nat : -c);
+    out.r[k] = fma(c + Pn, y, pn[k]) + fma(ws.d_nat, out.w[k], base);
+  }
+  return out;
+}
+
+// Wave-parallel PDAS at gamma from working set s (lane t = stage t).
+// Returns true on convergence; s, w, r then hold the final working set,
+// solution and multipliers.
+__device__ __forceinline__ bool wave_pdas(const QPConst& q, const WaveSet& ws, double gamma, int& s, double& w,
+                                          double& r, int max_it) {
+  for (int it = 0; it < max_it; ++it) {
+    const StageSol<1> sol = solve_stage<1>(q, ws, gamma, s);
+    w = sol.w[0];
+    r = sol.r[0];
+    const int ns = ws.lane < ws.N ? lq_move(q, s, lq_box(s), w, r) : s;
+    const bool changed = __any(ns != s);
+    s = ns;
+    if (!changed) return true;
+  }
+  return false;
+}
+
+// Wave-parallel primal active set (monotone), from w = 0 all at knot 0.
+__device__ __forceinline__ bool wave_primal_as(const QPConst& q, const WaveSet& ws, double gamma, int& s,
+                                               double& w, double& r, int max_it) {
+  const bool act = ws.lane < ws.N;
+  s = 0;
+  w = 0.0;
+  for (int it = 0; it < max_it; ++it) {
+    const StageSol<1> sol = solve_stage<1>(q, ws, gamma, s);
+    const Box b = lq_box(s);
+    const double p = sol.w[0] - w;
+    double al = INFINITY, bval = 0.0;
+    int ns = s;
+    if (act && (s & 1)) {
+      if (p > 0.0) { al = (b.hi - w) / p; ns = s + 1; bval = b.hi; }
+      else if (p < 0.0) { al = (b.lo - w) / p; ns = s - 1; bval = b.lo; }
+    }
+    double amin = al;
+    int j = ws.lane;
+    wave_argmin(amin, j);
+    if (amin >= 1.0) {
+      w = sol.w[0];
+      r = sol.r[0];
+      const double v = -r;
+      double viol = -INFINITY;
+      int vs = s;
+      if (act && !(s & 1)) {
+        const double up = v - b.shi, dn = b.slo - v;
+        if (up > dn) { viol = up; vs = s + 1; }
+        else { viol = dn; vs = s - 1; }
+      }
+      double nv = -viol;
+      int jv = ws.lane;
+      wave_argmin(nv, jv);
+      if (-nv <= q.tol_switch) return true;
+      if (ws.lane == jv) s = vs;
+    } else {
+      const double a = fmax(amin, 0.0);
+      w = fma(a, p, w);
+      if (ws.lane == j) {
+        w = bval;
+        s = ns;
+      }
+    }
+  }
+  return false;
+}
+
+// max KKT residual of (w, r) over the wave for the working set s
+__device__ __forceinline__ double wave_kkt(const QPConst& q, const WaveSet& ws, int s, double w, double r) {
+  const double res = ws.lane < ws.N ? lq_resid(q, lq_box(s), w, r) : 0.0;
+  return wave_max(res);
+}
+
+// Exact certified solve of one QP by the whole wave, PDAS from s, primal active set if needed.
+__device__ __forceinline__ bool wave_solve(const QPConst& q, const WaveSet& ws, double gamma, int& s, double& w,
+                                           double& r) {
+  bool ok = wave_pdas(q, ws, gamma, s, w, r, 4 * ws.N + 8);
+  if (ok) ok = wave_kkt(q, ws, s, w, r) <= q.tol_cert;
+  if (!ok) {
+    ok = wave_primal_as(q, ws, gamma, s, w, r, 16 * ws.N + 32);
+    if (ok) ok = wave_kkt(q, ws, s, w, r) <= q.tol_cert;
+  }
+  const Box b = lq_box(ws.lane < ws.N ? s : 0);
+  w = fmin(fmax(w, b.lo), b.hi);
+  return ok;
+}
+
+}  // namespace lqw

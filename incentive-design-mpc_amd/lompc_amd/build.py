@@ -11,7 +11,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(ROOT, "csrc")
 OUT = os.path.join(PKG, "liblompc_amd.so")
 SOURCES = ["lompc_kernels.hip"]
-DEPS = ["lompc_kernels.hip", "lompc_qp.hpp", os.path.join("..", "..", "include", "lompc_amd.h")]
+DEPS = ["lompc_kernels.hip", "lompc_qp.hpp", "lompc_wave.hpp", os.path.join("..", "..", "include", "lompc_amd.h")]
 ARCH = os.environ.get("LOMPC_OFFLOAD_ARCH", "gfx950")
 
 

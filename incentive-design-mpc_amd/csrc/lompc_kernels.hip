@@ -10,14 +10,18 @@
 //                   wave-parallel PDAS at the cell start, then parametric active-set
 //                   tracking (homotopy) to the cell end, pieces w = a + b gamma stored
 //                   with their working sets.  DIRECT mode: the central solution.
+//                   Every stored piece is KKT-certified at both ends of its gamma
+//                   interval; the KKT residual is convex in gamma along an affine piece,
+//                   so that certifies every gamma inside it.
 //   K2  k_eval      one EV per lane, one wave per workgroup (64 EVs of one set).
-//                   w = a + b gamma from the EV's piece, KKT certificate, cost / w0 /
-//                   price0 / A_bar error.  Uncertified EVs are re-solved in place by the
-//                   whole wave (wave_solve).  Epilogue through an LDS tile: coalesced w
-//                   stores and deterministic per-workgroup column sums.
+//                   w = a + b gamma from the EV's (certified) piece, cost / w0 / price0 /
+//                   A_bar error.  Epilogue through an LDS tile: coalesced w stores and
+//                   deterministic per-workgroup column sums.  EVs whose gamma no
+//                   certified piece covers go to a per-workgroup repair list.
 //   K2d k_direct    DIRECT mode: every EV solved by its own lane (PDAS warm-started
-//                   from the central working set), same certificate/repair/epilogue.
-//   K3  k_finalize  deterministic per-set reduction of the workgroup partials.
+//                   from the central working set) and KKT-certified; same epilogue.
+//   K3  k_finalize  per set: re-solves the listed EVs with the whole wave (wave_solve,
+//                   certified), then the deterministic reduction of the partials.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -60,7 +64,9 @@ struct KArgs {
   double* cost;
   double* w0;
   int8_t* status;
-  double* partial;  // [nblk][N+NPX]
+  double* partial;    // [nblk][N+NPX]
+  int* fail_cnt;      // [nblk]      EVs of the workgroup left for the repair pass
+  uint8_t* fail_lane; // [nblk][64]  their lanes, ascending
 };
 
 // block -> (set, first EV) for set-contiguous batches
@@ -114,22 +120,17 @@ __device__ __forceinline__ EVOut wave_outputs(const QPConst& q, const double* __
 }
 
 // Shared epilogue of K2 / K2d for one wave of EVs [start, start+64) of set s.
-// ok lanes carry a certified w[] and outputs; failed lanes are re-solved by the
-// whole wave starting from `st_fail` (per-lane working-set bytes, or nullptr).
+// ok lanes carry a certified w[] and outputs; valid-but-not-ok lanes are listed
+// for the repair pass in k_finalize (their rows are rewritten there).
 template <int NMAX>
-__device__ __forceinline__ void ev_epilogue(const QPConst& q, const KArgs& a, int b, int s, int64_t start,
-                                            int64_t end, double g, bool valid, bool ok, const double (&w)[NMAX],
-                                            const EVOut& o, const uint8_t* st_fail, int8_t ok_code) {
+__device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const KArgs& a, int b, int64_t start,
+                                            int64_t end, bool valid, bool ok, const double (&w)[NMAX],
+                                            const EVOut& o) {
   __shared__ double tile[EVAL_BLOCK * (NMAX + 3)];
-  const int N = q.N;
   const int TS = N + 3;  // odd for even N: conflict-free row-per-lane ds_write_b64
   const int lane = threadIdx.x;
   const int64_t i = start + lane;
   const bool active = i < end;
-  const double* __restrict__ sd = a.setdata + (size_t)s * lq_sd(N);
-  const bool fail = valid && !ok;
-  int8_t stat = !active ? 0 : (!valid ? LOMPC_QP_INVALID : (ok ? ok_code : LOMPC_QP_FAILED));
-  // rows: w, cost, price0, err
   const double fill = valid ? 0.0 : NAN;
 #pragma unroll
   for (int t = 0; t < NMAX; ++t)
@@ -137,32 +138,11 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const KArgs& a, in
   tile[lane * TS + N] = ok ? o.cost : fill;
   tile[lane * TS + N + 1] = ok ? o.price0 : 0.0;
   tile[lane * TS + N + 2] = ok ? o.err : 0.0;
-  // in-place repair of uncertified EVs: the whole wave solves each one
-  unsigned long long fm = __ballot(fail);
-  int n_rep = 0, n_fail = 0;
-  if (fm) {
-    lqw::WaveSet ws;
-    ws.load(sd, N);
-    while (fm) {
-      const int k = __ffsll((long long)fm) - 1;
-      fm &= fm - 1;
-      const double gk = __shfl(g, k, 64);
-      const uint8_t* sk = reinterpret_cast<const uint8_t*>(__shfl((long long)(uintptr_t)st_fail, k, 64));
-      int sl = lane < N ? (sk ? (int)sk[lane] : 1) : 0;
-      double wl = 0.0, rl = 0.0;
-      const bool okk = lqw::wave_solve(q, ws, gk, sl, wl, rl);
-      const EVOut ok_out = wave_outputs(q, sd, gk, lane, wl, a.want_err != 0);
-      if (lane < N) tile[k * TS + lane] = wl;
-      if (lane == 0) {
-        tile[k * TS + N] = ok_out.cost;
-        tile[k * TS + N + 1] = ok_out.price0;
-        tile[k * TS + N + 2] = ok_out.err;
-      }
-      if (lane == k) stat = okk ? LOMPC_QP_REPAIRED : LOMPC_QP_FAILED;
-      n_rep += okk ? 1 : 0;
-      n_fail += okk ? 0 : 1;
-    }
-  }
+  const unsigned long long okm = __ballot(ok);
+  const unsigned long long fm = __ballot(valid && !ok);
+  const unsigned long long im = __ballot(active && !valid);
+  if (valid && !ok) a.fail_lane[(size_t)b * EVAL_BLOCK + __popcll(fm & ((1ull << lane) - 1ull))] = (uint8_t)lane;
+  if (lane == 0) a.fail_cnt[b] = __popcll(fm);
   __syncthreads();
   // coalesced stores (row-major w[B][N])
   const int nrow = (int)min((int64_t)EVAL_BLOCK, end - start);
@@ -184,29 +164,25 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const KArgs& a, in
   if (active) {
     if (a.cost) a.cost[i] = tile[lane * TS + N];
     if (a.w0) a.w0[i] = tile[lane * TS + 0];
-    if (a.status) a.status[i] = stat;
+    if (a.status) a.status[i] = !valid ? LOMPC_QP_INVALID : (ok ? LOMPC_QP_OK : LOMPC_QP_FAILED);
   }
-  // per-workgroup partials: column sums over the valid rows (max for the error)
-  const unsigned long long vm = __ballot(valid);
-  const unsigned long long okm = __ballot(ok);
-  const unsigned long long im = __ballot(active && !valid);
+  // per-workgroup partials: column sums over the certified rows (max for the error)
   double* part = a.partial + (size_t)b * (N + NPX);
   for (int c = lane; c < TS; c += EVAL_BLOCK) {
     const bool is_max = (c == N + PX_MAX_ERR);
     double acc0 = 0.0, acc1 = 0.0;
     for (int r = 0; r < EVAL_BLOCK; r += 2) {
-      const double v0 = ((vm >> r) & 1ull) ? tile[r * TS + c] : 0.0;
-      const double v1 = ((vm >> (r + 1)) & 1ull) ? tile[(r + 1) * TS + c] : 0.0;
+      const double v0 = ((okm >> r) & 1ull) ? tile[r * TS + c] : 0.0;
+      const double v1 = ((okm >> (r + 1)) & 1ull) ? tile[(r + 1) * TS + c] : 0.0;
       acc0 = is_max ? fmax(acc0, v0) : acc0 + v0;
       acc1 = is_max ? fmax(acc1, v1) : acc1 + v1;
     }
     part[c] = is_max ? fmax(acc0, acc1) : acc0 + acc1;
   }
   if (lane == 0) {
-    const int nok = __popcll(okm);
-    part[N + PX_N_OK] = (double)(nok + n_rep);
-    part[N + PX_N_REPAIRED] = (double)n_rep;
-    part[N + PX_N_FAILED] = (double)n_fail;
+    part[N + PX_N_OK] = (double)__popcll(okm);
+    part[N + PX_N_REPAIRED] = 0.0;
+    part[N + PX_N_FAILED] = 0.0;
     part[N + PX_N_INVALID] = (double)__popcll(im);
   }
 }
@@ -313,6 +289,12 @@ __global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __r
     }
     const bool final_piece = (bj < 0) || (npc == LQ_PPL - 1);
     if (best > gcur || final_piece) {
+      // KKT certificate at both ends (convex in gamma along the piece => whole piece)
+      const Box bx = lq_box(lane < N ? sl : 0);
+      const double wa = fmin(fmax(fma(bv, gcur, av), bx.lo), bx.hi);
+      const double wz = fmin(fmax(fma(bv, best, av), bx.lo), bx.hi);
+      const double res = fmax(lqw::wave_kkt_point(q, ws, gcur, sl, wa), lqw::wave_kkt_point(q, ws, best, sl, wz));
+      if (!(res <= q.tol_cert)) break;  // coverage of the cell ends at gcur
       const size_t pidx = cb * LQ_PPL + npc;
       if (lane < N) {
         reinterpret_cast<double2*>(tab.ab + pidx * (size_t)N * 2)[lane] = make_double2(av, bv);
@@ -331,14 +313,15 @@ __global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __r
 }
 
 // ------------------------------------------------------------------- K2
-template <int NMAX>
+// NT = NMAX: exact-horizon instantiation (all stage guards fold away);
+// NT = 0: any N <= NMAX with runtime guards.
+template <int NMAX, int NT>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a) {
-  lq_tab_init(q);
   const int b = blockIdx.x;
   int s;
   int64_t start, end;
   block_set(a, b, s, start, end);
-  const int N = q.N;
+  const int N = NT ? NT : q.N;
   const int lane = threadIdx.x;
   const int64_t i = start + lane;
   const bool active = i < end;
@@ -349,46 +332,46 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a) {
 #pragma unroll
   for (int t = 0; t < NMAX; ++t) w[t] = 0.0;
   bool ok = false;
-  const uint8_t* stp = nullptr;
   if (valid) {
     const double invh = (double)LQ_G / q.y_max;
     const int cell = min(LQ_G - 1, (int)(g * invh));
     const size_t cb = (size_t)s * LQ_G + cell;
     const int cnt = a.tab.cnt[cb];
-    if (cnt > 0) {
-      int p = cnt - 1;
+    double ge[LQ_PPL];
 #pragma unroll
-      for (int pp = LQ_PPL - 1; pp >= 0; --pp)
-        if (pp < cnt && g <= a.tab.gend[cb * LQ_PPL + pp]) p = pp;
-      const size_t pidx = cb * LQ_PPL + p;
-      const double2* row = reinterpret_cast<const double2*>(a.tab.ab + pidx * (size_t)N * 2);
-      stp = a.tab.st + pidx * LQ_STB;
-      States<NMAX> st;
-      st.load_bytes(stp);
+    for (int pp = 0; pp < LQ_PPL; ++pp) ge[pp] = a.tab.gend[cb * LQ_PPL + pp];
+    int p = cnt - 1;
+    double glast = -1.0;
+#pragma unroll
+    for (int pp = LQ_PPL - 1; pp >= 0; --pp) {
+      if (pp < cnt && g <= ge[pp]) p = pp;
+      if (pp == cnt - 1) glast = ge[pp];
+    }
+    ok = (cnt > 0) && (g <= glast);  // inside a certified piece
+    if (ok) {
+      const double2* row = reinterpret_cast<const double2*>(a.tab.ab + (cb * LQ_PPL + p) * (size_t)N * 2);
 #pragma unroll
       for (int t = 0; t < NMAX; ++t)
         if (t < N) {
           const double2 ab = row[t];
-          const Box bx = lq_box(st.get(t));
-          w[t] = fmin(fmax(fma(ab.y, g, ab.x), bx.lo), bx.hi);
+          w[t] = fmin(fmax(fma(ab.y, g, ab.x), 0.0), q.w_max);
         }
-      ok = lq_kkt<NMAX>(q, sd, sd + N, g, st, w) <= q.tol_cert;
     }
   }
   EVOut o{0.0, 0.0, 0.0};
-  if (ok) o = lq_outputs<NMAX>(q, sd, g, w, a.want_err != 0);
-  ev_epilogue<NMAX>(q, a, b, s, start, end, g, valid, ok, w, o, stp, (int8_t)LOMPC_QP_OK);
+  if (ok) o = lq_outputs<NMAX>(q, N, sd, g, w, a.want_err != 0);
+  ev_epilogue<NMAX>(q, N, a, b, start, end, valid, ok, w, o);
 }
 
 // ------------------------------------------------------------------- K2d
-template <int NMAX>
+template <int NMAX, int NT>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_direct(QPConst q, KArgs a) {
   lq_tab_init(q);
   const int b = blockIdx.x;
   int s;
   int64_t start, end;
   block_set(a, b, s, start, end);
-  const int N = q.N;
+  const int N = NT ? NT : q.N;
   const int lane = threadIdx.x;
   const int64_t i = start + lane;
   const bool active = i < end;
@@ -403,29 +386,89 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_direct(QPConst q, KArgs a) {
   if (valid) {
     States<NMAX> st;
     st.load_bytes(cst);
-    ok = lq_pdas<NMAX>(q, sd, sd + N, g, st, w, 4 * N + 8);
+    ok = lq_pdas<NMAX>(q, N, sd, sd + N, g, st, w, 4 * N + 8);
     if (ok) {
-      lq_snap<NMAX>(q, st, w);
-      ok = lq_kkt<NMAX>(q, sd, sd + N, g, st, w) <= q.tol_cert;
+      lq_snap<NMAX>(N, st, w);
+      ok = lq_kkt<NMAX>(q, N, sd, sd + N, g, st, w) <= q.tol_cert;
     }
   }
   EVOut o{0.0, 0.0, 0.0};
-  if (ok) o = lq_outputs<NMAX>(q, sd, g, w, a.want_err != 0);
-  ev_epilogue<NMAX>(q, a, b, s, start, end, g, valid, ok, w, o, cst, (int8_t)LOMPC_QP_OK);
+  if (ok) o = lq_outputs<NMAX>(q, N, sd, g, w, a.want_err != 0);
+  ev_epilogue<NMAX>(q, N, a, b, start, end, valid, ok, w, o);
 }
 
 // ------------------------------------------------------------------- K3
-// One workgroup of 1024 threads per set: wave wv sums rows wv, wv+16, ... of
-// the set's partial records (lane = column), then the 16 waves combine in LDS.
-__global__ __launch_bounds__(1024) void k_finalize(int N, int S, const int* __restrict__ blk_prefix,
-                                                   const int64_t* __restrict__ set_off,
-                                                   const double* __restrict__ partial, double* __restrict__ set_sum_w,
+// One workgroup of 1024 threads (16 waves) per set.
+// (1) repair: wave wv re-solves the listed EVs of workgroups b0+wv, b0+wv+16, ...
+//     (wave_solve: PDAS from the cell's / central working set, primal active set
+//     if needed, KKT-certified) and writes their outputs;
+// (2) reduction: wave wv sums partial rows wv, wv+16, ... (lane = column), the 16
+//     waves and the repair accumulators combine in LDS in a fixed order.
+__global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode, double* __restrict__ set_sum_w,
                                                    double* __restrict__ set_stats, double* __restrict__ stats_int) {
+  lq_tab_init(q);
   __shared__ double red[16][LOMPC_MAX_N + NPX + 1];
+  __shared__ double rep[16][LOMPC_MAX_N + NPX + 1];
   const int s = blockIdx.x;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int N = q.N;
   const int W = N + NPX;
-  const int b0 = blk_prefix[s], b1 = blk_prefix[s + 1];
+  const int b0 = a.blk_prefix[s], b1 = a.blk_prefix[s + 1];
+  // ---- (1) repair pass
+  int anyf = 0;
+  for (int b = b0 + tid; b < b1; b += 1024) anyf |= a.fail_cnt[b];
+  anyf = __syncthreads_or(anyf);
+  double acc_w = 0.0, acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
+  int nrep = 0, nfail = 0;
+  if (anyf) {
+    const double* __restrict__ sd = a.setdata + (size_t)s * lq_sd(N);
+    lqw::WaveSet ws;
+    ws.load(sd, N);
+    for (int b = b0 + wv; b < b1; b += 16) {
+      const int nf = a.fail_cnt[b];
+      for (int k = 0; k < nf; ++k) {
+        const int l = a.fail_lane[(size_t)b * EVAL_BLOCK + k];
+        const int64_t i = a.set_off[s] + (int64_t)(b - b0) * EVAL_BLOCK + l;
+        const double g = a.gamma[i];
+        int sl = 1;
+        if (mode == LOMPC_MODE_PATH) {
+          const int cell = min(LQ_G - 1, (int)(g * ((double)LQ_G / q.y_max)));
+          const size_t cb = (size_t)s * LQ_G + cell;
+          if (a.tab.cnt[cb] > 0) sl = a.tab.st[cb * LQ_PPL * LQ_STB + lane];
+        } else {
+          sl = a.central[(size_t)s * LQ_STB + lane];
+        }
+        if (lane >= N) sl = 0;
+        double wl = 0.0, rl = 0.0;
+        const bool okk = lqw::wave_solve(q, ws, g, sl, wl, rl);
+        const EVOut o = wave_outputs(q, sd, g, lane, wl, a.want_err != 0);
+        if (a.w && lane < N) a.w[(size_t)i * N + lane] = wl;
+        if (lane == 0) {
+          if (a.cost) a.cost[i] = o.cost;
+          if (a.w0) a.w0[i] = wl;
+          if (a.status) a.status[i] = okk ? LOMPC_QP_REPAIRED : LOMPC_QP_FAILED;
+        }
+        acc_w += lane < N ? wl : 0.0;
+        acc_cost += o.cost;
+        acc_p0 += o.price0;
+        acc_err = fmax(acc_err, o.err);
+        nrep += okk ? 1 : 0;
+        nfail += okk ? 0 : 1;
+      }
+    }
+  }
+  if (lane < N) rep[wv][lane] = acc_w;
+  if (lane == 0) {
+    rep[wv][N + PX_COST] = acc_cost;
+    rep[wv][N + PX_PRICE0] = acc_p0;
+    rep[wv][N + PX_MAX_ERR] = acc_err;
+    rep[wv][N + PX_N_OK] = (double)nrep;
+    rep[wv][N + PX_N_REPAIRED] = (double)nrep;
+    rep[wv][N + PX_N_FAILED] = (double)nfail;
+    rep[wv][N + PX_N_INVALID] = 0.0;
+  }
+  // ---- (2) reduction of the workgroup partials
   for (int c = lane; c < W; c += 64) {
     const bool is_max = (c == N + PX_MAX_ERR);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -433,31 +476,30 @@ __global__ __launch_bounds__(1024) void k_finalize(int N, int S, const int* __re
     for (; b + 48 < b1; b += 64) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const double v = partial[(size_t)(b + 16 * u) * W + c];
+        const double v = a.partial[(size_t)(b + 16 * u) * W + c];
         acc[u] = is_max ? fmax(acc[u], v) : acc[u] + v;
       }
     }
     for (; b < b1; b += 16) {
-      const double v = partial[(size_t)b * W + c];
+      const double v = a.partial[(size_t)b * W + c];
       acc[0] = is_max ? fmax(acc[0], v) : acc[0] + v;
     }
     red[wv][c] = is_max ? fmax(fmax(acc[0], acc[1]), fmax(acc[2], acc[3])) : (acc[0] + acc[1]) + (acc[2] + acc[3]);
   }
   __syncthreads();
-  if (threadIdx.x < W) {
-    const int c = threadIdx.x;
+  if (tid < W) {
+    const int c = tid;
     const bool is_max = (c == N + PX_MAX_ERR);
     double acc = red[0][c];
     for (int k = 1; k < 16; ++k) acc = is_max ? fmax(acc, red[k][c]) : acc + red[k][c];
+    for (int k = 0; k < 16; ++k) acc = is_max ? fmax(acc, rep[k][c]) : acc + rep[k][c];
     red[0][c] = acc;
   }
   __syncthreads();
-  if (threadIdx.x < N) {
-    if (set_sum_w) set_sum_w[(size_t)s * N + threadIdx.x] = red[0][threadIdx.x];
-  }
-  if (threadIdx.x == 0) {
+  if (tid < N && set_sum_w) set_sum_w[(size_t)s * N + tid] = red[0][tid];
+  if (tid == 0) {
     double row[LOMPC_SET_STATS];
-    row[LOMPC_STAT_COUNT] = (double)(set_off[s + 1] - set_off[s]);
+    row[LOMPC_STAT_COUNT] = (double)(a.set_off[s + 1] - a.set_off[s]);
     row[LOMPC_STAT_SUM_W0] = red[0][0];
     row[LOMPC_STAT_SUM_PRICE0] = red[0][N + PX_PRICE0];
     row[LOMPC_STAT_MAX_ERR] = red[0][N + PX_MAX_ERR];
@@ -490,6 +532,8 @@ struct lompc_ctx {
   // batch workspaces
   int64_t nblk_cap = 0, soff_cap = 0, stats_cap = 0;
   double* d_partial = nullptr;
+  int* d_fail_cnt = nullptr;
+  uint8_t* d_fail_lane = nullptr;
   int* d_blk_prefix = nullptr;
   int64_t* d_set_off = nullptr;
   double* d_stats = nullptr;  // [S][LOMPC_SET_STATS], always written by k_finalize
@@ -551,14 +595,24 @@ static int pick_nmax(int N) {
   return 0;
 }
 
-#define DISPATCH_NMAX(nmax, ...)                            \
-  switch (nmax) {                                           \
-    case 16: { constexpr int NM = 16; __VA_ARGS__; } break; \
-    case 24: { constexpr int NM = 24; __VA_ARGS__; } break; \
-    case 32: { constexpr int NM = 32; __VA_ARGS__; } break; \
-    case 48: { constexpr int NM = 48; __VA_ARGS__; } break; \
-    case 64: { constexpr int NM = 64; __VA_ARGS__; } break; \
-    default: break;                                         \
+// (NM, NT): exact-horizon kernels for the common N, NMAX buckets with runtime N otherwise
+#define DISPATCH_N(N, nmax, ...)                                                    \
+  switch (N) {                                                                      \
+    case 12: { constexpr int NM = 12, NT = 12; __VA_ARGS__; } break;                \
+    case 16: { constexpr int NM = 16, NT = 16; __VA_ARGS__; } break;                \
+    case 24: { constexpr int NM = 24, NT = 24; __VA_ARGS__; } break;                \
+    case 32: { constexpr int NM = 32, NT = 32; __VA_ARGS__; } break;                \
+    case 48: { constexpr int NM = 48, NT = 48; __VA_ARGS__; } break;                \
+    case 64: { constexpr int NM = 64, NT = 64; __VA_ARGS__; } break;                \
+    default:                                                                        \
+      switch (nmax) {                                                               \
+        case 16: { constexpr int NM = 16, NT = 0; __VA_ARGS__; } break;             \
+        case 24: { constexpr int NM = 24, NT = 0; __VA_ARGS__; } break;             \
+        case 32: { constexpr int NM = 32, NT = 0; __VA_ARGS__; } break;             \
+        case 48: { constexpr int NM = 48, NT = 0; __VA_ARGS__; } break;             \
+        case 64: { constexpr int NM = 64, NT = 0; __VA_ARGS__; } break;             \
+        default: break;                                                             \
+      }                                                                             \
   }
 
 extern "C" {
@@ -645,7 +699,8 @@ int lompc_destroy(lompc_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   void* ptrs[] = {c->d_setdata, c->tab.cnt, c->tab.gend, c->tab.ab, c->tab.st, c->d_central, c->d_errflag,
-                  c->d_partial, c->d_blk_prefix, c->d_set_off, c->d_stats, c->d_single, c->d_single_status};
+                  c->d_partial, c->d_fail_cnt, c->d_fail_lane, c->d_blk_prefix, c->d_set_off, c->d_stats,
+                  c->d_single, c->d_single_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_pin_prefix) (void)hipHostFree(c->h_pin_prefix);
@@ -710,7 +765,9 @@ static int upload_block_map(lompc_ctx* c, const int64_t* set_off, int64_t S, int
   *nblk_out = (int)nb;
   if (nb > c->nblk_cap) {
     int rc;
-    if ((rc = grow(c, &c->d_partial, (size_t)nb * (c->N + NPX)))) return rc;
+    if ((rc = grow(c, &c->d_partial, (size_t)nb * (c->N + NPX))) || (rc = grow(c, &c->d_fail_cnt, (size_t)nb)) ||
+        (rc = grow(c, &c->d_fail_lane, (size_t)nb * EVAL_BLOCK)))
+      return rc;
     c->nblk_cap = nb;
   }
   if (S > c->stats_cap) {
@@ -775,6 +832,8 @@ int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_
   a.w0 = w0;
   a.status = status;
   a.partial = c->d_partial;
+  a.fail_cnt = c->d_fail_cnt;
+  a.fail_lane = c->d_fail_lane;
   if (nblk > 0) {
     dim3 grid((unsigned)nblk), block(EVAL_BLOCK);
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -784,9 +843,9 @@ int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_
       HIPCHK(c, hipEventRecord(e0, st));
     }
     if (c->params_mode == LOMPC_MODE_PATH) {
-      DISPATCH_NMAX(c->nmax, hipLaunchKernelGGL(k_eval<NM>, grid, block, 0, st, c->q, a));
+      DISPATCH_N(c->N, c->nmax, hipLaunchKernelGGL((k_eval<NM, NT>), grid, block, 0, st, c->q, a));
     } else {
-      DISPATCH_NMAX(c->nmax, hipLaunchKernelGGL(k_direct<NM>, grid, block, 0, st, c->q, a));
+      DISPATCH_N(c->N, c->nmax, hipLaunchKernelGGL((k_direct<NM, NT>), grid, block, 0, st, c->q, a));
     }
     HIPCHK(c, hipGetLastError());
     if (c->prof) {
@@ -795,8 +854,8 @@ int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_
       c->prof_ev.push_back(e1);
     }
   }
-  hipLaunchKernelGGL(k_finalize, dim3((unsigned)c->S), dim3(1024), 0, st, c->N, (int)c->S, c->d_blk_prefix,
-                     c->d_set_off, c->d_partial, set_sum_w, set_stats, c->d_stats);
+  hipLaunchKernelGGL(k_finalize, dim3((unsigned)c->S), dim3(1024), 0, st, c->q, a, c->params_mode, set_sum_w,
+                     set_stats, c->d_stats);
   HIPCHK(c, hipGetLastError());
   c->stats_S = c->S;
   return LOMPC_OK;

@@ -178,7 +178,7 @@ __device__ __forceinline__ double lq_rcp(double x) {  // v_rcp_f64 + two Newton 
 // Q >= c > 0, so every reciprocal is well defined.
 // ---------------------------------------------------------------------------
 template <int NMAX>
-__device__ __forceinline__ void lq_riccati(const QPConst& q, const double* __restrict__ d,
+__device__ __forceinline__ void lq_riccati(const QPConst& q, const int N, const double* __restrict__ d,
                                            const double* __restrict__ e, double gamma,
                                            const States<NMAX>& st, double (&w)[NMAX]) {
   double K[NMAX], k[NMAX];
@@ -186,7 +186,7 @@ __device__ __forceinline__ void lq_riccati(const QPConst& q, const double* __res
   const double cg = q.c * gamma;
 #pragma unroll
   for (int t = NMAX - 1; t >= 0; --t) {
-    if (t < q.N) {
+    if (t < N) {
       const double Q = q.c + P;
       const double qq = p - cg;
       const int s = st.get(t);
@@ -204,7 +204,7 @@ __device__ __forceinline__ void lq_riccati(const QPConst& q, const double* __res
   double y = 0.0;
 #pragma unroll
   for (int t = 0; t < NMAX; ++t) {
-    if (t < q.N) {
+    if (t < N) {
       w[t] = fma(K[t], y, k[t]);
       y += w[t];
     }
@@ -214,11 +214,11 @@ __device__ __forceinline__ void lq_riccati(const QPConst& q, const double* __res
 // Gradient of the smooth part: r_j = c (sum_{i>=j} y_i - (N-j) gamma) + d_j w_j + e_j,
 // computed on the fly with the prefix trick (total of y first, then running prefix).
 template <int NMAX>
-__device__ __forceinline__ double lq_sum_y(const QPConst& q, const double (&w)[NMAX]) {
+__device__ __forceinline__ double lq_sum_y(const int N, const double (&w)[NMAX]) {
   double y = 0.0, Z = 0.0;
 #pragma unroll
   for (int t = 0; t < NMAX; ++t)
-    if (t < q.N) {
+    if (t < N) {
       y += w[t];
       Z += y;
     }
@@ -228,17 +228,17 @@ __device__ __forceinline__ double lq_sum_y(const QPConst& q, const double (&w)[N
 // One PDAS (semismooth-Newton active-set) state update from the sub-problem
 // solution w.  Returns true if any coordinate changed state.
 template <int NMAX>
-__device__ __forceinline__ bool lq_pdas_update(const QPConst& q, const double* __restrict__ d,
+__device__ __forceinline__ bool lq_pdas_update(const QPConst& q, const int N, const double* __restrict__ d,
                                                const double* __restrict__ e, double gamma,
                                                const double (&w)[NMAX], States<NMAX>& st) {
-  const double Zt = lq_sum_y<NMAX>(q, w);
+  const double Zt = lq_sum_y<NMAX>(N, w);
   double y = 0.0, Z = 0.0;
   bool changed = false;
 #pragma unroll
   for (int t = 0; t < NMAX; ++t) {
-    if (t < q.N) {
+    if (t < N) {
       y += w[t];
-      const double r = q.c * (Zt - Z - (double)(q.N - t) * gamma) + d[t] * w[t] + e[t];
+      const double r = q.c * (Zt - Z - (double)(N - t) * gamma) + d[t] * w[t] + e[t];
       Z += y;
       const int s = st.get(t);
       const int ns = lq_move(q, s, lq_box(s), w[t], r);
@@ -250,109 +250,40 @@ __device__ __forceinline__ bool lq_pdas_update(const QPConst& q, const double* _
 }
 
 template <int NMAX>
-__device__ __forceinline__ bool lq_pdas(const QPConst& q, const double* __restrict__ d,
+__device__ __forceinline__ bool lq_pdas(const QPConst& q, const int N, const double* __restrict__ d,
                                         const double* __restrict__ e, double gamma, States<NMAX>& st,
                                         double (&w)[NMAX], int max_it) {
   bool done = false;
   for (int it = 0; it < max_it && !done; ++it) {
-    lq_riccati<NMAX>(q, d, e, gamma, st, w);
-    done = !lq_pdas_update<NMAX>(q, d, e, gamma, w, st);
+    lq_riccati<NMAX>(q, N, d, e, gamma, st, w);
+    done = !lq_pdas_update<NMAX>(q, N, d, e, gamma, w, st);
   }
   return done;
 }
 
 // Project onto the working set's box (free: clamp into the segment; fixed: the knot).
 template <int NMAX>
-__device__ __forceinline__ void lq_snap(const QPConst& q, const States<NMAX>& st, double (&w)[NMAX]) {
+__device__ __forceinline__ void lq_snap(const int N, const States<NMAX>& st, double (&w)[NMAX]) {
 #pragma unroll
   for (int t = 0; t < NMAX; ++t)
-    if (t < q.N) {
+    if (t < N) {
       const Box b = lq_box(st.get(t));
       w[t] = fmin(fmax(w[t], b.lo), b.hi);
     }
 }
 
-// Primal active-set method (Nocedal & Wright Alg. 16.3, PWL kinks as knots)
-// from w = 0 with every coordinate fixed at knot 0.  Monotone; last resort.
-template <int NMAX>
-__device__ __forceinline__ bool lq_primal_as(const QPConst& q, const double* __restrict__ d,
-                                             const double* __restrict__ e, double gamma, States<NMAX>& st,
-                                             double (&w)[NMAX], int max_it) {
-  st.fill(0);
-#pragma unroll
-  for (int t = 0; t < NMAX; ++t) w[t] = 0.0;
-  bool done = false;
-  for (int it = 0; it < max_it && !done; ++it) {
-    double wh[NMAX];
-    lq_riccati<NMAX>(q, d, e, gamma, st, wh);
-    double alpha = 1.0;
-    int blk = -1, bs = 0;
-    double bval = 0.0;
-#pragma unroll
-    for (int t = 0; t < NMAX; ++t) {
-      if (t < q.N) {
-        const int s = st.get(t);
-        if (s & 1) {
-          const Box b = lq_box(s);
-          const double pj = wh[t] - w[t];
-          if (pj > 0.0) {
-            const double a = (b.hi - w[t]) / pj;
-            if (a < alpha) { alpha = a; blk = t; bs = s + 1; bval = b.hi; }
-          } else if (pj < 0.0) {
-            const double a = (b.lo - w[t]) / pj;
-            if (a < alpha) { alpha = a; blk = t; bs = s - 1; bval = b.lo; }
-          }
-        }
-      }
-    }
-    if (blk < 0) {
-#pragma unroll
-      for (int t = 0; t < NMAX; ++t) w[t] = wh[t];
-      const double Zt = lq_sum_y<NMAX>(q, w);
-      double y = 0.0, Z = 0.0, best = q.tol_switch;
-      int bj = -1, bns = 0;
-#pragma unroll
-      for (int t = 0; t < NMAX; ++t) {
-        if (t < q.N) {
-          y += w[t];
-          const double r = q.c * (Zt - Z - (double)(q.N - t) * gamma) + d[t] * w[t] + e[t];
-          Z += y;
-          const int s = st.get(t);
-          if (!(s & 1)) {
-            const Box b = lq_box(s);
-            const double up = -r - b.shi, dn = b.slo + r;
-            if (up > best) { best = up; bj = t; bns = s + 1; }
-            if (dn > best) { best = dn; bj = t; bns = s - 1; }
-          }
-        }
-      }
-      if (bj < 0) done = true;
-      else st.set_rt(bj, bns);
-    } else {
-      alpha = fmax(alpha, 0.0);
-#pragma unroll
-      for (int t = 0; t < NMAX; ++t) {
-        w[t] = fma(alpha, wh[t] - w[t], w[t]);
-        if (t == blk) w[t] = bval;
-      }
-      st.set_rt(blk, bs);
-    }
-  }
-  return done;
-}
-
 // KKT certificate of (w, working set): max distance of -r from the state boxes.
 template <int NMAX>
-__device__ __forceinline__ double lq_kkt(const QPConst& q, const double* __restrict__ d,
+__device__ __forceinline__ double lq_kkt(const QPConst& q, const int N, const double* __restrict__ d,
                                          const double* __restrict__ e, double gamma, const States<NMAX>& st,
                                          const double (&w)[NMAX]) {
-  const double Zt = lq_sum_y<NMAX>(q, w);
+  const double Zt = lq_sum_y<NMAX>(N, w);
   double y = 0.0, Z = 0.0, res = 0.0;
 #pragma unroll
   for (int t = 0; t < NMAX; ++t) {
-    if (t < q.N) {
+    if (t < N) {
       y += w[t];
-      const double r = q.c * (Zt - Z - (double)(q.N - t) * gamma) + d[t] * w[t] + e[t];
+      const double r = q.c * (Zt - Z - (double)(N - t) * gamma) + d[t] * w[t] + e[t];
       Z += y;
       res = fmax(res, lq_resid(q, lq_box(st.get(t)), w[t], r));
     }
@@ -379,9 +310,8 @@ __device__ __forceinline__ double lq_price0(const QPConst& q, const double* __re
 }
 
 template <int NMAX>
-__device__ __forceinline__ EVOut lq_outputs(const QPConst& q, const double* __restrict__ sd, double gamma,
+__device__ __forceinline__ EVOut lq_outputs(const QPConst& q, const int N, const double* __restrict__ sd, double gamma,
                                             const double (&w)[NMAX], bool want_err) {
-  const int N = q.N;
   const double* d = sd;
   const double* e = sd + N;
   const double* wr = sd + 2 * N;

@@ -287,6 +287,25 @@ __device__ __forceinline__ double wave_kkt(const QPConst& q, const WaveSet& ws, 
   return wave_max(res);
 }
 
+// Max KKT residual at gamma of the point w (lane t = w_t) for working set s,
+// with the gradient recomputed from w itself (prefix scans), independent of
+// the Riccati costate:  r_t = c (sum_{i>=t} y_i - (N-t) gamma) + d_t w_t + e_t.
+__device__ __forceinline__ double wave_kkt_point(const QPConst& q, const WaveSet& ws, double gamma, int s,
+                                                 double w) {
+  const int N = ws.N;
+  const bool act = ws.lane < N;
+  Aff<1> h = Aff<1>::identity();
+  if (act) h.B[0] = w;
+  const double y = wave_scan(h).B[0];   // y_t = sum_{i<=t} w_i
+  Aff<1> z = Aff<1>::identity();
+  if (act) z.B[0] = y;
+  const double Z = wave_scan(z).B[0];   // Z_t = sum_{i<=t} y_i
+  const double Zt = __shfl(Z, N - 1, 64);
+  const double r = q.c * (Zt - Z + y - (double)(N - ws.lane) * gamma) + ws.d_nat * w + ws.e_nat;
+  const double res = act ? lq_resid(q, lq_box(s), w, r) : 0.0;
+  return wave_max(res);
+}
+
 // Exact certified solve of one QP by the whole wave, PDAS from s, primal active set if needed.
 __device__ __forceinline__ bool wave_solve(const QPConst& q, const WaveSet& ws, double gamma, int& s, double& w,
                                            double& r) {

@@ -55,8 +55,9 @@ struct KArgs {
   int want_err;
   int pad;
   const double* gamma;
-  const int* blk_prefix;   // [S+1]
-  const int64_t* set_off;  // [S+1]
+  const int* blk_prefix;       // [S+1]
+  const int64_t* set_off;      // [S+1]
+  const longlong4* blk_info;   // [nblk]  (set, first EV, end EV, -)
   const double* setdata;   // [S][SD]
   PathTable tab;
   const uint8_t* central;  // [S][LQ_STB]
@@ -69,17 +70,12 @@ struct KArgs {
   uint8_t* fail_lane; // [nblk][64]  their lanes, ascending
 };
 
-// block -> (set, first EV) for set-contiguous batches
+// block -> (set, first EV, end of set) for set-contiguous batches: one scalar load
 __device__ __forceinline__ void block_set(const KArgs& a, int b, int& s, int64_t& start, int64_t& end) {
-  int lo = 0, hi = a.S - 1;
-  while (lo < hi) {  // largest s with blk_prefix[s] <= b
-    const int mid = (lo + hi + 1) >> 1;
-    if (a.blk_prefix[mid] <= b) lo = mid;
-    else hi = mid - 1;
-  }
-  s = lo;
-  start = a.set_off[s] + (int64_t)(b - a.blk_prefix[s]) * EVAL_BLOCK;
-  end = a.set_off[s + 1];
+  const longlong4 info = a.blk_info[b];
+  s = (int)info.x;
+  start = info.y;
+  end = info.z;
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -148,16 +144,28 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const
   const int nrow = (int)min((int64_t)EVAL_BLOCK, end - start);
   if (a.w && nrow > 0) {
     double* wo = a.w + (size_t)start * N;
-    const int tot = nrow * N;
-    const int q64 = EVAL_BLOCK / N, r64 = EVAL_BLOCK % N;
-    int row = lane / N, col = lane % N;
-    for (int e = lane; e < tot; e += EVAL_BLOCK) {
-      wo[e] = tile[row * TS + col];
-      row += q64;
-      col += r64;
-      if (col >= N) {
-        col -= N;
-        row += 1;
+    if (nrow == EVAL_BLOCK && (N % 2) == 0) {  // full tile, 16 B per lane (start*N*8 is 16-B aligned)
+      double2* wo2 = reinterpret_cast<double2*>(wo);
+#pragma unroll
+      for (int r = 0; r < NMAX / 2; ++r) {
+        if (r < N / 2) {
+          const int e = 2 * (lane + EVAL_BLOCK * r);  // even element index
+          const int row = e / N, col = e - row * N;
+          wo2[lane + EVAL_BLOCK * r] = make_double2(tile[row * TS + col], tile[row * TS + col + 1]);
+        }
+      }
+    } else {
+      const int tot = nrow * N;
+      const int q64 = EVAL_BLOCK / N, r64 = EVAL_BLOCK % N;
+      int row = lane / N, col = lane % N;
+      for (int e = lane; e < tot; e += EVAL_BLOCK) {
+        wo[e] = tile[row * TS + col];
+        row += q64;
+        col += r64;
+        if (col >= N) {
+          col -= N;
+          row += 1;
+        }
       }
     }
   }
@@ -170,14 +178,19 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const
   double* part = a.partial + (size_t)b * (N + NPX);
   for (int c = lane; c < TS; c += EVAL_BLOCK) {
     const bool is_max = (c == N + PX_MAX_ERR);
-    double acc0 = 0.0, acc1 = 0.0;
-    for (int r = 0; r < EVAL_BLOCK; r += 2) {
-      const double v0 = ((okm >> r) & 1ull) ? tile[r * TS + c] : 0.0;
-      const double v1 = ((okm >> (r + 1)) & 1ull) ? tile[(r + 1) * TS + c] : 0.0;
-      acc0 = is_max ? fmax(acc0, v0) : acc0 + v0;
-      acc1 = is_max ? fmax(acc1, v1) : acc1 + v1;
+    double acc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = 0.0;
+#pragma unroll
+    for (int r = 0; r < EVAL_BLOCK; ++r) {
+      const double v = ((okm >> r) & 1ull) ? tile[r * TS + c] : 0.0;
+      acc[r & 7] = is_max ? fmax(acc[r & 7], v) : acc[r & 7] + v;
     }
-    part[c] = is_max ? fmax(acc0, acc1) : acc0 + acc1;
+#pragma unroll
+    for (int u = 4; u >= 1; u >>= 1)
+#pragma unroll
+      for (int k = 0; k < u; ++k) acc[k] = is_max ? fmax(acc[k], acc[k + u]) : acc[k] + acc[k + u];
+    part[c] = acc[0];
   }
   if (lane == 0) {
     part[N + PX_N_OK] = (double)__popcll(okm);
@@ -289,11 +302,14 @@ __global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __r
     }
     const bool final_piece = (bj < 0) || (npc == LQ_PPL - 1);
     if (best > gcur || final_piece) {
-      // KKT certificate at both ends (convex in gamma along the piece => whole piece)
+      // KKT certificate at the piece's end.  Its start is certified too: the first
+      // piece starts at the wave_solve point; a later one at the previous piece's
+      // certified end with the same w and r, where only the switched coordinate's
+      // box changed and it contains that coordinate's value.  The residual is
+      // convex in gamma along an affine piece => the whole piece is certified.
       const Box bx = lq_box(lane < N ? sl : 0);
-      const double wa = fmin(fmax(fma(bv, gcur, av), bx.lo), bx.hi);
       const double wz = fmin(fmax(fma(bv, best, av), bx.lo), bx.hi);
-      const double res = fmax(lqw::wave_kkt_point(q, ws, gcur, sl, wa), lqw::wave_kkt_point(q, ws, best, sl, wz));
+      const double res = lqw::wave_kkt_point(q, ws, best, sl, wz);
       if (!(res <= q.tol_cert)) break;  // coverage of the cell ends at gcur
       const size_t pidx = cb * LQ_PPL + npc;
       if (lane < N) {
@@ -536,6 +552,9 @@ struct lompc_ctx {
   uint8_t* d_fail_lane = nullptr;
   int* d_blk_prefix = nullptr;
   int64_t* d_set_off = nullptr;
+  longlong4* d_blk_info = nullptr;
+  longlong4* h_pin_info = nullptr;
+  int64_t info_cap = 0;
   double* d_stats = nullptr;  // [S][LOMPC_SET_STATS], always written by k_finalize
   int64_t stats_S = 0;
   int* h_pin_prefix = nullptr;
@@ -699,12 +718,13 @@ int lompc_destroy(lompc_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   void* ptrs[] = {c->d_setdata, c->tab.cnt, c->tab.gend, c->tab.ab, c->tab.st, c->d_central, c->d_errflag,
-                  c->d_partial, c->d_fail_cnt, c->d_fail_lane, c->d_blk_prefix, c->d_set_off, c->d_stats,
+                  c->d_partial, c->d_fail_cnt, c->d_fail_lane, c->d_blk_prefix, c->d_set_off, c->d_blk_info, c->d_stats,
                   c->d_single, c->d_single_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_pin_prefix) (void)hipHostFree(c->h_pin_prefix);
   if (c->h_pin_off) (void)hipHostFree(c->h_pin_off);
+  if (c->h_pin_info) (void)hipHostFree(c->h_pin_info);
   if (c->ev_map) (void)hipEventDestroy(c->ev_map);
   for (hipEvent_t ev : c->prof_ev) (void)hipEventDestroy(ev);
   delete c;
@@ -790,12 +810,25 @@ static int upload_block_map(lompc_ctx* c, const int64_t* set_off, int64_t S, int
     HIPCHK(c, hipHostMalloc((void**)&c->h_pin_off, (S + 1) * sizeof(int64_t), hipHostMallocDefault));
     c->soff_cap = S + 1;
   }
-  // the pinned staging buffer may still be read by the previous upload
+  if (nb > c->info_cap) {
+    int rc;
+    if ((rc = grow(c, &c->d_blk_info, (size_t)nb))) return rc;
+    if (c->h_pin_info) (void)hipHostFree(c->h_pin_info);
+    c->h_pin_info = nullptr;
+    HIPCHK(c, hipHostMalloc((void**)&c->h_pin_info, nb * sizeof(longlong4), hipHostMallocDefault));
+    c->info_cap = nb;
+  }
+  // the pinned staging buffers may still be read by the previous upload
   HIPCHK(c, hipEventSynchronize(c->ev_map));
   memcpy(c->h_pin_prefix, pre.data(), (S + 1) * sizeof(int));
   memcpy(c->h_pin_off, set_off, (S + 1) * sizeof(int64_t));
+  for (int64_t s = 0; s < S; ++s)
+    for (int b = pre[s]; b < pre[s + 1]; ++b)
+      c->h_pin_info[b] = make_longlong4(s, set_off[s] + (int64_t)(b - pre[s]) * EVAL_BLOCK, set_off[s + 1], 0);
   HIPCHK(c, hipMemcpyAsync(c->d_blk_prefix, c->h_pin_prefix, (S + 1) * sizeof(int), hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemcpyAsync(c->d_set_off, c->h_pin_off, (S + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
+  if (nb > 0)
+    HIPCHK(c, hipMemcpyAsync(c->d_blk_info, c->h_pin_info, nb * sizeof(longlong4), hipMemcpyHostToDevice, st));
   HIPCHK(c, hipEventRecord(c->ev_map, st));
   c->last_off.assign(set_off, set_off + S + 1);
   c->last_off_stream = (void*)st;
@@ -824,6 +857,7 @@ int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_
   a.gamma = gamma;
   a.blk_prefix = c->d_blk_prefix;
   a.set_off = c->d_set_off;
+  a.blk_info = c->d_blk_info;
   a.setdata = c->d_setdata;
   a.tab = c->tab;
   a.central = c->d_central;

@@ -32,19 +32,24 @@ __device__ __forceinline__ double dpp(double old, double x) {
 // value of lane l-1 (lane 0 gets `old`): DPP wave_shr:1
 __device__ __forceinline__ double shr1(double old, double x) { return dpp<0x138, 0xf>(old, x); }
 
-struct Mob {  // Moebius map P -> (a P + b) / (c P + 1)
-  double a, b, c;
-  __device__ __forceinline__ static Mob identity() { return {1.0, 0.0, 0.0}; }
-  __device__ __forceinline__ static Mob combine(const Mob& L, const Mob& R) {  // R o L (L applied first)
+struct Mob {  // Moebius map P -> (a P + b) / (c P + d), entries >= 0
+  double a, b, c, d;
+  __device__ __forceinline__ static Mob identity() { return {1.0, 0.0, 0.0, 1.0}; }
+  // R o L (L applied first).  Nonnegative entries, no cancellation; rescaled by an
+  // exact power of two (the exponent of d) instead of a reciprocal per step.
+  __device__ __forceinline__ static Mob combine(const Mob& L, const Mob& R) {
     const double a = fma(R.a, L.a, R.b * L.c);
-    const double b = fma(R.a, L.b, R.b);
-    const double c = fma(R.c, L.a, L.c);
-    const double inv = lq_rcp(fma(R.c, L.b, 1.0));  // >= 1: entries stay bounded
-    return {a * inv, b * inv, c * inv};
+    const double b = fma(R.a, L.b, R.b * L.d);
+    const double c = fma(R.c, L.a, R.d * L.c);
+    const double d = fma(R.c, L.b, R.d * L.d);
+    const int e = -__builtin_amdgcn_frexp_exp(d);  // d > 0
+    return {__builtin_amdgcn_ldexp(a, e), __builtin_amdgcn_ldexp(b, e), __builtin_amdgcn_ldexp(c, e),
+            __builtin_amdgcn_ldexp(d, e)};
   }
   template <int CTRL, int ROW_MASK>
   __device__ __forceinline__ Mob from() const {  // DPP source, identity where no source lane
-    return {dpp<CTRL, ROW_MASK>(1.0, a), dpp<CTRL, ROW_MASK>(0.0, b), dpp<CTRL, ROW_MASK>(0.0, c)};
+    return {dpp<CTRL, ROW_MASK>(1.0, a), dpp<CTRL, ROW_MASK>(0.0, b), dpp<CTRL, ROW_MASK>(0.0, c),
+            dpp<CTRL, ROW_MASK>(1.0, d)};
   }
 };
 
@@ -149,14 +154,11 @@ __device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const Wave
   // ---- (1) Moebius scan, reversed layout (lane l = stage N-1-l)
   const bool fr = act && (s_rev & 1);
   Mob f = Mob::identity();
-  if (fr) {
-    const double iv = lq_rcp(c + d_rev);
-    f = {d_rev * iv, d_rev * c * iv, iv};
-  } else if (act) {
-    f = {1.0, c, 0.0};
-  }
+  if (fr) f = {d_rev, d_rev * c, 1.0, c + d_rev};  // P -> d (c+P) / (c+P+d)
+  else if (act) f = {1.0, c, 0.0, 1.0};            // P -> c + P
   const Mob T = wave_scan(f);
-  const double P_next = shr1(0.0, T.b);  // P_{t+1}
+  const double P_here = T.b * lq_rcp(T.d);          // P_t = T_t(0)
+  const double P_next = shr1(0.0, P_here);          // P_{t+1}
   // ---- (2) affine scan for p
   const double Q = c + P_next;
   const double iv = lq_rcp(Q + d_rev);

@@ -23,10 +23,10 @@ reference, AkshayThiru/incentive-design-mpc @ 2025-10-17):
 * ``PriceSolver._get_w_err``          price_solver.py:196-214
 * ``PriceSolver.get_w0_price0``       price_solver.py:272-285
 
-Parity pinning: the reference ships no golden data and its tests have no
-assertions; cvxpy/clarabel are not importable in this
-container (ModuleNotFoundError, not a permission denial).  The oracle is
-pinned by (1) exact optimality certificates (KKT residual <= 1e-30 relative
+PARITY UNPINNED by reference artifacts: the reference ships no golden data and
+its tests have no assertions; cvxpy/clarabel are not
+importable in this container (ModuleNotFoundError, not a permission denial),
+so no reference output can be produced here.  The oracle is instead pinned by (1) exact optimality certificates (KKT residual <= 1e-30 relative
 in 50-digit arithmetic, ``refine_mp``), (2) known-answer cases
 (lambda = 0, gamma = 0 => w = 0), and (3) the reference's own test
 invariants (test_lompc.py:54-55, 83-86).

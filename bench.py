@@ -55,7 +55,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from lompc_amd import LoMPC, LoMPCConstants, _lib
+    from lompc_amd import BatchPlan, LoMPC, LoMPCConstants, _lib
     from lompc_amd.dist import allreduce_set_results
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -90,22 +90,26 @@ def main():
                         out={}, M=M))
 
     # the two EV types are independent: one HIP stream each, so their
-    # latency-bound path/finalize kernels overlap; the caller's stream joins both
+    # latency-bound path/finalize kernels overlap; the caller's stream joins both.
+    # Each type's price iteration is ONE C-ABI call (BatchPlan -> lompc_run).
     main = torch.cuda.current_stream()
     for e in eng:
         e["stream"] = main if args.serial else torch.cuda.Stream()
+        e["plan"] = BatchPlan(e["lompc"], e["gamma"], e["off"], w_ref=e["wr"], gamma_ref=e["gref"], want_w=True,
+                              want_cost=True, want_set=True, stream=e["stream"])
+        e["out"] = e["plan"].out
+        e["lm_ptr"] = [e["lm"][k].data_ptr() for k in range(nsteps)]
+        e["lr_ptr"] = e["lr"].data_ptr()
 
     def step(k):
+        if world > 1:  # the previous step's all-reduce reads the output buffers
+            for e in eng:
+                e["stream"].wait_stream(main)
         for e in eng:
-            e["stream"].wait_stream(main)
-            with torch.cuda.stream(e["stream"]):
-                lo = e["lompc"]
-                lo.set_params(e["lm"][k], e["lr"], w_ref=e["wr"], gamma_ref=e["gref"], validate=False)
-                lo.solve_batch(e["gamma"], e["off"], want_w=True, want_cost=True, want_set=True,
-                               out=e["out"], check=False)
-        for e in eng:
-            main.wait_stream(e["stream"])
+            e["plan"].run(e["lm_ptr"][k], e["lr_ptr"])
         if world > 1:
+            for e in eng:
+                main.wait_stream(e["stream"])
             for e in eng:
                 allreduce_set_results(e["out"]["set_sum_w"], e["out"]["set_stats"])
 

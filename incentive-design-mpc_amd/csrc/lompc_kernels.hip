@@ -895,6 +895,14 @@ int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_
   return LOMPC_OK;
 }
 
+int lompc_run(lompc_ctx* c, int64_t S, const double* lmbd, const double* lmbd_r, const double* w_ref,
+              const double* gamma_ref, int64_t B, const double* gamma, const int64_t* set_offsets, double* w,
+              double* cost, double* w0, int8_t* status, double* set_sum_w, double* set_stats, void* stream) {
+  const int rc = lompc_set_params(c, S, lmbd, lmbd_r, w_ref, gamma_ref, stream);
+  if (rc) return rc;
+  return lompc_solve_batch(c, B, gamma, set_offsets, w, cost, w0, status, set_sum_w, set_stats, stream);
+}
+
 int lompc_last_status(lompc_ctx* c, void* stream, int64_t* n_repaired, int64_t* n_failed, int64_t* n_invalid) {
   if (!c) return LOMPC_ERR_INVALID_ARG;
   HIPCHK(c, hipSetDevice(c->device));

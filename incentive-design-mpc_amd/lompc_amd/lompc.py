@@ -315,3 +315,57 @@ class LoMPC:
                                                         int(bool(reset))))
             return ms.value, n.value
         return None
+
+
+class BatchPlan:
+    """Repeated batched solves over a fixed EV batch with one C-ABI call each.
+
+    Validates and allocates once (gamma, set_offsets, outputs, w_ref,
+    gamma_ref); ``run(lmbd, lmbd_r)`` then issues ``lompc_run`` (K1 path
+    kernel + K2 evaluation + K3 finalize) with cached pointers — the host cost
+    of one price iteration is a single ctypes call.  lmbd: contiguous fp64
+    device tensor (S, 3N); lmbd_r: (S,) on the same device.  No synchronisation;
+    call ``lompc.check_last()`` when the status is needed.
+    """
+
+    def __init__(self, lompc: "LoMPC", gamma, set_offsets, *, w_ref=None, gamma_ref=None, want_w=True,
+                 want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None):
+        torch = _torch()
+        self.lompc = lompc
+        self.gamma = lompc._dev(gamma).reshape(-1)
+        B = self.gamma.numel()
+        self.off = np.ascontiguousarray(np.asarray(set_offsets, dtype=np.int64))
+        S = self.off.shape[0] - 1
+        if S < 1 or self.off[0] != 0 or self.off[-1] != B or np.any(np.diff(self.off) < 0):
+            raise ValueError("set_offsets must be non-decreasing from 0 to B")
+        if bool((self.gamma > lompc.y_max).any()):
+            raise AssertionError("gamma <= y_max required")
+        if bool(torch.logical_not(self.gamma >= 0).any()):
+            raise ValueError("Parameter value must be nonnegative.")
+        self.S, self.B, N = S, B, lompc.N
+        dev = f"cuda:{lompc.device}"
+        self.w_ref = None if w_ref is None else lompc._dev(w_ref).reshape(S, N)
+        self.gamma_ref = None if gamma_ref is None else lompc._dev(gamma_ref).reshape(S)
+        e = lambda shape, dt=torch.float64: torch.empty(shape, dtype=dt, device=dev)
+        self.out = {
+            "w": e((B, N)) if want_w else None,
+            "cost": e((B,)) if want_cost else None,
+            "w0": e((B,)) if want_w0 else None,
+            "status": e((B,), torch.int8) if want_status else None,
+            "set_sum_w": e((S, N)) if want_set else None,
+            "set_stats": e((S, _lib.LOMPC_SET_STATS)) if want_set else None,
+        }
+        self._stream = (stream if stream is not None else torch.cuda.current_stream(lompc.device)).cuda_stream
+        self._args = [_ptr(self.w_ref), _ptr(self.gamma_ref), B, _ptr(self.gamma), self.off.ctypes.data] + \
+            [_ptr(self.out[k]) for k in ("w", "cost", "w0", "status", "set_sum_w", "set_stats")] + [self._stream]
+
+    def run(self, lmbd, lmbd_r) -> dict:
+        """lmbd / lmbd_r: device tensors, or raw device pointers (int)."""
+        lo = self.lompc
+        pl = lmbd if isinstance(lmbd, int) else lmbd.data_ptr()
+        pr = lmbd_r if isinstance(lmbd_r, int) else lmbd_r.data_ptr()
+        rc = lo._lib.lompc_run(lo._ctx, self.S, pl, pr, *self._args)
+        if rc:
+            lo._check_rc(rc)
+        lo.S = self.S
+        return self.out

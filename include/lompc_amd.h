@@ -111,6 +111,14 @@ int lompc_solve_batch(lompc_ctx* ctx, int64_t B, const double* gamma,
                       double* w0, int8_t* status, double* set_sum_w,
                       double* set_stats, void* stream);
 
+/* lompc_set_params followed by lompc_solve_batch in ONE call (one host round
+ * trip; what a batched price iteration issues).  Arguments as in the two calls. */
+int lompc_run(lompc_ctx* ctx, int64_t S, const double* lmbd, const double* lmbd_r,
+              const double* w_ref, const double* gamma_ref, int64_t B,
+              const double* gamma, const int64_t* set_offsets, double* w,
+              double* cost, double* w0, int8_t* status, double* set_sum_w,
+              double* set_stats, void* stream);
+
 /* Synchronous single-QP convenience entry with host buffers.
  * Replaces LoMPC.solve_lompc (lompc.py:137-156) one-for-one:
  *   lmbd host [3N], lmbd_r, gamma -> w host [N], *cost. */

@@ -22,6 +22,7 @@ for s in $STEPS; do
     testsall) run pytest_gpu_all 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
     benchdirect) run bench_direct 600 python bench.py --mode direct --no-cpu-baseline ;;
+    sweep) run sweep 600 python scripts/sweep_eval.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     *) echo "unknown step $s" ;;
   esac

@@ -174,28 +174,31 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const
     if (a.w0) a.w0[i] = tile[lane * TS + 0];
     if (a.status) a.status[i] = !valid ? LOMPC_QP_INVALID : (ok ? LOMPC_QP_OK : LOMPC_QP_FAILED);
   }
-  // per-workgroup partials: column sums over the certified rows (max for the error)
+  // per-workgroup partials: column sums over the certified rows (max for the error);
+  // lanes l and l+32 each sum half of the rows of column l, then combine
   double* part = a.partial + (size_t)b * (N + NPX);
-  for (int c = lane; c < TS; c += EVAL_BLOCK) {
+  const int half = lane >> 5;
+  for (int c0 = 0; c0 < TS; c0 += 32) {
+    const int c = c0 + (lane & 31);
     const bool is_max = (c == N + PX_MAX_ERR);
-    double acc[8];
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (c < TS) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] = 0.0;
-#pragma unroll
-    for (int r = 0; r < EVAL_BLOCK; ++r) {
-      const double v = ((okm >> r) & 1ull) ? tile[r * TS + c] : 0.0;
-      acc[r & 7] = is_max ? fmax(acc[r & 7], v) : acc[r & 7] + v;
+      for (int rr = 0; rr < EVAL_BLOCK / 2; ++rr) {
+        const int r = half * (EVAL_BLOCK / 2) + rr;
+        const double v = ((okm >> r) & 1ull) ? tile[r * TS + c] : 0.0;
+        acc[rr & 3] = is_max ? fmax(acc[rr & 3], v) : acc[rr & 3] + v;
+      }
     }
-#pragma unroll
-    for (int u = 4; u >= 1; u >>= 1)
-#pragma unroll
-      for (int k = 0; k < u; ++k) acc[k] = is_max ? fmax(acc[k], acc[k + u]) : acc[k] + acc[k + u];
-    part[c] = acc[0];
+    double v = is_max ? fmax(fmax(acc[0], acc[1]), fmax(acc[2], acc[3])) : (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    const double o2 = __shfl_xor(v, 32, 64);
+    v = is_max ? fmax(v, o2) : v + o2;
+    if (half == 0 && c < TS) part[c] = v;
   }
   if (lane == 0) {
     part[N + PX_N_OK] = (double)__popcll(okm);
     part[N + PX_N_REPAIRED] = 0.0;
-    part[N + PX_N_FAILED] = 0.0;
+    part[N + PX_N_FAILED] = (double)__popcll(fm);  // pending: re-solved in k_finalize
     part[N + PX_N_INVALID] = (double)__popcll(im);
   }
 }
@@ -422,7 +425,6 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_direct(QPConst q, KArgs a) {
 //     waves and the repair accumulators combine in LDS in a fixed order.
 __global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode, double* __restrict__ set_sum_w,
                                                    double* __restrict__ set_stats, double* __restrict__ stats_int) {
-  lq_tab_init(q);
   __shared__ double red[16][LOMPC_MAX_N + NPX + 1];
   __shared__ double rep[16][LOMPC_MAX_N + NPX + 1];
   const int s = blockIdx.x;
@@ -431,13 +433,39 @@ __global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode,
   const int N = q.N;
   const int W = N + NPX;
   const int b0 = a.blk_prefix[s], b1 = a.blk_prefix[s + 1];
-  // ---- (1) repair pass
-  int anyf = 0;
-  for (int b = b0 + tid; b < b1; b += 1024) anyf |= a.fail_cnt[b];
-  anyf = __syncthreads_or(anyf);
-  double acc_w = 0.0, acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
-  int nrep = 0, nfail = 0;
-  if (anyf) {
+  // ---- (1) reduction of the workgroup partials (their N_FAILED column = pending repairs)
+  for (int c = lane; c < W; c += 64) {
+    const bool is_max = (c == N + PX_MAX_ERR);
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    int b = b0 + wv;
+    for (; b + 48 < b1; b += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double v = a.partial[(size_t)(b + 16 * u) * W + c];
+        acc[u] = is_max ? fmax(acc[u], v) : acc[u] + v;
+      }
+    }
+    for (; b < b1; b += 16) {
+      const double v = a.partial[(size_t)b * W + c];
+      acc[0] = is_max ? fmax(acc[0], v) : acc[0] + v;
+    }
+    red[wv][c] = is_max ? fmax(fmax(acc[0], acc[1]), fmax(acc[2], acc[3])) : (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  }
+  __syncthreads();
+  if (tid < W) {
+    const int c = tid;
+    const bool is_max = (c == N + PX_MAX_ERR);
+    double acc = red[0][c];
+    for (int k = 1; k < 16; ++k) acc = is_max ? fmax(acc, red[k][c]) : acc + red[k][c];
+    red[0][c] = acc;
+  }
+  __syncthreads();
+  const bool pending = red[0][N + PX_N_FAILED] > 0.0;  // block-uniform
+  // ---- (2) repair: wave wv re-solves the listed EVs of workgroups b0+wv, b0+wv+16, ...
+  if (pending) {
+    lq_tab_init(q);
+    double acc_w = 0.0, acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
+    int nrep = 0, nfail = 0;
     const double* __restrict__ sd = a.setdata + (size_t)s * lq_sd(N);
     lqw::WaveSet ws;
     ws.load(sd, N);
@@ -473,45 +501,26 @@ __global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode,
         nfail += okk ? 0 : 1;
       }
     }
-  }
-  if (lane < N) rep[wv][lane] = acc_w;
-  if (lane == 0) {
-    rep[wv][N + PX_COST] = acc_cost;
-    rep[wv][N + PX_PRICE0] = acc_p0;
-    rep[wv][N + PX_MAX_ERR] = acc_err;
-    rep[wv][N + PX_N_OK] = (double)nrep;
-    rep[wv][N + PX_N_REPAIRED] = (double)nrep;
-    rep[wv][N + PX_N_FAILED] = (double)nfail;
-    rep[wv][N + PX_N_INVALID] = 0.0;
-  }
-  // ---- (2) reduction of the workgroup partials
-  for (int c = lane; c < W; c += 64) {
-    const bool is_max = (c == N + PX_MAX_ERR);
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    int b = b0 + wv;
-    for (; b + 48 < b1; b += 64) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const double v = a.partial[(size_t)(b + 16 * u) * W + c];
-        acc[u] = is_max ? fmax(acc[u], v) : acc[u] + v;
-      }
+    if (lane < N) rep[wv][lane] = acc_w;
+    if (lane == 0) {
+      rep[wv][N + PX_COST] = acc_cost;
+      rep[wv][N + PX_PRICE0] = acc_p0;
+      rep[wv][N + PX_MAX_ERR] = acc_err;
+      rep[wv][N + PX_N_OK] = (double)nrep;
+      rep[wv][N + PX_N_REPAIRED] = (double)nrep;
+      rep[wv][N + PX_N_FAILED] = (double)nfail;
+      rep[wv][N + PX_N_INVALID] = 0.0;
     }
-    for (; b < b1; b += 16) {
-      const double v = a.partial[(size_t)b * W + c];
-      acc[0] = is_max ? fmax(acc[0], v) : acc[0] + v;
+    __syncthreads();
+    if (tid < W) {
+      const int c = tid;
+      const bool is_max = (c == N + PX_MAX_ERR);
+      double acc = (c == N + PX_N_FAILED) ? 0.0 : red[0][c];  // pending -> replaced by real failures
+      for (int k = 0; k < 16; ++k) acc = is_max ? fmax(acc, rep[k][c]) : acc + rep[k][c];
+      red[0][c] = acc;
     }
-    red[wv][c] = is_max ? fmax(fmax(acc[0], acc[1]), fmax(acc[2], acc[3])) : (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    __syncthreads();
   }
-  __syncthreads();
-  if (tid < W) {
-    const int c = tid;
-    const bool is_max = (c == N + PX_MAX_ERR);
-    double acc = red[0][c];
-    for (int k = 1; k < 16; ++k) acc = is_max ? fmax(acc, red[k][c]) : acc + red[k][c];
-    for (int k = 0; k < 16; ++k) acc = is_max ? fmax(acc, rep[k][c]) : acc + rep[k][c];
-    red[0][c] = acc;
-  }
-  __syncthreads();
   if (tid < N && set_sum_w) set_sum_w[(size_t)s * N + tid] = red[0][tid];
   if (tid == 0) {
     double row[LOMPC_SET_STATS];

@@ -235,15 +235,25 @@ __global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __r
   } else {
     ws.d_nat = ws.e_nat = ws.d_rev = ws.e_rev = 0.0;
   }
+  const double wr_nat = (w_ref && lane < N) ? w_ref[(size_t)s * N + lane] : 0.0;
+  const double c0 = q.theta * q.w_max * wave_sum(l2);  // lompc.py:128
+  const double kappa = lr / q.delta;                    // price_solver.py:191
+  const double ee = ws.e_nat;
+  double Ywr;  // prefix sums of w_ref
+  {
+    lqw::Sums<1> y;
+    y.v[0] = wr_nat;
+    Ywr = lqw::wave_scan(y, N).v[0];
+  }
   if (cell == 0) {  // one block per set writes the derived set record
     const int SD = lq_sd(N);
     double* out = setdata + (size_t)s * SD;
     if (lane < N) {
       out[lane] = ws.d_nat;
       out[N + lane] = ws.e_nat;
-      out[2 * N + lane] = w_ref ? w_ref[(size_t)s * N + lane] : 0.0;
+      out[2 * N + lane] = wr_nat;
     }
-    const double s2 = wave_sum(l2);
+    const double s2 = c0 / (q.theta * q.w_max);
     if (lane == 0) {
       if (!(lr >= 0.0)) atomicOr(errflag, 1);
       out[3 * N + 0] = q.theta * q.w_max * s2;  // c0, lompc.py:128
@@ -314,10 +324,43 @@ __global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __r
       const double wz = fmin(fmax(fma(bv, best, av), bx.lo), bx.hi);
       const double res = lqw::wave_kkt_point(q, ws, best, sl, wz);
       if (!(res <= q.tol_cert)) break;  // coverage of the cell ends at gcur
+      // cost and err^2 are quadratics in gamma on the piece (w = a + b gamma):
+      // per-lane terms, two prefix sums (Ya, Yb) and six wave totals
+      const bool act = lane < N;
+      lqw::Sums<2> pf;
+      pf.v[0] = act ? av : 0.0;
+      pf.v[1] = act ? bv : 0.0;
+      pf = lqw::wave_scan(pf, N);
+      const double Ya = pf.v[0], Yb = pf.v[1];
+      const double Ea = Ya - Ywr, da = av - wr_nat;
+      const double dd = ws.d_nat, cc = q.c;
+      const double sg = (sl & 1) ? bx.slo : 0.0;  // PWL slope of a free coordinate
+      double icpt = 0.0;                          // PWL value at w = 0 of its linear piece
+      if (!q.ev_small) {
+        const double wm = fma(bv, 0.5 * (gcur + best), av);
+        const double tw = q.theta * q.w_max;
+        icpt = fma(-sg, wm, tw * tw * lq_pwl(wm * q.inv_wmax));
+      }
+      double t[6];
+      t[0] = fma(0.5 * cc, Ya * Ya, fma(av, fma(0.5 * dd, av, ee + sg), icpt));
+      t[1] = fma(cc, fma(Ya, Yb, -Ya), fma(bv, fma(dd, av, ee + sg), 0.0));
+      t[2] = fma(0.5 * cc, Yb * Yb, fma(-cc, Yb, 0.5 * dd * bv * bv));
+      t[3] = fma(Ea, Ea, kappa * da * da);
+      t[4] = 2.0 * fma(Ea, Yb, kappa * da * bv);
+      t[5] = fma(Yb, Yb, kappa * bv * bv);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) t[k] = act ? t[k] : 0.0;
+      lqw::wave_totals(t, N);
       const size_t pidx = cb * LQ_PPL + npc;
       if (lane < N) {
         reinterpret_cast<double2*>(tab.ab + pidx * (size_t)N * 2)[lane] = make_double2(av, bv);
         tab.st[pidx * LQ_STB + lane] = (uint8_t)sl;
+      }
+      if (lane < 6) {  // row: K0, K1, K2 (cost), F0, F1, F2 (err^2), -, -
+        double v = t[0];
+#pragma unroll
+        for (int k = 1; k < 6; ++k) v = lane == k ? t[k] : v;
+        tab.coef[pidx * 8 + lane] = lane == 0 ? v + c0 : v;
       }
       if (lane == 0) tab.gend[pidx] = best;
       ++npc;
@@ -351,6 +394,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a) {
 #pragma unroll
   for (int t = 0; t < NMAX; ++t) w[t] = 0.0;
   bool ok = false;
+  EVOut o{0.0, 0.0, 0.0};
   if (valid) {
     const double invh = (double)LQ_G / q.y_max;
     const int cell = min(LQ_G - 1, (int)(g * invh));
@@ -368,17 +412,21 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a) {
     }
     ok = (cnt > 0) && (g <= glast);  // inside a certified piece
     if (ok) {
-      const double2* row = reinterpret_cast<const double2*>(a.tab.ab + (cb * LQ_PPL + p) * (size_t)N * 2);
+      const size_t pidx = cb * LQ_PPL + p;
+      const double2* row = reinterpret_cast<const double2*>(a.tab.ab + pidx * (size_t)N * 2);
+      const double4 cf0 = *reinterpret_cast<const double4*>(a.tab.coef + pidx * 8);
+      const double2 cf1 = *reinterpret_cast<const double2*>(a.tab.coef + pidx * 8 + 4);
 #pragma unroll
       for (int t = 0; t < NMAX; ++t)
         if (t < N) {
           const double2 ab = row[t];
           w[t] = fmin(fmax(fma(ab.y, g, ab.x), 0.0), q.w_max);
         }
+      o.cost = fma(fma(cf0.z, g, cf0.y), g, cf0.x);
+      o.err = a.want_err ? sqrt(fmax(fma(fma(cf1.y, g, cf1.x), g, cf0.w), 0.0)) : 0.0;
+      o.price0 = lq_price0(q, sd, w[0]);
     }
   }
-  EVOut o{0.0, 0.0, 0.0};
-  if (ok) o = lq_outputs<NMAX>(q, N, sd, g, w, a.want_err != 0);
   ev_epilogue<NMAX>(q, N, a, b, start, end, valid, ok, w, o);
 }
 
@@ -550,7 +598,7 @@ struct lompc_ctx {
   // parameter sets
   int64_t S = 0, S_cap = 0;
   double* d_setdata = nullptr;
-  PathTable tab{nullptr, nullptr, nullptr, nullptr};
+  PathTable tab{nullptr, nullptr, nullptr, nullptr, nullptr};
   uint8_t* d_central = nullptr;
   int* d_errflag = nullptr;
   int params_mode = -1;
@@ -726,7 +774,7 @@ int lompc_destroy(lompc_ctx* c) {
   if (!c) return LOMPC_OK;
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
-  void* ptrs[] = {c->d_setdata, c->tab.cnt, c->tab.gend, c->tab.ab, c->tab.st, c->d_central, c->d_errflag,
+  void* ptrs[] = {c->d_setdata, c->tab.cnt, c->tab.gend, c->tab.ab, c->tab.coef, c->tab.st, c->d_central, c->d_errflag,
                   c->d_partial, c->d_fail_cnt, c->d_fail_lane, c->d_blk_prefix, c->d_set_off, c->d_blk_info, c->d_stats,
                   c->d_single, c->d_single_status};
   for (void* p : ptrs)
@@ -767,6 +815,7 @@ int lompc_set_params(lompc_ctx* c, int64_t S, const double* lmbd, const double* 
     const size_t cells = (size_t)S * LQ_G;
     if ((rc = grow(c, &c->d_setdata, (size_t)S * lq_sd(N))) || (rc = grow(c, &c->tab.cnt, cells)) ||
         (rc = grow(c, &c->tab.gend, cells * LQ_PPL)) || (rc = grow(c, &c->tab.ab, cells * LQ_PPL * (size_t)N * 2)) ||
+        (rc = grow(c, &c->tab.coef, cells * LQ_PPL * 8)) ||
         (rc = grow(c, &c->tab.st, cells * LQ_PPL * LQ_STB)) || (rc = grow(c, &c->d_central, (size_t)S * LQ_STB)))
       return rc;
     c->S_cap = S;

@@ -57,10 +57,15 @@ struct QPConst {
 __host__ __device__ inline int lq_sd(int N) { return 3 * N + 8; }
 
 // Path table (device pointers). Cell l of set s covers gamma in [l h, (l+1) h], h = y_max / LQ_G.
+// On a piece (one working set) everything the per-EV outputs need is polynomial in gamma:
+//   w_j(gamma)      = a_j + b_j gamma
+//   cost(gamma)     = K0 + K1 gamma + K2 gamma^2     (lompc.py:155, incl. c0)
+//   err(gamma)^2    = F0 + F1 gamma + F2 gamma^2     (A_bar error vs w_ref, price_solver.py:207)
 struct PathTable {
   int* cnt;          // [S][G]              pieces stored in the cell (0 = cell unsolved)
   double* gend;      // [S][G][PPL]         upper gamma of each piece
-  double* ab;        // [S][G][PPL][N][2]   w_j(gamma) = a_j + b_j gamma
+  double* ab;        // [S][G][PPL][N][2]   (a_j, b_j)
+  double* coef;      // [S][G][PPL][8]      K0, K1, K2, F0, F1, F2, -, -
   uint8_t* st;       // [S][G][PPL][STB]    working set of the piece (one byte per stage)
 };
 

@@ -81,16 +81,55 @@ struct Aff {  // y -> A y + B[k]
   }
 };
 
-// Inclusive prefix scan across the 64 lanes (lane order = application order).
+// Inclusive prefix scan across the lanes [0, n) (lane order = application order);
+// lanes >= n hold identities.  DPP row_shr 1/2/4/8 scans each 16-lane row, row_bcast
+// 15 and 31 carry across rows; steps that only serve lanes >= n are skipped (n is
+// wave-uniform).
 template <typename T>
-__device__ __forceinline__ T wave_scan(T x) {
+__device__ __forceinline__ T wave_scan(T x, int n = 64) {
   x = T::combine(x.template from<0x111, 0xf>(), x);  // row_shr:1
   x = T::combine(x.template from<0x112, 0xf>(), x);  // row_shr:2
   x = T::combine(x.template from<0x114, 0xf>(), x);  // row_shr:4
   x = T::combine(x.template from<0x118, 0xf>(), x);  // row_shr:8
-  x = T::combine(x.template from<0x142, 0xa>(), x);  // row_bcast:15 -> rows 1, 3
-  x = T::combine(x.template from<0x143, 0xc>(), x);  // row_bcast:31 -> rows 2, 3
+  if (n > 16) x = T::combine(x.template from<0x142, 0xa>(), x);  // row_bcast:15 -> rows 1, 3
+  if (n > 32) x = T::combine(x.template from<0x143, 0xc>(), x);  // row_bcast:31 -> rows 2, 3
   return x;
+}
+
+template <int K>
+struct Sums {  // K independent running sums
+  double v[K];
+  __device__ __forceinline__ static Sums combine(const Sums& L, const Sums& R) {
+    Sums r;
+#pragma unroll
+    for (int k = 0; k < K; ++k) r.v[k] = L.v[k] + R.v[k];
+    return r;
+  }
+  template <int CTRL, int ROW_MASK>
+  __device__ __forceinline__ Sums from() const {
+    Sums r;
+#pragma unroll
+    for (int k = 0; k < K; ++k) r.v[k] = dpp<CTRL, ROW_MASK>(0.0, v[k]);
+    return r;
+  }
+};
+
+__device__ __forceinline__ double readlane_d(double x, int lane) {
+  const long long xi = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_readlane((int)xi, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(xi >> 32), lane);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// totals over lanes [0, n) of K values (lanes >= n must hold 0), broadcast
+template <int K>
+__device__ __forceinline__ void wave_totals(double (&v)[K], int n) {
+  Sums<K> x;
+#pragma unroll
+  for (int k = 0; k < K; ++k) x.v[k] = v[k];
+  x = wave_scan(x, n);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = readlane_d(x.v[k], n - 1);
 }
 
 __device__ __forceinline__ double bperm(int src_lane, double x) {
@@ -156,7 +195,7 @@ __device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const Wave
   Mob f = Mob::identity();
   if (fr) f = {d_rev, d_rev * c, 1.0, c + d_rev};  // P -> d (c+P) / (c+P+d)
   else if (act) f = {1.0, c, 0.0, 1.0};            // P -> c + P
-  const Mob T = wave_scan(f);
+  const Mob T = wave_scan(f, N);
   const double P_here = T.b * lq_rcp(T.d);          // P_t = T_t(0)
   const double P_next = shr1(0.0, P_here);          // P_{t+1}
   // ---- (2) affine scan for p
@@ -178,7 +217,7 @@ __device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const Wave
       g.B[NB - 1] = -c;
     }
   }
-  const Aff<NB> Gp = wave_scan(g);
+  const Aff<NB> Gp = wave_scan(g, N);
   double p_next[NB];
 #pragma unroll
   for (int k = 0; k < NB; ++k) p_next[k] = shr1(0.0, Gp.B[k]);
@@ -206,7 +245,7 @@ __device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const Wave
 #pragma unroll
     for (int k = 0; k < NB; ++k) h.B[k] = kk[k];
   }
-  const Aff<NB> Y = wave_scan(h);
+  const Aff<NB> Y = wave_scan(h, N);
   StageSol<NB> out;
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
@@ -298,10 +337,10 @@ __device__ __forceinline__ double wave_kkt_point(const QPConst& q, const WaveSet
   const bool act = ws.lane < N;
   Aff<1> h = Aff<1>::identity();
   if (act) h.B[0] = w;
-  const double y = wave_scan(h).B[0];   // y_t = sum_{i<=t} w_i
+  const double y = wave_scan(h, N).B[0];   // y_t = sum_{i<=t} w_i
   Aff<1> z = Aff<1>::identity();
   if (act) z.B[0] = y;
-  const double Z = wave_scan(z).B[0];   // Z_t = sum_{i<=t} y_i
+  const double Z = wave_scan(z, N).B[0];   // Z_t = sum_{i<=t} y_i
   const double Zt = __shfl(Z, N - 1, 64);
   const double r = q.c * (Zt - Z + y - (double)(N - ws.lane) * gamma) + ws.d_nat * w + ws.e_nat;
   const double res = act ? lq_resid(q, lq_box(s), w, r) : 0.0;

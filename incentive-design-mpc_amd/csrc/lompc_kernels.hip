@@ -4,24 +4,29 @@
 // per EV from PriceSolver._get_w_err (price_solver.py:203-209) and
 // PriceSolver.get_w0_price0 (price_solver.py:280-283).
 //
-// Kernels (K1 at set_params time, K2 (or K2d) -> K3 per solve):
+// Kernels (one batched price iteration = lompc_run = K1 -> K2 -> K3 on one stream):
 //   K1  k_path      one wave per (parameter set, gamma cell). PATH mode: the exact
 //                   piecewise-affine solution path w*(gamma) on the cell [l h, (l+1) h]:
 //                   wave-parallel PDAS at the cell start, then parametric active-set
-//                   tracking (homotopy) to the cell end, pieces w = a + b gamma stored
-//                   with their working sets.  DIRECT mode: the central solution.
-//                   Every stored piece is KKT-certified at both ends of its gamma
-//                   interval; the KKT residual is convex in gamma along an affine piece,
-//                   so that certifies every gamma inside it.
-//   K2  k_eval      one EV per lane, one wave per workgroup (64 EVs of one set).
-//                   w = a + b gamma from the EV's (certified) piece, cost / w0 / price0 /
-//                   A_bar error.  Epilogue through an LDS tile: coalesced w stores and
-//                   deterministic per-workgroup column sums.  EVs whose gamma no
-//                   certified piece covers go to a per-workgroup repair list.
+//                   tracking (homotopy) to the cell end.  Pieces w = a + b gamma are
+//                   stored with their working sets and the quadratic-in-gamma
+//                   coefficients of the cost and of the squared A_bar error.  Every
+//                   stored piece is KKT-certified at both ends; the KKT residual is
+//                   convex in gamma along an affine piece, so that certifies every gamma
+//                   inside it.  DIRECT mode: the central solution.
+//   K2  k_eval      one EV per lane, one wave per workgroup (64 EVs of one set):
+//                   w = a + b gamma, cost / err / price0 from the EV's piece; EVs no
+//                   certified piece covers are re-solved in place by the whole wave
+//                   (wave_solve, certified).  LDS-tile epilogue: coalesced w stores and
+//                   deterministic per-workgroup column sums.
 //   K2d k_direct    DIRECT mode: every EV solved by its own lane (PDAS warm-started
-//                   from the central working set) and KKT-certified; same epilogue.
-//   K3  k_finalize  per set: re-solves the listed EVs with the whole wave (wave_solve,
-//                   certified), then the deterministic reduction of the partials.
+//                   from the central working set) and KKT-certified; same epilogue,
+//                   uncertified EVs listed for K3.
+//   K3  k_finalize  per set: (DIRECT mode) re-solves the listed EVs with the whole wave,
+//                   then the deterministic reduction of the workgroup partials.
+// Inter-workgroup handoffs go through kernel boundaries: an in-kernel release/acquire
+// handoff costs an L2 writeback / invalidate per wave on the 8-XCD part (measured
+// 2-5x slower, profiles/r01_v8).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -115,30 +120,36 @@ __device__ __forceinline__ EVOut wave_outputs(const QPConst& q, const double* __
   return o;
 }
 
-// Shared epilogue of K2 / K2d for one wave of EVs [start, start+64) of set s.
-// ok lanes carry a certified w[] and outputs; valid-but-not-ok lanes are listed
-// for the repair pass in k_finalize (their rows are rewritten there).
-template <int NMAX>
+// Shared epilogue of the per-EV kernels for one wave of EVs [start, start+64) of set s.
+// !INPLACE (K2d): ok lanes carry a certified w[] and outputs; valid-but-not-ok lanes
+//   are listed for the repair pass in k_finalize (their rows are rewritten there).
+// INPLACE (fused path kernel): repairs already happened in the block; every valid
+//   lane carries its final w[] (rep = repaired, ok = certified) and is summed.
+template <int NMAX, bool INPLACE = false>
 __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const KArgs& a, int b, int64_t start,
                                             int64_t end, bool valid, bool ok, const double (&w)[NMAX],
-                                            const EVOut& o) {
+                                            const EVOut& o, bool rep = false) {
   __shared__ double tile[EVAL_BLOCK * (NMAX + 3)];
   const int TS = N + 3;  // odd for even N: conflict-free row-per-lane ds_write_b64
   const int lane = threadIdx.x;
   const int64_t i = start + lane;
   const bool active = i < end;
   const double fill = valid ? 0.0 : NAN;
+  const bool row = INPLACE ? valid : ok;  // rows that carry a result
 #pragma unroll
   for (int t = 0; t < NMAX; ++t)
-    if (t < N) tile[lane * TS + t] = ok ? w[t] : fill;
-  tile[lane * TS + N] = ok ? o.cost : fill;
-  tile[lane * TS + N + 1] = ok ? o.price0 : 0.0;
-  tile[lane * TS + N + 2] = ok ? o.err : 0.0;
-  const unsigned long long okm = __ballot(ok);
+    if (t < N) tile[lane * TS + t] = row ? w[t] : fill;
+  tile[lane * TS + N] = row ? o.cost : fill;
+  tile[lane * TS + N + 1] = row ? o.price0 : 0.0;
+  tile[lane * TS + N + 2] = row ? o.err : 0.0;
+  const unsigned long long okm = __ballot(row);
   const unsigned long long fm = __ballot(valid && !ok);
   const unsigned long long im = __ballot(active && !valid);
-  if (valid && !ok) a.fail_lane[(size_t)b * EVAL_BLOCK + __popcll(fm & ((1ull << lane) - 1ull))] = (uint8_t)lane;
-  if (lane == 0) a.fail_cnt[b] = __popcll(fm);
+  const unsigned long long rm = INPLACE ? __ballot(valid && ok && rep) : 0ull;
+  if (!INPLACE) {
+    if (valid && !ok) a.fail_lane[(size_t)b * EVAL_BLOCK + __popcll(fm & ((1ull << lane) - 1ull))] = (uint8_t)lane;
+    if (lane == 0) a.fail_cnt[b] = __popcll(fm);
+  }
   __syncthreads();
   // coalesced stores (row-major w[B][N])
   const int nrow = (int)min((int64_t)EVAL_BLOCK, end - start);
@@ -172,7 +183,8 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const
   if (active) {
     if (a.cost) a.cost[i] = tile[lane * TS + N];
     if (a.w0) a.w0[i] = tile[lane * TS + 0];
-    if (a.status) a.status[i] = !valid ? LOMPC_QP_INVALID : (ok ? LOMPC_QP_OK : LOMPC_QP_FAILED);
+    if (a.status)
+      a.status[i] = !valid ? LOMPC_QP_INVALID : (ok ? ((INPLACE && rep) ? LOMPC_QP_REPAIRED : LOMPC_QP_OK) : LOMPC_QP_FAILED);
   }
   // per-workgroup partials: column sums over the certified rows (max for the error);
   // lanes l and l+32 each sum half of the rows of column l, then combine
@@ -196,24 +208,51 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const
     if (half == 0 && c < TS) part[c] = v;
   }
   if (lane == 0) {
-    part[N + PX_N_OK] = (double)__popcll(okm);
-    part[N + PX_N_REPAIRED] = 0.0;
-    part[N + PX_N_FAILED] = (double)__popcll(fm);  // pending: re-solved in k_finalize
+    part[N + PX_N_OK] = (double)__popcll(INPLACE ? (okm & ~fm) : okm);
+    part[N + PX_N_REPAIRED] = (double)__popcll(rm);
+    part[N + PX_N_FAILED] = (double)__popcll(fm);  // !INPLACE: pending, re-solved in k_finalize
     part[N + PX_N_INVALID] = (double)__popcll(im);
   }
 }
 
 // ------------------------------------------------------------------- K1
-__global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __restrict__ lmbd,
-                                             const double* __restrict__ lmbd_r, const double* __restrict__ w_ref,
-                                             const double* __restrict__ gamma_ref, double* __restrict__ setdata,
-                                             int mode, PathTable tab, uint8_t* __restrict__ central,
-                                             int* __restrict__ errflag) {
-  lq_tab_init(q);
+#ifdef LOMPC_K1_STATS
+__device__ long long g_k1_stats[8192 * 4];  // per cell: PDAS iterations, pieces, cycles solve, cycles tracking
+#endif
+
+// A cell's count is tagged with the parameter epoch (set_params call) that wrote it:
+// tab.cnt[cell] = epoch << 4 | pieces.  K2 treats a cell of another epoch as unsolved.
+__device__ __forceinline__ void publish_cell(int* cnt, int epoch, int npc) {
+  if (threadIdx.x == 0) *cnt = (epoch << 4) | npc;
+}
+__device__ __forceinline__ int cell_epoch(int v) { return v >> 4; }
+__device__ __forceinline__ int cell_pieces(int v) { return v & 15; }
+
+struct PathArgs {
+  int S, mode, epoch, pad;
+  const double* lmbd;
+  const double* lmbd_r;
+  const double* w_ref;
+  const double* gamma_ref;
+  double* setdata;
+  uint8_t* central;
+  int* errflag;
+};
+
+__device__ __forceinline__ void path_cell(const QPConst& q, const PathArgs& pa, const PathTable& tab, int blk) {
+  const double* __restrict__ lmbd = pa.lmbd;
+  const double* __restrict__ lmbd_r = pa.lmbd_r;
+  const double* __restrict__ w_ref = pa.w_ref;
+  const double* __restrict__ gamma_ref = pa.gamma_ref;
+  double* __restrict__ setdata = pa.setdata;
+  uint8_t* __restrict__ central = pa.central;
+  int* __restrict__ errflag = pa.errflag;
+  const int mode = pa.mode;
   const int lane = threadIdx.x;
   const int N = q.N;
-  const int s = (mode == LOMPC_MODE_PATH) ? (int)(blockIdx.x / LQ_G) : (int)blockIdx.x;
-  const int cell = (mode == LOMPC_MODE_PATH) ? (int)(blockIdx.x % LQ_G) : 0;
+  const bool path = mode != LOMPC_MODE_DIRECT;
+  const int s = path ? blk / LQ_G : blk;
+  const int cell = path ? blk % LQ_G : 0;
   const double* L = lmbd + (size_t)s * 3 * N;
   const double lr = lmbd_r[s];
   const double tt = q.theta * q.theta;
@@ -236,7 +275,7 @@ __global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __r
     ws.d_nat = ws.e_nat = ws.d_rev = ws.e_rev = 0.0;
   }
   const double wr_nat = (w_ref && lane < N) ? w_ref[(size_t)s * N + lane] : 0.0;
-  const double c0 = q.theta * q.w_max * wave_sum(l2);  // lompc.py:128
+  const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);  // lompc.py:128
   const double kappa = lr / q.delta;                    // price_solver.py:191
   const double ee = ws.e_nat;
   double Ywr;  // prefix sums of w_ref
@@ -266,7 +305,11 @@ __global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __r
       out[3 * N + 7] = w_ref ? 1.0 : 0.0;
     }
   }
-  if (mode != LOMPC_MODE_PATH) {
+  if (mode == LOMPC_MODE_PATH_REPAIR) {  // diagnostics: no table, every EV re-solved
+    publish_cell(tab.cnt + (size_t)s * LQ_G + cell, pa.epoch, 0);
+    return;
+  }
+  if (!path) {
     const double g = gamma_ref ? gamma_ref[s] : 0.5 * q.y_max;
     int sl = lane < N ? 1 : 0;
     double w = 0.0, r = 0.0;
@@ -280,8 +323,16 @@ __global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __r
   const size_t cb = (size_t)s * LQ_G + cell;
   int sl = lane < N ? 1 : 0;
   double w = 0.0, r = 0.0;
-  if (!lqw::wave_solve(q, ws, glo, sl, w, r)) {
-    if (lane == 0) tab.cnt[cb] = 0;  // EVs of this cell are solved in K2 by wave_solve
+#ifdef LOMPC_K1_STATS
+  const long long t0 = clock64();
+  int nit = 0;
+  const bool solved = lqw::wave_solve(q, ws, glo, sl, w, r, &nit);
+  const long long t1 = clock64();
+#else
+  const bool solved = lqw::wave_solve(q, ws, glo, sl, w, r);
+#endif
+  if (!solved) {
+    publish_cell(tab.cnt + cb, pa.epoch, 0);  // EVs of this cell are re-solved by wave_solve
     return;
   }
   // parametric active-set tracking of w*(gamma) on [glo, ghi]
@@ -308,7 +359,7 @@ __global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __r
     }
     double best = gc;
     int bj = lane;
-    lqw::wave_argmin(best, bj);
+    lqw::wave_argmin(best, bj, N);
     if (!(best < ghi)) {
       best = ghi;
       bj = -1;
@@ -371,15 +422,27 @@ __global__ __launch_bounds__(64) void k_path(QPConst q, int S, const double* __r
     gcur = best;
     last = bj;
   }
-  if (lane == 0) tab.cnt[cb] = npc;
+  publish_cell(tab.cnt + cb, pa.epoch, npc);
+#ifdef LOMPC_K1_STATS
+  const long long t2 = clock64();
+  if (lane == 0 && cb < 8192) {
+    g_k1_stats[cb * 4 + 0] = nit;
+    g_k1_stats[cb * 4 + 1] = npc;
+    g_k1_stats[cb * 4 + 2] = t1 - t0;
+    g_k1_stats[cb * 4 + 3] = t2 - t1;
+  }
+#endif
+}
+
+__global__ __launch_bounds__(64) void k_path(QPConst q, PathArgs pa, PathTable tab) {
+  lq_tab_init(q);
+  path_cell(q, pa, tab, (int)blockIdx.x);
 }
 
 // ------------------------------------------------------------------- K2
-// NT = NMAX: exact-horizon instantiation (all stage guards fold away);
-// NT = 0: any N <= NMAX with runtime guards.
 template <int NMAX, int NT>
-__global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a) {
-  const int b = blockIdx.x;
+__global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a, int epoch) {
+  const int b = (int)blockIdx.x;
   int s;
   int64_t start, end;
   block_set(a, b, s, start, end);
@@ -390,16 +453,18 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a) {
   const double* __restrict__ sd = a.setdata + (size_t)s * lq_sd(N);
   const double g = active ? a.gamma[i] : 0.0;
   const bool valid = active && (g >= 0.0) && (g <= q.y_max);
+  const double invh = (double)LQ_G / q.y_max;
+  const int cell = valid ? min(LQ_G - 1, (int)(g * invh)) : 0;
+  const size_t cb = (size_t)s * LQ_G + cell;
+  const int raw = a.tab.cnt[cb];
+  const bool ready = cell_epoch(raw) == epoch;  // written by this parameter epoch
+  const int cnt = (valid && ready) ? cell_pieces(raw) : 0;
   double w[NMAX];
 #pragma unroll
   for (int t = 0; t < NMAX; ++t) w[t] = 0.0;
   bool ok = false;
   EVOut o{0.0, 0.0, 0.0};
-  if (valid) {
-    const double invh = (double)LQ_G / q.y_max;
-    const int cell = min(LQ_G - 1, (int)(g * invh));
-    const size_t cb = (size_t)s * LQ_G + cell;
-    const int cnt = a.tab.cnt[cb];
+  if (cnt > 0) {
     double ge[LQ_PPL];
 #pragma unroll
     for (int pp = 0; pp < LQ_PPL; ++pp) ge[pp] = a.tab.gend[cb * LQ_PPL + pp];
@@ -410,7 +475,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a) {
       if (pp < cnt && g <= ge[pp]) p = pp;
       if (pp == cnt - 1) glast = ge[pp];
     }
-    ok = (cnt > 0) && (g <= glast);  // inside a certified piece
+    ok = g <= glast;  // inside a certified piece
     if (ok) {
       const size_t pidx = cb * LQ_PPL + p;
       const double2* row = reinterpret_cast<const double2*>(a.tab.ab + pidx * (size_t)N * 2);
@@ -427,7 +492,41 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a) {
       o.price0 = lq_price0(q, sd, w[0]);
     }
   }
-  ev_epilogue<NMAX>(q, N, a, b, start, end, valid, ok, w, o);
+  // ---- in-place repair: EVs no certified piece covers are solved by the whole wave
+  bool rep = false;
+  unsigned long long need = __ballot(valid && !ok);
+  if (need) {  // wave-uniform (one wave per workgroup)
+    lq_tab_init(q);
+    __shared__ double stage[64];
+    lqw::WaveSet ws;
+    ws.load(sd, N);
+    while (need) {
+      const int l = (int)__builtin_ctzll(need);
+      need &= need - 1ull;
+      const double gl = lqw::readlane_d(g, l);
+      const int rawl = __builtin_amdgcn_readlane(raw, l);
+      const int celll = __builtin_amdgcn_readlane(cell, l);
+      int sl = 1;
+      if (cell_epoch(rawl) == epoch && cell_pieces(rawl) > 0)
+        sl = a.tab.st[((size_t)s * LQ_G + celll) * LQ_PPL * LQ_STB + lane];
+      if (lane >= N) sl = 0;
+      double wl = 0.0, rl = 0.0;
+      const bool okk = lqw::wave_solve(q, ws, gl, sl, wl, rl);
+      const EVOut ol = wave_outputs(q, sd, gl, lane, wl, a.want_err != 0);
+      stage[lane] = wl;
+      __syncthreads();
+      if (lane == l) {
+#pragma unroll
+        for (int t = 0; t < NMAX; ++t)
+          if (t < N) w[t] = stage[t];
+        o = ol;
+        ok = okk;
+        rep = true;
+      }
+      __syncthreads();
+    }
+  }
+  ev_epilogue<NMAX, true>(q, N, a, b, start, end, valid, ok, w, o, rep);
 }
 
 // ------------------------------------------------------------------- K2d
@@ -508,7 +607,9 @@ __global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode,
     red[0][c] = acc;
   }
   __syncthreads();
-  const bool pending = red[0][N + PX_N_FAILED] > 0.0;  // block-uniform
+  // DIRECT mode: N_FAILED counts EVs listed for repair; PATH partials hold final counts
+  // (k_eval repairs in place)
+  const bool pending = mode == LOMPC_MODE_DIRECT && red[0][N + PX_N_FAILED] > 0.0;  // block-uniform
   // ---- (2) repair: wave wv re-solves the listed EVs of workgroups b0+wv, b0+wv+16, ...
   if (pending) {
     lq_tab_init(q);
@@ -523,14 +624,7 @@ __global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode,
         const int l = a.fail_lane[(size_t)b * EVAL_BLOCK + k];
         const int64_t i = a.set_off[s] + (int64_t)(b - b0) * EVAL_BLOCK + l;
         const double g = a.gamma[i];
-        int sl = 1;
-        if (mode == LOMPC_MODE_PATH) {
-          const int cell = min(LQ_G - 1, (int)(g * ((double)LQ_G / q.y_max)));
-          const size_t cb = (size_t)s * LQ_G + cell;
-          if (a.tab.cnt[cb] > 0) sl = a.tab.st[cb * LQ_PPL * LQ_STB + lane];
-        } else {
-          sl = a.central[(size_t)s * LQ_STB + lane];
-        }
+        int sl = a.central[(size_t)s * LQ_STB + lane];  // DIRECT mode only
         if (lane >= N) sl = 0;
         double wl = 0.0, rl = 0.0;
         const bool okk = lqw::wave_solve(q, ws, g, sl, wl, rl);
@@ -612,7 +706,8 @@ struct lompc_ctx {
   longlong4* d_blk_info = nullptr;
   longlong4* h_pin_info = nullptr;
   int64_t info_cap = 0;
-  double* d_stats = nullptr;  // [S][LOMPC_SET_STATS], always written by k_finalize
+  double* d_stats = nullptr;  // [S][LOMPC_SET_STATS], always written by the set reduction
+  int epoch = 0;  // parameter epoch of the path table (tags tab.cnt)
   int64_t stats_S = 0;
   int* h_pin_prefix = nullptr;
   int64_t* h_pin_off = nullptr;
@@ -694,6 +789,17 @@ static int pick_nmax(int N) {
 extern "C" {
 
 int lompc_abi_version(void) { return 1; }
+
+#ifdef LOMPC_K1_STATS
+// diagnostic build only (scripts/k1_stats.py): per-cell K1 counters of the last launch
+int lompc_debug_k1_stats(long long* host, int n) {
+  if (n > 8192 * 4) n = 8192 * 4;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_k1_stats), sizeof(long long) * n, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? LOMPC_OK
+             : LOMPC_ERR_HIP;
+}
+#endif
 
 const char* lompc_status_string(int status) {
   switch (status) {
@@ -790,7 +896,8 @@ int lompc_destroy(lompc_ctx* c) {
 
 int lompc_set_mode(lompc_ctx* c, int mode) {
   if (!c) return LOMPC_ERR_INVALID_ARG;
-  if (mode != LOMPC_MODE_PATH && mode != LOMPC_MODE_DIRECT) return fail_arg(c, "mode must be PATH or DIRECT");
+  if (mode != LOMPC_MODE_PATH && mode != LOMPC_MODE_DIRECT && mode != LOMPC_MODE_PATH_REPAIR)
+    return fail_arg(c, "mode must be PATH, DIRECT or PATH_REPAIR");
   c->mode = mode;
   return LOMPC_OK;
 }
@@ -802,13 +909,13 @@ int lompc_get_info(const lompc_ctx* c, int* N, int* ev_type) {
   return LOMPC_OK;
 }
 
-int lompc_set_params(lompc_ctx* c, int64_t S, const double* lmbd, const double* lmbd_r, const double* w_ref,
-                     const double* gamma_ref, void* stream) {
+// Validate / size the parameter-set buffers and open a new cell epoch.
+static int prepare_params(lompc_ctx* c, int64_t S, const double* lmbd, const double* lmbd_r, PathArgs* pa,
+                          const double* w_ref, const double* gamma_ref) {
   if (!c) return LOMPC_ERR_INVALID_ARG;
   if (S < 1 || !lmbd || !lmbd_r) return fail_arg(c, "set_params: S >= 1 and lmbd, lmbd_r required");
   if (S > (1 << 20)) return fail_arg(c, "set_params: too many parameter sets");
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t st = (hipStream_t)stream;
   const int N = c->N;
   if (S > c->S_cap) {
     int rc;
@@ -818,13 +925,34 @@ int lompc_set_params(lompc_ctx* c, int64_t S, const double* lmbd, const double* 
         (rc = grow(c, &c->tab.coef, cells * LQ_PPL * 8)) ||
         (rc = grow(c, &c->tab.st, cells * LQ_PPL * LQ_STB)) || (rc = grow(c, &c->d_central, (size_t)S * LQ_STB)))
       return rc;
+    HIPCHK(c, hipMemset(c->tab.cnt, 0, cells * sizeof(int)));  // epoch 0 = never published
     c->S_cap = S;
   }
   c->S = S;
   c->params_mode = c->mode;
-  const unsigned grid = (unsigned)(c->mode == LOMPC_MODE_PATH ? S * LQ_G : S);
-  hipLaunchKernelGGL(k_path, dim3(grid), dim3(64), 0, st, c->q, (int)S, lmbd, lmbd_r, w_ref, gamma_ref,
-                     c->d_setdata, c->mode, c->tab, c->d_central, c->d_errflag);
+  c->epoch = (c->epoch + 1) & 0x7ffffff;
+  if (c->epoch == 0) c->epoch = 1;
+  pa->S = (int)S;
+  pa->mode = c->mode;
+  pa->epoch = c->epoch;
+  pa->pad = 0;
+  pa->lmbd = lmbd;
+  pa->lmbd_r = lmbd_r;
+  pa->w_ref = w_ref;
+  pa->gamma_ref = gamma_ref;
+  pa->setdata = c->d_setdata;
+  pa->central = c->d_central;
+  pa->errflag = c->d_errflag;
+  return LOMPC_OK;
+}
+
+int lompc_set_params(lompc_ctx* c, int64_t S, const double* lmbd, const double* lmbd_r, const double* w_ref,
+                     const double* gamma_ref, void* stream) {
+  PathArgs pa{};
+  const int rc = prepare_params(c, S, lmbd, lmbd_r, &pa, w_ref, gamma_ref);
+  if (rc) return rc;
+  const unsigned grid = (unsigned)(c->mode != LOMPC_MODE_DIRECT ? S * LQ_G : S);
+  hipLaunchKernelGGL(k_path, dim3(grid), dim3(64), 0, (hipStream_t)stream, c->q, pa, c->tab);
   HIPCHK(c, hipGetLastError());
   return LOMPC_OK;
 }
@@ -881,7 +1009,7 @@ static int upload_block_map(lompc_ctx* c, const int64_t* set_off, int64_t S, int
   memcpy(c->h_pin_prefix, pre.data(), (S + 1) * sizeof(int));
   memcpy(c->h_pin_off, set_off, (S + 1) * sizeof(int64_t));
   for (int64_t s = 0; s < S; ++s)
-    for (int b = pre[s]; b < pre[s + 1]; ++b)
+    for (int b = pre[s]; b < pre[s + 1]; ++b)  // (set, first EV, end EV, -)
       c->h_pin_info[b] = make_longlong4(s, set_off[s] + (int64_t)(b - pre[s]) * EVAL_BLOCK, set_off[s + 1], 0);
   HIPCHK(c, hipMemcpyAsync(c->d_blk_prefix, c->h_pin_prefix, (S + 1) * sizeof(int), hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemcpyAsync(c->d_set_off, c->h_pin_off, (S + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
@@ -893,17 +1021,14 @@ static int upload_block_map(lompc_ctx* c, const int64_t* set_off, int64_t S, int
   return LOMPC_OK;
 }
 
-int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_t* set_offsets, double* w,
-                      double* cost, double* w0, int8_t* status, double* set_sum_w, double* set_stats,
-                      void* stream) {
-  if (!c) return LOMPC_ERR_INVALID_ARG;
-  if (c->S < 1) return fail_arg(c, "solve_batch: call lompc_set_params first");
+// Per-EV work of one batch: k_eval (PATH) or k_direct (DIRECT), then k_finalize.
+static int launch_batch(lompc_ctx* c, int64_t B, const double* gamma,
+                        const int64_t* set_offsets, double* w, double* cost, double* w0, int8_t* status,
+                        double* set_sum_w, double* set_stats, hipStream_t st) {
   if (B < 0 || !set_offsets) return fail_arg(c, "solve_batch: invalid batch");
   if (set_offsets[0] != 0 || set_offsets[c->S] != B)
     return fail_arg(c, "solve_batch: set_offsets must start at 0 and end at B");
   if (B > 0 && !gamma) return fail_arg(c, "solve_batch: gamma required");
-  HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t st = (hipStream_t)stream;
   int nblk = 0;
   int rc = upload_block_map(c, set_offsets, c->S, &nblk, st);
   if (rc) return rc;
@@ -926,31 +1051,41 @@ int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_
   a.partial = c->d_partial;
   a.fail_cnt = c->d_fail_cnt;
   a.fail_lane = c->d_fail_lane;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->prof) {
+    HIPCHK(c, hipEventCreate(&e0));
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipEventRecord(e0, st));
+  }
   if (nblk > 0) {
     dim3 grid((unsigned)nblk), block(EVAL_BLOCK);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (c->prof) {
-      HIPCHK(c, hipEventCreate(&e0));
-      HIPCHK(c, hipEventCreate(&e1));
-      HIPCHK(c, hipEventRecord(e0, st));
-    }
-    if (c->params_mode == LOMPC_MODE_PATH) {
-      DISPATCH_N(c->N, c->nmax, hipLaunchKernelGGL((k_eval<NM, NT>), grid, block, 0, st, c->q, a));
+    if (c->params_mode != LOMPC_MODE_DIRECT) {
+      const int ep = c->epoch;
+      DISPATCH_N(c->N, c->nmax, hipLaunchKernelGGL((k_eval<NM, NT>), grid, block, 0, st, c->q, a, ep));
     } else {
       DISPATCH_N(c->N, c->nmax, hipLaunchKernelGGL((k_direct<NM, NT>), grid, block, 0, st, c->q, a));
     }
     HIPCHK(c, hipGetLastError());
-    if (c->prof) {
-      HIPCHK(c, hipEventRecord(e1, st));
-      c->prof_ev.push_back(e0);
-      c->prof_ev.push_back(e1);
-    }
   }
   hipLaunchKernelGGL(k_finalize, dim3((unsigned)c->S), dim3(1024), 0, st, c->q, a, c->params_mode, set_sum_w,
                      set_stats, c->d_stats);
   HIPCHK(c, hipGetLastError());
+  if (c->prof) {
+    HIPCHK(c, hipEventRecord(e1, st));
+    c->prof_ev.push_back(e0);
+    c->prof_ev.push_back(e1);
+  }
   c->stats_S = c->S;
   return LOMPC_OK;
+}
+
+int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_t* set_offsets, double* w,
+                      double* cost, double* w0, int8_t* status, double* set_sum_w, double* set_stats,
+                      void* stream) {
+  if (!c) return LOMPC_ERR_INVALID_ARG;
+  if (c->S < 1) return fail_arg(c, "solve_batch: call lompc_set_params first");
+  HIPCHK(c, hipSetDevice(c->device));
+  return launch_batch(c, B, gamma, set_offsets, w, cost, w0, status, set_sum_w, set_stats, (hipStream_t)stream);
 }
 
 int lompc_run(lompc_ctx* c, int64_t S, const double* lmbd, const double* lmbd_r, const double* w_ref,

@@ -120,6 +120,20 @@ __device__ __forceinline__ int lq_move(const QPConst& q, int s, const Box& b, do
   const bool dn = fr ? (w < b.lo - q.ktol) : (v < b.slo - q.tol_switch);
   return s + (up ? 1 : 0) - (dn ? 1 : 0);
 }
+// PDAS move with jumps: a free coordinate whose value left its segment goes straight
+// to the knot that bounds the value's segment on the side it came from (the lower
+// knot when moving up, the upper knot when moving down); fixed ones move as lq_move.
+__device__ __forceinline__ int lq_move_jump(const QPConst& q, int s, const Box& b, double w, double r) {
+  if (!(s & 1)) return lq_move(q, s, b, w, r);
+  const bool up = w > b.hi + q.ktol, dn = w < b.lo - q.ktol;
+  if (!up && !dn) return s;
+  if (!(w > q.knots[0])) return 0;
+  if (!(w < q.w_max)) return 2 * q.m;
+  int seg = 0;
+#pragma unroll
+  for (int k = 1; k < LQ_MAXSEG; ++k) seg += (k < q.m && w > q.knots[k]) ? 1 : 0;
+  return up ? 2 * seg : 2 * seg + 2;
+}
 // distance of (w, -r) from the state's box, in gradient units (w outside -> +inf)
 __device__ __forceinline__ double lq_resid(const QPConst& q, const Box& b, double w, double r) {
   const double v = -r;

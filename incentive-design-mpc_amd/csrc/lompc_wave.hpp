@@ -18,6 +18,10 @@
 #pragma once
 #include "lompc_qp.hpp"
 
+#ifndef LQ_JUMP_IT
+#define LQ_JUMP_IT 3  // PDAS iterations that may jump across segments
+#endif
+
 namespace lqw {
 
 // ---- DPP helpers (64-bit values as two 32-bit lanes) -----------------------
@@ -35,16 +39,12 @@ __device__ __forceinline__ double shr1(double old, double x) { return dpp<0x138,
 struct Mob {  // Moebius map P -> (a P + b) / (c P + d), entries >= 0
   double a, b, c, d;
   __device__ __forceinline__ static Mob identity() { return {1.0, 0.0, 0.0, 1.0}; }
-  // R o L (L applied first).  Nonnegative entries, no cancellation; rescaled by an
-  // exact power of two (the exponent of d) instead of a reciprocal per step.
+  // R o L (L applied first).  Every per-stage map enters with d = 1 and entries
+  // >= 0, so a composition of k maps has d >= 1 and entries <= ~2^k max(c, 1):
+  // no cancellation and no rescaling needed for k <= 64.
   __device__ __forceinline__ static Mob combine(const Mob& L, const Mob& R) {
-    const double a = fma(R.a, L.a, R.b * L.c);
-    const double b = fma(R.a, L.b, R.b * L.d);
-    const double c = fma(R.c, L.a, R.d * L.c);
-    const double d = fma(R.c, L.b, R.d * L.d);
-    const int e = -__builtin_amdgcn_frexp_exp(d);  // d > 0
-    return {__builtin_amdgcn_ldexp(a, e), __builtin_amdgcn_ldexp(b, e), __builtin_amdgcn_ldexp(c, e),
-            __builtin_amdgcn_ldexp(d, e)};
+    return {fma(R.a, L.a, R.b * L.c), fma(R.a, L.b, R.b * L.d), fma(R.c, L.a, R.d * L.c),
+            fma(R.c, L.b, R.d * L.d)};
   }
   template <int CTRL, int ROW_MASK>
   __device__ __forceinline__ Mob from() const {  // DPP source, identity where no source lane
@@ -140,22 +140,34 @@ __device__ __forceinline__ double bperm(int src_lane, double x) {
 }
 __device__ __forceinline__ int bperm_i(int src_lane, int x) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, x); }
 
-// min over the wave of (value, lane); ties to the lowest index; result on every lane
-__device__ __forceinline__ void wave_argmin(double& v, int& idx) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double ov = __shfl_xor(v, off, 64);
-    const int oi = __shfl_xor(idx, off, 64);
-    if (ov < v || (ov == v && oi < idx)) {
-      v = ov;
-      idx = oi;
-    }
-  }
+struct MinV {
+  double v;
+  __device__ __forceinline__ static MinV combine(const MinV& L, const MinV& R) { return {fmin(L.v, R.v)}; }
+  template <int CTRL, int ROW_MASK>
+  __device__ __forceinline__ MinV from() const { return {dpp<CTRL, ROW_MASK>(INFINITY, v)}; }
+};
+struct MaxV {
+  double v;
+  __device__ __forceinline__ static MaxV combine(const MaxV& L, const MaxV& R) { return {fmax(L.v, R.v)}; }
+  template <int CTRL, int ROW_MASK>
+  __device__ __forceinline__ MaxV from() const { return {dpp<CTRL, ROW_MASK>(-INFINITY, v)}; }
+};
+
+// min over lanes [0, n) of v and the lowest lane holding it; result on every lane.
+// DPP prefix scan (lane n-1 = the min) + ballot, no LDS round trips.
+__device__ __forceinline__ void wave_argmin(double& v, int& idx, int n) {
+  const double m = readlane_d(wave_scan(MinV{v}, n).v, n - 1);
+  const unsigned long long hit = __ballot(v == m) & (n >= 64 ? ~0ull : ((1ull << n) - 1));
+  idx = hit ? (int)__builtin_ctzll(hit) : 0;
+  v = m;
 }
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
-  return v;
+// max over lanes [0, n), on every lane
+__device__ __forceinline__ double wave_max(double v, int n) { return readlane_d(wave_scan(MaxV{v}, n).v, n - 1); }
+// sum over lanes [0, n), on every lane
+__device__ __forceinline__ double wave_sum(double v, int n) {
+  Sums<1> x;
+  x.v[0] = v;
+  return readlane_d(wave_scan(x, n).v[0], n - 1);
 }
 
 // Per-set stage data of one wave: lane t holds stage t (natural) and stage N-1-t (reversed).
@@ -193,8 +205,12 @@ __device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const Wave
   // ---- (1) Moebius scan, reversed layout (lane l = stage N-1-l)
   const bool fr = act && (s_rev & 1);
   Mob f = Mob::identity();
-  if (fr) f = {d_rev, d_rev * c, 1.0, c + d_rev};  // P -> d (c+P) / (c+P+d)
-  else if (act) f = {1.0, c, 0.0, 1.0};            // P -> c + P
+  if (fr) {  // P -> d (c+P) / (c+P+d), scaled to d-entry 1
+    const double u = lq_rcp(c + d_rev);
+    f = {d_rev * u, d_rev * c * u, u, 1.0};
+  } else if (act) {
+    f = {1.0, c, 0.0, 1.0};  // P -> c + P
+  }
   const Mob T = wave_scan(f, N);
   const double P_here = T.b * lq_rcp(T.d);          // P_t = T_t(0)
   const double P_next = shr1(0.0, P_here);          // P_{t+1}
@@ -262,16 +278,21 @@ __device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const Wave
 // Returns true on convergence; s, w, r then hold the final working set,
 // solution and multipliers.
 __device__ __forceinline__ bool wave_pdas(const QPConst& q, const WaveSet& ws, double gamma, int& s, double& w,
-                                          double& r, int max_it) {
+                                          double& r, int max_it, int* nit = nullptr) {
   for (int it = 0; it < max_it; ++it) {
     const StageSol<1> sol = solve_stage<1>(q, ws, gamma, s);
     w = sol.w[0];
     r = sol.r[0];
-    const int ns = ws.lane < ws.N ? lq_move(q, s, lq_box(s), w, r) : s;
+    const Box bx = lq_box(s);
+    const int ns = ws.lane < ws.N ? (it < LQ_JUMP_IT ? lq_move_jump(q, s, bx, w, r) : lq_move(q, s, bx, w, r)) : s;
     const bool changed = __any(ns != s);
     s = ns;
-    if (!changed) return true;
+    if (!changed) {
+      if (nit) *nit = it + 1;
+      return true;
+    }
   }
+  if (nit) *nit = max_it;
   return false;
 }
 
@@ -293,7 +314,7 @@ __device__ __forceinline__ bool wave_primal_as(const QPConst& q, const WaveSet& 
     }
     double amin = al;
     int j = ws.lane;
-    wave_argmin(amin, j);
+    wave_argmin(amin, j, ws.N);
     if (amin >= 1.0) {
       w = sol.w[0];
       r = sol.r[0];
@@ -307,7 +328,7 @@ __device__ __forceinline__ bool wave_primal_as(const QPConst& q, const WaveSet& 
       }
       double nv = -viol;
       int jv = ws.lane;
-      wave_argmin(nv, jv);
+      wave_argmin(nv, jv, ws.N);
       if (-nv <= q.tol_switch) return true;
       if (ws.lane == jv) s = vs;
     } else {
@@ -325,7 +346,7 @@ __device__ __forceinline__ bool wave_primal_as(const QPConst& q, const WaveSet& 
 // max KKT residual of (w, r) over the wave for the working set s
 __device__ __forceinline__ double wave_kkt(const QPConst& q, const WaveSet& ws, int s, double w, double r) {
   const double res = ws.lane < ws.N ? lq_resid(q, lq_box(s), w, r) : 0.0;
-  return wave_max(res);
+  return wave_max(res, ws.N);
 }
 
 // Max KKT residual at gamma of the point w (lane t = w_t) for working set s,
@@ -344,13 +365,13 @@ __device__ __forceinline__ double wave_kkt_point(const QPConst& q, const WaveSet
   const double Zt = __shfl(Z, N - 1, 64);
   const double r = q.c * (Zt - Z + y - (double)(N - ws.lane) * gamma) + ws.d_nat * w + ws.e_nat;
   const double res = act ? lq_resid(q, lq_box(s), w, r) : 0.0;
-  return wave_max(res);
+  return wave_max(res, N);
 }
 
 // Exact certified solve of one QP by the whole wave, PDAS from s, primal active set if needed.
 __device__ __forceinline__ bool wave_solve(const QPConst& q, const WaveSet& ws, double gamma, int& s, double& w,
-                                           double& r) {
-  bool ok = wave_pdas(q, ws, gamma, s, w, r, 4 * ws.N + 8);
+                                           double& r, int* nit = nullptr) {
+  bool ok = wave_pdas(q, ws, gamma, s, w, r, 4 * ws.N + 8, nit);
   if (ok) ok = wave_kkt(q, ws, s, w, r) <= q.tol_cert;
   if (!ok) {
     ok = wave_primal_as(q, ws, gamma, s, w, r, 16 * ws.N + 32);

@@ -25,6 +25,7 @@ LOMPC_EV_SMALL = 0
 LOMPC_EV_LARGE = 1
 LOMPC_MODE_PATH = 0
 LOMPC_MODE_DIRECT = 1
+LOMPC_MODE_PATH_REPAIR = 2
 
 LOMPC_QP_OK = 0
 LOMPC_QP_REPAIRED = 1

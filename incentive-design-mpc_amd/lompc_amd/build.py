@@ -29,17 +29,20 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(os.path.join(CSRC, d)) <= t for d in DEPS)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines: tuple = ()) -> str:
+    """Compile the extension; ``defines`` (e.g. ("LOMPC_K1_STATS",)) builds a diagnostic
+    variant into ``out`` (never the product library)."""
+    if not force and out == OUT and up_to_date():
         return OUT
-    tmp = OUT + ".tmp"
+    tmp = out + ".tmp"
     cmd = [_hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp]
+           "-Wno-unused-result"] + [f"-D{d}" for d in defines] + \
+        [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

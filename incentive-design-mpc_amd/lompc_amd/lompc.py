@@ -68,7 +68,7 @@ class LoMPC:
             N:      LoMPC horizon length.
             consts: LoMPC constants.
             device: HIP device index (default: torch's current device).
-            mode:   "path" (default) or "direct" — engine algorithm, see DESIGN.md.
+            mode:   "path" (default), "direct" or "path_repair" (diagnostics) — engine algorithm, see DESIGN.md.
         """
         # lompc.py:36-38
         assert (consts.y_max >= MIN_MAX_BAT_SOC) and (consts.y_max <= MAX_MAX_BAT_SOC)
@@ -187,7 +187,8 @@ class LoMPC:
 
     # ------------------------------------------------------------ batch API
     def set_mode(self, mode: str) -> None:
-        m = {"path": _lib.LOMPC_MODE_PATH, "direct": _lib.LOMPC_MODE_DIRECT}[mode]
+        m = {"path": _lib.LOMPC_MODE_PATH, "direct": _lib.LOMPC_MODE_DIRECT,
+             "path_repair": _lib.LOMPC_MODE_PATH_REPAIR}[mode]
         self._check_rc(self._lib.lompc_set_mode(self._ctx, m))
         self.mode = mode
 
@@ -321,11 +322,12 @@ class BatchPlan:
     """Repeated batched solves over a fixed EV batch with one C-ABI call each.
 
     Validates and allocates once (gamma, set_offsets, outputs, w_ref,
-    gamma_ref); ``run(lmbd, lmbd_r)`` then issues ``lompc_run`` (K1 path
-    kernel + K2 evaluation + K3 finalize) with cached pointers — the host cost
+    gamma_ref); ``run(lmbd, lmbd_r)`` then issues ``lompc_run`` with cached pointers — the host cost
     of one price iteration is a single ctypes call.  lmbd: contiguous fp64
     device tensor (S, 3N); lmbd_r: (S,) on the same device.  No synchronisation;
     call ``lompc.check_last()`` when the status is needed.
+    In PATH mode the call is ONE kernel launch (path cells, per-EV blocks and the
+    per-set reduction trees).
     """
 
     def __init__(self, lompc: "LoMPC", gamma, set_offsets, *, w_ref=None, gamma_ref=None, want_w=True,

@@ -43,6 +43,8 @@ extern "C" {
                                 KKT certificate and active-set repair (default)        */
 #define LOMPC_MODE_DIRECT 1  /* independent per-EV active-set solve, warm-started from the
                                 set's central solution                                  */
+#define LOMPC_MODE_PATH_REPAIR 2 /* diagnostics: PATH launch without the path table, so every
+                                    EV takes the in-place certified wave re-solve       */
 
 /* ---- per-EV status values written to ``status[B]`` */
 #define LOMPC_QP_OK        0 /* certified optimal (KKT residual <= tol)                 */
@@ -75,7 +77,7 @@ int lompc_create(int N, double delta, double theta, double y_max, double w_max,
 /* Release every device/host resource of the context. */
 int lompc_destroy(lompc_ctx* ctx);
 
-/* Select LOMPC_MODE_PATH (default) or LOMPC_MODE_DIRECT. */
+/* Select LOMPC_MODE_PATH (default), LOMPC_MODE_DIRECT or LOMPC_MODE_PATH_REPAIR. */
 int lompc_set_mode(lompc_ctx* ctx, int mode);
 
 /* Load S parameter sets and prepare them on device.

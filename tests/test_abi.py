@@ -51,7 +51,7 @@ def test_header_constants_match_python():
 
     src = open(HEADER).read()
     for name in ("LOMPC_OK", "LOMPC_ERR_INVALID_ARG", "LOMPC_ERR_NOT_CONVERGED", "LOMPC_QP_REPAIRED",
-                 "LOMPC_STAT_MAX_ERR", "LOMPC_SET_STATS", "LOMPC_MAX_N", "LOMPC_MODE_DIRECT"):
+                 "LOMPC_STAT_MAX_ERR", "LOMPC_SET_STATS", "LOMPC_MAX_N", "LOMPC_MODE_DIRECT", "LOMPC_MODE_PATH_REPAIR"):
         m = re.search(rf"#define {name}\s+(\d+)", src)
         assert m and int(m.group(1)) == getattr(_lib, name), name
 

@@ -12,10 +12,10 @@ reductions of price_solver.py:203-214; with N > 1 ranks the per-partition
 reductions are combined by one RCCL sum + one max all-reduce.  Weak scaling:
 262 144 EVs per GPU (config 3; at 8 GPUs this is config 4's 2 097 152).
 
-Rank 0 prints ONE JSON line.  ``roofline`` prices the dominant kernel — in
-PATH mode the single fused launch of a price iteration (k_fused: path cells,
-per-EV blocks, per-set reductions) — by its algorithmic bytes per QP (gamma in
-8 B, w out 8N B, cost out 8 B) over its HIP-event-timed launch duration; ``cpu_baseline`` times the C
+Rank 0 prints ONE JSON line.  ``roofline`` prices the per-EV kernel (k_eval in
+PATH mode, the only kernel whose work scales with the EV count) by its
+algorithmic bytes per QP (gamma in 8 B, w out 8N B, cost out 8 B) over its
+launch duration from HIP events attached to its dispatch; ``cpu_baseline`` times the C
 oracle (oracle/, dense active set) on a bounded sample of the same workload.
 """
 from __future__ import annotations
@@ -144,7 +144,7 @@ def main():
             rep, fail, inv = e["lompc"].check_last()
         assert fail == 0 and inv == 0
         repaired += rep
-    # dominant kernel (k_fused / k_direct) timing from HIP events on the launch stream
+    # per-EV kernel (k_eval / k_direct) timing: HIP events on its own dispatch (hipExtLaunchKernel)
     k_ms, k_n, k_qps = 0.0, 0, 0
     for e in eng:
         ms, n = e["lompc"].profile(read=True)
@@ -189,7 +189,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": None,
-            "kernel": "k_fused" if args.mode == "path" else "k_direct",
+            "kernel": "k_eval" if args.mode == "path" else "k_direct",
             "bytes_per_qp": bytes_per_qp,
             "qp_per_launch": qp_per_launch,
             "avg_launch_us": avg_launch_s * 1e6,

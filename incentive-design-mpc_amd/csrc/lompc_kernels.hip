@@ -25,8 +25,9 @@
 //   K3  k_finalize  per set: (DIRECT mode) re-solves the listed EVs with the whole wave,
 //                   then the deterministic reduction of the workgroup partials.
 // Inter-workgroup handoffs go through kernel boundaries: an in-kernel release/acquire
-// handoff costs an L2 writeback / invalidate per wave on the 8-XCD part (measured
-// 2-5x slower, profiles/r01_v8).
+// handoff costs an L2 writeback / invalidate per wave on the 8-XCD part (a fused
+// single-launch variant measured 2-5x slower; DESIGN.md, "Rejected designs").
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -719,7 +720,8 @@ struct lompc_ctx {
   int8_t* d_single_status = nullptr;
   // profiling
   bool prof = false;
-  std::vector<hipEvent_t> prof_ev;  // pairs
+  std::vector<hipEvent_t> prof_ev;    // pairs recorded since the last read
+  std::vector<hipEvent_t> prof_pool;  // recycled events (no creation inside timed loops)
   double prof_ms = 0.0;
   int64_t prof_n = 0;
   std::string err;
@@ -890,6 +892,7 @@ int lompc_destroy(lompc_ctx* c) {
   if (c->h_pin_info) (void)hipHostFree(c->h_pin_info);
   if (c->ev_map) (void)hipEventDestroy(c->ev_map);
   for (hipEvent_t ev : c->prof_ev) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : c->prof_pool) (void)hipEventDestroy(ev);
   delete c;
   return LOMPC_OK;
 }
@@ -1051,30 +1054,37 @@ static int launch_batch(lompc_ctx* c, int64_t B, const double* gamma,
   a.partial = c->d_partial;
   a.fail_cnt = c->d_fail_cnt;
   a.fail_lane = c->d_fail_lane;
+  // profiling: start/stop timestamps ride on the per-EV kernel's own dispatch
+  // (hipExtLaunchKernel), no marker packets between the kernels
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (c->prof) {
-    HIPCHK(c, hipEventCreate(&e0));
-    HIPCHK(c, hipEventCreate(&e1));
-    HIPCHK(c, hipEventRecord(e0, st));
+  if (c->prof && nblk > 0) {
+    for (hipEvent_t* e : {&e0, &e1}) {
+      if (!c->prof_pool.empty()) {
+        *e = c->prof_pool.back();
+        c->prof_pool.pop_back();
+      } else {
+        HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableSystemFence));
+      }
+    }
   }
   if (nblk > 0) {
     dim3 grid((unsigned)nblk), block(EVAL_BLOCK);
     if (c->params_mode != LOMPC_MODE_DIRECT) {
       const int ep = c->epoch;
-      DISPATCH_N(c->N, c->nmax, hipLaunchKernelGGL((k_eval<NM, NT>), grid, block, 0, st, c->q, a, ep));
+      DISPATCH_N(c->N, c->nmax,
+                 hipExtLaunchKernelGGL((k_eval<NM, NT>), grid, block, 0, st, e0, e1, 0, c->q, a, ep));
     } else {
-      DISPATCH_N(c->N, c->nmax, hipLaunchKernelGGL((k_direct<NM, NT>), grid, block, 0, st, c->q, a));
+      DISPATCH_N(c->N, c->nmax, hipExtLaunchKernelGGL((k_direct<NM, NT>), grid, block, 0, st, e0, e1, 0, c->q, a));
     }
     HIPCHK(c, hipGetLastError());
+    if (e0) {
+      c->prof_ev.push_back(e0);
+      c->prof_ev.push_back(e1);
+    }
   }
   hipLaunchKernelGGL(k_finalize, dim3((unsigned)c->S), dim3(1024), 0, st, c->q, a, c->params_mode, set_sum_w,
                      set_stats, c->d_stats);
   HIPCHK(c, hipGetLastError());
-  if (c->prof) {
-    HIPCHK(c, hipEventRecord(e1, st));
-    c->prof_ev.push_back(e0);
-    c->prof_ev.push_back(e1);
-  }
   c->stats_S = c->S;
   return LOMPC_OK;
 }
@@ -1162,6 +1172,12 @@ int lompc_solve_host(lompc_ctx* c, const double* lmbd, double lmbd_r, double gam
 int lompc_profile_enable(lompc_ctx* c, int enable) {
   if (!c) return LOMPC_ERR_INVALID_ARG;
   c->prof = enable != 0;
+  HIPCHK(c, hipSetDevice(c->device));
+  while (c->prof && c->prof_pool.size() < 512) {  // recorded pairs are recycled by lompc_profile_read
+    hipEvent_t e;  // timing only: no system-scope fence (an L2 writeback) per record
+    HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    c->prof_pool.push_back(e);
+  }
   return LOMPC_OK;
 }
 
@@ -1174,9 +1190,8 @@ int lompc_profile_read(lompc_ctx* c, double* total_ms, int64_t* launches, int re
     HIPCHK(c, hipEventElapsedTime(&ms, c->prof_ev[k], c->prof_ev[k + 1]));
     c->prof_ms += ms;
     c->prof_n += 1;
-    (void)hipEventDestroy(c->prof_ev[k]);
-    (void)hipEventDestroy(c->prof_ev[k + 1]);
   }
+  c->prof_pool.insert(c->prof_pool.end(), c->prof_ev.begin(), c->prof_ev.end());
   c->prof_ev.clear();
   if (total_ms) *total_ms = c->prof_ms;
   if (launches) *launches = c->prof_n;

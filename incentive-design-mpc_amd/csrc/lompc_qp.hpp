@@ -30,7 +30,9 @@
 
 #define LQ_MAXSEG 4                     // large EVs: 4 PWL segments (lompc.py:111)
 #define LQ_NSTATE (2 * LQ_MAXSEG + 1)   // 9 states
+#ifndef LQ_G
 #define LQ_G 64                         // path cells per parameter set (one wave each)
+#endif
 #define LQ_PPL 8                        // max affine pieces stored per cell
 #define LQ_STB 64                       // state bytes per stored working set (N <= 64)
 

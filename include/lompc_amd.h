@@ -132,10 +132,10 @@ int lompc_solve_host(lompc_ctx* ctx, const double* lmbd, double lmbd_r,
 int lompc_last_status(lompc_ctx* ctx, void* stream, int64_t* n_repaired,
                       int64_t* n_failed, int64_t* n_invalid);
 
-/* Profiling: when enabled, every lompc_solve_batch brackets its per-EV
- * evaluation kernel with HIP events on ``stream``; lompc_profile_read
- * synchronises and returns the summed milliseconds and launch count since
- * the last reset. */
+/* Profiling: when enabled, every lompc_solve_batch times its per-EV evaluation
+ * kernel with HIP events attached to that kernel's own dispatch on ``stream``
+ * (hipExtLaunchKernel start/stop events); lompc_profile_read synchronises and
+ * returns the summed milliseconds and launch count since the last reset. */
 int lompc_profile_enable(lompc_ctx* ctx, int enable);
 int lompc_profile_read(lompc_ctx* ctx, double* total_ms, int64_t* launches,
                        int reset);

@@ -25,6 +25,7 @@ for s in $STEPS; do
     sweep) run sweep 600 python scripts/sweep_eval.py ;;
     k1) run k1 300 python scripts/k1_stats.py ;;
     host) run host 300 python scripts/host_overhead.py ;;
+    fail) run fail 600 python scripts/find_failures.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     *) echo "unknown step $s" ;;
   esac

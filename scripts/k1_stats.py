@@ -28,7 +28,7 @@ lib.lompc_debug_k1_stats.restype = ctypes.c_int
 lib.lompc_debug_k1_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
 from lompc_amd import LoMPC, LoMPCConstants  # noqa: E402
 
-N, P, G = int(os.environ.get("K1_N", "24")), 12, 64
+N, P, G = int(os.environ.get("K1_N", "24")), 12, int(os.environ.get("K1_G", "64"))
 rng = np.random.default_rng(0)
 for name, c in [("small", LoMPCConstants(0.05, 10.0, 0.9, 0.25, "small")),
                 ("large", LoMPCConstants(0.025, 50.0, 0.9, 0.15, "large"))]:

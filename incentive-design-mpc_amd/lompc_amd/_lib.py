@@ -63,6 +63,8 @@ SIGNATURES = [
     ("lompc_status_string", ctypes.c_char_p, [_I]),
     ("lompc_last_error", ctypes.c_char_p, [_P]),
     ("lompc_abi_version", _I, []),
+    ("lompc_price_step", _I, [_I, _I, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P]),
+    ("lompc_lp_separable", _I, [_I, _I, _P, _P, _P, _P]),
 ]
 ABI_VERSION = 1
 

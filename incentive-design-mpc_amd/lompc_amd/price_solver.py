@@ -1,0 +1,383 @@
+"""CVXPY-free ``PriceSolver`` on the batched engine (chargingstation/price_solver.py:16-285).
+
+Same constructor, attributes and methods as the reference.  What runs where:
+
+* every LoMPC solve of a price iteration — the per-EV loop of ``_get_w_err``
+  (price_solver.py:203-209) AND the central solve at gamma_sc (:106, :132) — is
+  ONE ``lompc_run`` call: parameter set 0 holds this rank's EVs (fused sum of w,
+  max A_bar error), set 1 holds the single central QP (its w and cost come back
+  as set 1's sum of w and sum of cost);
+* the price-gradient step (:216-246) is ``lompc_price_step`` (exact non-negative
+  QP on the host, no CVXPY/Clarabel), the regularizer LP (:248-255) is
+  ``PriceRegularizer`` (closed-form separable LP);
+* ``get_w0_price0`` (:272-285) is one batched solve with fused price0 sums.
+
+The loop keeps the reference's numpy arrays and their aliasing
+(``lmbd_k = lmbd_k_new`` at :140 makes the two names one array, so from the
+second iteration on the price term of ``dual_cost_decrease_actual`` at :136 is
+zero) so ``solver_stats`` match the reference's entry by entry.
+
+Sharded mode (``group`` given): ``set_charge_levels`` receives this rank's EVs;
+the batch statistics (min / max / mean / count, price_solver.py:73-77) and the
+fused reductions are combined with torch.distributed (RCCL on ROCm); the price
+step runs redundantly on every rank with identical inputs.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from . import settings as _settings
+from .lompc import BatchPlan, LoMPC, LoMPCConstants, SolverError
+from .price_regularizer import PriceRegularizer
+from .settings import PRICE_SOLVER_EPS_REG, PRICE_SOLVER_EPS_TOL
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+class PriceSolver:
+    def __init__(self, N: int, consts: LoMPCConstants, price_type: str, device: int | None = None,
+                 mode: str | None = None, group=None) -> None:
+        """
+        Inputs:
+            N:          Horizon length.
+            consts:     LoMPC constants.
+            price_type: "linear" or "linear-convex".
+            device:     HIP device (default: torch's current device).
+            mode:       LoMPC engine mode ("path" default).
+            group:      torch.distributed process group when the EVs are sharded over ranks.
+        """
+        assert (price_type == "linear") or (price_type == "linear-convex")  # price_solver.py:24
+        self.lompc = LoMPC(N, consts, device=device, mode=mode)
+        self._set_constants(N, consts, price_type)
+        self.price_reg = PriceRegularizer(self.N, self.r)
+        self.group = group
+        self._lib = _lib.load()
+        torch = _torch()
+        dev = f"cuda:{self.lompc.device}"
+        self._dev = dev
+        self._lm2 = torch.zeros((2, 3 * N), dtype=torch.float64, device=dev)
+        self._lr2 = torch.zeros(2, dtype=torch.float64, device=dev)
+        self._wr2 = torch.zeros((2, N), dtype=torch.float64, device=dev)
+        self._h_sw = torch.zeros((2, N), dtype=torch.float64).pin_memory()
+        self._h_st = torch.zeros((2, _lib.LOMPC_SET_STATS), dtype=torch.float64).pin_memory()
+        self._plan = None
+        self._plan_w0 = None
+        self._A_bar_inv = None
+        self._kappa = None
+        self.n_batched_calls = 0
+
+    # ------------------------------------------------------------ price_solver.py
+    def _set_constants(self, N: int, consts: LoMPCConstants, price_type: str) -> None:
+        # price_solver.py:42-64
+        self.nEVs = None
+        self.N = N
+        if price_type == "linear":
+            self.r = 2 * self.N
+        else:
+            self.r = 3 * self.N
+        self.consts = consts
+        self.price_type = price_type
+        self.y0 = None
+        self.y0_rng = None
+        self.gamma_sc = None
+        self.prev_prices = np.zeros((self.r,))
+        self.A = self.lompc.get_input_mat()
+        self.eps_reg = PRICE_SOLVER_EPS_REG
+        self.eps_tol = PRICE_SOLVER_EPS_TOL
+        self.m = self.lompc.get_sc_modulus()
+
+    def _rank(self) -> int:
+        if self.group is None:
+            return 0
+        import torch.distributed as dist
+
+        return dist.get_rank(self.group)
+
+    def set_charge_levels(self, y0) -> None:
+        """price_solver.py:66-77.  y0: (nEVs,) ndarray or device tensor (this rank's shard
+        in sharded mode)."""
+        torch = _torch()
+        if isinstance(y0, torch.Tensor):
+            y0d = y0.to(device=self._dev, dtype=torch.float64).reshape(-1)
+            assert y0d.dim() == 1
+            if self.group is None:
+                assert bool(((y0d >= 0) & (y0d <= self.consts.y_max)).all())
+                n = int(y0d.numel())
+                if n == 0:
+                    raise ValueError("zero-size array to reduction operation maximum which has no identity")
+                stats = torch.stack([y0d.max(), y0d.min(), y0d.sum()]).cpu().numpy()
+                self.nEVs = n
+                y_hi, y_lo, y_mean = stats[0], stats[1], stats[2] / n
+            else:
+                y_hi, y_lo, y_mean = self._global_levels(y0d)
+            self.y0 = y0d
+            gamma = self.consts.y_max - y0d
+        else:
+            y0 = np.asarray(y0, dtype=np.float64)
+            assert all(y0 >= 0) and all(y0 <= self.consts.y_max)
+            assert len(y0.shape) == 1
+            if self.group is None:
+                self.nEVs = len(y0)
+                y_hi, y_lo, y_mean = np.max(y0), np.min(y0), np.mean(y0)
+            else:
+                y_hi, y_lo, y_mean = self._global_levels(torch.as_tensor(y0, device=self._dev))
+            self.y0 = y0
+            gamma = torch.as_tensor(self.consts.y_max - y0, device=self._dev)
+        self.y0_rng = (y_hi - y_lo) / 2  # = \bar{\Gamma}
+        self.gamma_sc = self.consts.y_max - (y_hi + y_lo) / 2
+        self.gamma_sm = self.consts.y_max - y_mean
+        self._build_plans(gamma)
+
+    def _global_levels(self, y0d):
+        """Global max / min / mean / count of a sharded y0 (one MAX + one SUM all-reduce)."""
+        torch = _torch()
+        import torch.distributed as dist
+
+        n = y0d.numel()
+        assert bool(((y0d >= 0) & (y0d <= self.consts.y_max)).all())
+        inf = float("inf")
+        mx = torch.tensor([y0d.max().item() if n else -inf, -(y0d.min().item()) if n else -inf],
+                          dtype=torch.float64, device=self._dev)
+        sm = torch.tensor([y0d.sum().item() if n else 0.0, float(n)], dtype=torch.float64, device=self._dev)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=self.group)
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM, group=self.group)
+        mx, sm = mx.cpu().numpy(), sm.cpu().numpy()
+        self.nEVs = int(sm[1])
+        return float(mx[0]), float(-mx[1]), float(sm[0] / sm[1])
+
+    def _build_plans(self, gamma) -> None:
+        """Batch layout of one price iteration: set 0 = this rank's EVs, set 1 = the central QP."""
+        torch = _torch()
+        B = int(gamma.numel())
+        central = 1 if self._rank() == 0 else 0
+        self._gam = torch.empty(B + central, dtype=torch.float64, device=self._dev)
+        self._gam[:B] = gamma
+        self._gcentral = None if not central else self._gam[B:]
+        if central:
+            self._gam[B] = float(self.gamma_sc)
+        off = np.array([0, B, B + central], dtype=np.int64)
+        self._plan = BatchPlan(self.lompc, self._gam, off, w_ref=self._wr2, want_w=False, want_cost=False,
+                               want_set=True)
+        self._plan_w0 = BatchPlan(self.lompc, self._gam[:B], np.array([0, B], dtype=np.int64), want_w=False,
+                                  want_cost=False, want_w0=True, want_set=True) if B else None
+        self._B = B
+
+    def compute_optimal_prices(self, w_ref: np.ndarray, lmbd_r: float) -> tuple[np.ndarray, dict]:
+        """
+        Inputs:
+            w_ref:  Reference w vector (team-optimal solution) from the BiMPC.
+            lmbd_r: Robustness price parameter.
+        Outputs:
+            lmbd:           Optimal unit price (incentive) vector.
+            solver_stats:   Additional solver info (price_solver.py:90-95).
+        """
+        PRINT_LEVEL = _settings.PRINT_LEVEL
+        w_ref = np.asarray(w_ref, dtype=np.float64)
+        # Convergence tolerance.
+        tol, w0_err_bound = self.get_robustness_bounds(lmbd_r)
+        # w-inner product metric.
+        A_bar, A_bar_inv = self._get_w_inner_product_metric(lmbd_r)
+
+        # Initialize price iterate from previous prices.
+        lmbd_k, lmbd_k_new = np.zeros((3 * self.N)), np.zeros((3 * self.N))
+        lmbd_k[: self.r] = self.prev_prices
+        phi_w_ref = self.lompc.phi(w_ref)
+        # one engine call: the batch error at lmbd_k and the central solve (price_solver.py:106)
+        errs, (w_k, dual_cost) = self._iterate(lmbd_k, lmbd_r, w_ref, A_bar)
+        dual_cost_decrease_ac = []
+        dual_cost_decrease_pred = []
+        # Gradient descent till convergence (price_solver.py:111-140):
+        for iter in range(_settings.MAX_PRICE_SOLVER_ITERATIONS):
+            w_err_max, _, w_avg_err = errs
+            if PRINT_LEVEL >= 2:
+                print(
+                    f"Iteration     : {iter:4d} || Error (max): {w_err_max:13.8f} | Tolerance: {tol:13.8f} "
+                    f"|| Error (avg): {w_avg_err:13.8f} | Tolerance: {tol:13.8f}",
+                    end="\r",
+                )
+                if iter % 10 == 0:
+                    print("")
+            if _settings.PRICE_SOLVER_TOL_TYPE == "max":
+                w_err = w_err_max
+            else:
+                w_err = w_avg_err
+            if w_err <= tol:
+                if (PRINT_LEVEL >= 2) and not (iter % 10 == 0):
+                    print("")
+                break
+            lmbd_k_new[: self.r], dual_cost_derease = self._price_gradient_descent_step(
+                A_bar_inv, w_ref, w_k, lmbd_k[: self.r]
+            )
+            # one engine call: central solve at lmbd_k_new (:132) + next iteration's batch error
+            errs, (w_k, dual_cost_new) = self._iterate(lmbd_k_new, lmbd_r, w_ref, A_bar)
+            dual_cost_decrease_ac.append(
+                dual_cost_new - dual_cost + (lmbd_k - lmbd_k_new) @ phi_w_ref
+            )
+            dual_cost_decrease_pred.append(dual_cost_derease)
+            dual_cost = dual_cost_new
+            lmbd_k = lmbd_k_new
+        # Regularize prices (price_solver.py:145-147).
+        price_pre = self.lompc.phi(w_k) @ lmbd_k
+        lmbd_k[: self.r] = self._regularize_prices(w_k, lmbd_k[: self.r])
+        price_new = self.lompc.phi(w_k) @ lmbd_k
+        if PRINT_LEVEL >= 1:
+            (w_err_max, w0_err, w_avg_err), (w_k_, _) = self._iterate(lmbd_k, lmbd_r, w_ref, A_bar)
+            if PRINT_LEVEL >= 2:
+                print(f"Regularization: Price  : {price_pre:9.3f} -> {price_new:9.3f}")
+                print(f"                w-error: {np.linalg.norm(w_k - w_k_):13.8f}")
+                print(f"w-error (max) : {w_err_max:13.8f} | Tolerance     : {tol:13.8f}")
+                print(f"w-error (avg) : {w_avg_err:13.8f} | Tolerance     : {tol:13.8f}")
+            if self._rank() == 0:
+                print(f"w0-error      : {w0_err:13.8f} | w0 error bound: {w0_err_bound:13.8f}")
+        # Update previous prices.
+        self.prev_prices = lmbd_k[: self.r]
+        solver_stats = {
+            "iter": iter,
+            "price_before_reg": price_pre,
+            "price_after_reg": price_new,
+            "dual_cost_decrease_actual": np.array(dual_cost_decrease_ac),
+            "dual_cost_decrease_predicted": np.array(dual_cost_decrease_pred),
+        }
+        return lmbd_k, solver_stats
+
+    def get_gamma_sc(self) -> float:
+        return self.gamma_sc
+
+    def get_gamma_sm(self) -> float:
+        return self.gamma_sm
+
+    def get_robustness_bounds(self, lmbd_r: float) -> tuple[float, float]:
+        """price_solver.py:182-186."""
+        kappa = lmbd_r / self.consts.delta + 1e-5
+        w_err_bound = np.sqrt(self.N) * self.y0_rng + self.eps_tol
+        w0_err_bound = w_err_bound * np.min((1, 1 / np.sqrt(kappa)))
+        return w_err_bound, w0_err_bound
+
+    def _get_w_inner_product_metric(self, lmbd_r: float) -> tuple[np.ndarray, np.ndarray]:
+        """price_solver.py:188-194."""
+        kappa = lmbd_r / self.consts.delta
+        A_bar = self.A.T @ self.A + kappa * np.eye(self.N)
+        A_bar_inv = np.linalg.inv(A_bar)
+        self._A_bar_inv, self._kappa = A_bar_inv, kappa
+        return A_bar, A_bar_inv
+
+    # ------------------------------------------------------------ engine calls
+    def _iterate(self, lmbd: np.ndarray, lmbd_r: float, w_ref: np.ndarray, A_bar: np.ndarray):
+        """ONE batched call at prices lmbd: returns
+        ((w_err_max, w0_err, w_avg_err) of price_solver.py:196-214, (w_central, cost_central))."""
+        torch = _torch()
+        if self._plan is None:
+            raise RuntimeError("set_charge_levels first")
+        lm = torch.from_numpy(np.ascontiguousarray(lmbd, dtype=np.float64))
+        self._lm2.copy_(lm.unsqueeze(0).expand(2, -1))
+        self._lr2.fill_(float(lmbd_r))
+        self._wr2.copy_(torch.from_numpy(w_ref).unsqueeze(0).expand(2, -1))
+        out = self._plan.run(self._lm2, self._lr2)
+        self.n_batched_calls += 1
+        sw, st = out["set_sum_w"], out["set_stats"]
+        if self.group is not None:
+            from .dist import allreduce_set_results
+
+            allreduce_set_results(sw, st, group=self.group)
+        self._h_sw.copy_(sw, non_blocking=True)
+        self._h_st.copy_(st, non_blocking=True)
+        torch.cuda.current_stream(self.lompc.device).synchronize()
+        sw, st = self._h_sw.numpy(), self._h_st.numpy()
+        self._check_stats(st)
+        # price_solver.py:210-214 from the fused sums
+        w_avg = sw[0] / self.nEVs
+        w_avg_err = np.sqrt((w_avg - w_ref) @ A_bar @ (w_avg - w_ref))
+        w0_err = np.abs(w_avg[0] - w_ref[0])
+        w_err_max = float(st[0, _lib.LOMPC_STAT_MAX_ERR])
+        w_c = sw[1].copy()
+        return (w_err_max, w0_err, w_avg_err), (w_c, float(st[1, _lib.LOMPC_STAT_SUM_COST]))
+
+    @staticmethod
+    def _check_stats(st: np.ndarray) -> None:
+        if np.any(st[:, _lib.LOMPC_STAT_N_INVALID] > 0):
+            raise AssertionError("gamma outside [0, y_max]")
+        if np.any(st[:, _lib.LOMPC_STAT_N_FAILED] > 0):
+            raise SolverError("LoMPC QPs without a certified optimum")
+
+    def _get_w_err(self, lmbd: np.ndarray, lmbd_r: float, w_ref: np.ndarray,
+                   A_bar: np.ndarray) -> tuple[float, float, float]:
+        """price_solver.py:196-214: (w_err_max, w0_err, w_avg_err) with the per-EV loop batched."""
+        kappa = lmbd_r / self.consts.delta
+        if not np.allclose(A_bar, self.A.T @ self.A + kappa * np.eye(self.N), rtol=1e-12, atol=1e-12):
+            raise ValueError("A_bar must be A'A + (lmbd_r/delta) I (price_solver.py:191-192)")
+        errs, _ = self._iterate(np.asarray(lmbd, dtype=np.float64), lmbd_r, np.asarray(w_ref, dtype=np.float64),
+                                A_bar)
+        return errs
+
+    def _kappa_of(self, A_bar_inv: np.ndarray) -> float:
+        if A_bar_inv is self._A_bar_inv:
+            return self._kappa
+        A_bar = np.linalg.inv(A_bar_inv)
+        kappa = A_bar[-1, -1] - 1.0
+        if not np.allclose(A_bar, self.A.T @ self.A + kappa * np.eye(self.N), rtol=1e-9, atol=1e-9):
+            raise ValueError("A_bar_inv must be (A'A + kappa I)^-1 (price_solver.py:191-193)")
+        return max(kappa, 0.0)
+
+    def _price_gradient_descent_step(self, A_bar_inv: np.ndarray, w_ref: np.ndarray, w: np.ndarray,
+                                     lmbd: np.ndarray) -> tuple[np.ndarray, float]:
+        """price_solver.py:216-246 -> (lmbd_next, dual_cost_decrease), exact on the host."""
+        w_ref = np.ascontiguousarray(w_ref, dtype=np.float64)
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        lm = np.ascontiguousarray(lmbd, dtype=np.float64)
+        if w.shape != (self.N,) or w_ref.shape != (self.N,) or lm.shape != (self.r,):
+            raise ValueError("price step: w, w_ref (N,) and lmbd (r,) required")
+        out = np.empty(self.r)
+        dec = ctypes.c_double(0.0)
+        iters = ctypes.c_int(0)
+        rc = self._lib.lompc_price_step(self.N, self.r, float(self.consts.theta), float(self.consts.w_max),
+                                        float(self.m), float(self._kappa_of(A_bar_inv)), float(self.eps_reg),
+                                        w_ref.ctypes.data, w.ctypes.data, lm.ctypes.data, out.ctypes.data,
+                                        ctypes.byref(dec), ctypes.byref(iters))
+        if rc == _lib.LOMPC_ERR_NOT_CONVERGED:
+            raise SolverError("price-gradient QP: no certified optimum")
+        if rc != _lib.LOMPC_OK:
+            raise ValueError(_lib.status_text(self._lib, None, rc))
+        self.last_step_iterations = iters.value
+        return out, dec.value
+
+    def _regularize_prices(self, w: np.ndarray, lmbd: np.ndarray) -> np.ndarray:
+        """price_solver.py:248-255."""
+        phi = self.lompc.phi(w)[: self.r]
+        Dphi = self.lompc.Dphi(w)[: self.r, :]
+        lmbd_reg = self.price_reg.solve_price_regularization(Dphi.T, Dphi.T @ lmbd, phi)
+        return lmbd_reg
+
+    def get_w0_price0(self, lmbd: np.ndarray, lmbd_r: float) -> tuple[np.ndarray, float]:
+        """price_solver.py:272-285 as one batched solve: (w0 of this rank's EVs, mean price0)."""
+        w0, price0_sum = self.get_w0_price0_device(lmbd, lmbd_r)
+        return (w0.cpu().numpy() if w0 is not None else np.zeros(0)), price0_sum / self.nEVs
+
+    def get_w0_price0_device(self, lmbd: np.ndarray, lmbd_r: float):
+        """(w0 device tensor of this rank's EVs, global sum of price0) — no host copy of w0."""
+        torch = _torch()
+        lmbd_ = np.zeros((3 * self.N))
+        lmbd_[: self.r] = lmbd
+        self._lm2[0].copy_(torch.from_numpy(lmbd_))
+        self._lr2.fill_(float(lmbd_r))
+        if self._plan_w0 is not None:
+            out = self._plan_w0.run(self._lm2[:1], self._lr2[:1])
+            st = out["set_stats"]
+            w0 = out["w0"]
+        else:
+            st = torch.zeros((1, _lib.LOMPC_SET_STATS), dtype=torch.float64, device=self._dev)
+            w0 = None
+        if self.group is not None:
+            import torch.distributed as dist
+
+            st = st.clone()
+            dist.all_reduce(st, op=dist.ReduceOp.SUM, group=self.group)
+        st = st.cpu().numpy()
+        self._check_stats(st)
+        return w0, float(st[0, _lib.LOMPC_STAT_SUM_PRICE0])

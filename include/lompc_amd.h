@@ -150,6 +150,39 @@ const char* lompc_last_error(const lompc_ctx* ctx);
 /* ABI version (bumped on any signature change). */
 int lompc_abi_version(void);
 
+/* ---------------------------------------------------------------------------
+ * Host-side solvers of the price iteration (no device, no context).  They run
+ * once per price iteration / per partition next to the convergence test, like
+ * the reference's CVXPY/Clarabel solves they replace.  Host buffers.
+ * ------------------------------------------------------------------------- */
+
+/* Price-gradient step.  Replaces PriceSolver._price_gradient_descent_step
+ * (price_solver.py:216-246) and its CVXPY problem (:257-270):
+ *   lmbd_next = argmin_{x >= 0} x'Px + q'x,
+ *   P = Dphi(w) A_bar^-1 Dphi(w)'/(2m) + eps_reg I,  q = -2 P lmbd - (phi(w) - phi(w_ref))
+ * with A_bar = A'A + kappa I (kappa = lmbd_r / delta, price_solver.py:188-194),
+ * phi/Dphi of lompc.py:172-187 truncated to the first r = 2N or 3N rows.
+ *   w_ref, w [N]; lmbd [r]  ->  lmbd_next [r]
+ *   *dual_cost_decrease = (lmbd'P lmbd + q'lmbd) - (x'Px + q'x)      (:236, :244-245)
+ *   *iterations = active-set iterations used (may be NULL)
+ * Exact (finite active-set method), KKT-certified; LOMPC_ERR_NOT_CONVERGED
+ * otherwise (cvxpy SolverError). */
+int lompc_price_step(int N, int r, double theta, double w_max, double m, double kappa,
+                     double eps_reg, const double* w_ref, const double* w, const double* lmbd,
+                     double* lmbd_next, double* dual_cost_decrease, int* iterations);
+
+/* Column-separable LP: min c'x s.t. A x = b, x >= 0, where every column of the
+ * row-major A [n_rows, n_cols] has at most one nonzero and c >= 0.
+ * Replaces PriceRegularizer.solve_price_regularization (price_regularizer.py:68-85),
+ * whose only caller passes A = Dphi(w)', b = Dphi(w)' lmbd, c = phi(w)
+ * (price_solver.py:248-255) — one nonzero per column (lompc.py:179-187).
+ * Each row is a one-row LP solved by its cheapest column per unit of b_j (ties:
+ * lowest column index; see DESIGN.md for the degenerate w_j = 0 case).
+ * LOMPC_ERR_UNSUPPORTED if A is not column-separable or c has a negative entry,
+ * LOMPC_ERR_NOT_CONVERGED if a row is infeasible. */
+int lompc_lp_separable(int n_rows, int n_cols, const double* A, const double* b,
+                       const double* c, double* x);
+
 #ifdef __cplusplus
 }
 #endif

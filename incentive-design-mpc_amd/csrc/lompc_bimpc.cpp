@@ -1,0 +1,541 @@
+// lompc_bimpc.cpp — host interior-point solver of the BiMPC team-optimal planner
+// (C-ABI in include/lompc_amd.h).
+//
+// Replaces the CVXPY/Clarabel conic solve of BiMPC.solve_bimpc (bimpc.py:267-292): ONE problem
+// per time step over P partitions (not per EV):
+//   variables  W_s, W_l in R^{P x N}, 0 <= W <= w_max            (bimpc.py:143-144, :182-183)
+//              u_g in R^N, 0 <= u_g <= u_g_max                     (:145, :185-186)
+//   cost       c_g sum_t u_g,t^1.7                                  (:220-221)
+//            + delta sum_{k, t} omega_kt ((A W_k)_t - g_k)^2        (:223-265; k = (type, partition))
+//   coupling   v = u_g - demand - theta_s Mp_s'W_s - theta_l Mp_l'W_l          (:189-194)
+//              -u_b_max + d_e e1 <= v <= u_b_max - d_e e1                       (:195-203)
+//              d_e <= x0 1 + A v <= x_max - d_e,  d_e = theta_s Mp_s'beta_s + theta_l Mp_l'beta_l  (:205-218)
+// The problem is smooth and strictly convex (u^1.7 and A'Omega A > 0 for every cost type with
+// omega > 0), so its optimum is unique; Clarabel's answer is that optimum up to its tolerance.
+//
+// Method: primal-dual interior point (Mehrotra predictor-corrector).  Box rows stay primal
+// feasible (slack = distance to the bound), the 4N coupling rows carry explicit slacks.  The
+// Newton matrix is
+//     M = blockdiag(H_k + D_k, D_u) + L'QL,   H_k = 2 delta A'Omega_k A,  Q = E'D_g E (N x N),
+// with L z = u_g + sum_k c_k W_k the aggregate storage input.  It is solved through the N x N
+// Schur complement (I + T Q) y = L Hb^-1 rhs, T = sum_k c_k^2 (H_k + D_k)^-1 + D_u^-1:
+// O(2P N^3) per iteration instead of O(((2P+1) N)^3).
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "lompc_dense.hpp"
+#include "../../include/lompc_amd.h"
+
+namespace {
+
+struct Bimpc {
+  int N = 0, P = 0, nb = 0, n = 0, mg = 0;
+  int cost_type = 0;
+  double delta = 0, c_g = 0, u_g_max = 0, u_b_max = 0, x_max = 0, exp_rate = 1;
+  double theta_s = 0, theta_l = 0, w_max_s = 0, w_max_l = 0;
+  // per-solve data
+  std::vector<double> omega;  // [nb][N] charging weights
+  std::vector<double> gk;     // [nb]    charging target
+  std::vector<double> ck;     // [nb]    coefficient of W_k in L z
+  std::vector<double> ub;     // [n]     upper bounds (lower bounds are 0)
+  std::vector<double> h;      // [4N]    coupling right-hand sides
+};
+
+// grad / Hessian pieces of f at z
+double f_value(const Bimpc& B, const double* z) {
+  const int N = B.N;
+  double f = 0.0;
+  for (int t = 0; t < N; ++t) f += B.c_g * std::pow(z[B.nb * N + t], 1.7);
+  double ch = 0.0;
+  for (int k = 0; k < B.nb; ++k) {
+    double y = 0.0;
+    for (int t = 0; t < N; ++t) {
+      y += z[k * N + t];
+      const double d = y - B.gk[k];
+      ch += B.omega[k * N + t] * d * d;
+    }
+  }
+  return f + B.delta * ch;
+}
+
+void f_grad(const Bimpc& B, const double* z, double* g) {
+  const int N = B.N;
+  std::vector<double> r(N);
+  for (int k = 0; k < B.nb; ++k) {
+    double y = 0.0;
+    for (int t = 0; t < N; ++t) {
+      y += z[k * N + t];
+      r[t] = 2.0 * B.delta * B.omega[k * N + t] * (y - B.gk[k]);
+    }
+    double s = 0.0;  // A' r = suffix sums
+    for (int t = N - 1; t >= 0; --t) {
+      s += r[t];
+      g[k * N + t] = s;
+    }
+  }
+  for (int t = 0; t < N; ++t) {
+    const double u = z[B.nb * N + t];
+    g[B.nb * N + t] = 1.7 * B.c_g * std::pow(u, 0.7);
+  }
+}
+
+// L z (N) and L' y (n)
+void mulL(const Bimpc& B, const double* z, double* y) {
+  const int N = B.N;
+  for (int t = 0; t < N; ++t) y[t] = z[B.nb * N + t];
+  for (int k = 0; k < B.nb; ++k)
+    if (B.ck[k] != 0.0)
+      for (int t = 0; t < N; ++t) y[t] += B.ck[k] * z[k * N + t];
+}
+void mulLt(const Bimpc& B, const double* y, double* z) {
+  const int N = B.N;
+  for (int k = 0; k < B.nb; ++k)
+    for (int t = 0; t < N; ++t) z[k * N + t] = B.ck[k] * y[t];
+  for (int t = 0; t < N; ++t) z[B.nb * N + t] = y[t];
+}
+// E y (4N) with E = [-I; I; -A; A];  E' v (N)
+void mulE(int N, const double* y, double* out) {
+  double c = 0.0;
+  for (int t = 0; t < N; ++t) {
+    c += y[t];
+    out[t] = -y[t];
+    out[N + t] = y[t];
+    out[2 * N + t] = -c;
+    out[3 * N + t] = c;
+  }
+}
+void mulEt(int N, const double* v, double* out) {
+  double s = 0.0;
+  for (int t = N - 1; t >= 0; --t) {
+    s += v[3 * N + t] - v[2 * N + t];
+    out[t] = v[N + t] - v[t] + s;
+  }
+}
+
+struct Newton {
+  int N = 0, nb = 0, n = 0;
+  std::vector<double> Hf;   // [nb][N*N] Cholesky factors of H_k + D_k
+  std::vector<double> Du;   // [N]
+  std::vector<double> Q;    // [N*N]
+  std::vector<double> K;    // [N*N] LU of I + T Q
+  std::vector<int> piv;
+  std::vector<double> ck;
+
+  // factor M for the current iterate; dk: [n] box barrier diagonal, dg: [4N] coupling D_g
+  bool factor(const Bimpc& B, const double* z, const double* dbox, const double* dg) {
+    N = B.N;
+    nb = B.nb;
+    n = B.n;
+    ck = B.ck;
+    Hf.assign((size_t)nb * N * N, 0.0);
+    std::vector<double> T((size_t)N * N, 0.0), X((size_t)N * N), col(N);
+    for (int k = 0; k < nb; ++k) {
+      double* H = &Hf[(size_t)k * N * N];
+      // 2 delta A'Omega A: (i,j) -> 2 delta sum_{t >= max(i,j)} omega_t
+      double s = 0.0;
+      std::vector<double> suf(N);
+      for (int t = N - 1; t >= 0; --t) {
+        s += B.omega[k * N + t];
+        suf[t] = 2.0 * B.delta * s;
+      }
+      for (int i = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j) H[i * N + j] = suf[std::max(i, j)];
+      for (int i = 0; i < N; ++i) H[i * N + i] += dbox[k * N + i];
+      // static regularisation (the EXP weights 5^(t-N+1) leave early steps with almost no
+      // curvature); iterative refinement against the exact matrix removes its bias
+      const double rho = 1e-11 * (1.0 + suf[0]);  // relative to the charging curvature, not the barrier
+      for (int i = 0; i < N; ++i) H[i * N + i] += rho;
+      if (!lqd::chol(H, N)) return false;
+      if (ck[k] != 0.0) {  // T += c_k^2 H_k^-1
+        for (int j = 0; j < N; ++j) {
+          std::fill(col.begin(), col.end(), 0.0);
+          col[j] = 1.0;
+          lqd::chol_solve(H, N, col.data());
+          for (int i = 0; i < N; ++i) T[i * N + j] += ck[k] * ck[k] * col[i];
+        }
+      }
+    }
+    Du.assign(N, 0.0);
+    for (int t = 0; t < N; ++t) {
+      const double u = z[nb * N + t];
+      Du[t] = 1.19 * B.c_g * std::pow(u, -0.3) + dbox[nb * N + t];  // f'' of c_g u^1.7
+      if (!(Du[t] > 0.0)) return false;
+      T[t * N + t] += 1.0 / Du[t];
+    }
+    // Q = E' D_g E = diag(d0 + d1) + A' diag(d2 + d3) A
+    Q.assign((size_t)N * N, 0.0);
+    {
+      double s = 0.0;
+      std::vector<double> suf(N);
+      for (int t = N - 1; t >= 0; --t) {
+        s += dg[2 * N + t] + dg[3 * N + t];
+        suf[t] = s;
+      }
+      for (int i = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j) Q[i * N + j] = suf[std::max(i, j)];
+      for (int i = 0; i < N; ++i) Q[i * N + i] += dg[i] + dg[N + i];
+    }
+    K.assign((size_t)N * N, 0.0);
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) {
+        double a = (i == j) ? 1.0 : 0.0;
+        for (int l = 0; l < N; ++l) a += T[i * N + l] * Q[l * N + j];
+        K[i * N + j] = a;
+      }
+    piv.assign(N, 0);
+    return lqd::lu(K.data(), N, piv.data());
+  }
+
+  void hb_solve(double* x) const {  // Hb^-1 in place
+    for (int k = 0; k < nb; ++k) lqd::chol_solve(&Hf[(size_t)k * N * N], N, x + (size_t)k * N);
+    for (int t = 0; t < N; ++t) x[nb * N + t] /= Du[t];
+  }
+
+  // y = M x with the exact (unregularised) Newton matrix
+  void apply(const Bimpc& B, const double* dbox, const double* x, double* y) const {
+    std::vector<double> r(N), Lx(N), Qy(N), tmp(n);
+    for (int k = 0; k < nb; ++k) {
+      double s = 0.0, acc = 0.0;
+      // 2 delta A'Omega A x_k: prefix sums then suffix sums
+      for (int t = 0; t < N; ++t) {
+        acc += x[k * N + t];
+        r[t] = 2.0 * B.delta * B.omega[k * N + t] * acc;
+      }
+      for (int t = N - 1; t >= 0; --t) {
+        s += r[t];
+        y[k * N + t] = s + dbox[k * N + t] * x[k * N + t];
+      }
+    }
+    for (int t = 0; t < N; ++t) y[nb * N + t] = Du[t] * x[nb * N + t];
+    mulL(B, x, Lx.data());
+    for (int i = 0; i < N; ++i) {
+      double a = 0.0;
+      for (int j = 0; j < N; ++j) a += Q[i * N + j] * Lx[j];
+      Qy[i] = a;
+    }
+    mulLt(B, Qy.data(), tmp.data());
+    for (int i = 0; i < n; ++i) y[i] += tmp[i];
+  }
+
+  // M dz = rhs: regularised Schur solve + iterative refinement against apply()
+  void solve(const Bimpc& B, const double* dbox, const double* rhs, double* dz) const {
+    // refinement stops as soon as it stops reducing the residual: in the nearly flat directions
+    // of the EXP weights it would diverge, and the regularised (proximal) step is kept there
+    solve_reg(B, rhs, dz);
+    std::vector<double> r(n), c(n), trial(n);
+    auto resid = [&](const double* x) {
+      apply(B, dbox, x, r.data());
+      double nr = 0.0;
+      for (int i = 0; i < n; ++i) {
+        r[i] = rhs[i] - r[i];
+        nr = std::max(nr, std::fabs(r[i]));
+      }
+      return nr;
+    };
+    double best = resid(dz);
+    for (int pass = 0; pass < 4 && best > 0.0; ++pass) {
+      solve_reg(B, r.data(), c.data());
+      for (int i = 0; i < n; ++i) trial[i] = dz[i] + c[i];
+      const double nr = resid(trial.data());
+      if (!(nr < 0.5 * best)) break;
+      best = nr;
+      std::copy(trial.begin(), trial.end(), dz);
+    }
+  }
+
+  void solve_reg(const Bimpc& B, const double* rhs, double* dz) const {
+    std::vector<double> t1(rhs, rhs + n), y(N), Qy(N), tmp(n);
+    hb_solve(t1.data());
+    mulL(B, t1.data(), y.data());
+    lqd::lu_solve(K.data(), N, piv.data(), y.data());
+    for (int i = 0; i < N; ++i) {
+      double a = 0.0;
+      for (int j = 0; j < N; ++j) a += Q[i * N + j] * y[j];
+      Qy[i] = a;
+    }
+    mulLt(B, Qy.data(), tmp.data());
+    hb_solve(tmp.data());
+    for (int i = 0; i < n; ++i) dz[i] = t1[i] - tmp[i];
+  }
+};
+
+double max_step(const std::vector<double>& s, const std::vector<double>& ds) {
+  double a = 1.0;
+  for (size_t i = 0; i < s.size(); ++i)
+    if (ds[i] < 0.0) a = std::min(a, -s[i] / ds[i]);
+  return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double c_g, double u_g_max,
+                      double u_b_max, double x_max, double exp_rate, double theta_s, double theta_l,
+                      double w_max_s, double w_max_l, const double* Mp_s, const double* Mp_l,
+                      const double* beta_s, const double* beta_l, const double* gamma_sm,
+                      const double* gamma_lm, double x0, const double* demand, double* w_hat_s,
+                      double* w_hat_l, double* u_g, double* duals, double* info) {
+  if (N < 1 || N > 4096 || P < 1 || !Mp_s || !Mp_l || !beta_s || !beta_l || !gamma_sm || !gamma_lm || !demand ||
+      !w_hat_s || !w_hat_l || !u_g)
+    return LOMPC_ERR_INVALID_ARG;
+  // bimpc.py:79-84
+  if (!(delta >= 0) || !(c_g >= 0) || !(u_g_max >= 0) || !(u_b_max >= 0) || !(x_max >= 0) || !(exp_rate >= 1))
+    return LOMPC_ERR_INVALID_ARG;
+  if (charging_cost_type < 0 || charging_cost_type > 2) return LOMPC_ERR_INVALID_ARG;
+  // strict interior of the boxes is required by the barrier
+  if (!(u_g_max > 0) || !(w_max_s > 0) || !(w_max_l > 0) || !(c_g > 0)) return LOMPC_ERR_UNSUPPORTED;
+  Bimpc B;
+  B.N = N;
+  B.P = P;
+  B.nb = 2 * P;
+  B.n = (2 * P + 1) * N;
+  B.mg = 4 * N;
+  B.cost_type = charging_cost_type;
+  B.delta = delta;
+  B.c_g = c_g;
+  B.u_g_max = u_g_max;
+  B.u_b_max = u_b_max;
+  B.x_max = x_max;
+  B.exp_rate = exp_rate;
+  B.theta_s = theta_s;
+  B.theta_l = theta_l;
+  B.w_max_s = w_max_s;
+  B.w_max_l = w_max_l;
+  const int nb = B.nb, n = B.n, mg = B.mg;
+  B.omega.assign((size_t)nb * N, 0.0);
+  B.gk.assign(nb, 0.0);
+  B.ck.assign(nb, 0.0);
+  B.ub.assign(n, 0.0);
+  for (int k = 0; k < nb; ++k) {
+    const bool small = k < P;
+    const int p = small ? k : k - P;
+    const double Mp = small ? Mp_s[p] : Mp_l[p];
+    const double th = small ? theta_s : theta_l;
+    B.ck[k] = -th * Mp;                      // bimpc.py:192-193
+    B.gk[k] = small ? gamma_sm[p] : gamma_lm[p];
+    for (int t = 0; t < N; ++t) {
+      double om;
+      if (charging_cost_type == 0)
+        om = th * th * Mp * Mp;  // weighted, :233-242: theta^2 ||Mp (A w - gamma)||^2
+      else if (charging_cost_type == 1)
+        om = 1.0;  // unweighted, :244-253
+      else
+        om = std::pow(exp_rate, (double)(t - N + 1));  // exp-unweighted, :255-265
+      B.omega[k * N + t] = om;
+      B.ub[k * N + t] = small ? w_max_s : w_max_l;
+    }
+  }
+  for (int t = 0; t < N; ++t) B.ub[nb * N + t] = u_g_max;
+  double d_e = 0.0;  // bimpc.py:177-178, :197-199
+  for (int p = 0; p < P; ++p) d_e += theta_s * Mp_s[p] * beta_s[p] + theta_l * Mp_l[p] * beta_l[p];
+  B.h.assign(mg, 0.0);
+  {
+    double Ad = 0.0;
+    for (int t = 0; t < N; ++t) {
+      Ad += demand[t];
+      const double e1 = t == 0 ? d_e : 0.0;
+      B.h[t] = u_b_max - e1 - demand[t];              // -(Lz)_t <= u_b_max - d_e e1 - dem   (:201)
+      B.h[N + t] = u_b_max - e1 + demand[t];          //  (Lz)_t <= u_b_max - d_e e1 + dem   (:203)
+      B.h[2 * N + t] = x0 - d_e - Ad;                 // -(A L z)_t <= x0 - d_e - (A dem)_t  (:216)
+      B.h[3 * N + t] = x_max - d_e - x0 + Ad;         //  (A L z)_t <= x_max - d_e - x0 + (A dem)_t (:218)
+    }
+  }
+  // ---- interior-point iterations
+  std::vector<double> z(n), llo(n), lhi(n), sg(mg), lg(mg);
+  for (int i = 0; i < n; ++i) z[i] = 0.5 * B.ub[i];
+  std::vector<double> grad(n), Lz(N), ELz(mg), rd(n), rg(mg), tmpN(N), tmpn(n), tmpm(mg);
+  f_grad(B, z.data(), grad.data());
+  double gmax = 0.0, hmax = 0.0;
+  for (int i = 0; i < n; ++i) gmax = std::max(gmax, std::fabs(grad[i]));
+  for (int i = 0; i < mg; ++i) hmax = std::max(hmax, std::fabs(B.h[i]));
+  double ubmax = 0.0;
+  for (int i = 0; i < n; ++i) ubmax = std::max(ubmax, B.ub[i]);
+  const double mu0 = 1.0 + 0.1 * gmax * ubmax;
+  mulL(B, z.data(), Lz.data());
+  mulE(N, Lz.data(), ELz.data());
+  for (int i = 0; i < n; ++i) {
+    llo[i] = mu0 / z[i];
+    lhi[i] = mu0 / (B.ub[i] - z[i]);
+  }
+  for (int i = 0; i < mg; ++i) {
+    sg[i] = std::max(B.h[i] - ELz[i], 0.1 * (1.0 + hmax));
+    lg[i] = mu0 / sg[i];
+  }
+  const int m_tot = 2 * n + mg;
+  Newton NW;
+  std::vector<double> dbox(n), dgv(mg), rhs(n), dz(n), dsg(mg), dlg(mg), dllo(n), dlhi(n);
+  std::vector<double> dz_a(n), dsg_a(mg), dlg_a(mg), dllo_a(n), dlhi_a(n);
+  std::vector<double> rclo(n), rchi(n), rcg(mg);
+  int it = 0, status = LOMPC_ERR_NOT_CONVERGED;
+  const bool trace = getenv("LOMPC_BIMPC_TRACE") != nullptr;
+  double pres = 0, dres = 0, gap = 0, fval = 0;
+  const int max_iter = (info && info[0] >= 1.0 && info[0] <= 1000.0) ? (int)info[0] : 200;  // info[0] in: cap
+  auto residuals = [&]() {
+    f_grad(B, z.data(), grad.data());
+    mulL(B, z.data(), Lz.data());
+    mulE(N, Lz.data(), ELz.data());
+    mulEt(N, lg.data(), tmpN.data());
+    mulLt(B, tmpN.data(), tmpn.data());
+    gmax = 0.0;
+    for (int i = 0; i < n; ++i) {
+      rd[i] = grad[i] - llo[i] + lhi[i] + tmpn[i];
+      gmax = std::max(gmax, std::fabs(grad[i]));
+    }
+    for (int i = 0; i < mg; ++i) rg[i] = ELz[i] + sg[i] - B.h[i];
+    double cs = 0.0;
+    for (int i = 0; i < n; ++i) cs += z[i] * llo[i] + (B.ub[i] - z[i]) * lhi[i];
+    for (int i = 0; i < mg; ++i) cs += sg[i] * lg[i];
+    pres = 0.0;
+    dres = 0.0;
+    for (int i = 0; i < mg; ++i) pres = std::max(pres, std::fabs(rg[i]));
+    for (int i = 0; i < n; ++i) dres = std::max(dres, std::fabs(rd[i]));
+    fval = f_value(B, z.data());
+    gap = cs;
+    return cs / m_tot;
+  };
+  // direction for complementarity targets rc (s dl + l ds = rc per row)
+  auto direction = [&](const std::vector<double>& rlo, const std::vector<double>& rhi, const std::vector<double>& rgc,
+                       std::vector<double>& dzo, std::vector<double>& dsgo, std::vector<double>& dlgo,
+                       std::vector<double>& dlloo, std::vector<double>& dlhio) {
+    // rhs = -rd + rlo/s_lo - rhi/s_hi - L'E'[(rgc + lg rg)/sg]
+    for (int i = 0; i < mg; ++i) tmpm[i] = (rgc[i] + lg[i] * rg[i]) / sg[i];
+    mulEt(N, tmpm.data(), tmpN.data());
+    mulLt(B, tmpN.data(), tmpn.data());
+    for (int i = 0; i < n; ++i) rhs[i] = -rd[i] + rlo[i] / z[i] - rhi[i] / (B.ub[i] - z[i]) - tmpn[i];
+    NW.solve(B, dbox.data(), rhs.data(), dzo.data());
+    mulL(B, dzo.data(), tmpN.data());
+    mulE(N, tmpN.data(), tmpm.data());
+    for (int i = 0; i < mg; ++i) {
+      dsgo[i] = -rg[i] - tmpm[i];
+      dlgo[i] = (rgc[i] - lg[i] * dsgo[i]) / sg[i];
+    }
+    for (int i = 0; i < n; ++i) {
+      dlloo[i] = (rlo[i] - llo[i] * dzo[i]) / z[i];
+      dlhio[i] = (rhi[i] + lhi[i] * dzo[i]) / (B.ub[i] - z[i]);
+    }
+  };
+  // largest steps keeping the primal (z in the boxes, coupling slacks) and the dual variables
+  // positive; separate primal / dual lengths
+  auto step_len = [&](const std::vector<double>& dzv, const std::vector<double>& dsgv, const std::vector<double>& dlgv,
+                      const std::vector<double>& dllov, const std::vector<double>& dlhiv, double& ap, double& ad) {
+    ap = 1.0;
+    for (int i = 0; i < n; ++i) {
+      if (dzv[i] < 0.0) ap = std::min(ap, -z[i] / dzv[i]);
+      if (dzv[i] > 0.0) ap = std::min(ap, (B.ub[i] - z[i]) / dzv[i]);
+    }
+    ap = std::min(ap, max_step(sg, dsgv));
+    ad = std::min(max_step(lg, dlgv), std::min(max_step(llo, dllov), max_step(lhi, dlhiv)));
+  };
+  // best iterate by the worst relative KKT measure; returned when the iteration stalls (the
+  // reference accepts Clarabel's "optimal_inaccurate" silently, lompc.py / bimpc.py never check status)
+  std::vector<double> zb(n), llob(n), lhib(n), lgb(mg);
+  double best_merit = INFINITY, bpres = 0, bdres = 0, bgap = 0, bf = 0;
+  int since_best = 0;
+  for (it = 0; it < max_iter; ++it) {
+    const double mu = residuals();
+    double merit = std::max({pres / (1.0 + hmax), dres / (1.0 + gmax), gap / (1.0 + std::fabs(fval))});
+    for (int i = 0; i < n && std::isfinite(merit); ++i)
+      if (!std::isfinite(z[i]) || !std::isfinite(rd[i])) merit = NAN;
+    if (!std::isfinite(merit)) break;
+    if (merit < best_merit) {
+      best_merit = merit;
+      zb = z;
+      llob = llo;
+      lhib = lhi;
+      lgb = lg;
+      bpres = pres;
+      bdres = dres;
+      bgap = gap;
+      bf = fval;
+      since_best = 0;
+    } else if (++since_best >= 15) {
+      break;
+    }
+    if (pres <= 1e-10 * (1.0 + hmax) && dres <= 1e-9 * (1.0 + gmax) && gap <= 1e-10 * (1.0 + std::fabs(fval))) {
+      status = LOMPC_OK;
+      break;
+    }
+    for (int i = 0; i < n; ++i) dbox[i] = llo[i] / z[i] + lhi[i] / (B.ub[i] - z[i]);
+    for (int i = 0; i < mg; ++i) dgv[i] = lg[i] / sg[i];
+    if (!NW.factor(B, z.data(), dbox.data(), dgv.data())) break;
+    // predictor
+    for (int i = 0; i < n; ++i) {
+      rclo[i] = -z[i] * llo[i];
+      rchi[i] = -(B.ub[i] - z[i]) * lhi[i];
+    }
+    for (int i = 0; i < mg; ++i) rcg[i] = -sg[i] * lg[i];
+    direction(rclo, rchi, rcg, dz_a, dsg_a, dlg_a, dllo_a, dlhi_a);
+    double ap = 1.0, ad = 1.0;
+    step_len(dz_a, dsg_a, dlg_a, dllo_a, dlhi_a, ap, ad);
+    double mu_aff = 0.0;
+    for (int i = 0; i < n; ++i) {
+      mu_aff += (z[i] + ap * dz_a[i]) * (llo[i] + ad * dllo_a[i]);
+      mu_aff += (B.ub[i] - z[i] - ap * dz_a[i]) * (lhi[i] + ad * dlhi_a[i]);
+    }
+    for (int i = 0; i < mg; ++i) mu_aff += (sg[i] + ap * dsg_a[i]) * (lg[i] + ad * dlg_a[i]);
+    mu_aff /= m_tot;
+    const double sigma = std::pow(std::min(1.0, mu_aff / mu), 3.0);
+    // corrector: target sigma mu, second-order term of the affine step
+    for (int i = 0; i < n; ++i) {
+      rclo[i] = sigma * mu - z[i] * llo[i] - dz_a[i] * dllo_a[i];
+      rchi[i] = sigma * mu - (B.ub[i] - z[i]) * lhi[i] + dz_a[i] * dlhi_a[i];
+    }
+    for (int i = 0; i < mg; ++i) rcg[i] = sigma * mu - sg[i] * lg[i] - dsg_a[i] * dlg_a[i];
+    direction(rclo, rchi, rcg, dz, dsg, dlg, dllo, dlhi);
+    step_len(dz, dsg, dlg, dllo, dlhi, ap, ad);
+    const double tau = std::max(0.99, 1.0 - mu);  // fraction to the boundary
+    ap = ad = std::min(1.0, tau * std::min(ap, ad));  // one step: the objective is nonlinear
+    if (trace)
+      fprintf(stderr, "it %3d mu %.3e pres %.3e dres %.3e gap %.3e f %.12g sigma %.3e alpha %.3e\n", it, mu, pres, dres,
+              gap, fval, sigma, ap);
+    if (!std::isfinite(ap) || !std::isfinite(ad) || !std::isfinite(sigma)) break;
+    for (int i = 0; i < n; ++i) {
+      z[i] += ap * dz[i];
+      llo[i] += ad * dllo[i];
+      lhi[i] += ad * dlhi[i];
+    }
+    for (int i = 0; i < mg; ++i) {
+      sg[i] += ap * dsg[i];
+      lg[i] += ad * dlg[i];
+    }
+  }
+  if (status != LOMPC_OK && std::isfinite(best_merit)) {
+    z = zb;
+    llo = llob;
+    lhi = lhib;
+    lg = lgb;
+    pres = bpres;
+    dres = bdres;
+    gap = bgap;
+    fval = bf;
+    if (best_merit <= 5e-5) status = LOMPC_OK;  // Clarabel's reduced tolerances ("almost solved")
+  }
+  for (int p = 0; p < P; ++p)
+    for (int t = 0; t < N; ++t) {
+      w_hat_s[p * N + t] = z[p * N + t];
+      w_hat_l[p * N + t] = z[(P + p) * N + t];
+    }
+  for (int t = 0; t < N; ++t) u_g[t] = z[nb * N + t];
+  if (duals) {  // [lower-bound duals (n) | upper-bound duals (n) | coupling duals (4N)]
+    memcpy(duals, llo.data(), n * sizeof(double));
+    memcpy(duals + n, lhi.data(), n * sizeof(double));
+    memcpy(duals + 2 * n, lg.data(), mg * sizeof(double));
+  }
+  if (info) {  // iterations, objective, primal residual, dual residual, complementarity
+    info[0] = (double)it;
+    info[1] = fval;
+    info[2] = pres;
+    info[3] = dres;
+    info[4] = gap;
+  }
+  return status;
+}
+
+}  // extern "C"

@@ -65,7 +65,12 @@ SIGNATURES = [
     ("lompc_abi_version", _I, []),
     ("lompc_price_step", _I, [_I, _I, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P]),
     ("lompc_lp_separable", _I, [_I, _I, _P, _P, _P, _P]),
+    ("lompc_bimpc_solve", _I, [_I, _I, _I] + [_D] * 10 + [_P] * 6 + [_D] + [_P] * 6),
 ]
+LOMPC_BIMPC_WEIGHTED = 0
+LOMPC_BIMPC_UNWEIGHTED = 1
+LOMPC_BIMPC_EXP_UNWEIGHTED = 2
+LOMPC_BIMPC_INFO = 5
 ABI_VERSION = 1
 
 _lock = threading.Lock()

@@ -183,6 +183,36 @@ int lompc_price_step(int N, int r, double theta, double w_max, double m, double 
 int lompc_lp_separable(int n_rows, int n_cols, const double* A, const double* b,
                        const double* c, double* x);
 
+/* BiMPC charging cost types (bimpc.py:12-15, BiMPCChargingCostType) */
+#define LOMPC_BIMPC_WEIGHTED       0
+#define LOMPC_BIMPC_UNWEIGHTED     1
+#define LOMPC_BIMPC_EXP_UNWEIGHTED 2
+#define LOMPC_BIMPC_INFO           5
+
+/* BiMPC team-optimal planner.  Replaces BiMPC.solve_bimpc (bimpc.py:267-292)
+ * and its CVXPY/Clarabel problem (bimpc.py:142-265):
+ *   constants  (bimpc.py:18-36, :116-140): N, P, charging_cost_type, delta, c_g,
+ *              u_g_max, u_b_max, x_max, exp_rate, theta_s, theta_l, w_max_s, w_max_l
+ *   parameters (BiMPCParameters, bimpc.py:39-59): Mp_s, Mp_l, beta_s, beta_l,
+ *              gamma_sm, gamma_lm [P]; x0; demand [N]
+ *   outputs    w_hat_s, w_hat_l [P, N] row-major, u_g [N]
+ *   duals      optional [2 (2P+1) N + 4N]: lower-bound, upper-bound and coupling
+ *              multipliers (for certificates), or NULL
+ *   info       optional [LOMPC_BIMPC_INFO]: iterations, objective, primal
+ *              residual, dual residual, complementarity sum
+ * Primal-dual interior point on the smooth strictly convex problem (exact Newton
+ * through an N x N Schur complement).  Asserts of bimpc.py:79-84 ->
+ * LOMPC_ERR_INVALID_ARG; no convergence in 200 iterations (e.g. infeasible
+ * storage bounds) -> LOMPC_ERR_NOT_CONVERGED with the last iterate written;
+ * u_g_max, w_max or c_g equal to 0 -> LOMPC_ERR_UNSUPPORTED. */
+int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double c_g,
+                      double u_g_max, double u_b_max, double x_max, double exp_rate,
+                      double theta_s, double theta_l, double w_max_s, double w_max_l,
+                      const double* Mp_s, const double* Mp_l, const double* beta_s,
+                      const double* beta_l, const double* gamma_sm, const double* gamma_lm,
+                      double x0, const double* demand, double* w_hat_s, double* w_hat_l,
+                      double* u_g, double* duals, double* info);
+
 #ifdef __cplusplus
 }
 #endif

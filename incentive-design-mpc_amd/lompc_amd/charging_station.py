@@ -1,0 +1,460 @@
+"""CVXPY-free ``ChargingStation`` (chargingstation/charging_station.py:15-433): the closed-loop
+BiMPC step on the batched engine.
+
+Same constants dataclass, constructor checks, ``simulate() -> logs`` and logs schema
+(charging_station.py:118-149) as the reference.  What runs where:
+
+* EV state (SoCs ``y_s``/``y_l``, partition index) lives on the device (torch fp64);
+  the full-charge re-draws come from the reference's legacy global ``np.random``
+  stream in EV-index order (charging_station.py:95-100, :339-341, :348-350), drawn
+  on the host and scattered, so a seeded run draws the same numbers.
+* partition statistics (count, min, max, mean per partition; charging_station.py:196-210
+  via price_solver.py:66-77, :182-186) are one device reduction per EV type;
+* the BiMPC (bimpc.py) is the host interior point of ``lompc_bimpc_solve``;
+* each (type, partition) price loop is ``PriceSolver.compute_optimal_prices`` (one
+  engine call per price iteration), in the reference's sequential order because
+  ``prev_prices`` chains the partitions (charging_station.py:275-307);
+* ``_get_w0_price0`` (charging_station.py:310-329) is ONE batched engine call per EV
+  type over all partitions (the prices are fixed by then), with fused price0 sums.
+
+Sharded mode (``group``): every rank holds a contiguous slice of each type's EVs;
+partition statistics, the price loops' reductions, price0 sums and the aggregate
+demand are combined with torch.distributed; the BiMPC and the price steps run
+redundantly on identical inputs; the re-draw replays the global random stream.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from . import settings as _settings
+from .bimpc import BiMPC, BiMPCConstants, BiMPCParameters
+from .lompc import LoMPCConstants, SolverError
+from .price_solver import PriceSolver
+from .settings import ADD_RESIDUAL_CHARGE_TO_BATTERY, MAX_INITIAL_SOC, MIN_FULL_CHARGE_FRACTION, MIN_INITIAL_SOC
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+@dataclass
+class ChargingStationConstants:
+    """
+    simulation_length:  Length of the simulation [hours].
+    horizon_bimpc:      BiMPC horizon.
+    horizon_lompc:      LoMPC horizon (<= BiMPC horizon).
+    nEVs_per_EV_type:   Number of small (and large) EVs.
+    npartitions:        Number of partitions per EV type.
+    demand:             External demand vector.
+    bimpc_consts:       Normalized constants for the BiMPC.
+    small_EV_consts:    Constants for the small EV LoMPC.
+    large_EV_consts:    Constants for the large EV LoMPC.
+    price_type:         "linear" or "linear-convex".
+    """
+
+    simulation_length: int
+    horizon_bimpc: int
+    horizon_lompc: int
+    nEVs_per_EV_type: int
+    npartitions: int
+    demand: np.ndarray
+    bimpc_consts: BiMPCConstants
+    small_EV_consts: LoMPCConstants
+    large_EV_consts: LoMPCConstants
+    price_type: str
+
+
+# ----------------------------------------------------------------- sharded helpers
+def shard_bounds(n: int, rank: int, world: int) -> tuple[int, int]:
+    base, rem = divmod(n, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def partition_stats(y, idx, P: int, group=None) -> np.ndarray:
+    """Per partition (count, max, min, sum) of y over the EVs with idx == p, combined over
+    ranks (one MAX and one SUM all-reduce).  Returns a host (P, 4) array; empty partitions
+    have count 0."""
+    torch = _torch()
+    dev = y.device
+    cnt = torch.bincount(idx, minlength=P).to(torch.float64)
+    sm = torch.zeros(P, dtype=torch.float64, device=dev).index_add_(0, idx, y)
+    mx = torch.full((P,), -float("inf"), dtype=torch.float64, device=dev).scatter_reduce(0, idx, y, "amax")
+    mn = torch.full((P,), float("inf"), dtype=torch.float64, device=dev).scatter_reduce(0, idx, y, "amin")
+    if group is not None:
+        import torch.distributed as dist
+
+        a = torch.cat([cnt, sm])
+        b = torch.cat([mx, -mn])
+        dist.all_reduce(a, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(b, op=dist.ReduceOp.MAX, group=group)
+        cnt, sm, mx, mn = a[:P], a[P:], b[:P], -b[P:]
+    return torch.stack([cnt, mx, mn, sm], dim=1).cpu().numpy()
+
+
+def redraw_full(y, mask, lo_val: float, hi_val: float, rng_random, group=None) -> int:
+    """y[mask] = lo + (hi - lo) * rng_random(count) with the draws in GLOBAL EV-index order
+    (charging_station.py:339-341): every rank draws the global vector from the same
+    (replicated) stream and keeps its own slice.  Returns the global count."""
+    torch = _torch()
+    local = int(mask.sum().item())
+    if group is None:
+        total, before = local, 0
+    else:
+        import torch.distributed as dist
+
+        world = dist.get_world_size(group)
+        t = torch.tensor([local], dtype=torch.int64, device=y.device)
+        allc = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allc, t, group=group)
+        counts = [int(c.item()) for c in allc]
+        total = sum(counts)
+        before = sum(counts[: dist.get_rank(group)])
+    draws = lo_val + (hi_val - lo_val) * rng_random((total,))
+    if local:
+        y[mask] = torch.as_tensor(draws[before:before + local], dtype=torch.float64, device=y.device)
+    return total
+
+
+class ChargingStation:
+    def __init__(self, consts: ChargingStationConstants, device: int | None = None, mode: str | None = None,
+                 group=None) -> None:
+        # charging_station.py:44-53
+        assert consts.simulation_length >= 1
+        assert (consts.horizon_bimpc >= consts.horizon_lompc) and (consts.horizon_lompc >= 1)
+        assert consts.nEVs_per_EV_type >= 1
+        assert consts.npartitions >= 1
+        assert (len(consts.demand.shape) == 1) and (
+            consts.demand.shape[0] >= consts.simulation_length + consts.horizon_bimpc + 1)
+        torch = _torch()
+        self.group = group
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self._dev = f"cuda:{self.device}"
+        # Set constants, initialize PriceSolvers and BiMPC.
+        self._set_constants(consts)
+        self.bimpc = BiMPC(self.N_bi, self.P, self.consts_bi, self.consts_s, self.consts_l)
+        self.price_solver_s = PriceSolver(self.N_lo, self.consts_s, self.price_type, device=self.device, mode=mode,
+                                          group=group)
+        self.price_solver_l = PriceSolver(self.N_lo, self.consts_l, self.price_type, device=self.device, mode=mode,
+                                          group=group)
+        # Initialize state variables = (EV SoCs, charge stored).
+        self._init_states()
+        # Initialize logs.
+        self._init_logs(consts)
+
+    def _set_constants(self, consts: ChargingStationConstants) -> None:
+        # charging_station.py:67-92
+        self.Tf = consts.simulation_length
+        self.N_bi = consts.horizon_bimpc
+        self.N_lo = consts.horizon_lompc
+        self.M_2 = consts.nEVs_per_EV_type
+        self.P = consts.npartitions
+        self.demand = consts.demand
+        self.consts_bi = consts.bimpc_consts
+        self.consts_s = consts.small_EV_consts
+        self.consts_l = consts.large_EV_consts
+        self.price_type = consts.price_type
+        if self.price_type == "linear":
+            self.r = 2 * self.N_lo
+        else:
+            self.r = 3 * self.N_lo
+        self.y0_min = MIN_INITIAL_SOC
+        self.y0_max = MAX_INITIAL_SOC
+        self.y0_s_rng = np.linspace(self.y0_min, self.consts_s.y_max, self.P + 1)
+        self.y0_l_rng = np.linspace(self.y0_min, self.consts_l.y_max, self.P + 1)
+        self.B = (self.consts_s.theta + self.consts_l.theta) * self.M_2
+        if self.group is None:
+            self._lo, self._hi = 0, self.M_2
+        else:
+            import torch.distributed as dist
+
+            self._lo, self._hi = shard_bounds(self.M_2, dist.get_rank(self.group), dist.get_world_size(self.group))
+
+    def _rank0(self) -> bool:
+        if self.group is None:
+            return True
+        import torch.distributed as dist
+
+        return dist.get_rank(self.group) == 0
+
+    def _init_states(self) -> None:
+        # charging_station.py:94-109 (global draws, this rank keeps its slice)
+        torch = _torch()
+        y_s = self.y0_min + (self.y0_max - self.y0_min) * np.random.random((self.M_2,))
+        y_l = self.y0_min + (self.y0_max - self.y0_min) * np.random.random((self.M_2,))
+        self.y_s = torch.as_tensor(y_s[self._lo:self._hi].copy(), device=self._dev)
+        self.y_l = torch.as_tensor(y_l[self._lo:self._hi].copy(), device=self._dev)
+        self.x = 0  # Storage battery SoC, normalized wrt B.
+        self.t = 0
+        self.ncharged_s = 0
+        self.ncharged_l = 0
+        n = self._hi - self._lo
+        self.idx_s = torch.zeros((n,), dtype=torch.int64, device=self._dev)
+        self.idx_l = torch.zeros((n,), dtype=torch.int64, device=self._dev)
+        self._update_indices()
+
+    def _update_indices(self) -> None:
+        # charging_station.py:111-116 (later partitions win on shared edges, as there)
+        for p in range(self.P):
+            mask_s = (self.y_s >= self.y0_s_rng[p]) & (self.y_s <= self.y0_s_rng[p + 1])
+            self.idx_s[mask_s] = p
+            mask_l = (self.y_l >= self.y0_l_rng[p]) & (self.y_l <= self.y0_l_rng[p + 1])
+            self.idx_l[mask_l] = p
+
+    def _init_logs(self, consts: ChargingStationConstants) -> None:
+        # charging_station.py:118-149
+        self.logs = {}
+        self.logs["constants"] = consts
+        self.logs["inputs"] = {
+            "w_s": np.zeros((self.P, self.Tf)),
+            "w_l": np.zeros((self.P, self.Tf)),
+            "w_hat_s": np.zeros((self.P, self.Tf)),
+            "w_hat_l": np.zeros((self.P, self.Tf)),
+            "u_g": np.zeros((self.Tf,)),
+        }
+        self.logs["states"] = {"x": np.zeros((self.Tf,))}
+        self.logs["bounds"] = {"beta_s": np.zeros((self.P, self.Tf)), "beta_l": np.zeros((self.P, self.Tf))}
+        self.logs["statistics"] = {
+            "ncharged_s": 0,
+            "ncharged_l": 0,
+            "gamma_sm": np.zeros((self.P, self.Tf)),
+            "gamma_lm": np.zeros((self.P, self.Tf)),
+            "niter_s": np.zeros((self.P, self.Tf), dtype=int),
+            "niter_l": np.zeros((self.P, self.Tf), dtype=int),
+            "Mp_s": np.zeros((self.P, self.Tf), dtype=int),
+            "Mp_l": np.zeros((self.P, self.Tf), dtype=int),
+        }
+        self.logs["prices"] = {
+            "lmbd_r": np.zeros((self.Tf)),
+            "avg_price_s": np.zeros((self.P, self.Tf)),
+            "avg_price_l": np.zeros((self.P, self.Tf)),
+            "price_red_s": np.zeros((self.P, self.Tf)),
+            "price_red_l": np.zeros((self.P, self.Tf)),
+        }
+
+    def simulate(self) -> dict:
+        for _ in range(self.Tf):
+            self._step()
+        return self.logs
+
+    def _step(self):
+        # charging_station.py:156-185
+        PRINT_LEVEL = _settings.PRINT_LEVEL
+        if PRINT_LEVEL >= 1 and self._rank0():
+            print("-" * 50)
+            print(f"Iteration {self.t}")
+            print("-" * 50)
+        lmbd_r = 0
+        w_hat_s, w_hat_l, u_g, stats_bi = self._get_bimpc_solution(lmbd_r)
+        prices_s, prices_l, stats_s, stats_l = self._get_optimal_prices(w_hat_s, w_hat_l, lmbd_r)
+        w0_s, w0_l, price0_s, price0_l, w0_stats = self._get_w0_price0(prices_s, prices_l, lmbd_r)
+        nu = (w_hat_s, w_hat_l, u_g, w0_s, w0_l)
+        stats = (stats_bi, stats_s, stats_l)
+        price0 = (price0_s, price0_l)
+        self._update_logs(lmbd_r, nu, stats, price0, w0_stats)
+        self._update_state(w0_s, w0_l, u_g[0], w0_stats)
+        self.t += 1
+
+    # ------------------------------------------------------------------ BiMPC
+    def _robustness(self, solver: PriceSolver, st_row, lmbd_r):
+        """set_charge_levels + get_robustness_bounds + get_gamma_sm (price_solver.py:66-77,
+        :182-186) from one row of partition statistics (count, max, min, sum)."""
+        n, ymax, ymin, ysum = st_row
+        y0_rng = (ymax - ymin) / 2
+        kappa = lmbd_r / solver.consts.delta + 1e-5
+        w_err_bound = np.sqrt(solver.N) * y0_rng + solver.eps_tol
+        beta = w_err_bound * np.min((1, 1 / np.sqrt(kappa)))
+        gamma_sm = solver.consts.y_max - ysum / n
+        return beta, gamma_sm
+
+    def _get_bimpc_solution(self, lmbd_r: float):
+        # charging_station.py:187-266
+        Mp_s, Mp_l = np.zeros((self.P,), dtype=int), np.zeros((self.P,), dtype=int)
+        beta_s, beta_l = np.zeros((self.P,)), np.zeros((self.P,))
+        gamma_sm, gamma_lm = np.zeros((self.P,)), np.zeros((self.P,))
+        st_s = partition_stats(self.y_s, self.idx_s, self.P, self.group)
+        st_l = partition_stats(self.y_l, self.idx_l, self.P, self.group)
+        for p in range(self.P):
+            Mp_s[p] = int(st_s[p, 0])
+            if Mp_s[p] > 0:
+                assert st_s[p, 2] >= 0 and st_s[p, 1] <= self.consts_s.y_max  # price_solver.py:71
+                beta_s[p], gamma_sm[p] = self._robustness(self.price_solver_s, st_s[p], lmbd_r)
+            Mp_l[p] = int(st_l[p, 0])
+            if Mp_l[p] > 0:
+                assert st_l[p, 2] >= 0 and st_l[p, 1] <= self.consts_l.y_max
+                beta_l[p], gamma_lm[p] = self._robustness(self.price_solver_l, st_l[p], lmbd_r)
+        self._pstats = (st_s, st_l)
+        Mp_s_ = Mp_s / self.B
+        Mp_l_ = Mp_l / self.B
+        demand = self.demand[self.t: self.t + self.N_bi] / self.B
+        bimpc_params = BiMPCParameters(Mp_s_, Mp_l_, beta_s, beta_l, gamma_sm, gamma_lm, self.x, demand)
+        w_hat_s, w_hat_l, u_g = self.bimpc.solve_bimpc(bimpc_params)
+        stats_bi = {"Mp_s": Mp_s, "Mp_l": Mp_l, "beta_s": beta_s, "beta_l": beta_l, "gamma_sm": gamma_sm,
+                    "gamma_lm": gamma_lm}
+        if _settings.PRINT_LEVEL >= 1 and self._rank0():
+            total_w0_hat = self.consts_s.theta * Mp_s_ @ w_hat_s[:, 0] + self.consts_l.theta * Mp_l_ @ w_hat_l[:, 0]
+            u0_b_hat = u_g[0] - demand[0] - total_w0_hat
+            u0_b_err = self.consts_s.theta * Mp_s_ @ beta_s + self.consts_l.theta * Mp_l_ @ beta_l
+            x_hat = self.x + u0_b_hat
+            print("EV distribution (small): " + " + ".join("{:4d}".format(n) for n in Mp_s)
+                  + " = {:4d}".format(np.sum(Mp_s)))
+            print("EV distribution (large): " + " + ".join("{:4d}".format(n) for n in Mp_l)
+                  + " = {:4d}".format(np.sum(Mp_l)))
+            print(f"Electricity generated  : {u_g[0]:13.8f} | Max: {self.consts_bi.u_g_max:13.8f}")
+            print(f"Demand                 : {demand[0]:13.8f}")
+            print(f"Predicted output (EVs) : {total_w0_hat:13.8f}")
+            print(f"Predicted battery input: [{u0_b_hat - u0_b_err:8.5f}, {u0_b_hat + u0_b_err:8.5f}] "
+                  f"| Max (mag): {self.consts_bi.u_b_max:8.5f}")
+            print(f"Current battery state  : {self.x}")
+            print(f"Predicted battery state: Min: 0 | [{x_hat - u0_b_err:8.5f}, {x_hat + u0_b_err:8.5f}] "
+                  f"| Max: {self.consts_bi.x_max:8.5f}")
+            if _settings.PRINT_LEVEL >= 2:
+                print("")
+        return w_hat_s, w_hat_l, u_g, stats_bi
+
+    # ------------------------------------------------------------------ prices
+    def _get_optimal_prices(self, w_hat_s, w_hat_l, lmbd_r: float):
+        # charging_station.py:268-308 (sequential: prev_prices chains the partitions)
+        PRINT_LEVEL = _settings.PRINT_LEVEL
+        w_hat_s_opt, w_hat_l_opt = w_hat_s[:, : self.N_lo], w_hat_l[:, : self.N_lo]
+        prices_s, prices_l = np.zeros((self.P, self.r)), np.zeros((self.P, self.r))
+        stats_s, stats_l = [], []
+        st_s, st_l = self._pstats
+        for p in range(self.P):
+            for kind, solver, y, idx, st, w_hat, prices, stats in (
+                    ("Small", self.price_solver_s, self.y_s, self.idx_s, st_s, w_hat_s_opt, prices_s, stats_s),
+                    ("Large", self.price_solver_l, self.y_l, self.idx_l, st_l, w_hat_l_opt, prices_l, stats_l)):
+                if st[p, 0] > 0:
+                    solver.set_charge_levels(y[idx == p])
+                    if PRINT_LEVEL >= 1 and self._rank0():
+                        print(f"{kind} EVs, partition {p:2d}: ", end="")
+                        if PRINT_LEVEL >= 2:
+                            print("\n" + "-" * 27)
+                    lmbd_, stats_ = solver.compute_optimal_prices(w_hat[p, :], lmbd_r)
+                    prices[p, :] = lmbd_[: self.r]
+                    stats.append(stats_)
+                    if PRINT_LEVEL >= 2:
+                        print("")
+                else:
+                    stats.append({})
+        return prices_s, prices_l, stats_s, stats_l
+
+    def _w0_batched(self, solver: PriceSolver, y, idx, prices, lmbd_r):
+        """All partitions of one EV type in ONE engine call (price_solver.py:272-285 per partition).
+        Returns (w0 in EV order, per-partition (sum w0, sum price0, count) combined over ranks)."""
+        torch = _torch()
+        N, P = self.N_lo, self.P
+        perm = torch.argsort(idx, stable=True)
+        counts = torch.bincount(idx, minlength=P)
+        off = np.concatenate([[0], np.cumsum(counts.cpu().numpy())]).astype(np.int64)
+        gamma = (solver.consts.y_max - y)[perm].contiguous()
+        lm = np.zeros((P, 3 * N))
+        lm[:, : self.r] = prices
+        lompc = solver.lompc
+        lompc.set_params(lm, np.full(P, float(lmbd_r)))
+        res = lompc.solve_batch(gamma, off, want_w=False, want_cost=False, want_w0=True, want_set=True, check=False)
+        st = res["set_stats"]
+        red = torch.stack([st[:, _lib.LOMPC_STAT_SUM_W0], st[:, _lib.LOMPC_STAT_SUM_PRICE0],
+                           st[:, _lib.LOMPC_STAT_COUNT], st[:, _lib.LOMPC_STAT_N_FAILED],
+                           st[:, _lib.LOMPC_STAT_N_INVALID]], dim=1).contiguous()
+        if self.group is not None:
+            import torch.distributed as dist
+
+            dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
+        w0 = torch.empty_like(y)
+        w0[perm] = res["w0"]
+        red = red.cpu().numpy()
+        if np.any(red[:, 4] > 0):
+            raise AssertionError("gamma outside [0, y_max]")
+        if np.any(red[:, 3] > 0):
+            raise SolverError("LoMPC QPs without a certified optimum")
+        return w0, red[:, :3]
+
+    def _get_w0_price0(self, prices_s, prices_l, lmbd_r: float):
+        # charging_station.py:310-329
+        w0_s, red_s = self._w0_batched(self.price_solver_s, self.y_s, self.idx_s, prices_s, lmbd_r)
+        w0_l, red_l = self._w0_batched(self.price_solver_l, self.y_l, self.idx_l, prices_l, lmbd_r)
+        price0_s, price0_l = np.zeros((self.P,)), np.zeros((self.P,))
+        for p in range(self.P):
+            if red_s[p, 2] > 0:
+                price0_s[p] = red_s[p, 1] / red_s[p, 2]
+            if red_l[p, 2] > 0:
+                price0_l[p] = red_l[p, 1] / red_l[p, 2]
+        return w0_s, w0_l, price0_s, price0_l, (red_s, red_l)
+
+    # ------------------------------------------------------------------ state
+    def _update_state(self, w0_s, w0_l, u0_g: float, w0_stats) -> None:
+        # charging_station.py:331-370
+        torch = _torch()
+        residual_charge = 0
+        self.y_s += w0_s
+        thr_s = MIN_FULL_CHARGE_FRACTION * self.consts_s.y_max
+        mask_s = self.y_s > thr_s
+        residual_charge += self.consts_s.theta * self._global_sum(torch.where(mask_s, self.y_s - thr_s, 0.0))
+        self.ncharged_s += redraw_full(self.y_s, mask_s, self.y0_min, self.y0_max, np.random.random, self.group)
+        self.y_l += w0_l
+        thr_l = MIN_FULL_CHARGE_FRACTION * self.consts_l.y_max
+        mask_l = self.y_l > thr_l
+        residual_charge += self.consts_l.theta * self._global_sum(torch.where(mask_l, self.y_l - thr_l, 0.0))
+        self.ncharged_l += redraw_full(self.y_l, mask_l, self.y0_min, self.y0_max, np.random.random, self.group)
+        self._update_indices()
+        if not ADD_RESIDUAL_CHARGE_TO_BATTERY:
+            residual_charge = 0
+        red_s, red_l = w0_stats
+        sum_w0_s, sum_w0_l = float(np.sum(red_s[:, 0])), float(np.sum(red_l[:, 0]))
+        u0_b = u0_g + (-self.consts_s.theta * sum_w0_s - self.consts_l.theta * sum_w0_l + residual_charge
+                       - self.demand[self.t]) / self.B
+        self.x += u0_b
+        if _settings.PRINT_LEVEL >= 1 and self._rank0():
+            print(f"# small EVs charged    : {self.ncharged_s:5d}")
+            print(f"# large EVs charged    : {self.ncharged_l:5d}")
+            print("")
+
+    def _global_sum(self, v) -> float:
+        s = v.sum()
+        if self.group is not None:
+            import torch.distributed as dist
+
+            s = s.reshape(1).clone()
+            dist.all_reduce(s, group=self.group)
+        return float(s.item())
+
+    def _update_logs(self, lmbd_r: float, nu: tuple, stats: tuple, price0: tuple, w0_stats) -> None:
+        # charging_station.py:372-433
+        w_hat_s, w_hat_l, u_g, w0_s, w0_l = nu
+        stats_bi, stats_s, stats_l = stats
+        price0_s, price0_l = price0
+        red_s, red_l = w0_stats
+        for p in range(self.P):  # mean w0 per partition (:380-384)
+            if red_s[p, 2] > 0:
+                self.logs["inputs"]["w_s"][p, self.t] = red_s[p, 0] / red_s[p, 2]
+            if red_l[p, 2] > 0:
+                self.logs["inputs"]["w_l"][p, self.t] = red_l[p, 0] / red_l[p, 2]
+        self.logs["inputs"]["w_hat_s"][:, self.t] = w_hat_s[:, 0]
+        self.logs["inputs"]["w_hat_l"][:, self.t] = w_hat_l[:, 0]
+        self.logs["inputs"]["u_g"][self.t] = u_g[0]
+        self.logs["states"]["x"][self.t] = self.x
+        self.logs["bounds"]["beta_s"][:, self.t] = stats_bi["beta_s"]
+        self.logs["bounds"]["beta_l"][:, self.t] = stats_bi["beta_l"]
+        self.logs["statistics"]["ncharged_s"] = self.ncharged_s
+        self.logs["statistics"]["ncharged_l"] = self.ncharged_l
+        self.logs["statistics"]["gamma_sm"][:, self.t] = stats_bi["gamma_sm"]
+        self.logs["statistics"]["gamma_lm"][:, self.t] = stats_bi["gamma_lm"]
+        for p in range(self.P):
+            self.logs["statistics"]["niter_s"][p, self.t] = stats_s[p]["iter"] if stats_s[p] else -1
+            self.logs["statistics"]["niter_l"][p, self.t] = stats_l[p]["iter"] if stats_l[p] else -1
+        self.logs["statistics"]["Mp_s"][:, self.t] = stats_bi["Mp_s"]
+        self.logs["statistics"]["Mp_l"][:, self.t] = stats_bi["Mp_l"]
+        self.logs["prices"]["lmbd_r"][self.t] = lmbd_r
+        self.logs["prices"]["avg_price_s"][:, self.t] = price0_s
+        self.logs["prices"]["avg_price_l"][:, self.t] = price0_l
+        for p in range(self.P):
+            self.logs["prices"]["price_red_s"][p, self.t] = (
+                stats_s[p]["price_after_reg"] - stats_s[p]["price_before_reg"] if stats_s[p] else np.nan)
+            self.logs["prices"]["price_red_l"][p, self.t] = (
+                stats_l[p]["price_after_reg"] - stats_l[p]["price_before_reg"] if stats_l[p] else np.nan)

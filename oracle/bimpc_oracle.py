@@ -145,18 +145,27 @@ class BiMPCLiteral:
         s[2 * n:] = np.maximum(s[2 * n:], 0.1 * (1 + np.max(np.abs(h[2 * n:]))))
         lam = mu0 / s
         it = 0
+        best = (np.inf, z, lam)
         for it in range(max_iter):
             g = self._grad(z)
             rd = g + G.T @ lam
             rp = G @ z + s - h
             mu = s @ lam / m
+            fz = self.objective(z)
+            merit = max(np.max(np.abs(rp)) / (1 + np.max(np.abs(h))), np.max(np.abs(rd)) / (1 + np.max(np.abs(g))),
+                        s @ lam / (1 + abs(fz)))
+            if not np.isfinite(merit):
+                break
+            if merit < best[0]:
+                best = (merit, z.copy(), lam.copy())
             if (np.max(np.abs(rp)) <= 1e-10 * (1 + np.max(np.abs(h))) and np.max(np.abs(rd)) <= tol * (1 + np.max(np.abs(g)))
-                    and s @ lam <= tol * (1 + abs(self.objective(z)))):
+                    and s @ lam <= tol * (1 + abs(fz))):
                 break
             H = Hq.copy()
             u = z[2 * self.P * N:]
             H[2 * self.P * N:, 2 * self.P * N:] += np.diag(1.19 * c_g * u ** -0.3)
             Mx = H + G.T @ (G * (lam / s)[:, None])
+            Mx[np.diag_indices(n)] += 1e-13 * (1.0 + np.max(np.diag(Mx)))
 
             def direction(rc):
                 rhs = -rd - G.T @ ((rc + lam * rp) / s)
@@ -173,7 +182,10 @@ class BiMPCLiteral:
                         a = min(a, float(np.min(-v[neg] / dv[neg])))
                 return a
 
-            dz_a, ds_a, dl_a = direction(-s * lam)
+            try:
+                dz_a, ds_a, dl_a = direction(-s * lam)
+            except np.linalg.LinAlgError:
+                break
             aa = alpha(ds_a, dl_a)
             mu_aff = (s + aa * ds_a) @ (lam + aa * dl_a) / m
             sigma = min(1.0, mu_aff / mu) ** 3
@@ -182,6 +194,8 @@ class BiMPCLiteral:
             z, s, lam = z + a * dz, s + a * ds, lam + a * dl
             if trace is not None:
                 trace.append((z.copy(), a, sigma))
+        if trace is None:  # best iterate (numerically flat directions can stall the last steps)
+            z, lam = best[1], best[2]
         return z, lam, it
 
     def _grad(self, z):

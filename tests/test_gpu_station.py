@@ -1,0 +1,122 @@
+"""GPU tests of the CVXPY-free closed loop (charging_station.py:42-433): the batched
+engine + host price / BiMPC solvers against the CPU oracle station
+(oracle/station_oracle.py), on the example's constants (real_time_price_control.py:
+11-52) with a small EV population, and the EV-sharded loop (2 ranks sharing the
+device over gloo) against the single-process loop.
+
+Tolerance: discrete quantities (partition sizes Mp, price iterations, EVs charged)
+must match exactly; continuous logs within 1e-6 (relative to the largest entry of
+each log, the north star's trajectory tolerance).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import lompc_oracle as O
+from lompc_amd import settings
+from lompc_amd.bimpc import BiMPCChargingCostType, BiMPCConstants
+from lompc_amd.charging_station import ChargingStation, ChargingStationConstants
+from lompc_amd.demand_data import medium_term_demand_forecast
+from lompc_amd.lompc import LoMPCConstants
+
+pytestmark = pytest.mark.gpu
+
+TF, N_LO, N_BI, P = 3, 12, 16, 12
+
+
+def consts(M_2, Tf=TF):
+    cs = LoMPCConstants(0.05, 10, 0.9, 0.25, "small")  # real_time_price_control.py:26-39
+    cl = LoMPCConstants(0.025, 50, 0.9, 0.15, "large")
+    bi = BiMPCConstants(1e3, 1, 1, 0.3, 0.3, BiMPCChargingCostType.EXP_UNWEIGHTED, 5)  # :42-52
+    demand = medium_term_demand_forecast(Tf + N_BI + 1, 1 / 4 * M_2 / 500, interpolate=False)  # scaled to M_2
+    return ChargingStationConstants(Tf, N_BI, N_LO, M_2, P, demand, bi, cs, cl, "linear-convex")
+
+
+def compare_logs(logs, ol):
+    L = {**logs["inputs"], **logs["bounds"], **logs["prices"], "x": logs["states"]["x"],
+         **{k: v for k, v in logs["statistics"].items() if k not in ("ncharged_s", "ncharged_l")}}
+    for k in ("Mp_s", "Mp_l", "niter_s", "niter_l"):
+        np.testing.assert_array_equal(L[k], ol[k], err_msg=k)
+    for k in ("w_s", "w_l", "w_hat_s", "w_hat_l", "beta_s", "beta_l", "gamma_sm", "gamma_lm", "avg_price_s",
+              "avg_price_l", "price_red_s", "price_red_l", "u_g", "x"):
+        a, b = np.asarray(L[k]), np.asarray(ol[k])
+        scale = max(1.0, float(np.nanmax(np.abs(b))))
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-6 * scale, err_msg=k)
+
+
+def test_closed_loop_matches_oracle(gpu, monkeypatch):
+    import station_oracle as SO
+
+    monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
+    M_2 = 60
+    c = consts(M_2)
+    np.random.seed(1)
+    cs = ChargingStation(c, device=0)
+    logs = cs.simulate()
+    np.random.seed(1)
+    bi = dict(delta=1e3, c_g=1, u_g_max=1, u_b_max=0.3, x_max=0.3, cost_type=2, exp_rate=5)
+    so = SO.OracleStation(N_BI, N_LO, M_2, P, c.demand, bi, O.small_consts(), O.large_consts(), "linear-convex", TF)
+    for _ in range(TF):
+        so.step()
+    compare_logs(logs, so.logs)
+    assert logs["statistics"]["ncharged_s"] == so.ncharged_s and logs["statistics"]["ncharged_l"] == so.ncharged_l
+    np.testing.assert_allclose(cs.y_s.cpu().numpy(), so.y_s, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(cs.y_l.cpu().numpy(), so.y_l, rtol=0, atol=1e-6)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, M_2, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    settings.PRINT_LEVEL = 0
+    torch.cuda.set_device(0)
+    np.random.seed(5)
+    cs = ChargingStation(consts(M_2, Tf=2), device=0, group=dist.group.WORLD)
+    logs = cs.simulate()
+    q.put((rank, logs["inputs"], logs["prices"], logs["statistics"], logs["states"]["x"], cs.y_s.cpu().numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_loop_matches_single_process(gpu, monkeypatch):
+    """Two EV shards (gloo over device tensors, both ranks on cuda:0) give the single-process
+    trajectory: partition statistics, fused reductions, price0 sums, aggregate demand and
+    the globally ordered full-charge re-draws are combined across ranks."""
+    import torch.multiprocessing as mp
+
+    monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
+    M_2 = 61  # odd: unequal shards
+    np.random.seed(5)
+    ref = ChargingStation(consts(M_2, Tf=2), device=0).simulate()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, M_2, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=300) for _ in range(2)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for _, inputs, prices, stats, x, _ in outs:
+        for k in ("w_s", "w_l", "w_hat_s", "w_hat_l", "u_g"):
+            np.testing.assert_allclose(inputs[k], ref["inputs"][k], rtol=0, atol=1e-9, err_msg=k)
+        for k in ("avg_price_s", "avg_price_l"):
+            np.testing.assert_allclose(prices[k], ref["prices"][k], rtol=0, atol=1e-9, err_msg=k)
+        for k in ("Mp_s", "Mp_l", "niter_s", "niter_l"):
+            np.testing.assert_array_equal(stats[k], ref["statistics"][k], err_msg=k)
+        assert stats["ncharged_s"] == ref["statistics"]["ncharged_s"]
+        np.testing.assert_allclose(x, ref["states"]["x"], rtol=0, atol=1e-12)

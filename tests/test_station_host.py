@@ -1,0 +1,86 @@
+"""CPU tests of the closed loop's sharded host logic (charging_station.py): partition
+statistics combined over ranks (charging_station.py:196-210 / price_solver.py:66-77)
+and the full-charge re-draw replaying the reference's global np.random stream in EV
+order (charging_station.py:339-341) — world_size 2 over gloo on CPU tensors."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from lompc_amd.charging_station import partition_stats, redraw_full, shard_bounds
+
+
+def test_shard_bounds_cover():
+    for n in (1, 2, 61, 1000):
+        for w in (1, 2, 3, 8):
+            b = [shard_bounds(n, r, w) for r in range(w)]
+            assert b[0][0] == 0 and b[-1][1] == n and all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+
+
+def test_partition_stats_single_process():
+    rng = np.random.default_rng(0)
+    y = torch.as_tensor(0.3 + 0.6 * rng.random(200))
+    idx = torch.as_tensor(rng.integers(0, 5, 200))
+    st = partition_stats(y, idx, 6)
+    yn, ix = y.numpy(), idx.numpy()
+    for p in range(6):
+        m = ix == p
+        assert st[p, 0] == m.sum()
+        if m.any():
+            assert st[p, 1] == yn[m].max() and st[p, 2] == yn[m].min()
+            assert abs(st[p, 3] - yn[m].sum()) <= 1e-12
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, y_all, idx_all, mask_all, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_bounds(len(y_all), rank, world)
+    y = torch.as_tensor(y_all[lo:hi].copy())
+    idx = torch.as_tensor(idx_all[lo:hi].copy())
+    st = partition_stats(y, idx, 6, group=dist.group.WORLD)
+    np.random.seed(42)  # replicated stream on every rank
+    n = redraw_full(y, torch.as_tensor(mask_all[lo:hi].copy()), 0.3, 0.5, np.random.random, group=dist.group.WORLD)
+    q.put((rank, st, n, y.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_stats_and_redraw_world2():
+    rng = np.random.default_rng(1)
+    n = 37
+    y_all = 0.3 + 0.6 * rng.random(n)
+    idx_all = rng.integers(0, 5, n)
+    mask_all = rng.random(n) < 0.4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, y_all, idx_all, mask_all, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=120) for _ in range(2)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref_st = partition_stats(torch.as_tensor(y_all), torch.as_tensor(idx_all), 6)
+    # the reference's single-process re-draw (charging_station.py:339-341)
+    np.random.seed(42)
+    y_ref = y_all.copy()
+    y_ref[mask_all] = 0.3 + (0.5 - 0.3) * np.random.random((mask_all.sum(),))
+    y_got = np.concatenate([o[3] for o in outs])
+    for _, st, cnt, _ in outs:
+        np.testing.assert_array_equal(st[:, :3], ref_st[:, :3])
+        np.testing.assert_allclose(st[:, 3], ref_st[:, 3], rtol=1e-14)
+        assert cnt == mask_all.sum()
+    np.testing.assert_array_equal(y_got, y_ref)

@@ -272,6 +272,172 @@ double max_step(const std::vector<double>& s, const std::vector<double>& ds) {
   return a;
 }
 
+// Active-set polish of the interior-point solution (cf. OSQP's solution polishing): the
+// constraints whose multiplier exceeds their slack are fixed as equalities, the resulting
+// equality-constrained problem is solved by Newton steps (only c_g u^1.7 is nonlinear) through
+// the |J| x |J| Schur complement of the per-block reduced Hessians, and the result replaces the
+// IPM point only if it is primal feasible and every multiplier has the right sign — then it is
+// the exact optimum up to round-off.
+static bool g_trace_polish = false;
+#define PFAIL(msg) do { if (g_trace_polish) fprintf(stderr, "polish: %s\n", msg); return false; } while (0)
+bool polish(const Bimpc& B, std::vector<double>& z, std::vector<double>& llo, std::vector<double>& lhi,
+            std::vector<double>& lg, const std::vector<double>& sg) {
+  const int N = B.N, nb = B.nb, n = B.n, mg = B.mg;
+  std::vector<int> fix(n, 0);  // -1 at the lower bound, +1 at the upper bound, 0 free
+  for (int i = 0; i < n; ++i) {
+    if (llo[i] > z[i])
+      fix[i] = -1;
+    else if (lhi[i] > B.ub[i] - z[i])
+      fix[i] = +1;
+  }
+  std::vector<int> J;
+  for (int j = 0; j < mg; ++j)
+    if (lg[j] > sg[j]) J.push_back(j);
+  std::vector<double> zp(z);
+  std::vector<double> Ej, nu, g(n), Lz(N), ELz(mg), S, rhs, col;
+  std::vector<int> piv;
+  int nJ = 0;
+  bool feasible = false;
+  // rounds: a free variable that leaves its box is fixed at that bound, a violated coupling row
+  // joins the active set, and the equality-constrained problem is solved again
+  for (int round = 0; round < 6 && !feasible; ++round) {
+    nJ = (int)J.size();
+    Ej.assign((size_t)nJ * N, 0.0);  // active rows of E = [-I; I; -A; A]
+    for (int a = 0; a < nJ; ++a) {
+      const int j = J[a], blk = j / N, t = j % N;
+      double* e = &Ej[(size_t)a * N];
+      if (blk == 0 || blk == 1)
+        e[t] = blk == 0 ? -1.0 : 1.0;
+      else
+        for (int u = 0; u <= t; ++u) e[u] = blk == 2 ? -1.0 : 1.0;
+    }
+    nu.assign(nJ, 0.0);
+    rhs.assign(nJ, 0.0);
+    piv.assign(std::max(nJ, 1), 0);
+    for (int i = 0; i < n; ++i) zp[i] = fix[i] < 0 ? 0.0 : (fix[i] > 0 ? B.ub[i] : zp[i]);
+    double step = INFINITY;
+    for (int newton = 0; newton < 8 && step > 1e-15; ++newton) {
+      f_grad(B, zp.data(), g.data());
+      mulL(B, zp.data(), Lz.data());
+      mulE(N, Lz.data(), ELz.data());
+      S.assign((size_t)nJ * nJ, 0.0);
+      std::fill(rhs.begin(), rhs.end(), 0.0);
+      std::vector<std::vector<double>> Y(nb + 1), hg(nb + 1);
+      std::vector<std::vector<int>> F(nb + 1);
+      for (int k = 0; k <= nb; ++k) {
+        for (int t = 0; t < N; ++t)
+          if (!fix[k * N + t]) F[k].push_back(t);
+        const int m = (int)F[k].size();
+        if (!m) continue;
+        const double ck = k < nb ? B.ck[k] : 1.0;
+        std::vector<double> H((size_t)m * m, 0.0);
+        if (k < nb) {
+          std::vector<double> suf(N);
+          double acc = 0.0;
+          for (int t = N - 1; t >= 0; --t) {
+            acc += B.omega[k * N + t];
+            suf[t] = 2.0 * B.delta * acc;
+          }
+          for (int a = 0; a < m; ++a)
+            for (int b = 0; b < m; ++b) H[a * m + b] = suf[std::max(F[k][a], F[k][b])];
+        } else {
+          for (int a = 0; a < m; ++a) {
+            const double u = zp[nb * N + F[k][a]];
+            if (!(u > 0.0)) PFAIL("u <= 0");
+            H[a * m + a] = 1.19 * B.c_g * std::pow(u, -0.3);
+          }
+        }
+        if (!lqd::chol(H.data(), m)) PFAIL("chol");
+        hg[k].resize(m);
+        for (int a = 0; a < m; ++a) hg[k][a] = g[k * N + F[k][a]];
+        lqd::chol_solve(H.data(), m, hg[k].data());
+        Y[k].assign((size_t)m * nJ, 0.0);
+        col.resize(m);
+        for (int q = 0; q < nJ; ++q) {
+          for (int a = 0; a < m; ++a) col[a] = ck * Ej[(size_t)q * N + F[k][a]];
+          lqd::chol_solve(H.data(), m, col.data());
+          for (int a = 0; a < m; ++a) Y[k][(size_t)a * nJ + q] = col[a];
+        }
+        for (int p = 0; p < nJ; ++p) {
+          double acc = 0.0;
+          for (int a = 0; a < m; ++a) acc += ck * Ej[(size_t)p * N + F[k][a]] * hg[k][a];
+          rhs[p] += acc;
+          for (int q = 0; q < nJ; ++q) {
+            double s2 = 0.0;
+            for (int a = 0; a < m; ++a) s2 += ck * Ej[(size_t)p * N + F[k][a]] * Y[k][(size_t)a * nJ + q];
+            S[(size_t)p * nJ + q] += s2;
+          }
+        }
+      }
+      // H dz + C' nu = -g, C dz = h_J - C z  =>  S nu = -(C H^-1 g + h_J - C z)
+      for (int a = 0; a < nJ; ++a) nu[a] = -(rhs[a] + B.h[J[a]] - ELz[J[a]]);
+      if (nJ) {
+        if (!lqd::lu(S.data(), nJ, piv.data())) PFAIL("schur singular");
+        lqd::lu_solve(S.data(), nJ, piv.data(), nu.data());
+      }
+      step = 0.0;
+      for (int k = 0; k <= nb; ++k)
+        for (int a = 0; a < (int)F[k].size(); ++a) {
+          double d = -hg[k][a];
+          for (int q = 0; q < nJ; ++q) d -= Y[k][(size_t)a * nJ + q] * nu[q];
+          zp[k * N + F[k][a]] += d;
+          step = std::max(step, std::fabs(d));
+        }
+    }
+    // primal feasibility (with repairs for the next round)
+    const double ptol = 1e-12;
+    feasible = true;
+    for (int i = 0; i < n; ++i) {
+      if (fix[i]) continue;
+      if (zp[i] < -ptol * B.ub[i]) {
+        fix[i] = -1;
+        feasible = false;
+      } else if (zp[i] > B.ub[i] * (1.0 + ptol)) {
+        fix[i] = +1;
+        feasible = false;
+      }
+    }
+    mulL(B, zp.data(), Lz.data());
+    mulE(N, Lz.data(), ELz.data());
+    for (int j = 0; j < mg; ++j)
+      if (ELz[j] > B.h[j] + ptol * (1.0 + std::fabs(B.h[j])) && std::find(J.begin(), J.end(), j) == J.end()) {
+        J.push_back(j);
+        feasible = false;
+      }
+  }
+  if (!feasible) PFAIL("primal");
+  f_grad(B, zp.data(), g.data());
+  double gmax = 0.0;
+  for (int i = 0; i < n; ++i) gmax = std::max(gmax, std::fabs(g[i]));
+  const double dtol = 1e-9 * (1.0 + gmax);
+  std::vector<double> lgn(mg, 0.0), tN(N), tn(n);
+  for (int a = 0; a < nJ; ++a) {
+    if (nu[a] < -dtol) PFAIL("coupling dual sign");
+    lgn[J[a]] = std::max(nu[a], 0.0);
+  }
+  mulEt(N, lgn.data(), tN.data());
+  mulLt(B, tN.data(), tn.data());
+  std::vector<double> llon(n, 0.0), lhin(n, 0.0);
+  for (int i = 0; i < n; ++i) {
+    const double r = g[i] + tn[i];  // = llo - lhi at a KKT point
+    if (fix[i] < 0) {
+      if (r < -dtol) PFAIL("lower dual sign");
+      llon[i] = std::max(r, 0.0);
+    } else if (fix[i] > 0) {
+      if (r > dtol) PFAIL("upper dual sign");
+      lhin[i] = std::max(-r, 0.0);
+    } else if (std::fabs(r) > dtol) {
+      if (g_trace_polish) fprintf(stderr, "polish: stationarity %d %g tol %g\n", i, r, dtol);
+      return false;
+    }
+  }
+  z = zp;
+  llo = llon;
+  lhi = lhin;
+  lg = lgn;
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -517,6 +683,12 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
     fval = bf;
     if (best_merit <= 5e-5) status = LOMPC_OK;  // Clarabel's reduced tolerances ("almost solved")
   }
+  bool polished = false;
+  g_trace_polish = trace;
+  if (status == LOMPC_OK && polish(B, z, llo, lhi, lg, sg)) {
+    polished = true;
+    residuals();  // report the polished point
+  }
   for (int p = 0; p < P; ++p)
     for (int t = 0; t < N; ++t) {
       w_hat_s[p * N + t] = z[p * N + t];
@@ -534,6 +706,7 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
     info[2] = pres;
     info[3] = dres;
     info[4] = gap;
+    if (trace) fprintf(stderr, "bimpc: %d iterations, polished %d\n", it, (int)polished);
   }
   return status;
 }

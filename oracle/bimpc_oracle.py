@@ -165,7 +165,7 @@ class BiMPCLiteral:
             u = z[2 * self.P * N:]
             H[2 * self.P * N:, 2 * self.P * N:] += np.diag(1.19 * c_g * u ** -0.3)
             Mx = H + G.T @ (G * (lam / s)[:, None])
-            Mx[np.diag_indices(n)] += 1e-13 * (1.0 + np.max(np.diag(Mx)))
+            Mx[np.diag_indices(n)] += 1e-15 * (1.0 + np.max(np.abs(Hq)))
 
             def direction(rc):
                 rhs = -rd - G.T @ ((rc + lam * rp) / s)

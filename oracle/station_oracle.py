@@ -95,6 +95,7 @@ class OracleStation:
         for k, v in (("beta_s", beta_s), ("beta_l", beta_l), ("gamma_sm", g_s), ("gamma_lm", g_l), ("Mp_s", Mp_s),
                      ("Mp_l", Mp_l)):
             self.logs[k][:, t] = v
+        self.logs["x"][t] = self.x  # _update_logs runs before _update_state (:181-183)
         # _update_state (:331-370), ADD_RESIDUAL_CHARGE_TO_BATTERY = False
         lo, hi = MIN_INITIAL_SOC, MAX_INITIAL_SOC
         self.y_s += w0["s"]
@@ -108,5 +109,4 @@ class OracleStation:
         self._update_indices()
         u0_b = u_g[0] + (-self.cs.theta * np.sum(w0["s"]) - self.cl.theta * np.sum(w0["l"]) - self.demand[t]) / self.B
         self.x += u0_b
-        self.logs["x"][t] = self.x
         self.t += 1

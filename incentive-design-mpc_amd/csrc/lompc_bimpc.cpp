@@ -297,6 +297,9 @@ bool polish(const Bimpc& B, std::vector<double>& z, std::vector<double>& llo, st
   std::vector<double> Ej, nu, g(n), Lz(N), ELz(mg), S, rhs, col;
   std::vector<int> piv;
   int nJ = 0;
+  std::vector<double> lgn, tN(N), tn(n), llon, lhin;
+  for (int outer = 0;; ++outer) {
+  if (outer >= 8) PFAIL("active set");
   bool feasible = false;
   // rounds: a free variable that leaves its box is fixed at that bound, a violated coupling row
   // joins the active set, and the equality-constrained problem is solved again
@@ -410,27 +413,44 @@ bool polish(const Bimpc& B, std::vector<double>& z, std::vector<double>& llo, st
   double gmax = 0.0;
   for (int i = 0; i < n; ++i) gmax = std::max(gmax, std::fabs(g[i]));
   const double dtol = 1e-9 * (1.0 + gmax);
-  std::vector<double> lgn(mg, 0.0), tN(N), tn(n);
+  // dual signs: a fixed variable or an active row with the wrong-sign multiplier is released
+  bool changed = false;
+  lgn.assign(mg, 0.0);
+  std::vector<int> Jn;
   for (int a = 0; a < nJ; ++a) {
-    if (nu[a] < -dtol) PFAIL("coupling dual sign");
+    if (nu[a] < -dtol) {
+      changed = true;
+      continue;
+    }
+    Jn.push_back(J[a]);
     lgn[J[a]] = std::max(nu[a], 0.0);
   }
   mulEt(N, lgn.data(), tN.data());
   mulLt(B, tN.data(), tn.data());
-  std::vector<double> llon(n, 0.0), lhin(n, 0.0);
+  llon.assign(n, 0.0);
+  lhin.assign(n, 0.0);
   for (int i = 0; i < n; ++i) {
     const double r = g[i] + tn[i];  // = llo - lhi at a KKT point
     if (fix[i] < 0) {
-      if (r < -dtol) PFAIL("lower dual sign");
+      if (r < -dtol) {
+        fix[i] = 0;
+        changed = true;
+      }
       llon[i] = std::max(r, 0.0);
     } else if (fix[i] > 0) {
-      if (r > dtol) PFAIL("upper dual sign");
+      if (r > dtol) {
+        fix[i] = 0;
+        changed = true;
+      }
       lhin[i] = std::max(-r, 0.0);
     } else if (std::fabs(r) > dtol) {
       if (g_trace_polish) fprintf(stderr, "polish: stationarity %d %g tol %g\n", i, r, dtol);
       return false;
     }
   }
+  if (!changed) break;
+  J = Jn;
+  }  // outer
   z = zp;
   llo = llon;
   lhi = lhin;

@@ -196,7 +196,58 @@ class BiMPCLiteral:
                 trace.append((z.copy(), a, sigma))
         if trace is None:  # best iterate (numerically flat directions can stall the last steps)
             z, lam = best[1], best[2]
+            zp = self.polish(z, lam, G, h, Hq)
+            if zp is not None:
+                z, lam = zp
         return z, lam, it
+
+    def polish(self, z, lam, G, h, Hq):
+        """Dense active-set polish: rows whose multiplier exceeds their slack become equalities;
+        Newton on the equality-constrained KKT system (dense solve); accepted only if primal
+        feasible with non-negative multipliers.  Returns (z, lam) or None."""
+        n, N = self.n, self.N
+        c_g = self.bi["c_g"]
+        s = h - G @ z
+        act = np.where(lam > s)[0]
+        for _outer in range(10):  # active-set corrections: add violated rows, drop wrong-sign ones
+            zp = z.copy()
+            for _ in range(6):
+                Ga = G[act]
+                for _ in range(20):
+                    g = self._grad(zp)
+                    H = Hq.copy()
+                    u = zp[2 * self.P * N:]
+                    if np.any(u <= 0):
+                        return None
+                    H[2 * self.P * N:, 2 * self.P * N:] += np.diag(1.19 * c_g * u ** -0.3)
+                    K = np.block([[H, Ga.T], [Ga, np.zeros((len(act), len(act)))]])
+                    rhs = np.concatenate([-g, h[act] - Ga @ zp])
+                    try:
+                        sol = np.linalg.solve(K, rhs)
+                    except np.linalg.LinAlgError:
+                        sol = np.linalg.lstsq(K, rhs, rcond=1e-14)[0]
+                    dz, nu = sol[:n], sol[n:]
+                    zp = zp + dz
+                    if np.max(np.abs(dz)) <= 1e-15:
+                        break
+                viol = np.setdiff1d(np.where(G @ zp - h > 1e-12 * (1 + np.abs(h)))[0], act)
+                if len(viol) == 0:
+                    break
+                act = np.union1d(act, viol)
+            if np.any(G @ zp - h > 1e-12 * (1 + np.abs(h))):
+                return None
+            g = self._grad(zp)
+            neg = nu < -1e-9 * (1 + np.max(np.abs(g)))
+            if not np.any(neg):
+                break
+            act = act[~neg]
+        else:
+            return None
+        lam_p = np.zeros(len(h))
+        lam_p[act] = np.maximum(nu, 0.0)
+        if np.max(np.abs(g + G.T @ lam_p)) > 1e-8 * (1 + np.max(np.abs(g))):
+            return None
+        return zp, lam_p
 
     def _grad(self, z):
         import torch

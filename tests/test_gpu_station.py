@@ -67,7 +67,8 @@ def test_closed_loop_matches_oracle(gpu, monkeypatch):
     for _ in range(TF):
         so.step()
     compare_logs(logs, so.logs)
-    assert logs["statistics"]["ncharged_s"] == so.ncharged_s and logs["statistics"]["ncharged_l"] == so.ncharged_l
+    # logs hold the count before the last state update (_update_logs precedes _update_state, :181-183)
+    assert cs.ncharged_s == so.ncharged_s and cs.ncharged_l == so.ncharged_l
     np.testing.assert_allclose(cs.y_s.cpu().numpy(), so.y_s, rtol=0, atol=1e-6)
     np.testing.assert_allclose(cs.y_l.cpu().numpy(), so.y_l, rtol=0, atol=1e-6)
 

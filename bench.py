@@ -48,6 +48,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--serial", action="store_true", help="both EV types on one stream")
+    ap.add_argument("--no-station", action="store_true", help="skip the BiMPC steps/sec leg")
+    ap.add_argument("--station-evs-per-gpu", type=int, default=262144, help="EVs per GPU, half per type")
+    ap.add_argument("--station-horizon", type=int, default=48)
+    ap.add_argument("--station-steps", type=int, default=3)
+    ap.add_argument("--station-warmup", type=int, default=1)
     return ap.parse_args()
 
 
@@ -207,10 +212,81 @@ def main():
             pass
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(eng, N, args.cpu_seconds)
+    if not args.no_station:
+        del eng
+        line["bimpc"] = station_leg(args, world, dev)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def station_leg(args, world, dev):
+    """BiMPC steps/sec (the second half of BASELINE.json's metric; config 5 weak-scaled).
+
+    One step = ``ChargingStation._step`` (charging_station.py:156-185) on the engine: partition
+    statistics, the BiMPC planner (host interior point), the 2 x P sequential price loops
+    (one batched engine call per price iteration + host price QP, regularizer LP at the end)
+    and the batched w0 / price0 pass, then the state update with the aggregate demand.
+    Config 5 shape: horizon N_lo = N_bi = 48, P = 12 partitions, linear-convex prices,
+    regularizer on, the example's BiMPC constants (real_time_price_control.py:42-52), demand
+    scaled by M_2 / 500; ``--station-evs-per-gpu`` EVs per rank (2 097 152
+    at 8 GPUs), sharded by EV index with the station's all-reduces."""
+    import torch
+    import torch.distributed as dist
+
+    from lompc_amd import settings
+    from lompc_amd.charging_station import ChargingStation
+    from lompc_amd.example import DEMAND_SCALE, NUM_EVS_PER_EV_TYPE, station_consts
+
+    settings.PRINT_LEVEL = 0
+    N, P = args.station_horizon, args.partitions
+    M_2 = (args.station_evs_per_gpu // 2) * world  # EVs per type, whole job
+    steps, warm = args.station_steps, args.station_warmup
+    # storage rate / capacity 0.5 (x_max = 0.5 is one of the example's listed values, :47): at
+    # horizon 48 the example's 0.3 / 0.3 makes the first BiMPC infeasible (example.station_consts)
+    consts = station_consts(steps + warm, M_2, n_lo=N, n_bi=N, partitions=P, price_type="linear-convex",
+                            demand_scale=DEMAND_SCALE * M_2 / NUM_EVS_PER_EV_TYPE, u_b_max=0.5, x_max=0.5)
+    group = dist.group.WORLD if world > 1 else None
+    out = {"metric": "BiMPC steps/sec", "unit": "steps/s", "steps": steps, "warmup": warm,
+           "config": {"workload": f"config5 shape: {2 * M_2} EVs ({args.station_evs_per_gpu} per GPU), horizon {N}, "
+                                  f"{P} partitions per type, linear-convex prices, regularizer on, storage "
+                                  "u_b_max = x_max = 0.5, full closed-loop step",
+                      "evs_total": 2 * M_2, "horizon": N, "partitions": P}}
+    try:
+        np.random.seed(args.seed)  # the reference's legacy global stream (charging_station.py:95-100)
+        st = ChargingStation(consts, device=dev.index, group=group)
+        for _ in range(warm):
+            st._step()
+
+        def calls():
+            return st.price_solver_s.n_batched_calls + st.price_solver_l.n_batched_calls
+
+        c0 = calls()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            st._step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        stats = st.logs["statistics"]
+        it = np.concatenate([stats["niter_s"][:, warm:].ravel(), stats["niter_l"][:, warm:].ravel()])
+        ncalls = calls() - c0
+        out.update({"value": steps / dt, "ms_per_step": dt / steps * 1e3,
+                    "price_iterations_per_step": float(np.sum(it[it >= 0])) / steps,
+                    "engine_calls_per_step": ncalls / steps,
+                    "lompc_qps_per_sec_est": (ncalls + 2 * P * steps) * M_2 / P / dt})
+    except Exception as e:  # reported, never hides the QP/s line
+        out["error"] = f"{type(e).__name__}: {e}"
+    return out
 
 
 def cpu_baseline(eng, N, seconds):

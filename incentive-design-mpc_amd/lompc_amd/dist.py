@@ -18,6 +18,7 @@ from . import _lib
 _SUM_COLS = [_lib.LOMPC_STAT_COUNT, _lib.LOMPC_STAT_SUM_W0, _lib.LOMPC_STAT_SUM_PRICE0,
              _lib.LOMPC_STAT_SUM_COST, _lib.LOMPC_STAT_N_REPAIRED, _lib.LOMPC_STAT_N_FAILED,
              _lib.LOMPC_STAT_N_INVALID]
+_COLS = {}
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -51,7 +52,9 @@ def allreduce_set_results(set_sum_w, set_stats, group=None):
     import torch.distributed as dist
 
     S, N = set_sum_w.shape
-    cols = torch.as_tensor(_SUM_COLS, device=set_stats.device)
+    cols = _COLS.get(set_stats.device)
+    if cols is None:  # cached: a fresh host->device index copy per call would stall the stream
+        cols = _COLS[set_stats.device] = torch.as_tensor(_SUM_COLS, device=set_stats.device)
     packed = torch.cat([set_sum_w.reshape(-1), set_stats[:, cols].reshape(-1)])
     dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
     mx = set_stats[:, _lib.LOMPC_STAT_MAX_ERR].contiguous()

@@ -326,8 +326,9 @@ class BatchPlan:
     of one price iteration is a single ctypes call.  lmbd: contiguous fp64
     device tensor (S, 3N); lmbd_r: (S,) on the same device.  No synchronisation;
     call ``lompc.check_last()`` when the status is needed.
-    In PATH mode the call is ONE kernel launch (path cells, per-EV blocks and the
-    per-set reduction trees).
+    In PATH mode the call is three dependent launches on the plan's stream: k_path
+    (solution path per parameter set), k_eval (per-EV evaluation) and k_finalize
+    (per-set reductions); see DESIGN.md.
     """
 
     def __init__(self, lompc: "LoMPC", gamma, set_offsets, *, w_ref=None, gamma_ref=None, want_w=True,

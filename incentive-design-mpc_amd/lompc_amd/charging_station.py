@@ -81,11 +81,14 @@ def partition_stats(y, idx, P: int, group=None) -> np.ndarray:
     ranks (one MAX and one SUM all-reduce).  Returns a host (P, 4) array; empty partitions
     have count 0."""
     torch = _torch()
-    dev = y.device
-    cnt = torch.bincount(idx, minlength=P).to(torch.float64)
-    sm = torch.zeros(P, dtype=torch.float64, device=dev).index_add_(0, idx, y)
-    mx = torch.full((P,), -float("inf"), dtype=torch.float64, device=dev).scatter_reduce(0, idx, y, "amax")
-    mn = torch.full((P,), float("inf"), dtype=torch.float64, device=dev).scatter_reduce(0, idx, y, "amin")
+    # masked column reductions over an (n, P) view: P is small, and scatter/atomic forms
+    # (bincount, index_add_, scatter_reduce) serialise n updates on P addresses
+    onehot = idx.unsqueeze(1) == torch.arange(P, device=y.device).unsqueeze(0)
+    yy = y.unsqueeze(1)
+    cnt = onehot.sum(0).to(torch.float64)
+    sm = torch.where(onehot, yy, 0.0).sum(0)
+    mx = torch.where(onehot, yy, -float("inf")).amax(0)
+    mn = torch.where(onehot, yy, float("inf")).amin(0)
     if group is not None:
         import torch.distributed as dist
 
@@ -350,7 +353,7 @@ class ChargingStation:
         torch = _torch()
         N, P = self.N_lo, self.P
         perm = torch.argsort(idx, stable=True)
-        counts = torch.bincount(idx, minlength=P)
+        counts = (idx.unsqueeze(1) == torch.arange(P, device=idx.device).unsqueeze(0)).sum(0)
         off = np.concatenate([[0], np.cumsum(counts.cpu().numpy())]).astype(np.int64)
         gamma = (solver.consts.y_max - y)[perm].contiguous()
         lm = np.zeros((P, 3 * N))

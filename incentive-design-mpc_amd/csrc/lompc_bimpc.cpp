@@ -123,8 +123,7 @@ struct Newton {
   std::vector<double> Hf;   // [nb][N*N] Cholesky factors of H_k + D_k
   std::vector<double> Du;   // [N]
   std::vector<double> Q;    // [N*N]
-  std::vector<double> K;    // [N*N] LU of I + T Q
-  std::vector<int> piv;
+  std::vector<double> W;    // [4N*4N] Cholesky of D_g^-1 + E T E'
   std::vector<double> ck;
 
   // factor M for the current iterate; dk: [n] box barrier diagonal, dg: [4N] coupling D_g
@@ -181,15 +180,36 @@ struct Newton {
         for (int j = 0; j < N; ++j) Q[i * N + j] = suf[std::max(i, j)];
       for (int i = 0; i < N; ++i) Q[i * N + i] += dg[i] + dg[N + i];
     }
-    K.assign((size_t)N * N, 0.0);
-    for (int i = 0; i < N; ++i)
+    // Woodbury in the coupling rows: M^-1 = Hb^-1 - Hb^-1 L'E' W^-1 E L Hb^-1 with the SPD
+    // W = D_g^-1 + E T E' (4N x 4N).  Unlike a solve with I + T Q, W stays well scaled as the
+    // interior point converges: active rows (D_g -> inf) keep E T E', inactive rows become a
+    // large diagonal.
+    const int m = 4 * N;
+    std::vector<double> ET((size_t)m * N);  // rows of E T: -T, T, -A T, A T
+    for (int t = 0; t < N; ++t)
       for (int j = 0; j < N; ++j) {
-        double a = (i == j) ? 1.0 : 0.0;
-        for (int l = 0; l < N; ++l) a += T[i * N + l] * Q[l * N + j];
-        K[i * N + j] = a;
+        const double v = T[t * N + j];
+        const double pv = (t ? ET[(size_t)(3 * N + t - 1) * N + j] : 0.0) + v;  // (A T)_t = sum_{u<=t} T_u
+        ET[(size_t)t * N + j] = -v;
+        ET[(size_t)(N + t) * N + j] = v;
+        ET[(size_t)(2 * N + t) * N + j] = -pv;
+        ET[(size_t)(3 * N + t) * N + j] = pv;
       }
-    piv.assign(N, 0);
-    return lqd::lu(K.data(), N, piv.data());
+    W.assign((size_t)m * m, 0.0);
+    std::vector<double> ps(N);
+    for (int a = 0; a < m; ++a) {
+      const double* e = &ET[(size_t)a * N];
+      double acc = 0.0;
+      for (int t = 0; t < N; ++t) ps[t] = (acc += e[t]);
+      for (int t = 0; t < N; ++t) {  // (E T E')_{a,b} for the four row blocks b of E
+        W[(size_t)a * m + t] = -e[t];
+        W[(size_t)a * m + N + t] = e[t];
+        W[(size_t)a * m + 2 * N + t] = -ps[t];
+        W[(size_t)a * m + 3 * N + t] = ps[t];
+      }
+      W[(size_t)a * m + a] += 1.0 / dg[a];
+    }
+    return lqd::chol(W.data(), m);
   }
 
   void hb_solve(double* x) const {  // Hb^-1 in place
@@ -250,16 +270,13 @@ struct Newton {
   }
 
   void solve_reg(const Bimpc& B, const double* rhs, double* dz) const {
-    std::vector<double> t1(rhs, rhs + n), y(N), Qy(N), tmp(n);
+    std::vector<double> t1(rhs, rhs + n), y(N), ey(4 * N), g(N), tmp(n);
     hb_solve(t1.data());
     mulL(B, t1.data(), y.data());
-    lqd::lu_solve(K.data(), N, piv.data(), y.data());
-    for (int i = 0; i < N; ++i) {
-      double a = 0.0;
-      for (int j = 0; j < N; ++j) a += Q[i * N + j] * y[j];
-      Qy[i] = a;
-    }
-    mulLt(B, Qy.data(), tmp.data());
+    mulE(N, y.data(), ey.data());
+    lqd::chol_solve(W.data(), 4 * N, ey.data());
+    mulEt(N, ey.data(), g.data());
+    mulLt(B, g.data(), tmp.data());
     hb_solve(tmp.data());
     for (int i = 0; i < n; ++i) dz[i] = t1[i] - tmp[i];
   }
@@ -279,6 +296,42 @@ double max_step(const std::vector<double>& s, const std::vector<double>& ds) {
 // IPM point only if it is primal feasible and every multiplier has the right sign — then it is
 // the exact optimum up to round-off.
 static bool g_trace_polish = false;
+
+// Cholesky of the symmetric PSD matrix S (nJ x nJ) in row order; the rows whose pivot is below
+// 1e-12 of the largest diagonal are linearly dependent on earlier rows: remove them from J.
+// Returns true when J changed.
+static bool prune_dependent(const std::vector<double>& S, int nJ, std::vector<int>& J) {
+  std::vector<double> L(S);
+  std::vector<char> drop(nJ, 0);
+  double dmax = 0.0;
+  for (int a = 0; a < nJ; ++a) dmax = std::max(dmax, S[(size_t)a * nJ + a]);
+  const double tol = 1e-12 * dmax;
+  bool any = false;
+  for (int j = 0; j < nJ; ++j) {
+    double d = L[(size_t)j * nJ + j];
+    for (int k = 0; k < j; ++k)
+      if (!drop[k]) d -= L[(size_t)j * nJ + k] * L[(size_t)j * nJ + k];
+    if (!(d > tol)) {
+      drop[j] = 1;
+      any = true;
+      continue;
+    }
+    const double r = std::sqrt(d);
+    L[(size_t)j * nJ + j] = r;
+    for (int i = j + 1; i < nJ; ++i) {
+      double t = L[(size_t)i * nJ + j];
+      for (int k = 0; k < j; ++k)
+        if (!drop[k]) t -= L[(size_t)i * nJ + k] * L[(size_t)j * nJ + k];
+      L[(size_t)i * nJ + j] = t / r;
+    }
+  }
+  if (!any) return false;
+  std::vector<int> Jn;
+  for (int a = 0; a < nJ; ++a)
+    if (!drop[a]) Jn.push_back(J[a]);
+  J.swap(Jn);
+  return true;
+}
 #define PFAIL(msg) do { if (g_trace_polish) fprintf(stderr, "polish: %s\n", msg); return false; } while (0)
 bool polish(const Bimpc& B, std::vector<double>& z, std::vector<double>& llo, std::vector<double>& lhi,
             std::vector<double>& lg, const std::vector<double>& sg) {
@@ -303,7 +356,8 @@ bool polish(const Bimpc& B, std::vector<double>& z, std::vector<double>& llo, st
   bool feasible = false;
   // rounds: a free variable that leaves its box is fixed at that bound, a violated coupling row
   // joins the active set, and the equality-constrained problem is solved again
-  for (int round = 0; round < 6 && !feasible; ++round) {
+  for (int round = 0, prunes = 0; round < 6 && !feasible; ++round) {
+    bool pruned = false;
     nJ = (int)J.size();
     Ej.assign((size_t)nJ * N, 0.0);  // active rows of E = [-I; I; -A; A]
     for (int a = 0; a < nJ; ++a) {
@@ -372,6 +426,13 @@ bool polish(const Bimpc& B, std::vector<double>& z, std::vector<double>& llo, st
           }
         }
       }
+      // degenerate vertex: an active row that is (numerically) a combination of earlier ones —
+      // e.g. one touching only fixed variables — gives a zero pivot of the PSD Schur matrix;
+      // drop it (its constraint is implied by the others) and solve again
+      if (nJ && prune_dependent(S, nJ, J)) {
+        pruned = true;
+        break;
+      }
       // H dz + C' nu = -g, C dz = h_J - C z  =>  S nu = -(C H^-1 g + h_J - C z)
       for (int a = 0; a < nJ; ++a) nu[a] = -(rhs[a] + B.h[J[a]] - ELz[J[a]]);
       if (nJ) {
@@ -386,6 +447,11 @@ bool polish(const Bimpc& B, std::vector<double>& z, std::vector<double>& llo, st
           zp[k * N + F[k][a]] += d;
           step = std::max(step, std::fabs(d));
         }
+    }
+    if (pruned) {
+      if (++prunes > B.mg) PFAIL("prune");
+      --round;
+      continue;
     }
     // primal feasibility (with repairs for the next round)
     const double ptol = 1e-12;
@@ -621,7 +687,7 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
   };
   // best iterate by the worst relative KKT measure; returned when the iteration stalls (the
   // reference accepts Clarabel's "optimal_inaccurate" silently, lompc.py / bimpc.py never check status)
-  std::vector<double> zb(n), llob(n), lhib(n), lgb(mg);
+  std::vector<double> zb(n), llob(n), lhib(n), lgb(mg), sgb(mg);
   double best_merit = INFINITY, bpres = 0, bdres = 0, bgap = 0, bf = 0;
   int since_best = 0;
   for (it = 0; it < max_iter; ++it) {
@@ -636,6 +702,7 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
       llob = llo;
       lhib = lhi;
       lgb = lg;
+      sgb = sg;
       bpres = pres;
       bdres = dres;
       bgap = gap;
@@ -697,6 +764,7 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
     llo = llob;
     lhi = lhib;
     lg = lgb;
+    sg = sgb;
     pres = bpres;
     dres = bdres;
     gap = bgap;
@@ -705,8 +773,13 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
   }
   bool polished = false;
   g_trace_polish = trace;
-  if (status == LOMPC_OK && polish(B, z, llo, lhi, lg, sg)) {
+  // the polish certifies its own result (primal feasibility, multiplier signs, stationarity), so
+  // it also runs from the best iterate of a stalled IPM: the late iterations of the exp-weighted
+  // cost (weights 5^(t-N+1)) lose Newton accuracy before the gap closes, while the active set is
+  // already identified
+  if (std::isfinite(best_merit) && polish(B, z, llo, lhi, lg, sg)) {
     polished = true;
+    status = LOMPC_OK;
     residuals();  // report the polished point
   }
   for (int p = 0; p < P; ++p)

@@ -121,6 +121,17 @@ __device__ __forceinline__ EVOut wave_outputs(const QPConst& q, const double* __
   return o;
 }
 
+// write-through (sc1) stores: 16 B through a buffer descriptor (aux 16 = sc1), 8 B as a relaxed
+// agent-scope atomic store (global_store_dwordx2 ... sc1)
+typedef unsigned int lq_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_wt16(__amdgpu_buffer_rsrc_t rs, int off, double x, double y) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(lq_v4u, make_double2(x, y)), rs, off, 0, 16);
+}
+__device__ __forceinline__ void st_wt8(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Shared epilogue of the per-EV kernels for one wave of EVs [start, start+64) of set s.
 // !INPLACE (K2d): ok lanes carry a certified w[] and outputs; valid-but-not-ok lanes
 //   are listed for the repair pass in k_finalize (their rows are rewritten there).
@@ -152,18 +163,21 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const
     if (lane == 0) a.fail_cnt[b] = __popcll(fm);
   }
   __syncthreads();
-  // coalesced stores (row-major w[B][N])
+  // coalesced WRITE-THROUGH stores (row-major w[B][N]): sc1 stores leave no dirty lines in the
+  // XCD's L2, so the kernel boundary behind this launch has no L2 writeback of the outputs to
+  // wait for (MI355X_MICROARCH.md: boundary + B / 6 TB/s for B dirty bytes; 16-B sc1 ~ plain)
   const int nrow = (int)min((int64_t)EVAL_BLOCK, end - start);
   if (a.w && nrow > 0) {
     double* wo = a.w + (size_t)start * N;
     if (nrow == EVAL_BLOCK && (N % 2) == 0) {  // full tile, 16 B per lane (start*N*8 is 16-B aligned)
-      double2* wo2 = reinterpret_cast<double2*>(wo);
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(wo, (short)0, EVAL_BLOCK * N * (int)sizeof(double), 0x00020000);
 #pragma unroll
       for (int r = 0; r < NMAX / 2; ++r) {
         if (r < N / 2) {
           const int e = 2 * (lane + EVAL_BLOCK * r);  // even element index
           const int row = e / N, col = e - row * N;
-          wo2[lane + EVAL_BLOCK * r] = make_double2(tile[row * TS + col], tile[row * TS + col + 1]);
+          st_wt16(rs, (lane + EVAL_BLOCK * r) * 16, tile[row * TS + col], tile[row * TS + col + 1]);
         }
       }
     } else {
@@ -171,7 +185,7 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const
       const int q64 = EVAL_BLOCK / N, r64 = EVAL_BLOCK % N;
       int row = lane / N, col = lane % N;
       for (int e = lane; e < tot; e += EVAL_BLOCK) {
-        wo[e] = tile[row * TS + col];
+        st_wt8(wo + e, tile[row * TS + col]);
         row += q64;
         col += r64;
         if (col >= N) {
@@ -182,8 +196,8 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const
     }
   }
   if (active) {
-    if (a.cost) a.cost[i] = tile[lane * TS + N];
-    if (a.w0) a.w0[i] = tile[lane * TS + 0];
+    if (a.cost) st_wt8(a.cost + i, tile[lane * TS + N]);
+    if (a.w0) st_wt8(a.w0 + i, tile[lane * TS + 0]);
     if (a.status)
       a.status[i] = !valid ? LOMPC_QP_INVALID : (ok ? ((INPLACE && rep) ? LOMPC_QP_REPAIRED : LOMPC_QP_OK) : LOMPC_QP_FAILED);
   }
@@ -457,7 +471,19 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a, int epo
   const double invh = (double)LQ_G / q.y_max;
   const int cell = valid ? min(LQ_G - 1, (int)(g * invh)) : 0;
   const size_t cb = (size_t)s * LQ_G + cell;
+  // the cell count and the piece ends are loaded together (cb is always a valid cell: one
+  // dependent memory round less than loading the ends behind the count test)
   const int raw = a.tab.cnt[cb];
+  double ge[LQ_PPL];
+  {
+    const double2* g2 = reinterpret_cast<const double2*>(a.tab.gend + cb * LQ_PPL);
+#pragma unroll
+    for (int pp = 0; pp < LQ_PPL / 2; ++pp) {
+      const double2 v = g2[pp];
+      ge[2 * pp] = v.x;
+      ge[2 * pp + 1] = v.y;
+    }
+  }
   const bool ready = cell_epoch(raw) == epoch;  // written by this parameter epoch
   const int cnt = (valid && ready) ? cell_pieces(raw) : 0;
   double w[NMAX];
@@ -466,9 +492,6 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a, int epo
   bool ok = false;
   EVOut o{0.0, 0.0, 0.0};
   if (cnt > 0) {
-    double ge[LQ_PPL];
-#pragma unroll
-    for (int pp = 0; pp < LQ_PPL; ++pp) ge[pp] = a.tab.gend[cb * LQ_PPL + pp];
     int p = cnt - 1;
     double glast = -1.0;
 #pragma unroll

@@ -26,7 +26,7 @@ for s in $STEPS; do
     k1) run k1 300 python scripts/k1_stats.py ;;
     host) run host 300 python scripts/host_overhead.py ;;
     fail) run fail 600 python scripts/find_failures.py ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-station ;;
     *) echo "unknown step $s" ;;
   esac
 done

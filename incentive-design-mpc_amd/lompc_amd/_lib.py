@@ -13,6 +13,9 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblompc_amd.so")
+# diagnostics only (scripts/ sweeps of compile-time variants): another in-tree build of the same C-ABI
+if os.environ.get("LOMPC_LIB"):
+    LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ["LOMPC_LIB"]))
 
 # status codes (include/lompc_amd.h)
 LOMPC_OK = 0

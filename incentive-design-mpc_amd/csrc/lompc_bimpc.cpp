@@ -26,6 +26,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <vector>
 
@@ -118,6 +123,125 @@ void mulEt(int N, const double* v, double* out) {
   }
 }
 
+// Persistent host worker pool for the independent per-block work of the Newton system
+// (2P blocks of N x N factorizations / solves).  Each block writes only its own buffers and
+// block results are combined afterwards in block order, so results do not depend on the
+// thread count.  LOMPC_HOST_THREADS caps the workers (default min(8, cores)).
+class BlockPool {
+ public:
+  static BlockPool& get() {
+    static BlockPool p;
+    return p;
+  }
+  void run(int n, const std::function<void(int)>& fn) {
+    if (workers_.empty() || n <= 1) {
+      for (int i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    std::lock_guard<std::mutex> call(call_mu_);  // one parallel region at a time
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_ = n;
+      next_.store(0);
+      busy_.store((int)workers_.size());
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    drain();
+    while (busy_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    fn_ = nullptr;
+  }
+  ~BlockPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_.store(true);
+      gen_.fetch_add(1);
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+
+ private:
+  BlockPool() {
+    int nt = (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char* e = getenv("LOMPC_HOST_THREADS")) nt = std::max(1, atoi(e));
+    for (int i = 1; i < nt; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  void drain() {
+    for (int i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
+  }
+  // workers spin briefly on the generation counter (a region follows the previous one within
+  // microseconds inside a solve) and sleep on the condition variable otherwise
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      bool got = false;
+      for (int spin = 0; spin < 20000 && !got; ++spin) {
+        got = gen_.load(std::memory_order_acquire) != seen;
+        if (!got) std::this_thread::yield();
+      }
+      if (!got) {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_.load() != seen; });
+      }
+      seen = gen_.load(std::memory_order_acquire);
+      if (stop_.load()) return;
+      drain();
+      busy_.fetch_sub(1, std::memory_order_acq_rel);
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex mu_, call_mu_;
+  std::condition_variable cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int n_ = 0;
+  std::atomic<int> next_{0}, busy_{0};
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<bool> stop_{false};
+};
+
+// Right-looking blocked Cholesky (row-major, lower factor in place like lqd::chol) with the
+// panel solves and the trailing updates of each step spread over the pool; used for the
+// 4N x 4N coupling matrix W.  Every entry is produced by exactly one task, so the result does
+// not depend on the thread count.
+static bool chol_blocked(double* a, int m) {
+  constexpr int BS = 32;
+  const int nbk = (m + BS - 1) / BS;
+  if (nbk <= 2) return lqd::chol(a, m);
+  for (int kb = 0; kb < nbk; ++kb) {
+    const int k0 = kb * BS, k1 = std::min(m, k0 + BS);
+    // diagonal block
+    for (int j = k0; j < k1; ++j) {
+      double* aj = a + (size_t)j * m;
+      const double s = aj[j] - lqd::dot(aj + k0, aj + k0, j - k0);
+      if (!(s > 0.0)) return false;
+      const double d = std::sqrt(s);
+      aj[j] = d;
+      for (int i = j + 1; i < k1; ++i) {
+        double* ai = a + (size_t)i * m;
+        ai[j] = (ai[j] - lqd::dot(ai + k0, aj + k0, j - k0)) / d;
+      }
+    }
+    if (k1 >= m) break;
+    // panel rows below: row i of the panel solves L_kk x = a_i (forward substitution)
+    BlockPool::get().run(m - k1, [&](int r) {
+      double* ai = a + (size_t)(k1 + r) * m;
+      for (int j = k0; j < k1; ++j) {
+        const double* aj = a + (size_t)j * m;
+        ai[j] = (ai[j] - lqd::dot(ai + k0, aj + k0, j - k0)) / aj[j];
+      }
+    });
+    // trailing update of the lower triangle, one task per row (longest rows first)
+    BlockPool::get().run(m - k1, [&](int r) {
+      const int i = m - 1 - r;
+      double* ai = a + (size_t)i * m;
+      for (int j = k1; j <= i; ++j) ai[j] -= lqd::dot(ai + k0, a + (size_t)j * m + k0, k1 - k0);
+    });
+  }
+  return true;
+}
+
 struct Newton {
   int N = 0, nb = 0, n = 0;
   std::vector<double> Hf;   // [nb][N*N] Cholesky factors of H_k + D_k
@@ -125,6 +249,7 @@ struct Newton {
   std::vector<double> Q;    // [N*N]
   std::vector<double> W;    // [4N*4N] Cholesky of D_g^-1 + E T E'
   std::vector<double> ck;
+  std::vector<double> Xk;   // [nb][N*N] H_k^-1 (scratch)
 
   // factor M for the current iterate; dk: [n] box barrier diagonal, dg: [4N] coupling D_g
   bool factor(const Bimpc& B, const double* z, const double* dbox, const double* dg) {
@@ -133,12 +258,14 @@ struct Newton {
     n = B.n;
     ck = B.ck;
     Hf.assign((size_t)nb * N * N, 0.0);
-    std::vector<double> T((size_t)N * N, 0.0), X((size_t)N * N), col(N);
-    for (int k = 0; k < nb; ++k) {
+    Xk.resize((size_t)nb * N * N);
+    std::vector<double> T((size_t)N * N, 0.0);
+    std::vector<char> okk(nb, 1);
+    BlockPool::get().run(nb, [&](int k) {
       double* H = &Hf[(size_t)k * N * N];
       // 2 delta A'Omega A: (i,j) -> 2 delta sum_{t >= max(i,j)} omega_t
       double s = 0.0;
-      std::vector<double> suf(N);
+      std::vector<double> suf(N), work((size_t)N * N);
       for (int t = N - 1; t >= 0; --t) {
         s += B.omega[k * N + t];
         suf[t] = 2.0 * B.delta * s;
@@ -150,15 +277,18 @@ struct Newton {
       // curvature); iterative refinement against the exact matrix removes its bias
       const double rho = 1e-11 * (1.0 + suf[0]);  // relative to the charging curvature, not the barrier
       for (int i = 0; i < N; ++i) H[i * N + i] += rho;
-      if (!lqd::chol(H, N)) return false;
-      if (ck[k] != 0.0) {  // T += c_k^2 H_k^-1
-        for (int j = 0; j < N; ++j) {
-          std::fill(col.begin(), col.end(), 0.0);
-          col[j] = 1.0;
-          lqd::chol_solve(H, N, col.data());
-          for (int i = 0; i < N; ++i) T[i * N + j] += ck[k] * ck[k] * col[i];
-        }
+      if (!lqd::chol(H, N)) {
+        okk[k] = 0;
+        return;
       }
+      if (ck[k] != 0.0) lqd::chol_inverse(H, N, &Xk[(size_t)k * N * N], work.data());  // H_k^-1
+    });
+    for (int k = 0; k < nb; ++k) {
+      if (!okk[k]) return false;
+      if (ck[k] == 0.0) continue;
+      const double c2 = ck[k] * ck[k];  // T += c_k^2 H_k^-1, in block order
+      const double* X = &Xk[(size_t)k * N * N];
+      for (size_t e = 0; e < (size_t)N * N; ++e) T[e] += c2 * X[e];
     }
     Du.assign(N, 0.0);
     for (int t = 0; t < N; ++t) {
@@ -209,7 +339,7 @@ struct Newton {
       }
       W[(size_t)a * m + a] += 1.0 / dg[a];
     }
-    return lqd::chol(W.data(), m);
+    return chol_blocked(W.data(), m);
   }
 
   void hb_solve(double* x) const {  // Hb^-1 in place

@@ -607,18 +607,19 @@ __global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode,
   // ---- (1) reduction of the workgroup partials (their N_FAILED column = pending repairs)
   for (int c = lane; c < W; c += 64) {
     const bool is_max = (c == N + PX_MAX_ERR);
+    // 16 independent (predicated) loads per round: one memory round trip per 256 partial
+    // rows of the set instead of one per row of the tail
+    constexpr int U = 16;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    int b = b0 + wv;
-    for (; b + 48 < b1; b += 64) {
+    for (int b = b0 + wv; b < b1; b += 16 * U) {
+      double v[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const double v = a.partial[(size_t)(b + 16 * u) * W + c];
-        acc[u] = is_max ? fmax(acc[u], v) : acc[u] + v;
+      for (int u = 0; u < U; ++u) {
+        const int bb = b + 16 * u;
+        v[u] = bb < b1 ? a.partial[(size_t)bb * W + c] : 0.0;  // 0: neutral for sums and for max of errors >= 0
       }
-    }
-    for (; b < b1; b += 16) {
-      const double v = a.partial[(size_t)b * W + c];
-      acc[0] = is_max ? fmax(acc[0], v) : acc[0] + v;
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u & 3] = is_max ? fmax(acc[u & 3], v[u]) : acc[u & 3] + v[u];
     }
     red[wv][c] = is_max ? fmax(fmax(acc[0], acc[1]), fmax(acc[2], acc[3])) : (acc[0] + acc[1]) + (acc[2] + acc[3]);
   }

@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--station-horizon", type=int, default=48)
     ap.add_argument("--station-steps", type=int, default=3)
     ap.add_argument("--station-warmup", type=int, default=1)
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL (the product path); gloo only to rehearse world > 1 on one GPU")
     return ap.parse_args()
 
 
@@ -69,8 +71,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        # one rank per GPU; with fewer GPUs than ranks (a gloo rehearsal on one card) ranks share
+        ndev = torch.cuda.device_count()
+        idx = local % max(ndev, 1)
+        torch.cuda.set_device(idx)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{idx}"))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device(f"cuda:{torch.cuda.current_device()}")

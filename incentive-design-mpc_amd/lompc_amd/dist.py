@@ -4,10 +4,12 @@ The per-EV QPs are independent (price_solver.py:203-209); the only exchange
 step of a price iteration is the set of per-partition reductions the
 PriceSolver consumes (sum of w, max A_bar error, sum of w0 / price0 — the
 aggregate demand of charging_station.py:356-366).  Each rank solves a
-contiguous shard of every set's EVs; ``allreduce_set_results`` then combines
-the fused per-set reductions with ONE sum all-reduce and ONE max all-reduce
-(RCCL over xGMI with the "nccl" backend; gloo on CPU in the tests).  Payload
-is S * (N + 7) doubles — a few KB — so the collective is latency-bound.
+contiguous shard of every set's EVs; ``combine_set_results`` then combines
+the fused per-set reductions (of one or several contexts, e.g. both EV types)
+with ONE all-gather and a local rank-ordered sum / max (RCCL over xGMI with
+the "nccl" backend; gloo on CPU in the tests).  Payload is S * (N + 8) doubles
+per rank — a few KB — so the collective is latency-bound and one collective
+per step beats a sum plus a max all-reduce per context.
 """
 from __future__ import annotations
 
@@ -15,10 +17,6 @@ import numpy as np
 
 from . import _lib
 
-_SUM_COLS = [_lib.LOMPC_STAT_COUNT, _lib.LOMPC_STAT_SUM_W0, _lib.LOMPC_STAT_SUM_PRICE0,
-             _lib.LOMPC_STAT_SUM_COST, _lib.LOMPC_STAT_N_REPAIRED, _lib.LOMPC_STAT_N_FAILED,
-             _lib.LOMPC_STAT_N_INVALID]
-_COLS = {}
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -48,18 +46,42 @@ def allreduce_set_results(set_sum_w, set_stats, group=None):
 
     Sum columns: set_sum_w and the count/sum/number columns of set_stats;
     max column: LOMPC_STAT_MAX_ERR."""
+    combine_set_results([(set_sum_w, set_stats)], group=group)
+    return set_sum_w, set_stats
+
+
+def combine_set_results(pairs, group=None):
+    """Combine several (set_sum_w, set_stats) pairs (e.g. both EV types of a step) with ONE
+    collective: every rank's packed records are all-gathered (RCCL over xGMI; ~KB payload, so
+    one latency instead of a sum and a max all-reduce per pair), then reduced locally in rank
+    order — sums for every column, max for LOMPC_STAT_MAX_ERR.  In place; deterministic."""
     import torch
     import torch.distributed as dist
 
-    S, N = set_sum_w.shape
-    cols = _COLS.get(set_stats.device)
-    if cols is None:  # cached: a fresh host->device index copy per call would stall the stream
-        cols = _COLS[set_stats.device] = torch.as_tensor(_SUM_COLS, device=set_stats.device)
-    packed = torch.cat([set_sum_w.reshape(-1), set_stats[:, cols].reshape(-1)])
-    dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
-    mx = set_stats[:, _lib.LOMPC_STAT_MAX_ERR].contiguous()
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
-    set_sum_w.copy_(packed[: S * N].reshape(S, N))
-    set_stats[:, cols] = packed[S * N:].reshape(S, len(_SUM_COLS))
-    set_stats[:, _lib.LOMPC_STAT_MAX_ERR] = mx
-    return set_sum_w, set_stats
+    world = dist.get_world_size(group)
+    flat = [torch.cat([sw.reshape(-1), st.reshape(-1)]) for sw, st in pairs]
+    packed = torch.cat(flat) if len(flat) > 1 else flat[0]
+    L = packed.numel()
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty(world * L, dtype=packed.dtype, device=packed.device)
+        dist.all_gather_into_tensor(out, packed, group=group)
+        rows = out.view(world, L)
+    else:  # gloo (CPU tests, one-GPU rehearsals)
+        parts = [torch.empty_like(packed) for _ in range(world)]
+        dist.all_gather(parts, packed, group=group)
+        rows = torch.stack(parts)
+    tot = rows[0].clone()
+    for r in range(1, world):  # fixed rank order
+        tot += rows[r]
+    mx = rows.amax(dim=0)
+    off = 0
+    for sw, st in pairs:
+        S, N = sw.shape
+        sw.copy_(tot[off:off + S * N].view(S, N))
+        off += S * N
+        K = st.shape[1]
+        sums = tot[off:off + S * K].view(S, K)
+        maxes = mx[off:off + S * K].view(S, K)
+        st.copy_(sums)
+        st[:, _lib.LOMPC_STAT_MAX_ERR] = maxes[:, _lib.LOMPC_STAT_MAX_ERR]
+        off += S * K

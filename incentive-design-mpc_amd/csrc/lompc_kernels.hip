@@ -249,6 +249,7 @@ struct PathArgs {
   const double* lmbd_r;
   const double* w_ref;
   const double* gamma_ref;
+  const double* window;  // [S][2] gamma window of the path, or null = [0, y_max]
   double* setdata;
   uint8_t* central;
   int* errflag;
@@ -299,6 +300,17 @@ __device__ __forceinline__ void path_cell(const QPConst& q, const PathArgs& pa, 
     y.v[0] = wr_nat;
     Ywr = lqw::wave_scan(y, N).v[0];
   }
+  // gamma window of this set's path (lompc_set_gamma_window), widened by a margin
+  double wlo = 0.0, whi = q.y_max;
+  if (pa.window) {
+    const double mg = 1e-7 * q.y_max;
+    wlo = fmin(fmax(pa.window[2 * s] - mg, 0.0), q.y_max);
+    whi = fmin(fmax(pa.window[2 * s + 1] + mg, wlo + mg), q.y_max);
+    if (!(whi > wlo)) {  // window at y_max (or NaN input): full range
+      wlo = 0.0;
+      whi = q.y_max;
+    }
+  }
   if (cell == 0) {  // one block per set writes the derived set record
     const int SD = lq_sd(N);
     double* out = setdata + (size_t)s * SD;
@@ -318,6 +330,8 @@ __device__ __forceinline__ void path_cell(const QPConst& q, const PathArgs& pa, 
       out[3 * N + 5] = lr / q.delta;  // kappa, price_solver.py:191
       out[3 * N + 6] = gamma_ref ? gamma_ref[s] : 0.5 * q.y_max;
       out[3 * N + 7] = w_ref ? 1.0 : 0.0;
+      out[3 * N + 8] = wlo;                         // path window start
+      out[3 * N + 9] = (double)LQ_G / (whi - wlo);  // cells per unit gamma
     }
   }
   if (mode == LOMPC_MODE_PATH_REPAIR) {  // diagnostics: no table, every EV re-solved
@@ -332,9 +346,9 @@ __device__ __forceinline__ void path_cell(const QPConst& q, const PathArgs& pa, 
     central[(size_t)s * LQ_STB + lane] = (uint8_t)(lane < N ? sl : 0);
     return;
   }
-  const double h = q.y_max / (double)LQ_G;
-  const double glo = (double)cell * h;
-  const double ghi = (cell == LQ_G - 1) ? q.y_max : (double)(cell + 1) * h;
+  const double h = (whi - wlo) / (double)LQ_G;
+  const double glo = cell == 0 ? wlo : fma((double)cell, h, wlo);
+  const double ghi = (cell == LQ_G - 1) ? whi : fma((double)(cell + 1), h, wlo);
   const size_t cb = (size_t)s * LQ_G + cell;
   int sl = lane < N ? 1 : 0;
   double w = 0.0, r = 0.0;
@@ -468,8 +482,9 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a, int epo
   const double* __restrict__ sd = a.setdata + (size_t)s * lq_sd(N);
   const double g = active ? a.gamma[i] : 0.0;
   const bool valid = active && (g >= 0.0) && (g <= q.y_max);
-  const double invh = (double)LQ_G / q.y_max;
-  const int cell = valid ? min(LQ_G - 1, (int)(g * invh)) : 0;
+  const double wlo = sd[3 * N + 8], invh = sd[3 * N + 9];  // path window (uniform loads)
+  const bool inwin = g >= wlo;                             // below the window: re-solved
+  const int cell = valid ? max(0, min(LQ_G - 1, (int)((g - wlo) * invh))) : 0;
   const size_t cb = (size_t)s * LQ_G + cell;
   // the cell count and the piece ends are loaded together (cb is always a valid cell: one
   // dependent memory round less than loading the ends behind the count test)
@@ -485,7 +500,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a, int epo
     }
   }
   const bool ready = cell_epoch(raw) == epoch;  // written by this parameter epoch
-  const int cnt = (valid && ready) ? cell_pieces(raw) : 0;
+  const int cnt = (valid && ready && inwin) ? cell_pieces(raw) : 0;
   double w[NMAX];
 #pragma unroll
   for (int t = 0; t < NMAX; ++t) w[t] = 0.0;
@@ -720,6 +735,7 @@ struct lompc_ctx {
   PathTable tab{nullptr, nullptr, nullptr, nullptr, nullptr};
   uint8_t* d_central = nullptr;
   int* d_errflag = nullptr;
+  const double* d_window = nullptr;  // lompc_set_gamma_window (caller-owned, sticky)
   int params_mode = -1;
   // batch workspaces
   int64_t nblk_cap = 0, soff_cap = 0, stats_cap = 0;
@@ -967,9 +983,16 @@ static int prepare_params(lompc_ctx* c, int64_t S, const double* lmbd, const dou
   pa->lmbd_r = lmbd_r;
   pa->w_ref = w_ref;
   pa->gamma_ref = gamma_ref;
+  pa->window = c->mode != LOMPC_MODE_DIRECT ? c->d_window : nullptr;
   pa->setdata = c->d_setdata;
   pa->central = c->d_central;
   pa->errflag = c->d_errflag;
+  return LOMPC_OK;
+}
+
+int lompc_set_gamma_window(lompc_ctx* c, const double* window) {
+  if (!c) return LOMPC_ERR_INVALID_ARG;
+  c->d_window = window;
   return LOMPC_OK;
 }
 

@@ -56,7 +56,7 @@ struct QPConst {
 // Per-set data record (doubles), stride SD(N) = 3N + 8:
 //   [0,N) d   [N,2N) e   [2N,3N) w_ref
 //   3N+0 c0, +1 lmbd1_0, +2 lmbd2_0, +3 lmbd3_0, +4 lmbd_r, +5 kappa, +6 gamma_ref, +7 has_wref
-__host__ __device__ inline int lq_sd(int N) { return 3 * N + 8; }
+__host__ __device__ inline int lq_sd(int N) { return 3 * N + 10; }  // + gamma window (lo, G / width)
 
 // Path table (device pointers). Cell l of set s covers gamma in [l h, (l+1) h], h = y_max / LQ_G.
 // On a piece (one working set) everything the per-EV outputs need is polynomial in gamma:

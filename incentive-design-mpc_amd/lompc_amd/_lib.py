@@ -56,6 +56,7 @@ SIGNATURES = [
     ("lompc_destroy", _I, [_P]),
     ("lompc_set_mode", _I, [_P, _I]),
     ("lompc_set_params", _I, [_P, _L, _P, _P, _P, _P, _P]),
+    ("lompc_set_gamma_window", _I, [_P, _P]),
     ("lompc_solve_batch", _I, [_P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_run", _I, [_P, _L, _P, _P, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_solve_host", _I, [_P, _P, _D, _D, _P, _P]),

@@ -233,6 +233,7 @@ class LoMPC:
             bad = torch.logical_not(lm >= 0).any() | torch.logical_not(lr >= 0).any()
             if bool(bad):
                 raise ValueError("Parameter value must be nonnegative.")
+        self._lib.lompc_set_gamma_window(self._ctx, None)  # full [0, y_max] path (BatchPlan sets its own)
         rc = self._lib.lompc_set_params(self._ctx, S, _ptr(lm), _ptr(lr), _ptr(wr), _ptr(gr), self._stream())
         self._check_rc(rc)
         self._keep = (lm, lr, wr, gr)
@@ -329,10 +330,13 @@ class BatchPlan:
     In PATH mode the call is three dependent launches on the plan's stream: k_path
     (solution path per parameter set), k_eval (per-EV evaluation) and k_finalize
     (per-set reductions); see DESIGN.md.
+    window=True: each set's path is computed only over the range of its EVs' gamma
+    (lompc_set_gamma_window, measured once here; gamma is fixed for the plan — values
+    changed later outside that range are still solved correctly, by the repair pass).
     """
 
     def __init__(self, lompc: "LoMPC", gamma, set_offsets, *, w_ref=None, gamma_ref=None, want_w=True,
-                 want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None):
+                 want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None, window=True):
         torch = _torch()
         self.lompc = lompc
         self.gamma = lompc._dev(gamma).reshape(-1)
@@ -358,6 +362,12 @@ class BatchPlan:
             "set_sum_w": e((S, N)) if want_set else None,
             "set_stats": e((S, _lib.LOMPC_SET_STATS)) if want_set else None,
         }
+        self.window = None
+        if window and B > 0:  # per-set (min, max) of gamma: two segment reductions
+            lens = torch.as_tensor(np.diff(self.off), device=dev)
+            lo_ = torch.segment_reduce(self.gamma, "min", lengths=lens, unsafe=True)
+            hi_ = torch.segment_reduce(self.gamma, "max", lengths=lens, unsafe=True)
+            self.window = torch.stack([lo_, hi_], dim=1).contiguous()
         self._stream = (stream if stream is not None else torch.cuda.current_stream(lompc.device)).cuda_stream
         self._args = [_ptr(self.w_ref), _ptr(self.gamma_ref), B, _ptr(self.gamma), self.off.ctypes.data] + \
             [_ptr(self.out[k]) for k in ("w", "cost", "w0", "status", "set_sum_w", "set_stats")] + [self._stream]
@@ -367,6 +377,7 @@ class BatchPlan:
         lo = self.lompc
         pl = lmbd if isinstance(lmbd, int) else lmbd.data_ptr()
         pr = lmbd_r if isinstance(lmbd_r, int) else lmbd_r.data_ptr()
+        lo._lib.lompc_set_gamma_window(lo._ctx, _ptr(self.window))
         rc = lo._lib.lompc_run(lo._ctx, self.S, pl, pr, *self._args)
         if rc:
             lo._check_rc(rc)

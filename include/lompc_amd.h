@@ -80,6 +80,17 @@ int lompc_destroy(lompc_ctx* ctx);
 /* Select LOMPC_MODE_PATH (default), LOMPC_MODE_DIRECT or LOMPC_MODE_PATH_REPAIR. */
 int lompc_set_mode(lompc_ctx* ctx, int mode);
 
+/* Gamma window of the solution path (PATH mode): the path of set s is computed on
+ * [window[2s], window[2s+1]] (clipped to [0, y_max], widened by 1e-7 y_max) instead of
+ * [0, y_max], so its 64 cells are narrower and carry fewer pieces.  The natural window of a
+ * (type, partition) set is the range of its EVs' gamma = y_max - y0 (price_solver.py:73-77
+ * computes those extremes).  EVs outside the window stay correct: they are re-solved
+ * individually (status REPAIRED).
+ *   window dev [S, 2] (lo, hi), or NULL = [0, y_max] for every set.
+ * Sticky: read by the path kernel of every later lompc_set_params / lompc_run on ctx
+ * (the buffer must stay valid until those launches have run). */
+int lompc_set_gamma_window(lompc_ctx* ctx, const double* window);
+
 /* Load S parameter sets and prepare them on device.
  * Replaces LoMPC._update_cvx_parameters (lompc.py:84-90) for S sets at once
  * (one set = one (EV type, partition) price vector in price_solver.py).

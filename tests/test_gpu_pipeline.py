@@ -51,7 +51,9 @@ def test_run_matches_two_calls_and_oracle(gpu, ev):
     lr = torch.as_tensor(3 * N * c.delta * rng.random(S), device="cuda:0")
     wr = torch.as_tensor(c.w_max * rng.random((S, N)), device="cuda:0")
     lompc = mk(c, N)
-    plan = BatchPlan(lompc, g, off, w_ref=wr, want_w=True, want_cost=True, want_w0=True, want_status=True)
+    # window=False: the full-range path, bitwise comparable with set_params + solve_batch
+    plan = BatchPlan(lompc, g, off, w_ref=wr, want_w=True, want_cost=True, want_w0=True, want_status=True,
+                     window=False)
     out = plan.run(lm, lr)
     torch.cuda.synchronize()
     rep, fail, inv = lompc.check_last()
@@ -131,3 +133,51 @@ def test_in_place_repair_path(gpu, ev, N):
             assert nf == 0
             np.testing.assert_allclose(w[a:b], wo, atol=TOL_W)
             np.testing.assert_allclose(cost[a:b], co, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("ev", ["small", "large"])
+@pytest.mark.parametrize("N", [24, 48])
+def test_gamma_window_matches_full_path(gpu, ev, N):
+    """lompc_set_gamma_window: paths over each set's own gamma range (BatchPlan default) give
+    the full-range answers; gamma moved outside the measured window afterwards is re-solved
+    (status REPAIRED) and still matches the oracle."""
+    rng = np.random.default_rng(77 + N + (ev == "large"))
+    c = O.small_consts() if ev == "small" else O.large_consts()
+    sizes = [4000, 1, 0, 2500, 640]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    S, B = len(sizes), int(off[-1])
+    # partitions by SoC: narrow gamma ranges per set (charging_station.py:111-116), one single-EV set
+    lo = np.array([0.05, 0.4, 0.0, 0.6, 0.3]) * c.y_max
+    gn = np.concatenate([lo[s] + 0.08 * c.y_max * rng.random(sizes[s]) for s in range(S)])
+    g = torch.as_tensor(gn, device="cuda:0")
+    lm = torch.as_tensor(c.theta * rng.random((S, 3 * N)), device="cuda:0")
+    lr = torch.as_tensor(3 * N * c.delta * rng.random(S), device="cuda:0")
+    wr = torch.as_tensor(c.w_max * rng.random((S, N)), device="cuda:0")
+    lompc = mk(c, N)
+    kw = dict(w_ref=wr, want_w=True, want_cost=True, want_status=True)
+    full = BatchPlan(lompc, g, off, window=False, **kw)
+    o_full = {k: (v.clone() if v is not None else None) for k, v in full.run(lm, lr).items()}
+    win = BatchPlan(lompc, g, off, **kw)
+    assert win.window is not None
+    o_win = win.run(lm, lr)
+    torch.cuda.synchronize()
+    rep, fail, inv = lompc.check_last()
+    assert fail == 0 and inv == 0 and rep == 0
+    np.testing.assert_allclose(o_win["w"].cpu().numpy(), o_full["w"].cpu().numpy(), rtol=0, atol=1e-12)
+    np.testing.assert_allclose(o_win["cost"].cpu().numpy(), o_full["cost"].cpu().numpy(), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(o_win["set_sum_w"].cpu().numpy(), o_full["set_sum_w"].cpu().numpy(), rtol=1e-11,
+                               atol=1e-10)
+    check_reductions(o_win, off, N)
+    # gamma changed in place outside the plan's window: repaired, still exact
+    g[off[0]:off[0] + 10] = torch.as_tensor(0.95 * c.y_max * np.ones(10), device="cuda:0")
+    o2 = win.run(lm, lr)
+    torch.cuda.synchronize()
+    rep, fail, inv = lompc.check_last()
+    assert fail == 0 and inv == 0 and rep >= 10
+    st = o2["status"].cpu().numpy()
+    assert np.all(st[:10] == _lib.LOMPC_QP_REPAIRED)
+    o = O.OracleLoMPC(N, c)
+    w2 = o2["w"].cpu().numpy()
+    for i in range(10):
+        wo, _ = o.solve_lompc(lm[0].cpu().numpy(), float(lr[0]), 0.95 * c.y_max)
+        assert np.max(np.abs(w2[i] - wo)) <= TOL_W

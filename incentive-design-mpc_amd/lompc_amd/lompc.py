@@ -336,7 +336,8 @@ class BatchPlan:
     """
 
     def __init__(self, lompc: "LoMPC", gamma, set_offsets, *, w_ref=None, gamma_ref=None, want_w=True,
-                 want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None, window=True):
+                 want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None, window=True,
+                 validate=True):
         torch = _torch()
         self.lompc = lompc
         self.gamma = lompc._dev(gamma).reshape(-1)
@@ -345,10 +346,11 @@ class BatchPlan:
         S = self.off.shape[0] - 1
         if S < 1 or self.off[0] != 0 or self.off[-1] != B or np.any(np.diff(self.off) < 0):
             raise ValueError("set_offsets must be non-decreasing from 0 to B")
-        if bool((self.gamma > lompc.y_max).any()):
-            raise AssertionError("gamma <= y_max required")
-        if bool(torch.logical_not(self.gamma >= 0).any()):
-            raise ValueError("Parameter value must be nonnegative.")
+        if validate:  # (callers that already checked 0 <= gamma <= y_max skip two host syncs)
+            if bool((self.gamma > lompc.y_max).any()):
+                raise AssertionError("gamma <= y_max required")
+            if bool(torch.logical_not(self.gamma >= 0).any()):
+                raise ValueError("Parameter value must be nonnegative.")
         self.S, self.B, N = S, B, lompc.N
         dev = f"cuda:{lompc.device}"
         self.w_ref = None if w_ref is None else lompc._dev(w_ref).reshape(S, N)

@@ -62,9 +62,15 @@ class PriceSolver:
         torch = _torch()
         dev = f"cuda:{self.lompc.device}"
         self._dev = dev
-        self._lm2 = torch.zeros((2, 3 * N), dtype=torch.float64, device=dev)
-        self._lr2 = torch.zeros(2, dtype=torch.float64, device=dev)
-        self._wr2 = torch.zeros((2, N), dtype=torch.float64, device=dev)
+        # per-iteration inputs [lmbd (2, 3N) | lmbd_r (2) | w_ref (2, N)]: staged in pinned host
+        # memory and moved by ONE async copy per engine call
+        n_in = 6 * N + 2 + 2 * N
+        self._in = torch.zeros(n_in, dtype=torch.float64, device=dev)
+        self._h_in = torch.zeros(n_in, dtype=torch.float64).pin_memory()
+        self._h_in_np = self._h_in.numpy()
+        self._lm2 = self._in[: 6 * N].view(2, 3 * N)
+        self._lr2 = self._in[6 * N: 6 * N + 2]
+        self._wr2 = self._in[6 * N + 2:].view(2, N)
         self._h_sw = torch.zeros((2, N), dtype=torch.float64).pin_memory()
         self._h_st = torch.zeros((2, _lib.LOMPC_SET_STATS), dtype=torch.float64).pin_memory()
         self._plan = None
@@ -163,10 +169,11 @@ class PriceSolver:
         if central:
             self._gam[B] = float(self.gamma_sc)
         off = np.array([0, B, B + central], dtype=np.int64)
+        # gamma = y_max - y0 with 0 <= y0 <= y_max asserted in set_charge_levels
         self._plan = BatchPlan(self.lompc, self._gam, off, w_ref=self._wr2, want_w=False, want_cost=False,
-                               want_set=True)
+                               want_set=True, validate=False)
         self._plan_w0 = BatchPlan(self.lompc, self._gam[:B], np.array([0, B], dtype=np.int64), want_w=False,
-                                  want_cost=False, want_w0=True, want_set=True) if B else None
+                                  want_cost=False, want_w0=True, want_set=True, validate=False) if B else None
         self._B = B
 
     def compute_optimal_prices(self, w_ref: np.ndarray, lmbd_r: float) -> tuple[np.ndarray, dict]:
@@ -275,10 +282,14 @@ class PriceSolver:
         torch = _torch()
         if self._plan is None:
             raise RuntimeError("set_charge_levels first")
-        lm = torch.from_numpy(np.ascontiguousarray(lmbd, dtype=np.float64))
-        self._lm2.copy_(lm.unsqueeze(0).expand(2, -1))
-        self._lr2.fill_(float(lmbd_r))
-        self._wr2.copy_(torch.from_numpy(w_ref).unsqueeze(0).expand(2, -1))
+        N3 = 3 * self.N
+        h = self._h_in_np  # free: the previous call synchronised after its copy
+        h[:N3] = lmbd
+        h[N3:2 * N3] = lmbd
+        h[2 * N3:2 * N3 + 2] = float(lmbd_r)
+        h[2 * N3 + 2:2 * N3 + 2 + self.N] = w_ref
+        h[2 * N3 + 2 + self.N:] = w_ref
+        self._in.copy_(self._h_in, non_blocking=True)
         out = self._plan.run(self._lm2, self._lr2)
         self.n_batched_calls += 1
         sw, st = out["set_sum_w"], out["set_stats"]
@@ -362,10 +373,12 @@ class PriceSolver:
     def get_w0_price0_device(self, lmbd: np.ndarray, lmbd_r: float):
         """(w0 device tensor of this rank's EVs, global sum of price0) — no host copy of w0."""
         torch = _torch()
-        lmbd_ = np.zeros((3 * self.N))
-        lmbd_[: self.r] = lmbd
-        self._lm2[0].copy_(torch.from_numpy(lmbd_))
-        self._lr2.fill_(float(lmbd_r))
+        N3 = 3 * self.N
+        h = self._h_in_np
+        h[:N3] = 0.0
+        h[: self.r] = lmbd
+        h[2 * N3:2 * N3 + 2] = float(lmbd_r)
+        self._in.copy_(self._h_in, non_blocking=True)
         if self._plan_w0 is not None:
             out = self._plan_w0.run(self._lm2[:1], self._lr2[:1])
             st = out["set_stats"]

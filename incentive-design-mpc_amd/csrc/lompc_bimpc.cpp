@@ -343,7 +343,7 @@ struct Newton {
   }
 
   void hb_solve(double* x) const {  // Hb^-1 in place
-    for (int k = 0; k < nb; ++k) lqd::chol_solve(&Hf[(size_t)k * N * N], N, x + (size_t)k * N);
+    BlockPool::get().run(nb, [&](int k) { lqd::chol_solve(&Hf[(size_t)k * N * N], N, x + (size_t)k * N); });
     for (int t = 0; t < N; ++t) x[nb * N + t] /= Du[t];
   }
 
@@ -477,7 +477,7 @@ bool polish(const Bimpc& B, std::vector<double>& z, std::vector<double>& llo, st
   for (int j = 0; j < mg; ++j)
     if (lg[j] > sg[j]) J.push_back(j);
   std::vector<double> zp(z);
-  std::vector<double> Ej, nu, g(n), Lz(N), ELz(mg), S, rhs, col;
+  std::vector<double> Ej, nu, g(n), Lz(N), ELz(mg), S, rhs;
   std::vector<int> piv;
   int nJ = 0;
   std::vector<double> lgn, tN(N), tn(n), llon, lhin;
@@ -509,15 +509,18 @@ bool polish(const Bimpc& B, std::vector<double>& z, std::vector<double>& llo, st
       mulE(N, Lz.data(), ELz.data());
       S.assign((size_t)nJ * nJ, 0.0);
       std::fill(rhs.begin(), rhs.end(), 0.0);
-      std::vector<std::vector<double>> Y(nb + 1), hg(nb + 1);
+      // per block k (independent, on the host pool): reduced Hessian on the free set F_k,
+      // hg = H^-1 g_F, YT = (H^-1 c_k E_F')' and the block's Schur term c_k E_F H^-1 c_k E_F'
+      std::vector<std::vector<double>> YT(nb + 1), hg(nb + 1), Sk(nb + 1), rk(nb + 1);
       std::vector<std::vector<int>> F(nb + 1);
-      for (int k = 0; k <= nb; ++k) {
+      std::vector<int> bad(nb + 1, 0);  // 1: u <= 0, 2: chol
+      BlockPool::get().run(nb + 1, [&](int k) {
         for (int t = 0; t < N; ++t)
           if (!fix[k * N + t]) F[k].push_back(t);
         const int m = (int)F[k].size();
-        if (!m) continue;
+        if (!m) return;
         const double ck = k < nb ? B.ck[k] : 1.0;
-        std::vector<double> H((size_t)m * m, 0.0);
+        std::vector<double> H((size_t)m * m, 0.0), EF((size_t)nJ * m);
         if (k < nb) {
           std::vector<double> suf(N);
           double acc = 0.0;
@@ -530,31 +533,47 @@ bool polish(const Bimpc& B, std::vector<double>& z, std::vector<double>& llo, st
         } else {
           for (int a = 0; a < m; ++a) {
             const double u = zp[nb * N + F[k][a]];
-            if (!(u > 0.0)) PFAIL("u <= 0");
+            if (!(u > 0.0)) {
+              bad[k] = 1;
+              return;
+            }
             H[a * m + a] = 1.19 * B.c_g * std::pow(u, -0.3);
           }
         }
-        if (!lqd::chol(H.data(), m)) PFAIL("chol");
+        if (!lqd::chol(H.data(), m)) {
+          bad[k] = 2;
+          return;
+        }
         hg[k].resize(m);
         for (int a = 0; a < m; ++a) hg[k][a] = g[k * N + F[k][a]];
         lqd::chol_solve(H.data(), m, hg[k].data());
-        Y[k].assign((size_t)m * nJ, 0.0);
-        col.resize(m);
+        for (int q = 0; q < nJ; ++q)
+          for (int a = 0; a < m; ++a) EF[(size_t)q * m + a] = ck * Ej[(size_t)q * N + F[k][a]];
+        YT[k].assign((size_t)nJ * m, 0.0);
         for (int q = 0; q < nJ; ++q) {
-          for (int a = 0; a < m; ++a) col[a] = ck * Ej[(size_t)q * N + F[k][a]];
-          lqd::chol_solve(H.data(), m, col.data());
-          for (int a = 0; a < m; ++a) Y[k][(size_t)a * nJ + q] = col[a];
+          double* y = &YT[k][(size_t)q * m];
+          std::copy(&EF[(size_t)q * m], &EF[(size_t)q * m] + m, y);
+          lqd::chol_solve(H.data(), m, y);
         }
+        Sk[k].assign((size_t)nJ * nJ, 0.0);
+        rk[k].assign(nJ, 0.0);
         for (int p = 0; p < nJ; ++p) {
-          double acc = 0.0;
-          for (int a = 0; a < m; ++a) acc += ck * Ej[(size_t)p * N + F[k][a]] * hg[k][a];
-          rhs[p] += acc;
-          for (int q = 0; q < nJ; ++q) {
-            double s2 = 0.0;
-            for (int a = 0; a < m; ++a) s2 += ck * Ej[(size_t)p * N + F[k][a]] * Y[k][(size_t)a * nJ + q];
-            S[(size_t)p * nJ + q] += s2;
+          rk[k][p] = lqd::dot(&EF[(size_t)p * m], hg[k].data(), m);
+          for (int q = p; q < nJ; ++q) {  // symmetric
+            const double v = lqd::dot(&EF[(size_t)p * m], &YT[k][(size_t)q * m], m);
+            Sk[k][(size_t)p * nJ + q] = v;
+            Sk[k][(size_t)q * nJ + p] = v;
           }
         }
+      });
+      for (int k = 0; k <= nb; ++k) {
+        if (bad[k] == 1) PFAIL("u <= 0");
+        if (bad[k] == 2) PFAIL("chol");
+      }
+      for (int k = 0; k <= nb; ++k) {  // block order: independent of the thread count
+        if (Sk[k].empty()) continue;
+        for (size_t e = 0; e < S.size(); ++e) S[e] += Sk[k][e];
+        for (int p = 0; p < nJ; ++p) rhs[p] += rk[k][p];
       }
       // degenerate vertex: an active row that is (numerically) a combination of earlier ones —
       // e.g. one touching only fixed variables — gives a zero pivot of the PSD Schur matrix;
@@ -572,8 +591,9 @@ bool polish(const Bimpc& B, std::vector<double>& z, std::vector<double>& llo, st
       step = 0.0;
       for (int k = 0; k <= nb; ++k)
         for (int a = 0; a < (int)F[k].size(); ++a) {
+          const int m = (int)F[k].size();
           double d = -hg[k][a];
-          for (int q = 0; q < nJ; ++q) d -= Y[k][(size_t)a * nJ + q] * nu[q];
+          for (int q = 0; q < nJ; ++q) d -= YT[k][(size_t)q * m + a] * nu[q];
           zp[k * N + F[k][a]] += d;
           step = std::max(step, std::fabs(d));
         }

@@ -343,7 +343,8 @@ struct Newton {
   }
 
   void hb_solve(double* x) const {  // Hb^-1 in place
-    BlockPool::get().run(nb, [&](int k) { lqd::chol_solve(&Hf[(size_t)k * N * N], N, x + (size_t)k * N); });
+    // sequential: ~2N^2 flops per block is below the pool's dispatch cost (measured on the GPU box)
+    for (int k = 0; k < nb; ++k) lqd::chol_solve(&Hf[(size_t)k * N * N], N, x + (size_t)k * N);
     for (int t = 0; t < N; ++t) x[nb * N + t] /= Du[t];
   }
 

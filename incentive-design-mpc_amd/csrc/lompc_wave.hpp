@@ -21,6 +21,13 @@
 #ifndef LQ_JUMP_IT
 #define LQ_JUMP_IT 3  // PDAS iterations that may jump across segments
 #endif
+#ifndef LQ_PDAS_CAP
+// PDAS iterations before the monotone primal active set takes over (warm-started from the
+// projected PDAS iterate).  Random price vectors converge in <= 15 at N = 48; the station's
+// structured large-EV prices can make PDAS cycle, which at the old cap of 4N + 8 cost up to
+// ~0.2 ms per path cell.
+#define LQ_PDAS_CAP 32
+#endif
 
 namespace lqw {
 
@@ -296,12 +303,28 @@ __device__ __forceinline__ bool wave_pdas(const QPConst& q, const WaveSet& ws, d
   return false;
 }
 
-// Wave-parallel primal active set (monotone), from w = 0 all at knot 0.
+// Wave-parallel primal active set (monotone).  Cold: from w = 0, all at knot 0.  Warm: from
+// the given w projected onto [0, w_max], each coordinate free in the segment that contains it
+// (a feasible point consistent with its working set, which is all the method needs).
 __device__ __forceinline__ bool wave_primal_as(const QPConst& q, const WaveSet& ws, double gamma, int& s,
-                                               double& w, double& r, int max_it) {
+                                               double& w, double& r, int max_it, bool warm = false) {
   const bool act = ws.lane < ws.N;
-  s = 0;
-  w = 0.0;
+  if (warm && act && w == w) {
+    w = fmin(fmax(w, q.knots[0]), q.knots[q.m]);
+    if (w <= q.knots[0]) {
+      s = 0;
+    } else if (w >= q.knots[q.m]) {
+      s = 2 * q.m;
+    } else {
+      int seg = 0;
+#pragma unroll
+      for (int k = 1; k < LQ_MAXSEG; ++k) seg += (k < q.m && w > q.knots[k]) ? 1 : 0;
+      s = 2 * seg + 1;
+    }
+  } else {
+    s = 0;
+    w = 0.0;
+  }
   for (int it = 0; it < max_it; ++it) {
     const StageSol<1> sol = solve_stage<1>(q, ws, gamma, s);
     const Box b = lq_box(s);
@@ -371,10 +394,10 @@ __device__ __forceinline__ double wave_kkt_point(const QPConst& q, const WaveSet
 // Exact certified solve of one QP by the whole wave, PDAS from s, primal active set if needed.
 __device__ __forceinline__ bool wave_solve(const QPConst& q, const WaveSet& ws, double gamma, int& s, double& w,
                                            double& r, int* nit = nullptr) {
-  bool ok = wave_pdas(q, ws, gamma, s, w, r, 4 * ws.N + 8, nit);
+  bool ok = wave_pdas(q, ws, gamma, s, w, r, min(4 * ws.N + 8, LQ_PDAS_CAP), nit);
   if (ok) ok = wave_kkt(q, ws, s, w, r) <= q.tol_cert;
   if (!ok) {
-    ok = wave_primal_as(q, ws, gamma, s, w, r, 16 * ws.N + 32);
+    ok = wave_primal_as(q, ws, gamma, s, w, r, 16 * ws.N + 32, true);
     if (ok) ok = wave_kkt(q, ws, s, w, r) <= q.tol_cert;
   }
   const Box b = lq_box(ws.lane < ws.N ? s : 0);

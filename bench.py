@@ -38,8 +38,8 @@ FP64_VALU_PEAK_TFLOPS = 78.6  # vendor datasheet (not in the container guide)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--evs-per-gpu", type=int, default=262144)
     ap.add_argument("--horizon", type=int, default=24)
     ap.add_argument("--partitions", type=int, default=12)

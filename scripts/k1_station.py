@@ -5,7 +5,7 @@ import ctypes
 import os
 import sys
 
-os.environ["LOMPC_LIB"] = "liblompc_amd_k1stats.so"
+os.environ["LOMPC_LIB"] = os.environ.get("K1_LIB", "liblompc_amd_k1stats.so")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

@@ -126,7 +126,7 @@ void mulEt(int N, const double* v, double* out) {
 // Persistent host worker pool for the independent per-block work of the Newton system
 // (2P blocks of N x N factorizations / solves).  Each block writes only its own buffers and
 // block results are combined afterwards in block order, so results do not depend on the
-// thread count.  LOMPC_HOST_THREADS caps the workers (default min(8, cores)).
+// thread count.  LOMPC_HOST_THREADS caps the workers (default min(16, cores)).
 class BlockPool {
  public:
   static BlockPool& get() {
@@ -164,7 +164,7 @@ class BlockPool {
 
  private:
   BlockPool() {
-    int nt = (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    int nt = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     if (const char* e = getenv("LOMPC_HOST_THREADS")) nt = std::max(1, atoi(e));
     for (int i = 1; i < nt; ++i) workers_.emplace_back([this] { loop(); });
   }

@@ -332,7 +332,8 @@ class BatchPlan:
     (per-set reductions); see DESIGN.md.
     window=True: each set's path is computed only over the range of its EVs' gamma
     (lompc_set_gamma_window, measured once here; gamma is fixed for the plan — values
-    changed later outside that range are still solved correctly, by the repair pass).
+    changed later outside that range are still solved correctly, by the repair pass);
+    an (S, 2) array gives the ranges directly (no measuring); False: [0, y_max].
     """
 
     def __init__(self, lompc: "LoMPC", gamma, set_offsets, *, w_ref=None, gamma_ref=None, want_w=True,
@@ -365,7 +366,9 @@ class BatchPlan:
             "set_stats": e((S, _lib.LOMPC_SET_STATS)) if want_set else None,
         }
         self.window = None
-        if window and B > 0:  # per-set (min, max) of gamma: two segment reductions
+        if window is not None and window is not True and window is not False:  # caller's (S, 2) ranges
+            self.window = torch.as_tensor(np.asarray(window, dtype=np.float64).reshape(S, 2), device=dev)
+        elif window and B > 0:  # per-set (min, max) of gamma: two segment reductions
             lens = torch.as_tensor(np.diff(self.off), device=dev)
             lo_ = torch.segment_reduce(self.gamma, "min", lengths=lens, unsafe=True)
             hi_ = torch.segment_reduce(self.gamma, "max", lengths=lens, unsafe=True)

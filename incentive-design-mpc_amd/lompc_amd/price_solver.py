@@ -114,11 +114,11 @@ class PriceSolver:
             y0d = y0.to(device=self._dev, dtype=torch.float64).reshape(-1)
             assert y0d.dim() == 1
             if self.group is None:
-                assert bool(((y0d >= 0) & (y0d <= self.consts.y_max)).all())
                 n = int(y0d.numel())
                 if n == 0:
                     raise ValueError("zero-size array to reduction operation maximum which has no identity")
-                stats = torch.stack([y0d.max(), y0d.min(), y0d.sum()]).cpu().numpy()
+                stats = torch.stack([y0d.max(), y0d.min(), y0d.sum()]).cpu().numpy()  # one host sync
+                assert stats[1] >= 0 and stats[0] <= self.consts.y_max  # 0 <= y0 <= y_max (NaN fails)
                 self.nEVs = n
                 y_hi, y_lo, y_mean = stats[0], stats[1], stats[2] / n
             else:
@@ -136,6 +136,7 @@ class PriceSolver:
                 y_hi, y_lo, y_mean = self._global_levels(torch.as_tensor(y0, device=self._dev))
             self.y0 = y0
             gamma = torch.as_tensor(self.consts.y_max - y0, device=self._dev)
+        self._y_hi, self._y_lo = float(y_hi), float(y_lo)
         self.y0_rng = (y_hi - y_lo) / 2  # = \bar{\Gamma}
         self.gamma_sc = self.consts.y_max - (y_hi + y_lo) / 2
         self.gamma_sm = self.consts.y_max - y_mean
@@ -170,10 +171,15 @@ class PriceSolver:
             self._gam[B] = float(self.gamma_sc)
         off = np.array([0, B, B + central], dtype=np.int64)
         # gamma = y_max - y0 with 0 <= y0 <= y_max asserted in set_charge_levels
+        # path windows from the batch statistics (gamma = y_max - y0): no measuring pass
+        ym = self.consts.y_max
+        g_rng = [ym - self._y_hi, ym - self._y_lo]
+        win = [g_rng, [float(self.gamma_sc)] * 2]  # set 1: the central QP (empty on ranks > 0)
         self._plan = BatchPlan(self.lompc, self._gam, off, w_ref=self._wr2, want_w=False, want_cost=False,
-                               want_set=True, validate=False)
+                               want_set=True, validate=False, window=win)
         self._plan_w0 = BatchPlan(self.lompc, self._gam[:B], np.array([0, B], dtype=np.int64), want_w=False,
-                                  want_cost=False, want_w0=True, want_set=True, validate=False) if B else None
+                                  want_cost=False, want_w0=True, want_set=True, validate=False,
+                                  window=[g_rng]) if B else None
         self._B = B
 
     def compute_optimal_prices(self, w_ref: np.ndarray, lmbd_r: float) -> tuple[np.ndarray, dict]:

@@ -46,8 +46,13 @@ def parse():
     ap.add_argument("--mode", choices=["path", "direct"], default="path")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--warm", action="store_true",
+                    help="plan warm start: every gamma cell's exact solve starts from the working set the "
+                         "previous step ended with there (as a price loop's plan does)")
+    ap.add_argument("--outputs", choices=["full", "cost", "set"], default="full",
+                    help="diagnostics: full = w + cost + reductions (the metric's workload); cost = no w rows; "
+                         "set = reductions only")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--serial", action="store_true", help="both EV types on one stream")
     ap.add_argument("--no-station", action="store_true", help="skip the BiMPC steps/sec leg")
     ap.add_argument("--station-evs-per-gpu", type=int, default=262144, help="EVs per GPU, half per type")
     ap.add_argument("--station-horizon", type=int, default=48)
@@ -97,46 +102,57 @@ def main():
         y0 = 0.3 + 0.2 * rng.random(M)
         gamma = torch.as_tensor(c.y_max - y0, device=dev)
         lm = torch.as_tensor(c.theta * rng.random((nsteps, P, 3 * N)), device=dev)
-        lr = torch.zeros(P, dtype=torch.float64, device=dev)
         wr = torch.as_tensor(c.w_max * rng.random((P, N)), device=dev)
-        gref = torch.as_tensor(c.y_max - 0.4 * np.ones(P), device=dev)
-        eng.append(dict(name=name, c=c, lompc=lompc, off=off, gamma=gamma, lm=lm, lr=lr, wr=wr, gref=gref,
-                        out={}, M=M))
+        eng.append(dict(name=name, c=c, lompc=lompc, off=off, gamma=gamma, lm=lm, wr=wr, M=M))
 
-    # the two EV types are independent: one HIP stream each, so their
-    # latency-bound path/finalize kernels overlap; the caller's stream joins both.
-    # Each type's price iteration is ONE C-ABI call (BatchPlan -> lompc_run).
     main = torch.cuda.current_stream()
-    for e in eng:
-        e["stream"] = main if args.serial else torch.cuda.Stream()
-        e["plan"] = BatchPlan(e["lompc"], e["gamma"], e["off"], w_ref=e["wr"], gamma_ref=e["gref"], want_w=True,
-                              want_cost=True, want_set=True, stream=e["stream"])
-        e["out"] = e["plan"].out
-        e["lm_ptr"] = [e["lm"][k].data_ptr() for k in range(nsteps)]
-        e["lr_ptr"] = e["lr"].data_ptr()
+    if args.mode == "path":
+        # ONE plan over both EV types: their 2P parameter sets stacked (small first), every step
+        # is one fused k_solve launch over all (set, gamma cell) waves + one k_reduce
+        off = np.concatenate([eng[0]["off"], eng[0]["M"] + eng[1]["off"][1:]])
+        gamma = torch.cat([e["gamma"] for e in eng])
+        lm = torch.cat([e["lm"] for e in eng], dim=1).contiguous()  # (nsteps, 2P, 3N)
+        wr = torch.cat([e["wr"] for e in eng]).contiguous()
+        lr = torch.zeros(2 * P, dtype=torch.float64, device=dev)
+        runs = [dict(plan=BatchPlan([e["lompc"] for e in eng], gamma, off, sets_per_ctx=[P, P], w_ref=wr,
+                                    want_w=args.outputs == "full", want_cost=args.outputs != "set", want_set=True,
+                                    stream=main, warm_start=args.warm), stream=main, lm_ptr=[lm[k].data_ptr() for k in range(nsteps)], lr_ptr=lr.data_ptr(),
+                     qps=B, keep=(gamma, lm, wr, lr))]
+    else:
+        # DIRECT mode: one context per EV type, each on its own stream
+        runs = []
+        for e in eng:
+            st = torch.cuda.Stream()
+            st.wait_stream(main)
+            lr = torch.zeros(P, dtype=torch.float64, device=dev)
+            plan = BatchPlan(e["lompc"], e["gamma"], e["off"], w_ref=e["wr"], gamma_ref=torch.full(
+                (P,), e["c"].y_max - 0.4, dtype=torch.float64, device=dev), want_w=True, want_cost=True,
+                want_set=True, stream=st)
+            runs.append(dict(plan=plan, stream=st, lm_ptr=[e["lm"][k].data_ptr() for k in range(nsteps)],
+                             lr_ptr=lr.data_ptr(), qps=e["M"], keep=(lr,)))
+    torch.cuda.synchronize()
 
     def step(k):
-        if world > 1:  # the previous step's all-reduce reads the output buffers
-            for e in eng:
-                e["stream"].wait_stream(main)
-        for e in eng:
-            e["plan"].run(e["lm_ptr"][k], e["lr_ptr"])
+        if world > 1:  # the previous step's collective reads the output buffers
+            for r in runs:
+                r["stream"].wait_stream(main)
+        for r in runs:
+            r["plan"].run(r["lm_ptr"][k], r["lr_ptr"])
         if world > 1:
-            for e in eng:
-                main.wait_stream(e["stream"])
-            # both types' per-partition reductions in ONE collective
-            combine_set_results([(e["out"]["set_sum_w"], e["out"]["set_stats"]) for e in eng])
+            for r in runs:
+                main.wait_stream(r["stream"])
+            # every set's reductions (both EV types) in ONE collective
+            combine_set_results([(r["plan"].out["set_sum_w"], r["plan"].out["set_stats"]) for r in runs])
 
     # warmup (and correctness gate: every QP certified)
     for k in range(args.warmup):
         step(k)
-    for e in eng:
-        with torch.cuda.stream(e["stream"]):
-            rep, fail, inv = e["lompc"].check_last()
-        assert fail == 0 and inv == 0, (e["name"], fail, inv)
-    for e in eng:
-        e["lompc"].profile(enable=True)
-        e["lompc"].profile(read=True, reset=True)
+    for r in runs:
+        rep, fail, inv = r["plan"].check()
+        assert fail == 0 and inv == 0, (fail, inv)
+    for r in runs:
+        r["plan"].profile(enable=True)
+        r["plan"].profile(read=True, reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -152,18 +168,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     repaired = 0
-    for e in eng:
-        with torch.cuda.stream(e["stream"]):
-            rep, fail, inv = e["lompc"].check_last()
+    for r in runs:
+        rep, fail, inv = r["plan"].check()
         assert fail == 0 and inv == 0
         repaired += rep
-    # per-EV kernel (k_eval / k_direct) timing: HIP events on its own dispatch (hipExtLaunchKernel)
+    # per-EV kernel (k_solve / k_direct) timing: HIP events on its own dispatch (hipExtLaunchKernel)
     k_ms, k_n, k_qps = 0.0, 0, 0
-    for e in eng:
-        ms, n = e["lompc"].profile(read=True)
+    for r in runs:
+        ms, n = r["plan"].profile(read=True)
         k_ms += ms
         k_n += n
-        k_qps += e["M"] * n
+        k_qps += r["qps"] * n
     avg_launch_s = (k_ms / 1e3) / max(k_n, 1)
     qp_per_launch = k_qps / max(k_n, 1)
     bytes_per_qp = 8 * (N + 2)
@@ -192,8 +207,10 @@ def main():
             "horizon": N,
             "parameter_sets": 2 * P,
             "mode": args.mode,
+            "outputs": args.outputs,
+            "warm_start": bool(args.warm),
             "parallelism": f"dp{world} (EV shards, one RCCL all-gather of both types' per-set reductions per step)",
-            "streams": 1 if args.serial else len(eng),
+            "launches_per_step": 2 if args.mode == "path" else 6,
         },
         "roofline": {
             "bound": "hbm",
@@ -202,7 +219,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": None,
-            "kernel": "k_eval" if args.mode == "path" else "k_direct",
+            "kernel": "k_solve" if args.mode == "path" else "k_direct",
             "bytes_per_qp": bytes_per_qp,
             "qp_per_launch": qp_per_launch,
             "avg_launch_us": avg_launch_s * 1e6,
@@ -221,7 +238,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(eng, N, args.cpu_seconds)
     if not args.no_station:
-        del eng
+        del eng, runs
         line["bimpc"] = station_leg(args, world, dev)
     if rank == 0:
         print(json.dumps(line), flush=True)

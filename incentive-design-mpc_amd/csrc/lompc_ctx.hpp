@@ -1,0 +1,158 @@
+// lompc_ctx.hpp — host-side state of the C-ABI objects (include/lompc_amd.h):
+// lompc_ctx (one EV type on one device, LoMPC.__init__, lompc.py:30-71) and
+// lompc_plan (a fixed EV batch solved repeatedly at new prices: the per-EV loops of
+// price_solver.py:203-209 / :280-283 over one price loop or one time step).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "lompc_qp.hpp"
+#include "../../include/lompc_amd.h"
+
+#define NPX 7  // partial / reduction record: [0,N) sum_w, then NPX scalars
+enum {      // columns after the N sums
+  PX_COST = 0,
+  PX_PRICE0 = 1,
+  PX_MAX_ERR = 2,
+  PX_N_OK = 3,
+  PX_N_REPAIRED = 4,
+  PX_N_FAILED = 5,
+  PX_N_INVALID = 6
+};
+
+struct lompc_ctx {
+  int device = 0;
+  int N = 0;
+  int ev_type = 0;
+  int mode = LOMPC_MODE_PATH;
+  int nmax = 0;
+  QPConst q{};
+  // parameter sets of the last lompc_set_params (PATH mode reads them at solve time)
+  int64_t S = 0, S_cap = 0;
+  const double* p_lmbd = nullptr;
+  const double* p_lmbd_r = nullptr;
+  const double* p_w_ref = nullptr;
+  const double* p_gamma_ref = nullptr;
+  int params_mode = -1;
+  // DIRECT mode: derived set records + central working sets (k_central)
+  double* d_setdata = nullptr;
+  uint8_t* d_central = nullptr;
+  int* d_errflag = nullptr;
+  // DIRECT mode batch workspaces
+  int64_t nblk_cap = 0, soff_cap = 0, stats_cap = 0;
+  double* d_partial = nullptr;
+  int* d_fail_cnt = nullptr;
+  uint8_t* d_fail_lane = nullptr;
+  int* d_blk_prefix = nullptr;
+  int64_t* d_set_off = nullptr;
+  longlong4* d_blk_info = nullptr;
+  longlong4* h_pin_info = nullptr;
+  int64_t info_cap = 0;
+  double* d_stats = nullptr;  // [S][LOMPC_SET_STATS] of the last batch (lompc_last_status)
+  int64_t stats_S = 0;
+  int* h_pin_prefix = nullptr;
+  int64_t* h_pin_off = nullptr;
+  hipEvent_t ev_map = nullptr;
+  std::vector<int64_t> last_off;
+  void* last_off_stream = nullptr;
+  // PATH mode: the transient plan behind lompc_solve_batch (re-prepared every call)
+  struct lompc_plan* tplan = nullptr;
+  // single-solve scratch (3N + N + 8 doubles)
+  double* d_single = nullptr;
+  int8_t* d_single_status = nullptr;
+  // profiling of the per-EV kernel
+  bool prof = false;
+  std::vector<hipEvent_t> prof_ev;    // pairs recorded since the last read
+  std::vector<hipEvent_t> prof_pool;  // recycled events (no creation inside timed loops)
+  double prof_ms = 0.0;
+  int64_t prof_n = 0;
+  std::string err;
+};
+
+#define LQ_PLAN_MAX_CTX LOMPC_PLAN_MAX_CTX
+
+struct lompc_plan {
+  int device = 0;
+  int N = 0;
+  int nctx = 0;
+  int flags = 0;
+  lompc_ctx* ctx[LQ_PLAN_MAX_CTX] = {};
+  QPConst* d_q = nullptr;       // [nctx]
+  int64_t B = 0, S = 0;
+  int G = 0;                    // gamma cells per set (bucket G of a set = invalid gamma)
+  int64_t cap_B = 0, cap_S = 0, cap_bk = 0;
+  size_t cap_tmp = 0;
+  const double* w_ref = nullptr;  // caller's [S][N] (read at every run) or null
+  double* d_stats_own = nullptr;  // [S][8] when the plan owns its status rows
+  double* d_stats = nullptr;      // where k_reduce writes the status rows
+  // device workspaces
+  uint8_t* d_set_ctx = nullptr;   // [S]
+  int64_t* d_set_off = nullptr;   // [S+1]
+  double* d_window = nullptr;     // [S][2] (lo, hi) of the set's valid gamma, widened
+  uint32_t* d_keys = nullptr;     // [2][B] radix-sort keys (bucket) in / out
+  uint32_t* d_vals = nullptr;     // [2][B] original EV index in / out (out = perm)
+  int* d_bucket_off = nullptr;    // [S*(G+1)+1]
+  double* d_gs = nullptr;         // [B] gamma in bucket order
+  double* d_partial = nullptr;    // [S*(G+1)][N+NPX]
+  uint8_t* d_ws = nullptr;        // [S*(G+1)][64] working set at each cell start (warm start)
+  void* d_tmp = nullptr;          // radix-sort temporary storage
+  int* d_errflag = nullptr;
+  unsigned* d_arrive = nullptr;   // [S] per-set arrival counters of k_solve's fused reduction
+  uint32_t* d_perm = nullptr;     // = the sorted value buffer
+  // pinned staging of the host set arrays
+  int64_t* h_off = nullptr;
+  uint8_t* h_ctx = nullptr;
+  int64_t cap_h = 0;
+  hipEvent_t ev_stage = nullptr;
+  // profiling of k_solve
+  bool prof = false;
+  std::vector<hipEvent_t> prof_ev, prof_pool;
+  double prof_ms = 0.0;
+  int64_t prof_n = 0;
+  std::string err;
+};
+
+#define HIPCHK(obj, call)                                                        \
+  do {                                                                           \
+    hipError_t e__ = (call);                                                     \
+    if (e__ != hipSuccess) {                                                     \
+      if (obj) (obj)->err = std::string(#call) + ": " + hipGetErrorString(e__); \
+      return LOMPC_ERR_HIP;                                                      \
+    }                                                                            \
+  } while (0)
+
+template <typename O>
+static inline int fail_arg(O* o, const char* msg) {
+  if (o) o->err = msg;
+  return LOMPC_ERR_INVALID_ARG;
+}
+
+template <typename O, typename T>
+static inline int grow(O* o, T** p, size_t n_elems) {
+  if (*p) {
+    hipError_t e = hipFree(*p);
+    if (e != hipSuccess) {
+      o->err = std::string("hipFree: ") + hipGetErrorString(e);
+      return LOMPC_ERR_HIP;
+    }
+  }
+  *p = nullptr;
+  hipError_t e = hipMalloc((void**)p, std::max<size_t>(n_elems, 1) * sizeof(T));
+  if (e != hipSuccess) {
+    o->err = std::string("hipMalloc: ") + hipGetErrorString(e);
+    return LOMPC_ERR_HIP;
+  }
+  return LOMPC_OK;
+}
+
+// Shared by lompc_kernels.hip (transient plan of lompc_solve_batch) and lompc_plan.hip.
+int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64_t* sets_per_ctx, int64_t B,
+                    const double* gamma, const int64_t* set_offsets, const double* w_ref, int flags,
+                    hipStream_t st);
+int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
+                   int8_t* status, double* set_sum_w, double* set_stats, hipStream_t st, lompc_ctx* prof_ctx);
+void lq_plan_free(lompc_plan* p);

@@ -1,32 +1,21 @@
-// lompc_kernels.hip — MI355X (gfx950) kernels and the C-ABI of include/lompc_amd.h.
+// lompc_kernels.hip — MI355X (gfx950) contexts, the DIRECT-mode kernels and the per-context
+// C-ABI of include/lompc_amd.h.
 //
 // Hot path replaced: LoMPC.solve_lompc (chargingstation/lompc.py:137-156) called once
 // per EV from PriceSolver._get_w_err (price_solver.py:203-209) and
 // PriceSolver.get_w0_price0 (price_solver.py:280-283).
 //
-// Kernels (one batched price iteration = lompc_run = K1 -> K2 -> K3 on one stream):
-//   K1  k_path      one wave per (parameter set, gamma cell). PATH mode: the exact
-//                   piecewise-affine solution path w*(gamma) on the cell [l h, (l+1) h]:
-//                   wave-parallel PDAS at the cell start, then parametric active-set
-//                   tracking (homotopy) to the cell end.  Pieces w = a + b gamma are
-//                   stored with their working sets and the quadratic-in-gamma
-//                   coefficients of the cost and of the squared A_bar error.  Every
-//                   stored piece is KKT-certified at both ends; the KKT residual is
-//                   convex in gamma along an affine piece, so that certifies every gamma
-//                   inside it.  DIRECT mode: the central solution.
-//   K2  k_eval      one EV per lane, one wave per workgroup (64 EVs of one set):
-//                   w = a + b gamma, cost / err / price0 from the EV's piece; EVs no
-//                   certified piece covers are re-solved in place by the whole wave
-//                   (wave_solve, certified).  LDS-tile epilogue: coalesced w stores and
-//                   deterministic per-workgroup column sums.
-//   K2d k_direct    DIRECT mode: every EV solved by its own lane (PDAS warm-started
-//                   from the central working set) and KKT-certified; same epilogue,
-//                   uncertified EVs listed for K3.
-//   K3  k_finalize  per set: (DIRECT mode) re-solves the listed EVs with the whole wave,
-//                   then the deterministic reduction of the workgroup partials.
-// Inter-workgroup handoffs go through kernel boundaries: an in-kernel release/acquire
-// handoff costs an L2 writeback / invalidate per wave on the 8-XCD part (a fused
-// single-launch variant measured 2-5x slower; DESIGN.md, "Rejected designs").
+// PATH mode (default) runs through a plan (lompc_plan.hip): lompc_solve_batch prepares the
+// context's transient plan for the batch and launches k_solve + k_reduce with the parameter
+// sets recorded by lompc_set_params.
+// DIRECT mode (this file), one batched solve = K1 -> K2d -> K3 on one stream:
+//   K1  k_central   one wave per parameter set: derived set record + the central solution's
+//                   working set (wave-parallel PDAS at gamma_ref).
+//   K2d k_direct    every EV solved by its own lane (PDAS warm-started from the central
+//                   working set) and KKT-certified; LDS-tile epilogue with coalesced w stores
+//                   and deterministic per-workgroup column sums; uncertified EVs listed for K3.
+//   K3  k_finalize  per set: re-solves the listed EVs with the whole wave, then the
+//                   deterministic reduction of the workgroup partials.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -37,23 +26,10 @@
 #include <string>
 #include <vector>
 
-#include "lompc_qp.hpp"
+#include "lompc_ctx.hpp"
 #include "lompc_wave.hpp"
-#include "../../include/lompc_amd.h"
 
 #define EVAL_BLOCK 64  // one wave per workgroup
-#define NPX 7          // partial record: [0,N) sum_w, then NPX scalars
-
-enum {  // partial columns after the N sums
-  PX_COST = 0,
-  PX_PRICE0 = 1,
-  PX_MAX_ERR = 2,
-  PX_N_OK = 3,
-  PX_N_REPAIRED = 4,
-  PX_N_FAILED = 5,
-  PX_N_INVALID = 6
-};
-
 struct KArgs {
   int64_t B;
   int S;
@@ -65,7 +41,6 @@ struct KArgs {
   const int64_t* set_off;      // [S+1]
   const longlong4* blk_info;   // [nblk]  (set, first EV, end EV, -)
   const double* setdata;   // [S][SD]
-  PathTable tab;
   const uint8_t* central;  // [S][LQ_STB]
   double* w;
   double* cost;
@@ -132,36 +107,30 @@ __device__ __forceinline__ void st_wt8(double* p, double v) {
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Shared epilogue of the per-EV kernels for one wave of EVs [start, start+64) of set s.
-// !INPLACE (K2d): ok lanes carry a certified w[] and outputs; valid-but-not-ok lanes
-//   are listed for the repair pass in k_finalize (their rows are rewritten there).
-// INPLACE (fused path kernel): repairs already happened in the block; every valid
-//   lane carries its final w[] (rep = repaired, ok = certified) and is summed.
-template <int NMAX, bool INPLACE = false>
+// Epilogue of k_direct for one wave of EVs [start, start+64) of set s: ok lanes carry a
+// certified w[] and outputs; valid-but-not-ok lanes are listed for the repair pass in
+// k_finalize (their rows are rewritten there).
+template <int NMAX>
 __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const KArgs& a, int b, int64_t start,
                                             int64_t end, bool valid, bool ok, const double (&w)[NMAX],
-                                            const EVOut& o, bool rep = false) {
+                                            const EVOut& o) {
   __shared__ double tile[EVAL_BLOCK * (NMAX + 3)];
   const int TS = N + 3;  // odd for even N: conflict-free row-per-lane ds_write_b64
   const int lane = threadIdx.x;
   const int64_t i = start + lane;
   const bool active = i < end;
   const double fill = valid ? 0.0 : NAN;
-  const bool row = INPLACE ? valid : ok;  // rows that carry a result
 #pragma unroll
   for (int t = 0; t < NMAX; ++t)
-    if (t < N) tile[lane * TS + t] = row ? w[t] : fill;
-  tile[lane * TS + N] = row ? o.cost : fill;
-  tile[lane * TS + N + 1] = row ? o.price0 : 0.0;
-  tile[lane * TS + N + 2] = row ? o.err : 0.0;
-  const unsigned long long okm = __ballot(row);
+    if (t < N) tile[lane * TS + t] = ok ? w[t] : fill;
+  tile[lane * TS + N] = ok ? o.cost : fill;
+  tile[lane * TS + N + 1] = ok ? o.price0 : 0.0;
+  tile[lane * TS + N + 2] = ok ? o.err : 0.0;
+  const unsigned long long okm = __ballot(ok);
   const unsigned long long fm = __ballot(valid && !ok);
   const unsigned long long im = __ballot(active && !valid);
-  const unsigned long long rm = INPLACE ? __ballot(valid && ok && rep) : 0ull;
-  if (!INPLACE) {
-    if (valid && !ok) a.fail_lane[(size_t)b * EVAL_BLOCK + __popcll(fm & ((1ull << lane) - 1ull))] = (uint8_t)lane;
-    if (lane == 0) a.fail_cnt[b] = __popcll(fm);
-  }
+  if (valid && !ok) a.fail_lane[(size_t)b * EVAL_BLOCK + __popcll(fm & ((1ull << lane) - 1ull))] = (uint8_t)lane;
+  if (lane == 0) a.fail_cnt[b] = __popcll(fm);
   __syncthreads();
   // coalesced WRITE-THROUGH stores (row-major w[B][N]): sc1 stores leave no dirty lines in the
   // XCD's L2, so the kernel boundary behind this launch has no L2 writeback of the outputs to
@@ -198,8 +167,7 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const
   if (active) {
     if (a.cost) st_wt8(a.cost + i, tile[lane * TS + N]);
     if (a.w0) st_wt8(a.w0 + i, tile[lane * TS + 0]);
-    if (a.status)
-      a.status[i] = !valid ? LOMPC_QP_INVALID : (ok ? ((INPLACE && rep) ? LOMPC_QP_REPAIRED : LOMPC_QP_OK) : LOMPC_QP_FAILED);
+    if (a.status) a.status[i] = !valid ? LOMPC_QP_INVALID : (ok ? LOMPC_QP_OK : LOMPC_QP_FAILED);
   }
   // per-workgroup partials: column sums over the certified rows (max for the error);
   // lanes l and l+32 each sum half of the rows of column l, then combine
@@ -223,56 +191,35 @@ __device__ __forceinline__ void ev_epilogue(const QPConst& q, const int N, const
     if (half == 0 && c < TS) part[c] = v;
   }
   if (lane == 0) {
-    part[N + PX_N_OK] = (double)__popcll(INPLACE ? (okm & ~fm) : okm);
-    part[N + PX_N_REPAIRED] = (double)__popcll(rm);
-    part[N + PX_N_FAILED] = (double)__popcll(fm);  // !INPLACE: pending, re-solved in k_finalize
+    part[N + PX_N_OK] = (double)__popcll(okm);
+    part[N + PX_N_REPAIRED] = 0.0;
+    part[N + PX_N_FAILED] = (double)__popcll(fm);  // pending, re-solved in k_finalize
     part[N + PX_N_INVALID] = (double)__popcll(im);
   }
 }
 
-// ------------------------------------------------------------------- K1
-#ifdef LOMPC_K1_STATS
-__device__ long long g_k1_stats[8192 * 4];  // per cell: PDAS iterations, pieces, cycles solve, cycles tracking
-#endif
-
-// A cell's count is tagged with the parameter epoch (set_params call) that wrote it:
-// tab.cnt[cell] = epoch << 4 | pieces.  K2 treats a cell of another epoch as unsolved.
-__device__ __forceinline__ void publish_cell(int* cnt, int epoch, int npc) {
-  if (threadIdx.x == 0) *cnt = (epoch << 4) | npc;
-}
-__device__ __forceinline__ int cell_epoch(int v) { return v >> 4; }
-__device__ __forceinline__ int cell_pieces(int v) { return v & 15; }
-
-struct PathArgs {
-  int S, mode, epoch, pad;
+// ------------------------------------------------------------------- K1 (DIRECT)
+struct CentralArgs {
+  int S, pad;
   const double* lmbd;
   const double* lmbd_r;
   const double* w_ref;
   const double* gamma_ref;
-  const double* window;  // [S][2] gamma window of the path, or null = [0, y_max]
   double* setdata;
   uint8_t* central;
   int* errflag;
 };
 
-__device__ __forceinline__ void path_cell(const QPConst& q, const PathArgs& pa, const PathTable& tab, int blk) {
-  const double* __restrict__ lmbd = pa.lmbd;
-  const double* __restrict__ lmbd_r = pa.lmbd_r;
-  const double* __restrict__ w_ref = pa.w_ref;
-  const double* __restrict__ gamma_ref = pa.gamma_ref;
-  double* __restrict__ setdata = pa.setdata;
-  uint8_t* __restrict__ central = pa.central;
-  int* __restrict__ errflag = pa.errflag;
-  const int mode = pa.mode;
+// One wave per parameter set: the derived set record (d, e, w_ref, c0, price-0 scalars,
+// kappa) and the central solution's working set at gamma_ref (the warm start of k_direct).
+__global__ __launch_bounds__(64) void k_central(QPConst q, CentralArgs pa) {
+  lq_tab_init(q);
   const int lane = threadIdx.x;
   const int N = q.N;
-  const bool path = mode != LOMPC_MODE_DIRECT;
-  const int s = path ? blk / LQ_G : blk;
-  const int cell = path ? blk % LQ_G : 0;
-  const double* L = lmbd + (size_t)s * 3 * N;
-  const double lr = lmbd_r[s];
+  const int s = blockIdx.x;
+  const double* L = pa.lmbd + (size_t)s * 3 * N;
+  const double lr = pa.lmbd_r[s];
   const double tt = q.theta * q.theta;
-  // per-stage data, natural (stage = lane) and reversed (stage = N-1-lane) layouts
   lqw::WaveSet ws;
   ws.N = N;
   ws.lane = lane;
@@ -281,7 +228,7 @@ __device__ __forceinline__ void path_cell(const QPConst& q, const PathArgs& pa, 
   if (lane < N) {
     const double l1 = L[lane], l3 = L[2 * N + lane];
     l2 = L[N + lane];
-    if (!(l1 >= 0.0 && l2 >= 0.0 && l3 >= 0.0)) atomicOr(errflag, 1);
+    if (!(l1 >= 0.0 && l2 >= 0.0 && l3 >= 0.0)) atomicOr(pa.errflag, 1);
     ws.d_nat = 2.0 * lr * tt + 2.0 * q.q_scale * l3 + q.dsmall;
     ws.e_nat = q.theta * (l1 - l2);
     const int tr = ws.rsrc;
@@ -290,282 +237,32 @@ __device__ __forceinline__ void path_cell(const QPConst& q, const PathArgs& pa, 
   } else {
     ws.d_nat = ws.e_nat = ws.d_rev = ws.e_rev = 0.0;
   }
-  const double wr_nat = (w_ref && lane < N) ? w_ref[(size_t)s * N + lane] : 0.0;
+  const double wr_nat = (pa.w_ref && lane < N) ? pa.w_ref[(size_t)s * N + lane] : 0.0;
   const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);  // lompc.py:128
-  const double kappa = lr / q.delta;                    // price_solver.py:191
-  const double ee = ws.e_nat;
-  double Ywr;  // prefix sums of w_ref
-  {
-    lqw::Sums<1> y;
-    y.v[0] = wr_nat;
-    Ywr = lqw::wave_scan(y, N).v[0];
+  double* out = pa.setdata + (size_t)s * lq_sd(N);
+  if (lane < N) {
+    out[lane] = ws.d_nat;
+    out[N + lane] = ws.e_nat;
+    out[2 * N + lane] = wr_nat;
   }
-  // gamma window of this set's path (lompc_set_gamma_window), widened by a margin
-  double wlo = 0.0, whi = q.y_max;
-  if (pa.window) {
-    const double mg = 1e-7 * q.y_max;
-    wlo = fmin(fmax(pa.window[2 * s] - mg, 0.0), q.y_max);
-    whi = fmin(fmax(pa.window[2 * s + 1] + mg, wlo + mg), q.y_max);
-    if (!(whi > wlo)) {  // window at y_max (or NaN input): full range
-      wlo = 0.0;
-      whi = q.y_max;
-    }
+  if (lane == 0) {
+    if (!(lr >= 0.0)) atomicOr(pa.errflag, 1);
+    out[3 * N + 0] = c0;
+    out[3 * N + 1] = L[0];
+    out[3 * N + 2] = L[N];
+    out[3 * N + 3] = L[2 * N];
+    out[3 * N + 4] = lr;
+    out[3 * N + 5] = lr / q.delta;  // kappa, price_solver.py:191
+    out[3 * N + 6] = pa.gamma_ref ? pa.gamma_ref[s] : 0.5 * q.y_max;
+    out[3 * N + 7] = pa.w_ref ? 1.0 : 0.0;
+    out[3 * N + 8] = 0.0;
+    out[3 * N + 9] = 0.0;
   }
-  if (cell == 0) {  // one block per set writes the derived set record
-    const int SD = lq_sd(N);
-    double* out = setdata + (size_t)s * SD;
-    if (lane < N) {
-      out[lane] = ws.d_nat;
-      out[N + lane] = ws.e_nat;
-      out[2 * N + lane] = wr_nat;
-    }
-    const double s2 = c0 / (q.theta * q.w_max);
-    if (lane == 0) {
-      if (!(lr >= 0.0)) atomicOr(errflag, 1);
-      out[3 * N + 0] = q.theta * q.w_max * s2;  // c0, lompc.py:128
-      out[3 * N + 1] = L[0];
-      out[3 * N + 2] = L[N];
-      out[3 * N + 3] = L[2 * N];
-      out[3 * N + 4] = lr;
-      out[3 * N + 5] = lr / q.delta;  // kappa, price_solver.py:191
-      out[3 * N + 6] = gamma_ref ? gamma_ref[s] : 0.5 * q.y_max;
-      out[3 * N + 7] = w_ref ? 1.0 : 0.0;
-      out[3 * N + 8] = wlo;                         // path window start
-      out[3 * N + 9] = (double)LQ_G / (whi - wlo);  // cells per unit gamma
-    }
-  }
-  if (mode == LOMPC_MODE_PATH_REPAIR) {  // diagnostics: no table, every EV re-solved
-    publish_cell(tab.cnt + (size_t)s * LQ_G + cell, pa.epoch, 0);
-    return;
-  }
-  if (!path) {
-    const double g = gamma_ref ? gamma_ref[s] : 0.5 * q.y_max;
-    int sl = lane < N ? 1 : 0;
-    double w = 0.0, r = 0.0;
-    if (!lqw::wave_solve(q, ws, g, sl, w, r)) sl = lane < N ? 1 : 0;
-    central[(size_t)s * LQ_STB + lane] = (uint8_t)(lane < N ? sl : 0);
-    return;
-  }
-  const double h = (whi - wlo) / (double)LQ_G;
-  const double glo = cell == 0 ? wlo : fma((double)cell, h, wlo);
-  const double ghi = (cell == LQ_G - 1) ? whi : fma((double)(cell + 1), h, wlo);
-  const size_t cb = (size_t)s * LQ_G + cell;
+  const double g = pa.gamma_ref ? pa.gamma_ref[s] : 0.5 * q.y_max;
   int sl = lane < N ? 1 : 0;
   double w = 0.0, r = 0.0;
-#ifdef LOMPC_K1_STATS
-  const long long t0 = clock64();
-  int nit = 0;
-  const bool solved = lqw::wave_solve(q, ws, glo, sl, w, r, &nit);
-  const long long t1 = clock64();
-#else
-  const bool solved = lqw::wave_solve(q, ws, glo, sl, w, r);
-#endif
-  if (!solved) {
-    publish_cell(tab.cnt + cb, pa.epoch, 0);  // EVs of this cell are re-solved by wave_solve
-    return;
-  }
-  // parametric active-set tracking of w*(gamma) on [glo, ghi]
-  double gcur = glo;
-  int last = -1, npc = 0;
-  const int max_iter = 4 * LQ_PPL + 16;
-  for (int it = 0; it < max_iter && npc < LQ_PPL; ++it) {
-    const lqw::StageSol<2> sol = lqw::solve_stage<2>(q, ws, 0.0, sl);
-    const double av = sol.w[0], bv = sol.w[1], r0 = sol.r[0], r1 = sol.r[1];
-    double gc = INFINITY;
-    int ns = sl;
-    if (lane < N) {
-      const Box bx = lq_box(sl);
-      if (sl & 1) {  // free: w(gamma) = a + b gamma leaves [lo, hi]
-        if (bv > 0.0) { gc = (bx.hi - av) / bv; ns = sl + 1; }
-        else if (bv < 0.0) { gc = (bx.lo - av) / bv; ns = sl - 1; }
-      } else {       // fixed: v(gamma) = -r0 - r1 gamma leaves [slo, shi]
-        if (r1 < 0.0) { gc = -(bx.shi + r0) / r1; ns = sl + 1; }
-        else if (r1 > 0.0) { gc = -(bx.slo + r0) / r1; ns = sl - 1; }
-      }
-      if (!(gc == gc)) gc = INFINITY;  // NaN guard
-      if (lane == last && gc <= gcur) gc = INFINITY;
-      gc = fmax(gc, gcur);
-    }
-    double best = gc;
-    int bj = lane;
-    lqw::wave_argmin(best, bj, N);
-    if (!(best < ghi)) {
-      best = ghi;
-      bj = -1;
-    }
-    const bool final_piece = (bj < 0) || (npc == LQ_PPL - 1);
-    if (best > gcur || final_piece) {
-      // KKT certificate at the piece's end.  Its start is certified too: the first
-      // piece starts at the wave_solve point; a later one at the previous piece's
-      // certified end with the same w and r, where only the switched coordinate's
-      // box changed and it contains that coordinate's value.  The residual is
-      // convex in gamma along an affine piece => the whole piece is certified.
-      const Box bx = lq_box(lane < N ? sl : 0);
-      const double wz = fmin(fmax(fma(bv, best, av), bx.lo), bx.hi);
-      const double res = lqw::wave_kkt_point(q, ws, best, sl, wz);
-      if (!(res <= q.tol_cert)) break;  // coverage of the cell ends at gcur
-      // cost and err^2 are quadratics in gamma on the piece (w = a + b gamma):
-      // per-lane terms, two prefix sums (Ya, Yb) and six wave totals
-      const bool act = lane < N;
-      lqw::Sums<2> pf;
-      pf.v[0] = act ? av : 0.0;
-      pf.v[1] = act ? bv : 0.0;
-      pf = lqw::wave_scan(pf, N);
-      const double Ya = pf.v[0], Yb = pf.v[1];
-      const double Ea = Ya - Ywr, da = av - wr_nat;
-      const double dd = ws.d_nat, cc = q.c;
-      const double sg = (sl & 1) ? bx.slo : 0.0;  // PWL slope of a free coordinate
-      double icpt = 0.0;                          // PWL value at w = 0 of its linear piece
-      if (!q.ev_small) {
-        const double wm = fma(bv, 0.5 * (gcur + best), av);
-        const double tw = q.theta * q.w_max;
-        icpt = fma(-sg, wm, tw * tw * lq_pwl(wm * q.inv_wmax));
-      }
-      double t[6];
-      t[0] = fma(0.5 * cc, Ya * Ya, fma(av, fma(0.5 * dd, av, ee + sg), icpt));
-      t[1] = fma(cc, fma(Ya, Yb, -Ya), fma(bv, fma(dd, av, ee + sg), 0.0));
-      t[2] = fma(0.5 * cc, Yb * Yb, fma(-cc, Yb, 0.5 * dd * bv * bv));
-      t[3] = fma(Ea, Ea, kappa * da * da);
-      t[4] = 2.0 * fma(Ea, Yb, kappa * da * bv);
-      t[5] = fma(Yb, Yb, kappa * bv * bv);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) t[k] = act ? t[k] : 0.0;
-      lqw::wave_totals(t, N);
-      const size_t pidx = cb * LQ_PPL + npc;
-      if (lane < N) {
-        reinterpret_cast<double2*>(tab.ab + pidx * (size_t)N * 2)[lane] = make_double2(av, bv);
-        tab.st[pidx * LQ_STB + lane] = (uint8_t)sl;
-      }
-      if (lane < 6) {  // row: K0, K1, K2 (cost), F0, F1, F2 (err^2), -, -
-        double v = t[0];
-#pragma unroll
-        for (int k = 1; k < 6; ++k) v = lane == k ? t[k] : v;
-        tab.coef[pidx * 8 + lane] = lane == 0 ? v + c0 : v;
-      }
-      if (lane == 0) tab.gend[pidx] = best;
-      ++npc;
-    }
-    if (bj < 0) break;
-    const int bns = __shfl(ns, bj, 64);
-    if (lane == bj) sl = bns;
-    gcur = best;
-    last = bj;
-  }
-  publish_cell(tab.cnt + cb, pa.epoch, npc);
-#ifdef LOMPC_K1_STATS
-  const long long t2 = clock64();
-  if (lane == 0 && cb < 8192) {
-    g_k1_stats[cb * 4 + 0] = nit;
-    g_k1_stats[cb * 4 + 1] = npc;
-    g_k1_stats[cb * 4 + 2] = t1 - t0;
-    g_k1_stats[cb * 4 + 3] = t2 - t1;
-  }
-#endif
-}
-
-__global__ __launch_bounds__(64) void k_path(QPConst q, PathArgs pa, PathTable tab) {
-  lq_tab_init(q);
-  path_cell(q, pa, tab, (int)blockIdx.x);
-}
-
-// ------------------------------------------------------------------- K2
-template <int NMAX, int NT>
-__global__ __launch_bounds__(EVAL_BLOCK) void k_eval(QPConst q, KArgs a, int epoch) {
-  const int b = (int)blockIdx.x;
-  int s;
-  int64_t start, end;
-  block_set(a, b, s, start, end);
-  const int N = NT ? NT : q.N;
-  const int lane = threadIdx.x;
-  const int64_t i = start + lane;
-  const bool active = i < end;
-  const double* __restrict__ sd = a.setdata + (size_t)s * lq_sd(N);
-  const double g = active ? a.gamma[i] : 0.0;
-  const bool valid = active && (g >= 0.0) && (g <= q.y_max);
-  const double wlo = sd[3 * N + 8], invh = sd[3 * N + 9];  // path window (uniform loads)
-  const bool inwin = g >= wlo;                             // below the window: re-solved
-  const int cell = valid ? max(0, min(LQ_G - 1, (int)((g - wlo) * invh))) : 0;
-  const size_t cb = (size_t)s * LQ_G + cell;
-  // the cell count and the piece ends are loaded together (cb is always a valid cell: one
-  // dependent memory round less than loading the ends behind the count test)
-  const int raw = a.tab.cnt[cb];
-  double ge[LQ_PPL];
-  {
-    const double2* g2 = reinterpret_cast<const double2*>(a.tab.gend + cb * LQ_PPL);
-#pragma unroll
-    for (int pp = 0; pp < LQ_PPL / 2; ++pp) {
-      const double2 v = g2[pp];
-      ge[2 * pp] = v.x;
-      ge[2 * pp + 1] = v.y;
-    }
-  }
-  const bool ready = cell_epoch(raw) == epoch;  // written by this parameter epoch
-  const int cnt = (valid && ready && inwin) ? cell_pieces(raw) : 0;
-  double w[NMAX];
-#pragma unroll
-  for (int t = 0; t < NMAX; ++t) w[t] = 0.0;
-  bool ok = false;
-  EVOut o{0.0, 0.0, 0.0};
-  if (cnt > 0) {
-    int p = cnt - 1;
-    double glast = -1.0;
-#pragma unroll
-    for (int pp = LQ_PPL - 1; pp >= 0; --pp) {
-      if (pp < cnt && g <= ge[pp]) p = pp;
-      if (pp == cnt - 1) glast = ge[pp];
-    }
-    ok = g <= glast;  // inside a certified piece
-    if (ok) {
-      const size_t pidx = cb * LQ_PPL + p;
-      const double2* row = reinterpret_cast<const double2*>(a.tab.ab + pidx * (size_t)N * 2);
-      const double4 cf0 = *reinterpret_cast<const double4*>(a.tab.coef + pidx * 8);
-      const double2 cf1 = *reinterpret_cast<const double2*>(a.tab.coef + pidx * 8 + 4);
-#pragma unroll
-      for (int t = 0; t < NMAX; ++t)
-        if (t < N) {
-          const double2 ab = row[t];
-          w[t] = fmin(fmax(fma(ab.y, g, ab.x), 0.0), q.w_max);
-        }
-      o.cost = fma(fma(cf0.z, g, cf0.y), g, cf0.x);
-      o.err = a.want_err ? sqrt(fmax(fma(fma(cf1.y, g, cf1.x), g, cf0.w), 0.0)) : 0.0;
-      o.price0 = lq_price0(q, sd, w[0]);
-    }
-  }
-  // ---- in-place repair: EVs no certified piece covers are solved by the whole wave
-  bool rep = false;
-  unsigned long long need = __ballot(valid && !ok);
-  if (need) {  // wave-uniform (one wave per workgroup)
-    lq_tab_init(q);
-    __shared__ double stage[64];
-    lqw::WaveSet ws;
-    ws.load(sd, N);
-    while (need) {
-      const int l = (int)__builtin_ctzll(need);
-      need &= need - 1ull;
-      const double gl = lqw::readlane_d(g, l);
-      const int rawl = __builtin_amdgcn_readlane(raw, l);
-      const int celll = __builtin_amdgcn_readlane(cell, l);
-      int sl = 1;
-      if (cell_epoch(rawl) == epoch && cell_pieces(rawl) > 0)
-        sl = a.tab.st[((size_t)s * LQ_G + celll) * LQ_PPL * LQ_STB + lane];
-      if (lane >= N) sl = 0;
-      double wl = 0.0, rl = 0.0;
-      const bool okk = lqw::wave_solve(q, ws, gl, sl, wl, rl);
-      const EVOut ol = wave_outputs(q, sd, gl, lane, wl, a.want_err != 0);
-      stage[lane] = wl;
-      __syncthreads();
-      if (lane == l) {
-#pragma unroll
-        for (int t = 0; t < NMAX; ++t)
-          if (t < N) w[t] = stage[t];
-        o = ol;
-        ok = okk;
-        rep = true;
-      }
-      __syncthreads();
-    }
-  }
-  ev_epilogue<NMAX, true>(q, N, a, b, start, end, valid, ok, w, o, rep);
+  if (!lqw::wave_solve(q, ws, g, sl, w, r)) sl = lane < N ? 1 : 0;
+  pa.central[(size_t)s * LQ_STB + lane] = (uint8_t)(lane < N ? sl : 0);
 }
 
 // ------------------------------------------------------------------- K2d
@@ -604,12 +301,12 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_direct(QPConst q, KArgs a) {
 
 // ------------------------------------------------------------------- K3
 // One workgroup of 1024 threads (16 waves) per set.
-// (1) repair: wave wv re-solves the listed EVs of workgroups b0+wv, b0+wv+16, ...
-//     (wave_solve: PDAS from the cell's / central working set, primal active set
-//     if needed, KKT-certified) and writes their outputs;
-// (2) reduction: wave wv sums partial rows wv, wv+16, ... (lane = column), the 16
-//     waves and the repair accumulators combine in LDS in a fixed order.
-__global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode, double* __restrict__ set_sum_w,
+// (1) reduction: wave wv sums partial rows wv, wv+16, ... (lane = column), the 16 waves
+//     combine in LDS in a fixed order;
+// (2) repair: wave wv re-solves the listed EVs of workgroups b0+wv, b0+wv+16, ...
+//     (wave_solve: PDAS from the central working set, primal active set if needed,
+//     KKT-certified), writes their outputs and adds them to the reduction in a fixed order.
+__global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, double* __restrict__ set_sum_w,
                                                    double* __restrict__ set_stats, double* __restrict__ stats_int) {
   __shared__ double red[16][LOMPC_MAX_N + NPX + 1];
   __shared__ double rep[16][LOMPC_MAX_N + NPX + 1];
@@ -619,11 +316,9 @@ __global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode,
   const int N = q.N;
   const int W = N + NPX;
   const int b0 = a.blk_prefix[s], b1 = a.blk_prefix[s + 1];
-  // ---- (1) reduction of the workgroup partials (their N_FAILED column = pending repairs)
   for (int c = lane; c < W; c += 64) {
     const bool is_max = (c == N + PX_MAX_ERR);
-    // 16 independent (predicated) loads per round: one memory round trip per 256 partial
-    // rows of the set instead of one per row of the tail
+    // 16 independent (predicated) loads per round: one memory round trip per 256 partial rows
     constexpr int U = 16;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     for (int b = b0 + wv; b < b1; b += 16 * U) {
@@ -647,10 +342,7 @@ __global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode,
     red[0][c] = acc;
   }
   __syncthreads();
-  // DIRECT mode: N_FAILED counts EVs listed for repair; PATH partials hold final counts
-  // (k_eval repairs in place)
-  const bool pending = mode == LOMPC_MODE_DIRECT && red[0][N + PX_N_FAILED] > 0.0;  // block-uniform
-  // ---- (2) repair: wave wv re-solves the listed EVs of workgroups b0+wv, b0+wv+16, ...
+  const bool pending = red[0][N + PX_N_FAILED] > 0.0;  // block-uniform
   if (pending) {
     lq_tab_init(q);
     double acc_w = 0.0, acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
@@ -664,7 +356,7 @@ __global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode,
         const int l = a.fail_lane[(size_t)b * EVAL_BLOCK + k];
         const int64_t i = a.set_off[s] + (int64_t)(b - b0) * EVAL_BLOCK + l;
         const double g = a.gamma[i];
-        int sl = a.central[(size_t)s * LQ_STB + lane];  // DIRECT mode only
+        int sl = a.central[(size_t)s * LQ_STB + lane];
         if (lane >= N) sl = 0;
         double wl = 0.0, rl = 0.0;
         const bool okk = lqw::wave_solve(q, ws, g, sl, wl, rl);
@@ -722,83 +414,6 @@ __global__ __launch_bounds__(1024) void k_finalize(QPConst q, KArgs a, int mode,
 }
 
 // ===================================================================== host
-struct lompc_ctx {
-  int device = 0;
-  int N = 0;
-  int ev_type = 0;
-  int mode = LOMPC_MODE_PATH;
-  int nmax = 0;
-  QPConst q{};
-  // parameter sets
-  int64_t S = 0, S_cap = 0;
-  double* d_setdata = nullptr;
-  PathTable tab{nullptr, nullptr, nullptr, nullptr, nullptr};
-  uint8_t* d_central = nullptr;
-  int* d_errflag = nullptr;
-  const double* d_window = nullptr;  // lompc_set_gamma_window (caller-owned, sticky)
-  int params_mode = -1;
-  // batch workspaces
-  int64_t nblk_cap = 0, soff_cap = 0, stats_cap = 0;
-  double* d_partial = nullptr;
-  int* d_fail_cnt = nullptr;
-  uint8_t* d_fail_lane = nullptr;
-  int* d_blk_prefix = nullptr;
-  int64_t* d_set_off = nullptr;
-  longlong4* d_blk_info = nullptr;
-  longlong4* h_pin_info = nullptr;
-  int64_t info_cap = 0;
-  double* d_stats = nullptr;  // [S][LOMPC_SET_STATS], always written by the set reduction
-  int epoch = 0;  // parameter epoch of the path table (tags tab.cnt)
-  int64_t stats_S = 0;
-  int* h_pin_prefix = nullptr;
-  int64_t* h_pin_off = nullptr;
-  hipEvent_t ev_map = nullptr;
-  std::vector<int64_t> last_off;
-  void* last_off_stream = nullptr;
-  // single-solve scratch (3N + N + 8 doubles)
-  double* d_single = nullptr;
-  int8_t* d_single_status = nullptr;
-  // profiling
-  bool prof = false;
-  std::vector<hipEvent_t> prof_ev;    // pairs recorded since the last read
-  std::vector<hipEvent_t> prof_pool;  // recycled events (no creation inside timed loops)
-  double prof_ms = 0.0;
-  int64_t prof_n = 0;
-  std::string err;
-};
-
-#define HIPCHK(ctx, call)                                                        \
-  do {                                                                           \
-    hipError_t e__ = (call);                                                     \
-    if (e__ != hipSuccess) {                                                     \
-      if (ctx) (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e__); \
-      return LOMPC_ERR_HIP;                                                      \
-    }                                                                            \
-  } while (0)
-
-static int fail_arg(lompc_ctx* ctx, const char* msg) {
-  if (ctx) ctx->err = msg;
-  return LOMPC_ERR_INVALID_ARG;
-}
-
-template <typename T>
-static int grow(lompc_ctx* ctx, T** p, size_t n_elems) {
-  if (*p) {
-    hipError_t e = hipFree(*p);
-    if (e != hipSuccess) {
-      ctx->err = std::string("hipFree: ") + hipGetErrorString(e);
-      return LOMPC_ERR_HIP;
-    }
-  }
-  *p = nullptr;
-  hipError_t e = hipMalloc((void**)p, std::max<size_t>(n_elems, 1) * sizeof(T));
-  if (e != hipSuccess) {
-    ctx->err = std::string("hipMalloc: ") + hipGetErrorString(e);
-    return LOMPC_ERR_HIP;
-  }
-  return LOMPC_OK;
-}
-
 static int pick_nmax(int N) {
   if (N <= 16) return 16;
   if (N <= 24) return 24;
@@ -828,20 +443,18 @@ static int pick_nmax(int N) {
       }                                                                             \
   }
 
+static int ensure_stats(lompc_ctx* c, int64_t S) {
+  if (S > c->stats_cap) {
+    int rc;
+    if ((rc = grow(c, &c->d_stats, (size_t)S * LOMPC_SET_STATS))) return rc;
+    c->stats_cap = S;
+  }
+  return LOMPC_OK;
+}
+
 extern "C" {
 
-int lompc_abi_version(void) { return 1; }
-
-#ifdef LOMPC_K1_STATS
-// diagnostic build only (scripts/k1_stats.py): per-cell K1 counters of the last launch
-int lompc_debug_k1_stats(long long* host, int n) {
-  if (n > 8192 * 4) n = 8192 * 4;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_k1_stats), sizeof(long long) * n, 0, hipMemcpyDeviceToHost) ==
-                 hipSuccess
-             ? LOMPC_OK
-             : LOMPC_ERR_HIP;
-}
-#endif
+int lompc_abi_version(void) { return LOMPC_ABI_VERSION; }
 
 const char* lompc_status_string(int status) {
   switch (status) {
@@ -922,9 +535,9 @@ int lompc_destroy(lompc_ctx* c) {
   if (!c) return LOMPC_OK;
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
-  void* ptrs[] = {c->d_setdata, c->tab.cnt, c->tab.gend, c->tab.ab, c->tab.coef, c->tab.st, c->d_central, c->d_errflag,
-                  c->d_partial, c->d_fail_cnt, c->d_fail_lane, c->d_blk_prefix, c->d_set_off, c->d_blk_info, c->d_stats,
-                  c->d_single, c->d_single_status};
+  if (c->tplan) lq_plan_free(c->tplan);
+  void* ptrs[] = {c->d_setdata, c->d_central, c->d_errflag, c->d_partial, c->d_fail_cnt, c->d_fail_lane,
+                  c->d_blk_prefix, c->d_set_off, c->d_blk_info, c->d_stats, c->d_single, c->d_single_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_pin_prefix) (void)hipHostFree(c->h_pin_prefix);
@@ -939,8 +552,8 @@ int lompc_destroy(lompc_ctx* c) {
 
 int lompc_set_mode(lompc_ctx* c, int mode) {
   if (!c) return LOMPC_ERR_INVALID_ARG;
-  if (mode != LOMPC_MODE_PATH && mode != LOMPC_MODE_DIRECT && mode != LOMPC_MODE_PATH_REPAIR)
-    return fail_arg(c, "mode must be PATH, DIRECT or PATH_REPAIR");
+  if (mode != LOMPC_MODE_PATH && mode != LOMPC_MODE_DIRECT)
+    return fail_arg(c, "mode must be LOMPC_MODE_PATH or LOMPC_MODE_DIRECT");
   c->mode = mode;
   return LOMPC_OK;
 }
@@ -952,57 +565,36 @@ int lompc_get_info(const lompc_ctx* c, int* N, int* ev_type) {
   return LOMPC_OK;
 }
 
-// Validate / size the parameter-set buffers and open a new cell epoch.
-static int prepare_params(lompc_ctx* c, int64_t S, const double* lmbd, const double* lmbd_r, PathArgs* pa,
-                          const double* w_ref, const double* gamma_ref) {
+int lompc_set_params(lompc_ctx* c, int64_t S, const double* lmbd, const double* lmbd_r, const double* w_ref,
+                     const double* gamma_ref, void* stream) {
   if (!c) return LOMPC_ERR_INVALID_ARG;
   if (S < 1 || !lmbd || !lmbd_r) return fail_arg(c, "set_params: S >= 1 and lmbd, lmbd_r required");
   if (S > (1 << 20)) return fail_arg(c, "set_params: too many parameter sets");
   HIPCHK(c, hipSetDevice(c->device));
+  c->S = S;
+  c->params_mode = c->mode;
+  c->p_lmbd = lmbd;
+  c->p_lmbd_r = lmbd_r;
+  c->p_w_ref = w_ref;
+  c->p_gamma_ref = gamma_ref;
+  if (c->mode != LOMPC_MODE_DIRECT) return LOMPC_OK;  // PATH: read by the solve's k_solve
   const int N = c->N;
   if (S > c->S_cap) {
     int rc;
-    const size_t cells = (size_t)S * LQ_G;
-    if ((rc = grow(c, &c->d_setdata, (size_t)S * lq_sd(N))) || (rc = grow(c, &c->tab.cnt, cells)) ||
-        (rc = grow(c, &c->tab.gend, cells * LQ_PPL)) || (rc = grow(c, &c->tab.ab, cells * LQ_PPL * (size_t)N * 2)) ||
-        (rc = grow(c, &c->tab.coef, cells * LQ_PPL * 8)) ||
-        (rc = grow(c, &c->tab.st, cells * LQ_PPL * LQ_STB)) || (rc = grow(c, &c->d_central, (size_t)S * LQ_STB)))
+    if ((rc = grow(c, &c->d_setdata, (size_t)S * lq_sd(N))) || (rc = grow(c, &c->d_central, (size_t)S * LQ_STB)))
       return rc;
-    HIPCHK(c, hipMemset(c->tab.cnt, 0, cells * sizeof(int)));  // epoch 0 = never published
     c->S_cap = S;
   }
-  c->S = S;
-  c->params_mode = c->mode;
-  c->epoch = (c->epoch + 1) & 0x7ffffff;
-  if (c->epoch == 0) c->epoch = 1;
-  pa->S = (int)S;
-  pa->mode = c->mode;
-  pa->epoch = c->epoch;
-  pa->pad = 0;
-  pa->lmbd = lmbd;
-  pa->lmbd_r = lmbd_r;
-  pa->w_ref = w_ref;
-  pa->gamma_ref = gamma_ref;
-  pa->window = c->mode != LOMPC_MODE_DIRECT ? c->d_window : nullptr;
-  pa->setdata = c->d_setdata;
-  pa->central = c->d_central;
-  pa->errflag = c->d_errflag;
-  return LOMPC_OK;
-}
-
-int lompc_set_gamma_window(lompc_ctx* c, const double* window) {
-  if (!c) return LOMPC_ERR_INVALID_ARG;
-  c->d_window = window;
-  return LOMPC_OK;
-}
-
-int lompc_set_params(lompc_ctx* c, int64_t S, const double* lmbd, const double* lmbd_r, const double* w_ref,
-                     const double* gamma_ref, void* stream) {
-  PathArgs pa{};
-  const int rc = prepare_params(c, S, lmbd, lmbd_r, &pa, w_ref, gamma_ref);
-  if (rc) return rc;
-  const unsigned grid = (unsigned)(c->mode != LOMPC_MODE_DIRECT ? S * LQ_G : S);
-  hipLaunchKernelGGL(k_path, dim3(grid), dim3(64), 0, (hipStream_t)stream, c->q, pa, c->tab);
+  CentralArgs pa{};
+  pa.S = (int)S;
+  pa.lmbd = lmbd;
+  pa.lmbd_r = lmbd_r;
+  pa.w_ref = w_ref;
+  pa.gamma_ref = gamma_ref;
+  pa.setdata = c->d_setdata;
+  pa.central = c->d_central;
+  pa.errflag = c->d_errflag;
+  hipLaunchKernelGGL(k_central, dim3((unsigned)S), dim3(64), 0, (hipStream_t)stream, c->q, pa);
   HIPCHK(c, hipGetLastError());
   return LOMPC_OK;
 }
@@ -1025,11 +617,6 @@ static int upload_block_map(lompc_ctx* c, const int64_t* set_off, int64_t S, int
         (rc = grow(c, &c->d_fail_lane, (size_t)nb * EVAL_BLOCK)))
       return rc;
     c->nblk_cap = nb;
-  }
-  if (S > c->stats_cap) {
-    int rc;
-    if ((rc = grow(c, &c->d_stats, (size_t)S * LOMPC_SET_STATS))) return rc;
-    c->stats_cap = S;
   }
   const bool same = (int64_t)c->last_off.size() == S + 1 && c->last_off_stream == (void*)st &&
                     memcmp(c->last_off.data(), set_off, (S + 1) * sizeof(int64_t)) == 0;
@@ -1071,14 +658,10 @@ static int upload_block_map(lompc_ctx* c, const int64_t* set_off, int64_t S, int
   return LOMPC_OK;
 }
 
-// Per-EV work of one batch: k_eval (PATH) or k_direct (DIRECT), then k_finalize.
-static int launch_batch(lompc_ctx* c, int64_t B, const double* gamma,
-                        const int64_t* set_offsets, double* w, double* cost, double* w0, int8_t* status,
-                        double* set_sum_w, double* set_stats, hipStream_t st) {
-  if (B < 0 || !set_offsets) return fail_arg(c, "solve_batch: invalid batch");
-  if (set_offsets[0] != 0 || set_offsets[c->S] != B)
-    return fail_arg(c, "solve_batch: set_offsets must start at 0 and end at B");
-  if (B > 0 && !gamma) return fail_arg(c, "solve_batch: gamma required");
+// DIRECT mode: k_direct then k_finalize
+static int launch_direct(lompc_ctx* c, int64_t B, const double* gamma, const int64_t* set_offsets, double* w,
+                         double* cost, double* w0, int8_t* status, double* set_sum_w, double* set_stats,
+                         hipStream_t st) {
   int nblk = 0;
   int rc = upload_block_map(c, set_offsets, c->S, &nblk, st);
   if (rc) return rc;
@@ -1092,7 +675,6 @@ static int launch_batch(lompc_ctx* c, int64_t B, const double* gamma,
   a.set_off = c->d_set_off;
   a.blk_info = c->d_blk_info;
   a.setdata = c->d_setdata;
-  a.tab = c->tab;
   a.central = c->d_central;
   a.w = w;
   a.cost = cost;
@@ -1101,8 +683,6 @@ static int launch_batch(lompc_ctx* c, int64_t B, const double* gamma,
   a.partial = c->d_partial;
   a.fail_cnt = c->d_fail_cnt;
   a.fail_lane = c->d_fail_lane;
-  // profiling: start/stop timestamps ride on the per-EV kernel's own dispatch
-  // (hipExtLaunchKernel), no marker packets between the kernels
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->prof && nblk > 0) {
     for (hipEvent_t* e : {&e0, &e1}) {
@@ -1116,23 +696,15 @@ static int launch_batch(lompc_ctx* c, int64_t B, const double* gamma,
   }
   if (nblk > 0) {
     dim3 grid((unsigned)nblk), block(EVAL_BLOCK);
-    if (c->params_mode != LOMPC_MODE_DIRECT) {
-      const int ep = c->epoch;
-      DISPATCH_N(c->N, c->nmax,
-                 hipExtLaunchKernelGGL((k_eval<NM, NT>), grid, block, 0, st, e0, e1, 0, c->q, a, ep));
-    } else {
-      DISPATCH_N(c->N, c->nmax, hipExtLaunchKernelGGL((k_direct<NM, NT>), grid, block, 0, st, e0, e1, 0, c->q, a));
-    }
+    DISPATCH_N(c->N, c->nmax, hipExtLaunchKernelGGL((k_direct<NM, NT>), grid, block, 0, st, e0, e1, 0, c->q, a));
     HIPCHK(c, hipGetLastError());
     if (e0) {
       c->prof_ev.push_back(e0);
       c->prof_ev.push_back(e1);
     }
   }
-  hipLaunchKernelGGL(k_finalize, dim3((unsigned)c->S), dim3(1024), 0, st, c->q, a, c->params_mode, set_sum_w,
-                     set_stats, c->d_stats);
+  hipLaunchKernelGGL(k_finalize, dim3((unsigned)c->S), dim3(1024), 0, st, c->q, a, set_sum_w, set_stats, c->d_stats);
   HIPCHK(c, hipGetLastError());
-  c->stats_S = c->S;
   return LOMPC_OK;
 }
 
@@ -1141,8 +713,31 @@ int lompc_solve_batch(lompc_ctx* c, int64_t B, const double* gamma, const int64_
                       void* stream) {
   if (!c) return LOMPC_ERR_INVALID_ARG;
   if (c->S < 1) return fail_arg(c, "solve_batch: call lompc_set_params first");
+  if (B < 0 || !set_offsets) return fail_arg(c, "solve_batch: invalid batch");
+  if (set_offsets[0] != 0 || set_offsets[c->S] != B)
+    return fail_arg(c, "solve_batch: set_offsets must start at 0 and end at B");
+  if (B > 0 && !gamma) return fail_arg(c, "solve_batch: gamma required");
   HIPCHK(c, hipSetDevice(c->device));
-  return launch_batch(c, B, gamma, set_offsets, w, cost, w0, status, set_sum_w, set_stats, (hipStream_t)stream);
+  const hipStream_t st = (hipStream_t)stream;
+  int rc = ensure_stats(c, c->S);
+  if (rc) return rc;
+  c->stats_S = c->S;
+  if (c->params_mode == LOMPC_MODE_DIRECT)
+    return launch_direct(c, B, gamma, set_offsets, w, cost, w0, status, set_sum_w, set_stats, st);
+  // PATH: the context's transient plan for this batch
+  if (!c->tplan) c->tplan = new lompc_plan();
+  lompc_plan* p = c->tplan;
+  lompc_ctx* cs[1] = {c};
+  const int64_t S = c->S;
+  rc = lq_plan_prepare(p, 1, cs, &S, B, gamma, set_offsets, c->p_w_ref, 0, st);
+  if (rc) {
+    c->err = p->err;
+    return rc;
+  }
+  p->d_stats = c->d_stats;
+  rc = lq_plan_launch(p, c->p_lmbd, c->p_lmbd_r, w, cost, w0, status, set_sum_w, set_stats, st, c);
+  if (rc) c->err = p->err;
+  return rc;
 }
 
 int lompc_run(lompc_ctx* c, int64_t S, const double* lmbd, const double* lmbd_r, const double* w_ref,
@@ -1157,11 +752,13 @@ int lompc_last_status(lompc_ctx* c, void* stream, int64_t* n_repaired, int64_t* 
   if (!c) return LOMPC_ERR_INVALID_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<double> h((size_t)std::max<int64_t>(c->stats_S, 1) * LOMPC_SET_STATS, 0.0);
-  int ef = 0;
+  int ef = 0, ef2 = 0;
   if (c->stats_S > 0)
     HIPCHK(c, hipMemcpyAsync(h.data(), c->d_stats, c->stats_S * LOMPC_SET_STATS * sizeof(double),
                              hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(c, hipMemcpyAsync(&ef, c->d_errflag, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  if (c->tplan && c->tplan->d_errflag)
+    HIPCHK(c, hipMemcpyAsync(&ef2, c->tplan->d_errflag, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
   double rep = 0, fail = 0, inv = 0;
   for (int64_t s = 0; s < c->stats_S; ++s) {
@@ -1172,8 +769,9 @@ int lompc_last_status(lompc_ctx* c, void* stream, int64_t* n_repaired, int64_t* 
   if (n_repaired) *n_repaired = (int64_t)rep;
   if (n_failed) *n_failed = (int64_t)fail;
   if (n_invalid) *n_invalid = (int64_t)inv;
-  if (ef) {
+  if (ef || ef2) {
     HIPCHK(c, hipMemsetAsync(c->d_errflag, 0, sizeof(int), (hipStream_t)stream));
+    if (ef2) HIPCHK(c, hipMemsetAsync(c->tplan->d_errflag, 0, sizeof(int), (hipStream_t)stream));
     return fail_arg(c, "negative or NaN price parameter (lmbd >= 0, lmbd_r >= 0 required)");
   }
   return LOMPC_OK;

@@ -28,7 +28,9 @@ LOMPC_EV_SMALL = 0
 LOMPC_EV_LARGE = 1
 LOMPC_MODE_PATH = 0
 LOMPC_MODE_DIRECT = 1
-LOMPC_MODE_PATH_REPAIR = 2
+LOMPC_PLAN_MAX_CTX = 4
+LOMPC_PLAN_WARM_START = 1
+LOMPC_PLAN_DIAG_REPAIR = 2
 
 LOMPC_QP_OK = 0
 LOMPC_QP_REPAIRED = 1
@@ -56,7 +58,6 @@ SIGNATURES = [
     ("lompc_destroy", _I, [_P]),
     ("lompc_set_mode", _I, [_P, _I]),
     ("lompc_set_params", _I, [_P, _L, _P, _P, _P, _P, _P]),
-    ("lompc_set_gamma_window", _I, [_P, _P]),
     ("lompc_solve_batch", _I, [_P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_run", _I, [_P, _L, _P, _P, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_solve_host", _I, [_P, _P, _D, _D, _P, _P]),
@@ -70,12 +71,20 @@ SIGNATURES = [
     ("lompc_price_step", _I, [_I, _I, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P]),
     ("lompc_lp_separable", _I, [_I, _I, _P, _P, _P, _P]),
     ("lompc_bimpc_solve", _I, [_I, _I, _I] + [_D] * 10 + [_P] * 6 + [_D] + [_P] * 6),
+    ("lompc_plan_create", _I, [_I, _P, _P, _L, _P, _P, _P, _I, _P, ctypes.POINTER(_P)]),
+    ("lompc_plan_run", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    ("lompc_plan_status", _I, [_P, _P, _P, _P, _P]),
+    ("lompc_plan_get_info", _I, [_P, _P, _P, _P]),
+    ("lompc_plan_profile_enable", _I, [_P, _I]),
+    ("lompc_plan_profile_read", _I, [_P, _P, _P, _I]),
+    ("lompc_plan_last_error", ctypes.c_char_p, [_P]),
+    ("lompc_plan_destroy", _I, [_P]),
 ]
 LOMPC_BIMPC_WEIGHTED = 0
 LOMPC_BIMPC_UNWEIGHTED = 1
 LOMPC_BIMPC_EXP_UNWEIGHTED = 2
 LOMPC_BIMPC_INFO = 5
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lock = threading.Lock()
 _lib = None
@@ -104,7 +113,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
-def status_text(lib, ctx, rc: int) -> str:
-    msg = lib.lompc_last_error(ctx) if ctx else b""
+def status_text(lib, ctx, rc: int, plan=None) -> str:
+    msg = lib.lompc_plan_last_error(plan) if plan else (lib.lompc_last_error(ctx) if ctx else b"")
     base = lib.lompc_status_string(rc).decode()
     return f"{base}: {msg.decode()}" if msg else base

@@ -68,7 +68,7 @@ class LoMPC:
             N:      LoMPC horizon length.
             consts: LoMPC constants.
             device: HIP device index (default: torch's current device).
-            mode:   "path" (default), "direct" or "path_repair" (diagnostics) — engine algorithm, see DESIGN.md.
+            mode:   "path" (default) or "direct" — engine algorithm, see DESIGN.md.
         """
         # lompc.py:36-38
         assert (consts.y_max >= MIN_MAX_BAT_SOC) and (consts.y_max <= MAX_MAX_BAT_SOC)
@@ -187,8 +187,7 @@ class LoMPC:
 
     # ------------------------------------------------------------ batch API
     def set_mode(self, mode: str) -> None:
-        m = {"path": _lib.LOMPC_MODE_PATH, "direct": _lib.LOMPC_MODE_DIRECT,
-             "path_repair": _lib.LOMPC_MODE_PATH_REPAIR}[mode]
+        m = {"path": _lib.LOMPC_MODE_PATH, "direct": _lib.LOMPC_MODE_DIRECT}[mode]
         self._check_rc(self._lib.lompc_set_mode(self._ctx, m))
         self.mode = mode
 
@@ -233,7 +232,6 @@ class LoMPC:
             bad = torch.logical_not(lm >= 0).any() | torch.logical_not(lr >= 0).any()
             if bool(bad):
                 raise ValueError("Parameter value must be nonnegative.")
-        self._lib.lompc_set_gamma_window(self._ctx, None)  # full [0, y_max] path (BatchPlan sets its own)
         rc = self._lib.lompc_set_params(self._ctx, S, _ptr(lm), _ptr(lr), _ptr(wr), _ptr(gr), self._stream())
         self._check_rc(rc)
         self._keep = (lm, lr, wr, gr)
@@ -320,42 +318,61 @@ class LoMPC:
 
 
 class BatchPlan:
-    """Repeated batched solves over a fixed EV batch with one C-ABI call each.
+    """A fixed EV batch solved at new prices every price iteration: one C-ABI call per run.
 
-    Validates and allocates once (gamma, set_offsets, outputs, w_ref,
-    gamma_ref); ``run(lmbd, lmbd_r)`` then issues ``lompc_run`` with cached pointers — the host cost
-    of one price iteration is a single ctypes call.  lmbd: contiguous fp64
-    device tensor (S, 3N); lmbd_r: (S,) on the same device.  No synchronisation;
-    call ``lompc.check_last()`` when the status is needed.
-    In PATH mode the call is three dependent launches on the plan's stream: k_path
-    (solution path per parameter set), k_eval (per-EV evaluation) and k_finalize
-    (per-set reductions); see DESIGN.md.
-    window=True: each set's path is computed only over the range of its EVs' gamma
-    (lompc_set_gamma_window, measured once here; gamma is fixed for the plan — values
-    changed later outside that range are still solved correctly, by the repair pass);
-    an (S, 2) array gives the ranges directly (no measuring); False: [0, y_max].
+    Wraps ``lompc_plan_create`` / ``lompc_plan_run`` (include/lompc_amd.h).  ``lompc`` is one
+    ``LoMPC`` or a list of them (EV types of the same horizon and device); their parameter
+    sets are stacked in list order (``sets_per_ctx`` gives how many each owns) and every
+    ``run`` is ONE fused launch over all of them plus the per-set reduction.
+    At construction the batch is validated, grouped by gamma cell on the device (the plan
+    keeps its own copy of gamma: a plan is built per price loop / time step, where
+    gamma_i = y_max - y0_i is fixed, price_solver.py:66-77) and the outputs are allocated.
+    ``run(lmbd, lmbd_r)`` then issues one ``lompc_plan_run`` with cached pointers; lmbd:
+    contiguous fp64 device tensor (S, 3N), lmbd_r (S,) on the same device (or raw device
+    pointers).  No synchronisation; ``check()`` synchronises and raises on failures.
+    w_ref (S, N) is read at every run (update it in place).  ``warm_start``: every gamma
+    cell's exact solve starts from the working set the previous run ended with.  ``diag_repair``
+    (diagnostics): no solution path, every EV is re-solved individually.
+    DIRECT-mode contexts fall back to ``lompc_run`` (one context only).
     """
 
-    def __init__(self, lompc: "LoMPC", gamma, set_offsets, *, w_ref=None, gamma_ref=None, want_w=True,
-                 want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None, window=True,
-                 validate=True):
+    def __init__(self, lompc, gamma, set_offsets, *, sets_per_ctx=None, w_ref=None, gamma_ref=None, want_w=True,
+                 want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None, validate=True,
+                 warm_start=False, diag_repair=False):
         torch = _torch()
-        self.lompc = lompc
-        self.gamma = lompc._dev(gamma).reshape(-1)
+        lompcs = list(lompc) if isinstance(lompc, (list, tuple)) else [lompc]
+        self.lompcs = lompcs
+        self.lompc = lompcs[0]
+        lo = self.lompc
+        N = lo.N
+        if any(x.N != N or x.device != lo.device for x in lompcs):
+            raise ValueError("BatchPlan: every LoMPC must have the same horizon and device")
+        if len(lompcs) > _lib.LOMPC_PLAN_MAX_CTX:
+            raise ValueError(f"BatchPlan: at most {_lib.LOMPC_PLAN_MAX_CTX} contexts")
+        self.gamma = lo._dev(gamma).reshape(-1)
         B = self.gamma.numel()
         self.off = np.ascontiguousarray(np.asarray(set_offsets, dtype=np.int64))
         S = self.off.shape[0] - 1
         if S < 1 or self.off[0] != 0 or self.off[-1] != B or np.any(np.diff(self.off) < 0):
             raise ValueError("set_offsets must be non-decreasing from 0 to B")
+        if sets_per_ctx is None:
+            if len(lompcs) != 1:
+                raise ValueError("sets_per_ctx required with several contexts")
+            sets_per_ctx = [S]
+        self.sets_per_ctx = np.ascontiguousarray(np.asarray(sets_per_ctx, dtype=np.int64))
+        if self.sets_per_ctx.shape != (len(lompcs),) or int(self.sets_per_ctx.sum()) != S:
+            raise ValueError("sets_per_ctx must give one count per context, summing to S")
         if validate:  # (callers that already checked 0 <= gamma <= y_max skip two host syncs)
-            if bool((self.gamma > lompc.y_max).any()):
+            ym = np.repeat([x.y_max for x in lompcs], self.sets_per_ctx)
+            ymax_ev = torch.as_tensor(np.repeat(ym, np.diff(self.off)), device=self.gamma.device)
+            if bool((self.gamma > ymax_ev).any()):
                 raise AssertionError("gamma <= y_max required")
             if bool(torch.logical_not(self.gamma >= 0).any()):
                 raise ValueError("Parameter value must be nonnegative.")
-        self.S, self.B, N = S, B, lompc.N
-        dev = f"cuda:{lompc.device}"
-        self.w_ref = None if w_ref is None else lompc._dev(w_ref).reshape(S, N)
-        self.gamma_ref = None if gamma_ref is None else lompc._dev(gamma_ref).reshape(S)
+        self.S, self.B, self.N = S, B, N
+        dev = f"cuda:{lo.device}"
+        self.w_ref = None if w_ref is None else lo._dev(w_ref).reshape(S, N)
+        self.gamma_ref = None if gamma_ref is None else lo._dev(gamma_ref).reshape(S)
         e = lambda shape, dt=torch.float64: torch.empty(shape, dtype=dt, device=dev)
         self.out = {
             "w": e((B, N)) if want_w else None,
@@ -365,26 +382,89 @@ class BatchPlan:
             "set_sum_w": e((S, N)) if want_set else None,
             "set_stats": e((S, _lib.LOMPC_SET_STATS)) if want_set else None,
         }
-        self.window = None
-        if window is not None and window is not True and window is not False:  # caller's (S, 2) ranges
-            self.window = torch.as_tensor(np.asarray(window, dtype=np.float64).reshape(S, 2), device=dev)
-        elif window and B > 0:  # per-set (min, max) of gamma: two segment reductions
-            lens = torch.as_tensor(np.diff(self.off), device=dev)
-            lo_ = torch.segment_reduce(self.gamma, "min", lengths=lens, unsafe=True)
-            hi_ = torch.segment_reduce(self.gamma, "max", lengths=lens, unsafe=True)
-            self.window = torch.stack([lo_, hi_], dim=1).contiguous()
-        self._stream = (stream if stream is not None else torch.cuda.current_stream(lompc.device)).cuda_stream
-        self._args = [_ptr(self.w_ref), _ptr(self.gamma_ref), B, _ptr(self.gamma), self.off.ctypes.data] + \
-            [_ptr(self.out[k]) for k in ("w", "cost", "w0", "status", "set_sum_w", "set_stats")] + [self._stream]
+        self._stream = (stream if stream is not None else torch.cuda.current_stream(lo.device)).cuda_stream
+        self._outs = [_ptr(self.out[k]) for k in ("w", "cost", "w0", "status", "set_sum_w", "set_stats")]
+        self._lib = lo._lib
+        self._plan = None
+        self.direct = any(x.mode == "direct" for x in lompcs)
+        if self.direct:
+            if len(lompcs) != 1:
+                raise ValueError("DIRECT mode plans hold one context")
+            self._args = [_ptr(self.w_ref), _ptr(self.gamma_ref), B, _ptr(self.gamma), self.off.ctypes.data] + \
+                self._outs + [self._stream]
+            return
+        ctxs = (ctypes.c_void_p * len(lompcs))(*[x._ctx.value for x in lompcs])
+        plan = ctypes.c_void_p()
+        flags = (_lib.LOMPC_PLAN_WARM_START if warm_start else 0) | (_lib.LOMPC_PLAN_DIAG_REPAIR if diag_repair else 0)
+        rc = self._lib.lompc_plan_create(len(lompcs), ctypes.cast(ctxs, ctypes.c_void_p), self.sets_per_ctx.ctypes.data,
+                                         B, _ptr(self.gamma), self.off.ctypes.data, _ptr(self.w_ref), flags,
+                                         self._stream, ctypes.byref(plan))
+        if rc != _lib.LOMPC_OK:
+            lo._check_rc(rc)
+        self._plan = plan
+        cells = ctypes.c_int(0)
+        self._lib.lompc_plan_get_info(plan, None, None, ctypes.byref(cells))
+        self.cells = cells.value
+
+    def __del__(self):
+        if getattr(self, "_plan", None) is not None:
+            try:
+                self._lib.lompc_plan_destroy(self._plan)
+            except Exception:
+                pass
+            self._plan = None
+
+    def _check_rc(self, rc: int) -> None:
+        if rc == _lib.LOMPC_OK:
+            return
+        text = _lib.status_text(self._lib, None, rc, plan=self._plan)
+        if rc == _lib.LOMPC_ERR_INVALID_ARG:
+            raise ValueError(text)
+        if rc == _lib.LOMPC_ERR_NOT_CONVERGED:
+            raise SolverError(text)
+        raise RuntimeError(text)
 
     def run(self, lmbd, lmbd_r) -> dict:
         """lmbd / lmbd_r: device tensors, or raw device pointers (int)."""
-        lo = self.lompc
         pl = lmbd if isinstance(lmbd, int) else lmbd.data_ptr()
         pr = lmbd_r if isinstance(lmbd_r, int) else lmbd_r.data_ptr()
-        lo._lib.lompc_set_gamma_window(lo._ctx, _ptr(self.window))
-        rc = lo._lib.lompc_run(lo._ctx, self.S, pl, pr, *self._args)
+        if self.direct:
+            lo = self.lompc
+            rc = lo._lib.lompc_run(lo._ctx, self.S, pl, pr, *self._args)
+            if rc:
+                lo._check_rc(rc)
+            lo.S = self.S
+            return self.out
+        rc = self._lib.lompc_plan_run(self._plan, pl, pr, *self._outs, self._stream)
         if rc:
-            lo._check_rc(rc)
-        lo.S = self.S
+            self._check_rc(rc)
         return self.out
+
+    def check(self) -> tuple[int, int, int]:
+        """Synchronise the plan's stream; raise on uncertified QPs; returns (repaired, failed, invalid)."""
+        if self.direct:
+            torch = _torch()
+            with torch.cuda.stream(torch.cuda.ExternalStream(self._stream)):
+                return self.lompc.check_last()
+        rep, fail, inv = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        rc = self._lib.lompc_plan_status(self._plan, self._stream, ctypes.byref(rep), ctypes.byref(fail),
+                                         ctypes.byref(inv))
+        self._check_rc(rc)
+        if inv.value:
+            raise AssertionError(f"{inv.value} EVs with gamma outside [0, y_max]")
+        if fail.value:
+            raise SolverError(f"{fail.value} LoMPC QPs without a certified optimum")
+        return rep.value, fail.value, inv.value
+
+    def profile(self, enable: bool | None = None, read: bool = False, reset: bool = False):
+        """HIP-event timing of the fused solve kernel (k_solve; DIRECT: k_direct)."""
+        if self.direct:
+            return self.lompc.profile(enable=enable, read=read, reset=reset)
+        if enable is not None:
+            self._check_rc(self._lib.lompc_plan_profile_enable(self._plan, int(bool(enable))))
+        if read:
+            ms, n = ctypes.c_double(0.0), ctypes.c_int64(0)
+            self._check_rc(self._lib.lompc_plan_profile_read(self._plan, ctypes.byref(ms), ctypes.byref(n),
+                                                             int(bool(reset))))
+            return ms.value, n.value
+        return None

@@ -170,16 +170,13 @@ class PriceSolver:
         if central:
             self._gam[B] = float(self.gamma_sc)
         off = np.array([0, B, B + central], dtype=np.int64)
-        # gamma = y_max - y0 with 0 <= y0 <= y_max asserted in set_charge_levels
-        # path windows from the batch statistics (gamma = y_max - y0): no measuring pass
-        ym = self.consts.y_max
-        g_rng = [ym - self._y_hi, ym - self._y_lo]
-        win = [g_rng, [float(self.gamma_sc)] * 2]  # set 1: the central QP (empty on ranks > 0)
+        # gamma = y_max - y0 with 0 <= y0 <= y_max asserted in set_charge_levels.  The price
+        # iterations change the prices a little at a time: each gamma cell's exact solve starts
+        # from the working set the previous iteration ended with there.
         self._plan = BatchPlan(self.lompc, self._gam, off, w_ref=self._wr2, want_w=False, want_cost=False,
-                               want_set=True, validate=False, window=win)
+                               want_set=True, validate=False, warm_start=True)
         self._plan_w0 = BatchPlan(self.lompc, self._gam[:B], np.array([0, B], dtype=np.int64), want_w=False,
-                                  want_cost=False, want_w0=True, want_set=True, validate=False,
-                                  window=[g_rng]) if B else None
+                                  want_cost=False, want_w0=True, want_set=True, validate=False) if B else None
         self._B = B
 
     def compute_optimal_prices(self, w_ref: np.ndarray, lmbd_r: float) -> tuple[np.ndarray, dict]:

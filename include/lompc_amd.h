@@ -39,12 +39,11 @@ extern "C" {
 #define LOMPC_EV_LARGE 1
 
 /* ---- solve modes */
-#define LOMPC_MODE_PATH   0  /* exact solution path in gamma per set + per-EV evaluation,
-                                KKT certificate and active-set repair (default)        */
+#define LOMPC_MODE_PATH   0  /* exact solution path in gamma per (set, gamma cell), fused with the
+                                per-EV evaluation; KKT-certified; individual re-solve of any EV a
+                                certified piece does not cover (default)                 */
 #define LOMPC_MODE_DIRECT 1  /* independent per-EV active-set solve, warm-started from the
                                 set's central solution                                  */
-#define LOMPC_MODE_PATH_REPAIR 2 /* diagnostics: PATH launch without the path table, so every
-                                    EV takes the in-place certified wave re-solve       */
 
 /* ---- per-EV status values written to ``status[B]`` */
 #define LOMPC_QP_OK        0 /* certified optimal (KKT residual <= tol)                 */
@@ -77,30 +76,19 @@ int lompc_create(int N, double delta, double theta, double y_max, double w_max,
 /* Release every device/host resource of the context. */
 int lompc_destroy(lompc_ctx* ctx);
 
-/* Select LOMPC_MODE_PATH (default), LOMPC_MODE_DIRECT or LOMPC_MODE_PATH_REPAIR. */
+/* Select LOMPC_MODE_PATH (default) or LOMPC_MODE_DIRECT. */
 int lompc_set_mode(lompc_ctx* ctx, int mode);
 
-/* Gamma window of the solution path (PATH mode): the path of set s is computed on
- * [window[2s], window[2s+1]] (clipped to [0, y_max], widened by 1e-7 y_max) instead of
- * [0, y_max], so its 64 cells are narrower and carry fewer pieces.  The natural window of a
- * (type, partition) set is the range of its EVs' gamma = y_max - y0 (price_solver.py:73-77
- * computes those extremes).  EVs outside the window stay correct: they are re-solved
- * individually (status REPAIRED).
- *   window dev [S, 2] (lo, hi), or NULL = [0, y_max] for every set.
- * Sticky: read by the path kernel of every later lompc_set_params / lompc_run on ctx
- * (the buffer must stay valid until those launches have run). */
-int lompc_set_gamma_window(lompc_ctx* ctx, const double* window);
-
-/* Load S parameter sets and prepare them on device.
+/* Load S parameter sets.
  * Replaces LoMPC._update_cvx_parameters (lompc.py:84-90) for S sets at once
  * (one set = one (EV type, partition) price vector in price_solver.py).
+ * The device buffers are read by the next lompc_solve_batch (PATH mode) or by the
+ * preparation kernel this call launches (DIRECT mode); keep them valid until then.
  *   lmbd   dev  [S, 3N]  unit prices lambda >= 0        (lompc.py:78)
  *   lmbd_r dev  [S]      robustness price >= 0           (lompc.py:80)
  *   w_ref  dev  [S, N]   reference w for the A_bar error (price_solver.py:196), or NULL
  *   gamma_ref dev [S]    central gamma per set (gamma_sc, price_solver.py:76), or NULL
- *                        (NULL = y_max / 2); only used by LOMPC_MODE_DIRECT
- * Launches the per-set preparation kernel (derived data + exact solution
- * path in gamma, or the central solution in DIRECT mode). */
+ *                        (NULL = y_max / 2); only used by LOMPC_MODE_DIRECT */
 int lompc_set_params(lompc_ctx* ctx, int64_t S, const double* lmbd,
                      const double* lmbd_r, const double* w_ref,
                      const double* gamma_ref, void* stream);
@@ -118,7 +106,8 @@ int lompc_set_params(lompc_ctx* ctx, int64_t S, const double* lmbd,
  *   set_sum_w    dev  [S, N]   sum_i w_i per set (price_solver.py:205), or NULL
  *   set_stats    dev  [S, LOMPC_SET_STATS] fused per-set reductions, or NULL
  * Errors detected on device are reported through ``status``/``set_stats`` and
- * ``lompc_last_status``. */
+ * ``lompc_last_status``.  PATH mode groups the batch by gamma cell on every call (a device
+ * radix sort); a batch solved at many prices should use a plan (lompc_plan_create) instead. */
 int lompc_solve_batch(lompc_ctx* ctx, int64_t B, const double* gamma,
                       const int64_t* set_offsets, double* w, double* cost,
                       double* w0, int8_t* status, double* set_sum_w,
@@ -159,7 +148,63 @@ const char* lompc_status_string(int status);
 const char* lompc_last_error(const lompc_ctx* ctx);
 
 /* ABI version (bumped on any signature change). */
+#define LOMPC_ABI_VERSION 2
 int lompc_abi_version(void);
+
+/* ---------------------------------------------------------------------------
+ * Plans: a fixed EV batch solved at new prices every price iteration.
+ * Replaces the per-EV loops of PriceSolver._get_w_err (price_solver.py:203-209) and
+ * get_w0_price0 (price_solver.py:280-283) over the iterations of one price loop (gamma_i =
+ * y_max - y0_i is fixed between set_charge_levels calls, price_solver.py:66-77), and the
+ * charging station's per-type passes over all partitions (charging_station.py:275-329).
+ * One plan may span several contexts (EV types) of the same horizon and device: their sets
+ * are stacked (sets of ctxs[0] first) and every run is ONE fused launch over all of them.
+ * ------------------------------------------------------------------------- */
+typedef struct lompc_plan lompc_plan;
+#define LOMPC_PLAN_MAX_CTX 4
+#define LOMPC_PLAN_WARM_START 1 /* flag: start each gamma cell's exact solve from the working
+                                   set the previous run of the plan ended with there (prices
+                                   that change little between price iterations) */
+#define LOMPC_PLAN_DIAG_REPAIR 2 /* diagnostics: no solution path, every EV takes the individual
+                                    whole-wave re-solve (status REPAIRED) */
+
+/* Build a plan over B EVs grouped by set (S = sum of sets_per_ctx sets):
+ *   ctxs         host [n_ctx]   contexts (same N and device), n_ctx <= LOMPC_PLAN_MAX_CTX
+ *   sets_per_ctx host [n_ctx]   parameter sets of each context
+ *   gamma        dev  [B]       gamma_i = y_max - y0_i; COPIED (the plan keeps its own grouped
+ *                               copy: later changes to the caller's buffer are not seen)
+ *   set_offsets  host [S+1]     EVs of set s are [set_offsets[s], set_offsets[s+1])
+ *   w_ref        dev  [S, N]    reference w of the A_bar error, read at every run, or NULL
+ * The grouping (per-set gamma window, gamma cells, a stable device radix sort) runs
+ * asynchronously on ``stream``. */
+int lompc_plan_create(int n_ctx, lompc_ctx* const* ctxs, const int64_t* sets_per_ctx,
+                      int64_t B, const double* gamma, const int64_t* set_offsets,
+                      const double* w_ref, int flags, void* stream, lompc_plan** out);
+
+/* One price iteration of the whole batch: the exact LoMPC optimum of every EV at the
+ * prices of its set plus the fused per-set reductions.  Outputs as lompc_solve_batch, in
+ * the caller's EV order (each may be NULL):
+ *   lmbd dev [S, 3N], lmbd_r dev [S]; w dev [B, N]; cost, w0 dev [B]; status dev [B];
+ *   set_sum_w dev [S, N]; set_stats dev [S, LOMPC_SET_STATS]
+ * Two launches on ``stream`` (the fused per-cell solve, then the per-set reduction); no
+ * synchronisation.  A plan is not re-entrant: runs are stream-ordered. */
+int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, double* w,
+                   double* cost, double* w0, int8_t* status, double* set_sum_w,
+                   double* set_stats, void* stream);
+
+/* Synchronise ``stream``; counters of the plan's last run (as lompc_last_status). */
+int lompc_plan_status(lompc_plan* plan, void* stream, int64_t* n_repaired,
+                      int64_t* n_failed, int64_t* n_invalid);
+
+/* Batch size, total parameter sets and gamma cells per set of the plan. */
+int lompc_plan_get_info(const lompc_plan* plan, int64_t* B, int64_t* S, int* cells);
+
+/* HIP-event timing of the plan's fused solve kernel (as lompc_profile_*). */
+int lompc_plan_profile_enable(lompc_plan* plan, int enable);
+int lompc_plan_profile_read(lompc_plan* plan, double* total_ms, int64_t* launches, int reset);
+
+const char* lompc_plan_last_error(const lompc_plan* plan);
+int lompc_plan_destroy(lompc_plan* plan);
 
 /* ---------------------------------------------------------------------------
  * Host-side solvers of the price iteration (no device, no context).  They run

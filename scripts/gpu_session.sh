@@ -18,13 +18,26 @@ run() {
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    quick) run pytest_quick 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_parity.py tests/test_gpu_baseline_configs.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     testsall) run pytest_gpu_all 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
+    bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
+    bench20q) run bench20q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-station ;;
+    bench100q) run bench100q 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bcost) run bcost 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs cost ;;
+    bset) run bset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs set ;;
+    bfused) LOMPC_REDUCE_FUSED=1 run bfused 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bwarm) run bwarm 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --warm ;;
+    bwarmset) run bwarmset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --warm --outputs set ;;
+    stampsw) KS_WARM=1 run stampsw 300 python scripts/kstamps.py && KS_WARM=1 KS_OUTPUTS=set run stampsw_set 300 python scripts/kstamps.py ;;
+    bg32) LOMPC_CELLS=32 run bg32 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bg128) LOMPC_CELLS=128 run bg128 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bg256) LOMPC_CELLS=256 run bg256 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
     benchdirect) run bench_direct 600 python bench.py --mode direct --no-cpu-baseline ;;
     sweep) run sweep 600 python scripts/sweep_eval.py ;;
-    k1) run k1 300 python scripts/k1_stats.py ;;
     host) run host 300 python scripts/host_overhead.py ;;
+    stamps) run stamps 300 python scripts/kstamps.py && KS_OUTPUTS=set run stamps_set 300 python scripts/kstamps.py && run stamps48 300 python scripts/kstamps.py 48 ;;
     fail) run fail 600 python scripts/find_failures.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-station ;;
     *) echo "unknown step $s" ;;

@@ -26,7 +26,8 @@ def libpath():
 
 def test_header_declares_entry_points():
     fns = header_functions()
-    for f in ("lompc_create", "lompc_set_params", "lompc_solve_batch", "lompc_solve_host", "lompc_destroy"):
+    for f in ("lompc_create", "lompc_set_params", "lompc_solve_batch", "lompc_solve_host", "lompc_destroy",
+              "lompc_plan_create", "lompc_plan_run", "lompc_plan_destroy"):
         assert f in fns
 
 
@@ -51,9 +52,11 @@ def test_header_constants_match_python():
 
     src = open(HEADER).read()
     for name in ("LOMPC_OK", "LOMPC_ERR_INVALID_ARG", "LOMPC_ERR_NOT_CONVERGED", "LOMPC_QP_REPAIRED",
-                 "LOMPC_STAT_MAX_ERR", "LOMPC_SET_STATS", "LOMPC_MAX_N", "LOMPC_MODE_DIRECT", "LOMPC_MODE_PATH_REPAIR"):
+                 "LOMPC_STAT_MAX_ERR", "LOMPC_SET_STATS", "LOMPC_MAX_N", "LOMPC_MODE_DIRECT", "LOMPC_PLAN_MAX_CTX",
+                 "LOMPC_PLAN_WARM_START", "LOMPC_ABI_VERSION"):
         m = re.search(rf"#define {name}\s+(\d+)", src)
-        assert m and int(m.group(1)) == getattr(_lib, name), name
+        attr = "ABI_VERSION" if name == "LOMPC_ABI_VERSION" else name
+        assert m and int(m.group(1)) == getattr(_lib, attr), name
 
 
 def test_gfx950_code_object(libpath):

@@ -1,10 +1,14 @@
-"""GPU tests of the PATH pipeline behind lompc_run / BatchPlan (K1 path cells ->
-K2 per-EV blocks with in-place repairs -> K3 per-set reductions): one call per
-price iteration, parameter epochs across runs, ragged / empty / very large sets.
+"""GPU tests of the PATH engine behind lompc_plan_* / BatchPlan (plan: per-set gamma window,
+gamma cells, stable device radix sort; run: ONE fused k_solve over (set, cell) waves that
+computes the certified path pieces and writes every EV's outputs, then k_reduce): one call per
+price iteration, repeated runs, several EV types in one plan, ragged / empty / very large sets,
+invalid gamma, warm starts, the individual-repair path.
 
-Tolerances as in test_gpu_parity.py (|dw| <= 1e-9, cost 1e-9 relative);
-reductions equal the sums of the per-EV outputs to 1e-11 relative (sums of up to 3e5 terms).
+Tolerances as in test_gpu_parity.py (|dw| <= 1e-9, cost 1e-9 relative); reductions equal the
+sums of the per-EV outputs to 1e-11 relative (sums of up to 3e5 terms).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -37,9 +41,22 @@ def check_reductions(out, off, N):
         assert st[s, _lib.LOMPC_STAT_N_FAILED] == 0 and st[s, _lib.LOMPC_STAT_N_INVALID] == 0
 
 
+def oracle_check(out, g, lm, lr, off, c, N, rng, k=64):
+    wn, gn, lmn, lrn = out["w"].cpu().numpy(), g.cpu().numpy(), lm.cpu().numpy(), lr.cpu().numpy()
+    cn = out["cost"].cpu().numpy()
+    for s in range(len(off) - 1):
+        if off[s + 1] == off[s]:
+            continue
+        idx = rng.choice(np.arange(off[s], off[s + 1]), min(k, off[s + 1] - off[s]), replace=False)
+        wo, co, nf = oracle_c.solve_batch(N, c, lmn[s], lrn[s], gn[idx])
+        assert nf == 0
+        np.testing.assert_allclose(wn[idx], wo, atol=TOL_W)
+        np.testing.assert_allclose(cn[idx], co, rtol=1e-9, atol=1e-9)
+
+
 @pytest.mark.parametrize("ev", ["small", "large"])
-def test_run_matches_two_calls_and_oracle(gpu, ev):
-    """Ragged sets: empty, one full block, one partial block, ~4.7k blocks."""
+def test_plan_matches_solve_batch_and_oracle(gpu, ev):
+    """Ragged sets: empty, one full block, one partial block, 300k EVs (G = 2048 cells)."""
     rng = np.random.default_rng(31 + (ev == "large"))
     c = O.small_consts() if ev == "small" else O.large_consts()
     N = 24
@@ -51,16 +68,13 @@ def test_run_matches_two_calls_and_oracle(gpu, ev):
     lr = torch.as_tensor(3 * N * c.delta * rng.random(S), device="cuda:0")
     wr = torch.as_tensor(c.w_max * rng.random((S, N)), device="cuda:0")
     lompc = mk(c, N)
-    # window=False: the full-range path, bitwise comparable with set_params + solve_batch
-    plan = BatchPlan(lompc, g, off, w_ref=wr, want_w=True, want_cost=True, want_w0=True, want_status=True,
-                     window=False)
+    plan = BatchPlan(lompc, g, off, w_ref=wr, want_w=True, want_cost=True, want_w0=True, want_status=True)
     out = plan.run(lm, lr)
-    torch.cuda.synchronize()
-    rep, fail, inv = lompc.check_last()
+    rep, fail, inv = plan.check()
     assert fail == 0 and inv == 0
     w1 = out["w"].clone()
     st1 = out["set_stats"].clone()
-    # the same batch through set_params + solve_batch (two launches)
+    # the same batch through set_params + solve_batch (the context's transient plan): bitwise
     lompc.set_params(lm, lr, w_ref=wr)
     r2 = lompc.solve_batch(g, off, want_status=True)
     assert torch.equal(w1, r2["w"]) and torch.equal(st1, r2["set_stats"])
@@ -68,21 +82,11 @@ def test_run_matches_two_calls_and_oracle(gpu, ev):
     st = out["status"].cpu().numpy()
     assert np.all((st == _lib.LOMPC_QP_OK) | (st == _lib.LOMPC_QP_REPAIRED))
     np.testing.assert_array_equal(out["w0"].cpu().numpy(), w1[:, 0].cpu().numpy())
-    # subsample of every non-empty set against the C oracle
-    wn, gn, lmn, lrn = w1.cpu().numpy(), g.cpu().numpy(), lm.cpu().numpy(), lr.cpu().numpy()
-    cn = out["cost"].cpu().numpy()
-    for s in range(S):
-        if off[s + 1] == off[s]:
-            continue
-        idx = rng.choice(np.arange(off[s], off[s + 1]), min(64, off[s + 1] - off[s]), replace=False)
-        wo, co, nf = oracle_c.solve_batch(N, c, lmn[s], lrn[s], gn[idx])
-        assert nf == 0
-        np.testing.assert_allclose(wn[idx], wo, atol=TOL_W)
-        np.testing.assert_allclose(cn[idx], co, rtol=1e-9, atol=1e-9)
+    oracle_check(out, g, lm, lr, off, c, N, rng)
 
 
-def test_epochs_across_runs(gpu):
-    """Alternating price vectors through one plan: each run sees only its own table."""
+def test_repeated_runs(gpu):
+    """Alternating price vectors through one plan: every run depends only on its own prices."""
     rng = np.random.default_rng(5)
     c = O.large_consts()
     N, S, per = 24, 12, 4096
@@ -105,8 +109,8 @@ def test_epochs_across_runs(gpu):
 
 @pytest.mark.parametrize("ev", ["small", "large"])
 @pytest.mark.parametrize("N", [12, 24])
-def test_in_place_repair_path(gpu, ev, N):
-    """PATH_REPAIR publishes empty cells: every EV takes the in-place wave re-solve."""
+def test_individual_repair_path(gpu, ev, N):
+    """LOMPC_PLAN_DIAG_REPAIR: no path pieces, every EV takes the whole-wave certified re-solve."""
     rng = np.random.default_rng(77 + N + (ev == "large"))
     c = O.small_consts() if ev == "small" else O.large_consts()
     sizes = [150, 0, 64, 9]
@@ -116,10 +120,11 @@ def test_in_place_repair_path(gpu, ev, N):
     gn[:2] = [0.0, c.y_max]
     lmn = c.theta * rng.random((S, 3 * N))
     lrn = np.array([0.0, 1.0, 3 * N * c.delta * rng.random(), 0.5])
-    lompc = mk(c, N, mode="path_repair")
-    plan = BatchPlan(lompc, torch.as_tensor(gn, device="cuda:0"), off, want_status=True)
+    lompc = mk(c, N)
+    plan = BatchPlan(lompc, torch.as_tensor(gn, device="cuda:0"), off, want_status=True, diag_repair=True)
     out = plan.run(torch.as_tensor(lmn, device="cuda:0"), torch.as_tensor(lrn, device="cuda:0"))
-    torch.cuda.synchronize()
+    rep, fail, inv = plan.check()
+    assert rep == B and fail == 0 and inv == 0
     st = out["status"].cpu().numpy()
     assert np.all(st == _lib.LOMPC_QP_REPAIRED)
     stats = out["set_stats"].cpu().numpy()
@@ -135,49 +140,121 @@ def test_in_place_repair_path(gpu, ev, N):
             np.testing.assert_allclose(cost[a:b], co, rtol=1e-9, atol=1e-9)
 
 
+@pytest.mark.parametrize("N", [24, 48])
+def test_two_ev_types_in_one_plan(gpu, N):
+    """Both EV types' sets stacked in one plan (one fused launch) give the per-type plans'
+    answers bit for bit (same cell count), and match the oracle."""
+    rng = np.random.default_rng(900 + N)
+    cs = [O.small_consts(), O.large_consts()]
+    P = 3
+    sizes = [[700, 1, 2000], [1500, 0, 333]]
+    lms, offs, gs, wrs = [], [], [], []
+    for c, sz in zip(cs, sizes):
+        offs.append(np.concatenate([[0], np.cumsum(sz)]).astype(np.int64))
+        gs.append(torch.as_tensor(c.y_max - (0.3 + 0.2 * rng.random(sum(sz))), device="cuda:0"))
+        lms.append(torch.as_tensor(c.theta * rng.random((P, 3 * N)), device="cuda:0"))
+        wrs.append(torch.as_tensor(c.w_max * rng.random((P, N)), device="cuda:0"))
+    lr = torch.zeros(2 * P, dtype=torch.float64, device="cuda:0")
+    lompcs = [mk(c, N) for c in cs]
+    off = np.concatenate([offs[0], offs[0][-1] + offs[1][1:]])
+    both = BatchPlan(lompcs, torch.cat(gs), off, sets_per_ctx=[P, P], w_ref=torch.cat(wrs), want_status=True)
+    ob = both.run(torch.cat(lms), lr)
+    assert both.check()[1:] == (0, 0)
+    B0 = int(offs[0][-1])
+    for k in range(2):
+        one = BatchPlan(lompcs[k], gs[k], offs[k], w_ref=wrs[k])
+        assert one.cells == both.cells
+        o1 = one.run(lms[k], lr[:P])
+        torch.cuda.synchronize()
+        sl = slice(0, B0) if k == 0 else slice(B0, None)
+        assert torch.equal(o1["w"], ob["w"][sl]) and torch.equal(o1["cost"], ob["cost"][sl])
+        assert torch.equal(o1["set_stats"], ob["set_stats"][k * P:(k + 1) * P])
+        oracle_check(o1, gs[k], lms[k], lr[:P], offs[k], cs[k], N, rng, k=40)
+    check_reductions(ob, off, N)
+
+
+@pytest.mark.parametrize("ev", ["small", "large"])
+def test_invalid_gamma_and_snapshot(gpu, ev):
+    """gamma outside [0, y_max] or NaN: status INVALID, NaN outputs, counted per set, the rest
+    exact; the plan keeps its own copy of gamma (later changes to the caller's buffer unseen)."""
+    rng = np.random.default_rng(12 + (ev == "large"))
+    c = O.small_consts() if ev == "small" else O.large_consts()
+    N = 24
+    sizes = [500, 300]
+    off = np.array([0, 500, 800], dtype=np.int64)
+    gn = c.y_max * rng.random(800)
+    bad = [3, 17, 501, 799]
+    gn[bad] = [-0.1, np.nan, c.y_max + 1e-9, 5.0]
+    g = torch.as_tensor(gn, device="cuda:0")
+    lm = torch.as_tensor(c.theta * rng.random((2, 3 * N)), device="cuda:0")
+    lr = torch.zeros(2, dtype=torch.float64, device="cuda:0")
+    lompc = mk(c, N)
+    plan = BatchPlan(lompc, g, off, want_status=True, want_w0=True, validate=False)
+    out = plan.run(lm, lr)
+    with pytest.raises(AssertionError):
+        plan.check()
+    st = out["status"].cpu().numpy()
+    assert np.all(st[bad] == _lib.LOMPC_QP_INVALID)
+    good = np.setdiff1d(np.arange(800), bad)
+    assert np.all(st[good] == _lib.LOMPC_QP_OK)
+    w = out["w"].cpu().numpy()
+    assert np.all(np.isnan(w[bad])) and np.all(np.isnan(out["cost"].cpu().numpy()[bad]))
+    stats = out["set_stats"].cpu().numpy()
+    np.testing.assert_array_equal(stats[:, _lib.LOMPC_STAT_N_INVALID], [2, 2])
+    np.testing.assert_allclose(stats[:, _lib.LOMPC_STAT_SUM_W0], [w[good[good < 500], 0].sum(),
+                                                                 w[good[good >= 500], 0].sum()], rtol=1e-11)
+    for s, idx in ((0, good[good < 500][:50]), (1, good[good >= 500][:50])):
+        wo, _, nf = oracle_c.solve_batch(N, c, lm[s].cpu().numpy(), 0.0, gn[idx])
+        np.testing.assert_allclose(w[idx], wo, atol=TOL_W)
+    w_before = out["w"].clone()
+    g.fill_(0.0)  # the plan solved its snapshot
+    out2 = plan.run(lm, lr)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.nan_to_num(out2["w"], nan=-1.0), torch.nan_to_num(w_before, nan=-1.0))
+
+
 @pytest.mark.parametrize("ev", ["small", "large"])
 @pytest.mark.parametrize("N", [24, 48])
-def test_gamma_window_matches_full_path(gpu, ev, N):
-    """lompc_set_gamma_window: paths over each set's own gamma range (BatchPlan default) give
-    the full-range answers; gamma moved outside the measured window afterwards is re-solved
-    (status REPAIRED) and still matches the oracle."""
-    rng = np.random.default_rng(77 + N + (ev == "large"))
+def test_warm_start_and_cell_counts(gpu, ev, N):
+    """The answer does not depend on how the path is computed: warm-started cells (from the
+    previous run's working sets), 16 / 64 / 512 cells and clustered gamma per set (station
+    partitions by SoC) all give the same outputs to 1e-12 and match the oracle."""
+    rng = np.random.default_rng(40 + N + (ev == "large"))
     c = O.small_consts() if ev == "small" else O.large_consts()
     sizes = [4000, 1, 0, 2500, 640]
     off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-    S, B = len(sizes), int(off[-1])
-    # partitions by SoC: narrow gamma ranges per set (charging_station.py:111-116), one single-EV set
+    S = len(sizes)
     lo = np.array([0.05, 0.4, 0.0, 0.6, 0.3]) * c.y_max
     gn = np.concatenate([lo[s] + 0.08 * c.y_max * rng.random(sizes[s]) for s in range(S)])
     g = torch.as_tensor(gn, device="cuda:0")
-    lm = torch.as_tensor(c.theta * rng.random((S, 3 * N)), device="cuda:0")
+    lms = [torch.as_tensor(c.theta * rng.random((S, 3 * N)), device="cuda:0") for _ in range(3)]
     lr = torch.as_tensor(3 * N * c.delta * rng.random(S), device="cuda:0")
     wr = torch.as_tensor(c.w_max * rng.random((S, N)), device="cuda:0")
     lompc = mk(c, N)
     kw = dict(w_ref=wr, want_w=True, want_cost=True, want_status=True)
-    full = BatchPlan(lompc, g, off, window=False, **kw)
-    o_full = {k: (v.clone() if v is not None else None) for k, v in full.run(lm, lr).items()}
-    win = BatchPlan(lompc, g, off, **kw)
-    assert win.window is not None
-    o_win = win.run(lm, lr)
-    torch.cuda.synchronize()
-    rep, fail, inv = lompc.check_last()
-    assert fail == 0 and inv == 0 and rep == 0
-    np.testing.assert_allclose(o_win["w"].cpu().numpy(), o_full["w"].cpu().numpy(), rtol=0, atol=1e-12)
-    np.testing.assert_allclose(o_win["cost"].cpu().numpy(), o_full["cost"].cpu().numpy(), rtol=1e-12, atol=1e-12)
-    np.testing.assert_allclose(o_win["set_sum_w"].cpu().numpy(), o_full["set_sum_w"].cpu().numpy(), rtol=1e-11,
-                               atol=1e-10)
-    check_reductions(o_win, off, N)
-    # gamma changed in place outside the plan's window: repaired, still exact
-    g[off[0]:off[0] + 10] = torch.as_tensor(0.95 * c.y_max * np.ones(10), device="cuda:0")
-    o2 = win.run(lm, lr)
-    torch.cuda.synchronize()
-    rep, fail, inv = lompc.check_last()
-    assert fail == 0 and inv == 0 and rep >= 10
-    st = o2["status"].cpu().numpy()
-    assert np.all(st[:10] == _lib.LOMPC_QP_REPAIRED)
-    o = O.OracleLoMPC(N, c)
-    w2 = o2["w"].cpu().numpy()
-    for i in range(10):
-        wo, _ = o.solve_lompc(lm[0].cpu().numpy(), float(lr[0]), 0.95 * c.y_max)
-        assert np.max(np.abs(w2[i] - wo)) <= TOL_W
+    cold = BatchPlan(lompc, g, off, **kw)
+    warm = BatchPlan(lompc, g, off, warm_start=True, **kw)
+    for k in range(3):
+        oc = {n: v.clone() for n, v in cold.run(lms[k], lr).items() if v is not None}
+        ow = warm.run(lms[k], lr)
+        assert cold.check()[1:] == (0, 0) and warm.check()[1:] == (0, 0)
+        np.testing.assert_allclose(ow["w"].cpu().numpy(), oc["w"].cpu().numpy(), rtol=0, atol=1e-12)
+        np.testing.assert_allclose(ow["cost"].cpu().numpy(), oc["cost"].cpu().numpy(), rtol=1e-12, atol=1e-12)
+        check_reductions(ow, off, N)
+    oracle_check(oc, g, lms[2], lr, off, c, N, rng)
+    old = os.environ.get("LOMPC_CELLS")
+    try:
+        for G in (16, 512):
+            os.environ["LOMPC_CELLS"] = str(G)
+            p = BatchPlan(lompc, g, off, **kw)
+            assert p.cells == G
+            o = p.run(lms[2], lr)
+            assert p.check()[1:] == (0, 0)
+            np.testing.assert_allclose(o["w"].cpu().numpy(), oc["w"].cpu().numpy(), rtol=0, atol=1e-12)
+            np.testing.assert_allclose(o["set_sum_w"].cpu().numpy(), oc["set_sum_w"].cpu().numpy(), rtol=1e-11,
+                                       atol=1e-10)
+    finally:
+        if old is None:
+            os.environ.pop("LOMPC_CELLS", None)
+        else:
+            os.environ["LOMPC_CELLS"] = old

@@ -83,32 +83,40 @@ struct lompc_plan {
   lompc_ctx* ctx[LQ_PLAN_MAX_CTX] = {};
   QPConst* d_q = nullptr;       // [nctx]
   int64_t B = 0, S = 0;
-  int G = 0;                    // gamma cells per set (bucket G of a set = invalid gamma)
-  int64_t cap_B = 0, cap_S = 0, cap_bk = 0;
-  size_t cap_tmp = 0;
+  int G = 0;                    // gamma cells per set (k_path waves per set)
+  int nblk = 0;                 // k_eval workgroups (blocks of one set's EVs)
+  int n_cu = 0;
+  int64_t cap_S = 0, cap_blk = 0, cap_cells = 0;
+  const double* gamma = nullptr;  // caller's [B] (read at every run)
   const double* w_ref = nullptr;  // caller's [S][N] (read at every run) or null
   double* d_stats_own = nullptr;  // [S][8] when the plan owns its status rows
-  double* d_stats = nullptr;      // where k_reduce writes the status rows
+  double* d_stats = nullptr;      // where k_finalize writes the status rows
   // device workspaces
   uint8_t* d_set_ctx = nullptr;   // [S]
   int64_t* d_set_off = nullptr;   // [S+1]
+  int* d_blk_prefix = nullptr;    // [S+1] k_eval workgroups per set
+  int4* d_blk = nullptr;          // [nblk] (set, first EV, end EV, -)
   double* d_window = nullptr;     // [S][2] (lo, hi) of the set's valid gamma, widened
-  uint32_t* d_keys = nullptr;     // [2][B] radix-sort keys (bucket) in / out
-  uint32_t* d_vals = nullptr;     // [2][B] original EV index in / out (out = perm)
-  int* d_bucket_off = nullptr;    // [S*(G+1)+1]
-  double* d_gs = nullptr;         // [B] gamma in bucket order
-  double* d_partial = nullptr;    // [S*(G+1)][N+NPX]
-  uint8_t* d_ws = nullptr;        // [S*(G+1)][64] working set at each cell start (warm start)
-  void* d_tmp = nullptr;          // radix-sort temporary storage
+  double* d_partial = nullptr;    // [nblk][N+NPX] k_eval workgroup records
+  int* d_fail_cnt = nullptr;      // [nblk][waves] EVs listed for k_finalize's individual re-solve
+  int* d_fail_idx = nullptr;      // [nblk][EVs]
+  // path table: per cell count / first piece / coverage start / working set; per set a compact
+  // range of G*LQ_PPL piece slots and its fill counter
+  int* t_cnt = nullptr;
+  int* t_base = nullptr;
+  int* t_np = nullptr;
+  double* t_lo = nullptr;
+  double* t_ge = nullptr;
+  double* t_cf = nullptr;
+  double2* t_ab = nullptr;
+  uint8_t* t_sl = nullptr;
+  uint8_t* d_ws = nullptr;        // [S*G][64] working set at each cell start (warm start)
   int* d_errflag = nullptr;
-  unsigned* d_arrive = nullptr;   // [S] per-set arrival counters of k_solve's fused reduction
-  uint32_t* d_perm = nullptr;     // = the sorted value buffer
-  // pinned staging of the host set arrays
-  int64_t* h_off = nullptr;
-  uint8_t* h_ctx = nullptr;
+  // pinned staging of the host arrays
+  char* h_buf = nullptr;
   int64_t cap_h = 0;
   hipEvent_t ev_stage = nullptr;
-  // profiling of k_solve
+  // profiling of k_eval
   bool prof = false;
   std::vector<hipEvent_t> prof_ev, prof_pool;
   double prof_ms = 0.0;

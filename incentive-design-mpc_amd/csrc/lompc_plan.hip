@@ -1,31 +1,31 @@
 // lompc_plan.hip — the PATH engine: a fixed EV batch (one price loop / one time step) solved
-// at new prices by ONE fused kernel per price iteration plus a per-set reduction.
+// at new prices every price iteration.
 //
 // Hot path replaced: LoMPC.solve_lompc (chargingstation/lompc.py:137-156) called once per EV
 // from PriceSolver._get_w_err (price_solver.py:203-209) and PriceSolver.get_w0_price0
 // (price_solver.py:280-283).  Within one parameter set (an (EV type, partition) price vector)
 // every EV solves the same QP except gamma_i = y_max - y0_i (price_solver.py:202, :281), so
-// w*(gamma) is a continuous piecewise-affine path.
+// w*(gamma) is a continuous piecewise-affine path with a handful of breakpoints over the
+// set's gamma range.
 //
-// Plan (once per batch, lompc_plan_create): each set's gamma window [lo, hi] is cut into G
-// cells; every EV is keyed by (set, cell) — cell G of a set collects invalid gamma — and the
-// keys are radix-sorted (stable, rocPRIM) so each cell's EVs are contiguous: perm[j] is the
-// caller index of sorted position j, gs[j] its gamma.
+// Plan (once per batch, lompc_plan_create): per-set gamma window [lo, hi] (range of the set's
+// valid gamma, k_plan_window) cut into G cells; the block map of k_eval (256 consecutive EVs of
+// one set per workgroup).
 //
-// Run (every price iteration, lompc_plan_run):
-//   k_solve   one 64-lane wave per (set, cell), lane t = horizon stage t:
-//             (1) exact solve at the cell start (wave-parallel PDAS, KKT-certified),
-//             (2) parametric active-set tracking of w*(gamma) across the cell: pieces
-//                 w = a + b gamma, each KKT-certified at its end (the residual is convex along
-//                 an affine piece, so both ends certify the whole piece), kept in LDS with the
-//                 cost / squared A_bar error as quadratics in gamma,
-//             (3) the cell's EVs: lane = EV for the scalar outputs (cost, w0, status, price0,
-//                 A_bar error) and the per-piece moments (count, sum gamma); lane = stage for
-//                 the w rows (16-B write-through stores to the caller's row perm[j]); EVs no
-//                 certified piece covers are re-solved individually by the whole wave,
-//             (4) the cell's partial reduction record (sum w from the piece moments).
-//   k_reduce  one workgroup per set: deterministic sum / max of its cells' records.
-// No path table, no dependent kernel between the path and the per-EV outputs.
+// Run (every price iteration, lompc_plan_run), three launches for ALL EV types of the plan:
+//   k_path    one 64-lane wave per (set, cell), lane t = horizon stage t: exact solve at the
+//             cell start (fp32 working-set search + fp64 PDAS, KKT-certified), then parametric
+//             active-set tracking of w*(gamma) across the cell; every piece w = a + b gamma is
+//             KKT-certified at its end (the residual is convex along an affine piece, so both
+//             ends certify the whole piece) and stored with the cost and the squared A_bar
+//             error as quadratics in gamma.  Latency-bound: wave-parallel DPP scans.
+//   k_eval    256 EVs of one set per workgroup in the caller's order: the set's pieces staged
+//             in LDS (a few KB), per EV (lane = EV) its piece, cost, w0, status, price0, A_bar
+//             error; the w rows (lane = stage) as contiguous 16-B write-through stores; EVs no
+//             certified piece covers listed for k_finalize; per-workgroup sums in a fixed
+//             order.  HBM-bound: 8(N+2) B per EV.
+//   k_finalize one workgroup per set: deterministic sum / max of its workgroups' records, and the
+//             individual certified re-solve of any EV k_eval listed (no certified piece covers it).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -34,14 +34,19 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include "lompc_ctx.hpp"
 #include "lompc_wave.hpp"
 
 #ifdef LOMPC_STAMPS
-// diagnostic build only (scripts/kstamps.py): per-wave s_memtime at k_solve's phase boundaries
+// diagnostic build only (scripts/kstamps.py): per-wave s_memtime at k_path's and k_eval's phase
+// boundaries (k_eval: workgroup b at g_stamps[(32768 + b) * 8 + k])
 __device__ long long g_stamps[65536 * 8];
+#define LQ_STAMPE(k)                                                                        \
+  do {                                                                                      \
+    const long long t__ = __builtin_amdgcn_s_memtime();                                     \
+    if (threadIdx.x == 0 && blockIdx.x < 32768) g_stamps[(32768 + blockIdx.x) * 8 + (k)] = t__; \
+  } while (0)
 #define LQ_STAMP(k)                                                                         \
   do {                                                                                      \
     const long long t__ = __builtin_amdgcn_s_memtime();                                     \
@@ -49,7 +54,15 @@ __device__ long long g_stamps[65536 * 8];
   } while (0)
 #else
 #define LQ_STAMP(k)
+#define LQ_STAMPE(k)
 #endif
+
+#define EVAL_WAVES 16                      // k_eval: waves per workgroup
+#define EVAL_EVS (64 * EVAL_WAVES)         // k_eval: threads per workgroup
+#define EVAL_PASSES 2                      // k_eval: EVs per thread, at most
+#define EVAL_MAXB (EVAL_EVS * EVAL_PASSES)  // k_eval: EVs per workgroup, at most
+#define LQ_PIECE_CAP 96                    // k_eval: max pieces of one set staged in LDS (more: re-solved)
+#define LQ_GMAX 1024                       // max cells per set
 
 namespace {
 
@@ -57,7 +70,7 @@ typedef unsigned int lq_v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int lq_v2u __attribute__((ext_vector_type(2)));
 
 // write-through (sc1) stores: the outputs leave no dirty lines in the XCD's L2, so the kernel
-// boundary behind k_solve has no L2 writeback to wait for (MI355X_MICROARCH.md, price list)
+// boundary behind k_eval has no L2 writeback to wait for (MI355X_MICROARCH.md, price list)
 __device__ __forceinline__ void st_wt16(__amdgpu_buffer_rsrc_t rs, int off, double x, double y) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(lq_v4u, make_double2(x, y)), rs, off, 0, 16);
 }
@@ -71,30 +84,21 @@ __device__ __forceinline__ void st_wt8(double* p, double v) {
 
 __device__ __forceinline__ double clampw(double x, double wmax) { return fmin(fmax(x, 0.0), wmax); }
 
-struct PlanArgs {
-  int S, G, nbk, pad;
-  int64_t B;
+// ---------------------------------------------------------------- plan kernel
+struct WindowArgs {
   const QPConst* qd;
   const uint8_t* set_ctx;
   const int64_t* set_off;
-  double* window;
   const double* gamma;
-  uint32_t* keys;
-  uint32_t* vals;
-  uint32_t* keys_out;
-  uint32_t* vals_out;
-  int* bucket_off;
-  double* gs;
+  double* window;
 };
 
-// ---------------------------------------------------------------- plan kernels
 // per set: [lo, hi] = range of its valid gamma, widened by 1e-7 y_max (a zero-width set still
 // gets cells of positive width), clipped to [0, y_max]; no valid EV -> [0, y_max]
-__global__ __launch_bounds__(256) void k_plan_window(PlanArgs a) {
+__global__ __launch_bounds__(256) void k_plan_window(WindowArgs a) {
   __shared__ double smin[256], smax[256];
   const int s = blockIdx.x;
-  const QPConst& q = a.qd[a.set_ctx[s]];
-  const double ym = q.y_max;
+  const double ym = a.qd[a.set_ctx[s]].y_max;
   double lo = INFINITY, hi = -INFINITY;
   for (int64_t i = a.set_off[s] + threadIdx.x; i < a.set_off[s + 1]; i += 256) {
     const double g = a.gamma[i];
@@ -119,244 +123,53 @@ __global__ __launch_bounds__(256) void k_plan_window(PlanArgs a) {
     if (smin[0] <= smax[0]) {
       wlo = fmin(fmax(smin[0] - mg, 0.0), ym);
       whi = fmin(fmax(smax[0] + mg, wlo + mg), ym);
-      if (!(whi > wlo)) {
-        wlo = fmax(whi - 2.0 * mg, 0.0);
-      }
+      if (!(whi > wlo)) wlo = fmax(whi - 2.0 * mg, 0.0);
     }
     a.window[2 * s] = wlo;
     a.window[2 * s + 1] = whi;
   }
 }
 
-__device__ __forceinline__ int set_of(const int64_t* off, int S, int64_t i) {  // off[s] <= i < off[s+1]
-  int lo = 0, hi = S - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (off[mid] <= i) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-
-// cell of gamma in set s (the same arithmetic as k_solve's cell bounds; G = invalid)
-__device__ __forceinline__ int cell_of(double g, double ym, double lo, double hi, int G) {
-  if (!(g >= 0.0 && g <= ym)) return G;
-  const double x = (g - lo) * ((double)G / (hi - lo));
+// cell of a valid gamma in a set's window (k_eval), the same arithmetic as k_path's cell bounds
+__device__ __forceinline__ int cell_of(double g, double lo, double inv_h, int G) {
+  const double x = (g - lo) * inv_h;
   return x <= 0.0 ? 0 : (x >= (double)(G - 1) ? G - 1 : (int)x);
 }
 
-__global__ __launch_bounds__(256) void k_plan_keys(PlanArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.B) return;
-  const int s = set_of(a.set_off, a.S, i);
-  const double ym = a.qd[a.set_ctx[s]].y_max;
-  const int c = cell_of(a.gamma[i], ym, a.window[2 * s], a.window[2 * s + 1], a.G);
-  a.keys[i] = (uint32_t)s * (uint32_t)(a.G + 1) + (uint32_t)c;
-  a.vals[i] = (uint32_t)i;
-}
-
-// bucket offsets from the sorted keys (every bucket's start written exactly once) and the
-// gamma of each sorted position
-__global__ __launch_bounds__(256) void k_plan_finish(PlanArgs a) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= a.B) return;
-  const int64_t kj = a.keys_out[j];
-  const int64_t kp = j ? (int64_t)a.keys_out[j - 1] : -1;
-  for (int64_t k = kp + 1; k <= kj; ++k) a.bucket_off[k] = (int)j;
-  if (j == a.B - 1)
-    for (int64_t k = kj + 1; k <= a.nbk; ++k) a.bucket_off[k] = (int)a.B;
-  a.gs[j] = a.gamma[a.vals_out[j]];
-}
-
-// ---------------------------------------------------------------- k_solve
-// k_solve<SOLVE_WAVES, SOLVE_PATHS>: SOLVE_WAVES waves per (set, cell) workgroup all evaluate the
-// cell's EVs; the first SOLVE_PATHS of them compute the path of one sub-cell each
-#ifndef LQ_SOLVE_WAVES
-#define LQ_SOLVE_WAVES 2
-#endif
-#ifndef LQ_SOLVE_PATHS
-#define LQ_SOLVE_PATHS 1
-#endif
-#define LQ_PPLX 8  // max certified pieces per sub-cell
-#define LQ_WS_MAX 8  // warm-start buffer: working sets per cell
-
-struct SolveArgs {
-  int S, G, flags, want_err, N, pad;
-  int64_t B;
+// ---------------------------------------------------------------- k_path
+struct PathArgs {
+  int S, G, N, flags;
   const QPConst* qd;
   const uint8_t* set_ctx;
   const double* window;
-  const int* bucket_off;
-  const double* gs;
-  const uint32_t* perm;
   const double* lmbd;    // [S][3N]
   const double* lmbd_r;  // [S]
   const double* w_ref;   // [S][N] or null
-  uint8_t* ws;           // [nbk][64] warm-start working sets or null
-  double* w;
-  double* cost;
-  double* w0;
-  int8_t* status;
-  double* partial;       // [nbk][N + NPX]
+  uint8_t* ws;           // [S*G][64] warm-start working sets or null
+  // per cell
+  int* t_cnt;            // [S*G]             certified pieces of the cell (0: none)
+  int* t_base;           // [S*G]             its first piece in the set's compact range
+  double* t_lo;          // [S*G]             coverage start
+  uint8_t* t_sl;         // [S*G][64]         working set at the cell start (repairs)
+  // per set: pieces in a compact range [0, t_np[s]) of G*PPL slots, cells in arrival order
+  int* t_np;             // [S]               pieces of the set (k_reduce resets it to 0)
+  double* t_ge;          // [S][G*PPL]        gamma at each piece's end
+  double* t_cf;          // [S][G*PPL][8]     K0 K1 K2 (cost) F0 F1 F2 (err^2) a_0 b_0
+  double2* t_ab;         // [S][G*PPL][N]     (a_t, b_t)
   int* errflag;
-  int w_rsrc_ok;         // B*N*8 fits a buffer descriptor's 31-bit offsets
-  // per-set reduction by the set's last-arriving workgroup (null arrive: k_reduce does it)
-  unsigned* arrive;      // [S] arrival counters, 0 between launches
-  const int64_t* set_off;
-  double* set_sum_w;
-  double* set_stats;
-  double* stats;
 };
 
-struct SetData {  // per-set scalars every lane holds (uniform)
-  double c0, kappa, l10, l20, l30, lr;
-};
-
-// cost / A_bar error / price0 of a QP solved by the whole wave (lane t = w_t), valid on every lane
-__device__ __forceinline__ void wave_ev_outputs(const QPConst& q, const lqw::WaveSet& ws, const SetData& sd,
-                                                double wr, double gamma, double w, double& cost, double& err,
-                                                double& price0) {
-  const int N = ws.N, lane = ws.lane;
-  const bool act = lane < N;
-  lqw::Aff<2> h = lqw::Aff<2>::identity();
-  if (act) {
-    h.B[0] = w;
-    h.B[1] = w - wr;
-  }
-  const lqw::Aff<2> Y = lqw::wave_scan(h, N);
-  double t[3] = {0.0, 0.0, 0.0};
-  double pwl = 0.0;
-  if (act) {
-    const double y = Y.B[0], ey = Y.B[1];
-    t[0] = 0.5 * q.c * y * y - q.c * gamma * y + w * fma(0.5 * ws.d_nat, w, ws.e_nat);
-    if (!q.ev_small) pwl = lq_pwl(w * q.inv_wmax);
-    t[1] = ey * ey;
-    t[2] = (w - wr) * (w - wr);
-  }
-  const double tw = q.theta * q.w_max;
-  double v[4] = {t[0], t[1], t[2], q.ev_small ? 0.0 : pwl};
-  lqw::wave_totals(v, N);
-  cost = v[0] + sd.c0 + tw * tw * v[3];
-  err = sqrt(fmax(v[1] + sd.kappa * v[2], 0.0));
-  const double w0 = __shfl(w, 0, 64);
-  price0 = q.theta * (w0 * sd.l10 + (q.w_max - w0) * sd.l20) + q.q_scale * w0 * w0 * sd.l30 +
-           q.theta * q.theta * w0 * w0 * sd.lr;
-}
-
-__device__ __forceinline__ double ld_wt8(const double* p) {  // global_load ... sc1 (L2-served, not L1)
-  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
-                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// Called by ONE wave per workgroup after it wrote the workgroup's record write-through (sc1).
-// Hand-off of the G+1 cell records of set s to the set's last-arriving workgroup
-// (MI355X_MICROARCH.md, "Valid forms": sc1 stores drained by s_waitcnt vmcnt(0) before one
-// agent-scope add per workgroup; the adder that sees G + 1 arrivals reads every record with sc1
-// loads after its add returned): sum / max in a fixed order -> set_sum_w, set_stats.
-__device__ __forceinline__ void arrive_reduce(const SolveArgs& a, int s, int lane, int N) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  unsigned old = 0;
-  if (lane == 0) old = __hip_atomic_fetch_add(a.arrive + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  old = (unsigned)__shfl((int)old, 0, 64);
-  if (old != (unsigned)a.G) return;  // G + 1 workgroups per set; the last one reduces
-  const int W = N + NPX, G1 = a.G + 1;
-  const double* base = a.partial + (size_t)s * G1 * W;
-  double col[2] = {0.0, 0.0};
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int c = lane + 64 * h;
-    if (c < W) {
-      const bool is_max = c == N + PX_MAX_ERR;
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-      constexpr int U = 32;  // all records of a set in one or two memory rounds
-      for (int b = 0; b < G1; b += U) {
-        double v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = b + u < G1 ? ld_wt8(base + (size_t)(b + u) * W + c) : 0.0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc[u & 3] = is_max ? fmax(acc[u & 3], v[u]) : acc[u & 3] + v[u];
-      }
-      col[h] = is_max ? fmax(fmax(acc[0], acc[1]), fmax(acc[2], acc[3])) : (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    }
-  }
-  if (lane < N && a.set_sum_w) a.set_sum_w[(size_t)s * N + lane] = col[0];
-  // stats row: lane t < 8 takes its column's total
-  int src = 0;
-  switch (lane) {
-    case LOMPC_STAT_SUM_W0: src = 0; break;
-    case LOMPC_STAT_SUM_PRICE0: src = N + PX_PRICE0; break;
-    case LOMPC_STAT_MAX_ERR: src = N + PX_MAX_ERR; break;
-    case LOMPC_STAT_SUM_COST: src = N + PX_COST; break;
-    case LOMPC_STAT_N_REPAIRED: src = N + PX_N_REPAIRED; break;
-    case LOMPC_STAT_N_FAILED: src = N + PX_N_FAILED; break;
-    case LOMPC_STAT_N_INVALID: src = N + PX_N_INVALID; break;
-    default: src = 0; break;
-  }
-  const double v0 = __shfl(col[0], src & 63, 64), v1 = __shfl(col[1], src & 63, 64);
-  double v = src < 64 ? v0 : v1;
-  if (lane == LOMPC_STAT_COUNT) v = (double)(a.set_off[s + 1] - a.set_off[s]);
-  if (lane < LOMPC_SET_STATS) {
-    if (a.set_stats) a.set_stats[(size_t)s * LOMPC_SET_STATS + lane] = v;
-    a.stats[(size_t)s * LOMPC_SET_STATS + lane] = v;
-  }
-  if (lane == 0) __hip_atomic_store(a.arrive + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One workgroup of SOLVE_WAVES waves per (set, gamma cell).  The cell is split into
-// SOLVE_PATHS sub-cells: waves 0..SOLVE_PATHS-1 (one per SIMD) each compute one sub-cell's
-// certified path pieces into LDS (latency-bound wave-parallel scans; the other waves wait at the
-// barrier and cost no issue slots), then all waves split the cell's EVs in 64-EV chunks.
-template <int SOLVE_WAVES, int SOLVE_PATHS>
-__global__ __launch_bounds__(64 * SOLVE_WAVES) void k_solve(SolveArgs a) {
-  constexpr int NSLOT = SOLVE_PATHS * LQ_PPLX;  // piece slots: sub-cell k owns [k PPL, (k+1) PPL)
-  __shared__ double2 s_ab[NSLOT][64];                              // piece rows (a_t, b_t), lane t
-  __shared__ __attribute__((aligned(16))) double s_cf[NSLOT][8];  // K0 K1 K2 (cost) F0 F1 F2 (err^2) a_0 b_0
-  __shared__ double s_ge[NSLOT];                                   // gamma at each piece's end
-  __shared__ double s_g[SOLVE_WAVES][64];                          // chunk: gamma, piece slot (-1 re-solved,
-  __shared__ int s_p[SOLVE_WAVES][64];                             //   -2 invalid), caller row
-  __shared__ int s_o[SOLVE_WAVES][64];
-  __shared__ double s_mom[SOLVE_WAVES][NSLOT][2];                  // per wave and piece: count, sum gamma
-  __shared__ double s_red[SOLVE_WAVES][8];                         // per wave: cost, price0, max err, counts
-  __shared__ double s_repw[SOLVE_WAVES][64];                       // per wave: sum of re-solved rows (lane t)
-  __shared__ double s_cov[SOLVE_PATHS][2];                         // sub-cell coverage [glo, gcov]
-  __shared__ int s_npc[SOLVE_PATHS];
-  __shared__ uint8_t s_sl0[SOLVE_PATHS][64];                       // working set at each sub-cell start
-  const int blk = (int)blockIdx.x;
-  const int G = a.G, G1 = a.G + 1;
-  const int s = blk / G1;
-  const int cell = blk - s * G1;
-  const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
-  const int N = a.N;  // every context of a plan has the same horizon
-  const int W = N + NPX;
-  const int b0 = a.bucket_off[blk], b1 = a.bucket_off[blk + 1];
-  // the first chunk of this wave: issued before anything waits on memory
-  const int j0 = b0 + 64 * wv + lane;
-  const double g_pre = j0 < b1 ? a.gs[j0] : 0.0;
-  const int o_pre = j0 < b1 ? (int)a.perm[j0] : 0;
-  const QPConst& q = a.qd[a.set_ctx[s]];  // uniform: scalar loads, no register copy
-  LQ_STAMP(0);
-  lq_tab_init(q);
-  double* part = a.partial + (size_t)blk * W;
-  if (b1 <= b0) {  // empty cell (workgroup-uniform)
-    if (wv == 0) {
-      for (int c = lane; c < W; c += 64) st_wt8(part + c, 0.0);
-      if (a.arrive) arrive_reduce(a, s, lane, N);
-    }
-    return;
-  }
+// per-stage data of set s from its prices (lompc.py:92-135 in standard form)
+__device__ __forceinline__ void load_set(const QPConst& q, const double* __restrict__ L, double lr, int N,
+                                         int lane, lqw::WaveSet& ws, double& l2) {
   const double tt = q.theta * q.theta;
-  // ---- per-set data (lompc.py:92-135 in standard form); every wave holds it
-  const double* __restrict__ L = a.lmbd + (size_t)s * 3 * N;
-  const double lr = a.lmbd_r[s];
-  lqw::WaveSet ws;
   ws.N = N;
   ws.lane = lane;
   ws.rsrc = lane < N ? N - 1 - lane : lane;
-  double l2 = 0.0;
+  l2 = 0.0;
   if (lane < N) {
     const double l1 = L[lane], l3 = L[2 * N + lane];
     l2 = L[N + lane];
-    if (wv == 0 && !(l1 >= 0.0 && l2 >= 0.0 && l3 >= 0.0)) atomicOr(a.errflag, 1);
     ws.d_nat = 2.0 * lr * tt + 2.0 * q.q_scale * l3 + q.dsmall;
     ws.e_nat = q.theta * (l1 - l2);
     const int tr = ws.rsrc;
@@ -365,368 +178,510 @@ __global__ __launch_bounds__(64 * SOLVE_WAVES) void k_solve(SolveArgs a) {
   } else {
     ws.d_nat = ws.e_nat = ws.d_rev = ws.e_rev = 0.0;
   }
-  if (wv == 0 && lane == 0 && !(lr >= 0.0)) atomicOr(a.errflag, 1);
+}
+
+__global__ __launch_bounds__(64) void k_path(PathArgs a) {
+  __shared__ double2 p_ab[LQ_PPL][64];
+  __shared__ double p_cf[LQ_PPL][8];
+  __shared__ double p_ge[LQ_PPL];
+  const int blk = (int)blockIdx.x;
+  const int G = a.G;
+  const int s = blk / G;
+  const int cell = blk - s * G;
+  const int lane = (int)threadIdx.x;
+  const int N = a.N;
+  const double* __restrict__ L = a.lmbd + (size_t)s * 3 * N;
+  const double lr = a.lmbd_r[s];
   const double wr_nat = (a.w_ref && lane < N) ? a.w_ref[(size_t)s * N + lane] : 0.0;
-  SetData sd;
-  sd.c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);  // lompc.py:128
-  sd.kappa = lr / q.delta;                            // price_solver.py:191
-  sd.l10 = L[0];
-  sd.l20 = L[N];
-  sd.l30 = L[2 * N];
-  sd.lr = lr;
-  const int want_err = a.want_err;
-  const bool invalid_cell = cell == G;
-  // the cell [clo, chi] of the set's window and its SOLVE_PATHS sub-cells
   const double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
+  const QPConst& q = a.qd[a.set_ctx[s]];  // uniform: scalar loads, no register copy
+  LQ_STAMP(0);
+  lq_tab_init(q);
+  lqw::WaveSet ws;
+  double l2;
+  load_set(q, L, lr, N, lane, ws, l2);
+  if (lane < N && !(L[lane] >= 0.0 && l2 >= 0.0 && L[2 * N + lane] >= 0.0)) atomicOr(a.errflag, 1);
+  if (lane == 0 && !(lr >= 0.0)) atomicOr(a.errflag, 1);
+  const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);  // lompc.py:128
+  const double kappa = lr / q.delta;                            // price_solver.py:191
+  double Ywr;
+  {
+    lqw::Sums<1> y;
+    y.v[0] = wr_nat;
+    Ywr = lqw::wave_scan(y, N).v[0];
+  }
   const double h = (whi - wlo) / (double)G;
-  const double clo = cell == 0 ? wlo : fma((double)cell, h, wlo);
-  const double chi = cell >= G - 1 ? whi : fma((double)(cell + 1), h, wlo);
-  const double hs = (chi - clo) / (double)SOLVE_PATHS;
+  const double mg = 1e-13 * q.y_max;  // cells overlap by a rounding margin
+  const double glo = fmax((cell == 0 ? wlo : fma((double)cell, h, wlo)) - mg, 0.0);
+  const double ghi = fmin((cell == G - 1 ? whi : fma((double)(cell + 1), h, wlo)) + mg, q.y_max);
   LQ_STAMP(1);
-  // ---- waves 0..SOLVE_PATHS-1: sub-cell wv's path pieces
-  if (wv < SOLVE_PATHS) {
-    const int k = wv;
-    int npc = 0;
-    double glo = 0.0, gcov = -INFINITY;  // certified coverage [glo, gcov]
-    int sl0 = lane < N ? 1 : 0;
-    if (!invalid_cell && !(a.flags & LOMPC_PLAN_DIAG_REPAIR)) {
-      const double mg = 1e-13 * q.y_max;  // sub-cells overlap by a rounding margin
-      glo = fmax((k == 0 ? clo : fma((double)k, hs, clo)) - mg, 0.0);
-      const double ghi = fmin((k == SOLVE_PATHS - 1 ? chi : fma((double)(k + 1), hs, clo)) + mg, q.y_max);
-      double Ywr;
-      {
-        lqw::Sums<1> y;
-        y.v[0] = wr_nat;
-        Ywr = lqw::wave_scan(y, N).v[0];
-      }
-      const size_t wso = ((size_t)blk * LQ_WS_MAX + k) * 64 + lane;
-      int sl = sl0;
-      if (a.ws) {
-        const int v = a.ws[wso];
-        sl = (lane < N && v >= 0 && v <= 2 * q.m) ? v : sl0;
-      }
-      double w = 0.0, r = 0.0;
-      const bool solved = lqw::wave_solve(q, ws, glo, sl, w, r);
-      LQ_STAMP(2);
-      if (solved) {
-        sl0 = sl;
-        if (a.ws) a.ws[wso] = (uint8_t)sl;
-        // ---- parametric active-set tracking of w*(gamma) on [glo, ghi]
-        double gcur = glo;
-        int last = -1;
-        const int max_iter = 4 * LQ_PPLX + 16;
-        const double ee = ws.e_nat;
-        for (int it = 0; it < max_iter && npc < LQ_PPLX; ++it) {
-          const lqw::StageSol<2> sol = lqw::solve_stage<2>(q, ws, 0.0, sl);
-          const double av = sol.w[0], bv = sol.w[1], r0 = sol.r[0], r1 = sol.r[1];
-          double gc = INFINITY;
-          int ns = sl;
-          if (lane < N) {
-            const Box bx = lq_box(sl);
-            if (sl & 1) {  // free: w(gamma) = a + b gamma leaves [lo, hi]
-              if (bv > 0.0) { gc = (bx.hi - av) / bv; ns = sl + 1; }
-              else if (bv < 0.0) { gc = (bx.lo - av) / bv; ns = sl - 1; }
-            } else {       // fixed: v(gamma) = -r0 - r1 gamma leaves [slo, shi]
-              if (r1 < 0.0) { gc = -(bx.shi + r0) / r1; ns = sl + 1; }
-              else if (r1 > 0.0) { gc = -(bx.slo + r0) / r1; ns = sl - 1; }
-            }
-            if (!(gc == gc)) gc = INFINITY;  // NaN guard
-            if (lane == last && gc <= gcur) gc = INFINITY;
-            gc = fmax(gc, gcur);
+  int npc = 0;
+  int sl0 = lane < N ? 1 : 0;
+  if (!(a.flags & LOMPC_PLAN_DIAG_REPAIR)) {
+    int sl = sl0;
+    if (a.ws) {
+      const int v = a.ws[(size_t)blk * 64 + lane];
+      sl = (lane < N && v >= 0 && v <= 2 * q.m) ? v : sl0;
+    }
+    double w = 0.0, r = 0.0;
+    const bool solved = lqw::wave_solve(q, ws, glo, sl, w, r);
+    LQ_STAMP(2);
+    if (solved) {
+      sl0 = sl;
+      if (a.ws) a.ws[(size_t)blk * 64 + lane] = (uint8_t)sl;
+      // ---- parametric active-set tracking of w*(gamma) on [glo, ghi]
+      double gcur = glo;
+      int last = -1;
+      const int max_iter = 4 * LQ_PPL + 16;
+      const double ee = ws.e_nat;
+      for (int it = 0; it < max_iter && npc < LQ_PPL; ++it) {
+        const lqw::StageSol<2> sol = lqw::solve_stage<2>(q, ws, 0.0, sl);
+        const double av = sol.w[0], bv = sol.w[1], r0 = sol.r[0], r1 = sol.r[1];
+        double gc = INFINITY;
+        int ns = sl;
+        if (lane < N) {
+          const Box bx = lq_box(sl);
+          if (sl & 1) {  // free: w(gamma) = a + b gamma leaves [lo, hi]
+            if (bv > 0.0) { gc = (bx.hi - av) / bv; ns = sl + 1; }
+            else if (bv < 0.0) { gc = (bx.lo - av) / bv; ns = sl - 1; }
+          } else {       // fixed: v(gamma) = -r0 - r1 gamma leaves [slo, shi]
+            if (r1 < 0.0) { gc = -(bx.shi + r0) / r1; ns = sl + 1; }
+            else if (r1 > 0.0) { gc = -(bx.slo + r0) / r1; ns = sl - 1; }
           }
-          double best = gc;
-          int bj = lane;
-          lqw::wave_argmin(best, bj, N);
-          if (!(best < ghi)) {
-            best = ghi;
-            bj = -1;
-          }
-          const bool final_piece = (bj < 0) || (npc == LQ_PPLX - 1);
-          if (best > gcur || final_piece) {
-            // KKT certificate at the piece's end; its start is the previous certified end (same
-            // w and r, only the switched coordinate's box changed and it contains the value)
-            const Box bx = lq_box(lane < N ? sl : 0);
-            const double wz = fmin(fmax(fma(bv, best, av), bx.lo), bx.hi);
-            const double res = lqw::wave_kkt_point(q, ws, best, sl, wz);
-            if (!(res <= q.tol_cert)) break;  // coverage ends at gcur
-            // cost and err^2 are quadratics in gamma on the piece
-            const bool act = lane < N;
-            lqw::Sums<2> pf;
-            pf.v[0] = act ? av : 0.0;
-            pf.v[1] = act ? bv : 0.0;
-            pf = lqw::wave_scan(pf, N);
-            const double Ya = pf.v[0], Yb = pf.v[1];
-            const double Ea = Ya - Ywr, da = av - wr_nat;
-            const double dd = ws.d_nat, cc = q.c;
-            const double sg = (sl & 1) ? bx.slo : 0.0;  // PWL slope of a free coordinate
-            double icpt = 0.0;                          // PWL value at w = 0 of its linear piece
-            if (!q.ev_small) {
-              const double wm = fma(bv, 0.5 * (gcur + best), av);
-              const double tw = q.theta * q.w_max;
-              icpt = fma(-sg, wm, tw * tw * lq_pwl(wm * q.inv_wmax));
-            }
-            double t[6];
-            t[0] = fma(0.5 * cc, Ya * Ya, fma(av, fma(0.5 * dd, av, ee + sg), icpt));
-            t[1] = fma(cc, fma(Ya, Yb, -Ya), bv * fma(dd, av, ee + sg));
-            t[2] = fma(0.5 * cc, Yb * Yb, fma(-cc, Yb, 0.5 * dd * bv * bv));
-            t[3] = fma(Ea, Ea, sd.kappa * da * da);
-            t[4] = 2.0 * fma(Ea, Yb, sd.kappa * da * bv);
-            t[5] = fma(Yb, Yb, sd.kappa * bv * bv);
-#pragma unroll
-            for (int kk = 0; kk < 6; ++kk) t[kk] = act ? t[kk] : 0.0;
-            lqw::wave_totals(t, N);
-            const int slot = k * LQ_PPLX + npc;
-            s_ab[slot][lane] = make_double2(act ? av : 0.0, act ? bv : 0.0);
-            const double a0 = __shfl(av, 0, 64), b0v = __shfl(bv, 0, 64);
-            if (lane < 8) {
-              double v = t[0] + sd.c0;
-#pragma unroll
-              for (int kk = 1; kk < 6; ++kk) v = lane == kk ? t[kk] : v;
-              v = lane == 6 ? a0 : (lane == 7 ? b0v : v);
-              s_cf[slot][lane] = v;
-            }
-            if (lane == 0) s_ge[slot] = best;
-            gcov = best;
-            ++npc;
-          }
-          if (bj < 0) break;
-          const int bns = __shfl(ns, bj, 64);
-          if (lane == bj) sl = bns;
-          gcur = best;
-          last = bj;
+          if (!(gc == gc)) gc = INFINITY;  // NaN guard
+          if (lane == last && gc <= gcur) gc = INFINITY;
+          gc = fmax(gc, gcur);
         }
+        double best = gc;
+        int bj = lane;
+        lqw::wave_argmin(best, bj, N);
+        if (!(best < ghi)) {
+          best = ghi;
+          bj = -1;
+        }
+        const bool final_piece = (bj < 0) || (npc == LQ_PPL - 1);
+        if (best > gcur || final_piece) {
+          // KKT certificate at the piece's end; its start is the previous certified end (same w
+          // and r, only the switched coordinate's box changed and it contains the value)
+          const Box bx = lq_box(lane < N ? sl : 0);
+          const double wz = fmin(fmax(fma(bv, best, av), bx.lo), bx.hi);
+          const double res = lqw::wave_kkt_point(q, ws, best, sl, wz);
+          if (!(res <= q.tol_cert)) break;  // coverage ends at gcur
+          // cost and err^2 are quadratics in gamma on the piece
+          const bool act = lane < N;
+          lqw::Sums<2> pf;
+          pf.v[0] = act ? av : 0.0;
+          pf.v[1] = act ? bv : 0.0;
+          pf = lqw::wave_scan(pf, N);
+          const double Ya = pf.v[0], Yb = pf.v[1];
+          const double Ea = Ya - Ywr, da = av - wr_nat;
+          const double dd = ws.d_nat, cc = q.c;
+          const double sg = (sl & 1) ? bx.slo : 0.0;  // PWL slope of a free coordinate
+          double icpt = 0.0;                          // PWL value at w = 0 of its linear piece
+          if (!q.ev_small) {
+            const double wm = fma(bv, 0.5 * (gcur + best), av);
+            const double tw = q.theta * q.w_max;
+            icpt = fma(-sg, wm, tw * tw * lq_pwl(wm * q.inv_wmax));
+          }
+          double t[6];
+          t[0] = fma(0.5 * cc, Ya * Ya, fma(av, fma(0.5 * dd, av, ee + sg), icpt));
+          t[1] = fma(cc, fma(Ya, Yb, -Ya), bv * fma(dd, av, ee + sg));
+          t[2] = fma(0.5 * cc, Yb * Yb, fma(-cc, Yb, 0.5 * dd * bv * bv));
+          t[3] = fma(Ea, Ea, kappa * da * da);
+          t[4] = 2.0 * fma(Ea, Yb, kappa * da * bv);
+          t[5] = fma(Yb, Yb, kappa * bv * bv);
+#pragma unroll
+          for (int k = 0; k < 6; ++k) t[k] = act ? t[k] : 0.0;
+          lqw::wave_totals(t, N);
+          p_ab[npc][lane] = make_double2(av, bv);
+          const double a0 = __shfl(av, 0, 64), b0v = __shfl(bv, 0, 64);
+          if (lane < 8) {
+            double v = t[0] + c0;
+#pragma unroll
+            for (int k = 1; k < 6; ++k) v = lane == k ? t[k] : v;
+            v = lane == 6 ? a0 : (lane == 7 ? b0v : v);
+            p_cf[npc][lane] = v;
+          }
+          if (lane == 0) p_ge[npc] = best;
+          ++npc;
+        }
+        if (bj < 0) break;
+        const int bns = __shfl(ns, bj, 64);
+        if (lane == bj) sl = bns;
+        gcur = best;
+        last = bj;
       }
     }
-    s_sl0[k][lane] = (uint8_t)sl0;
-    if (lane == 0) {
-      s_npc[k] = npc;
-      s_cov[k][0] = glo;
-      s_cov[k][1] = gcov;
+  }
+  // reserve the cell's pieces in the set's compact range (one agent-scope add per cell; the
+  // order of the cells in it does not change any output), then write them
+  int base = 0;
+  if (lane == 0 && npc > 0) base = atomicAdd(a.t_np + s, npc);
+  base = __shfl(base, 0, 64);
+  __builtin_amdgcn_wave_barrier();
+  const size_t sb = (size_t)s * G * LQ_PPL + base;
+  for (int k = 0; k < npc; ++k) {  // npc is wave-uniform
+    if (lane < N) a.t_ab[(sb + k) * N + lane] = p_ab[k][lane];
+    if (lane < 8) a.t_cf[(sb + k) * 8 + lane] = p_cf[k][lane];
+  }
+  if (lane < npc) a.t_ge[sb + lane] = p_ge[lane];
+  a.t_sl[(size_t)blk * 64 + lane] = (uint8_t)sl0;
+  if (lane == 0) {
+    a.t_cnt[blk] = npc;
+    a.t_base[blk] = base;
+    a.t_lo[blk] = glo;
+  }
+  LQ_STAMP(3);
+#ifdef LOMPC_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 65536) g_stamps[blockIdx.x * 8 + 6] = npc;
+#endif
+}
+
+// ---------------------------------------------------------------- k_eval
+struct EvalArgs {
+  int S, G, N, want_err;
+  const QPConst* qd;
+  const uint8_t* set_ctx;
+  const int4* blk;        // [nblk] (set, first EV, end EV, -): <= EVAL_MAXB EVs of one set
+  const int64_t* set_off; // [S+1]
+  const double* window;
+  const double* gamma;    // caller's [B]
+  const double* lmbd;
+  const double* lmbd_r;
+  const double* w_ref;
+  const int* t_cnt;
+  const int* t_base;
+  const double* t_lo;
+  const uint8_t* t_sl;
+  const int* t_np;
+  const double* t_ge;
+  const double* t_cf;
+  const double2* t_ab;
+  double* w;
+  double* cost;
+  double* w0;
+  int8_t* status;
+  double* partial;        // [nblk][N + NPX]
+  int* fail_cnt;          // [nblk][EVAL_WAVES]  EVs left for the individual re-solve (k_finalize)
+  int* fail_idx;          // [nblk][EVAL_MAXB]   their indices, per wave in row order
+  int w_rsrc_ok;          // B*N*8 fits a buffer descriptor's 31-bit offsets
+  int cap;                // pieces staged in LDS (a set with more re-solves the rest individually)
+};
+
+// cost / A_bar error / price0 of a QP solved by the whole wave (lane t = w_t), valid on every lane
+__device__ __forceinline__ void wave_ev_outputs(const QPConst& q, const lqw::WaveSet& ws, double c0, double kappa,
+                                                const double* l0, double lr, double wr, double gamma, double w,
+                                                double& cost, double& err, double& price0) {
+  const int N = ws.N, lane = ws.lane;
+  const bool act = lane < N;
+  lqw::Aff<2> h = lqw::Aff<2>::identity();
+  if (act) {
+    h.B[0] = w;
+    h.B[1] = w - wr;
+  }
+  const lqw::Aff<2> Y = lqw::wave_scan(h, N);
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  if (act) {
+    const double y = Y.B[0], ey = Y.B[1];
+    v[0] = 0.5 * q.c * y * y - q.c * gamma * y + w * fma(0.5 * ws.d_nat, w, ws.e_nat);
+    v[1] = ey * ey;
+    v[2] = (w - wr) * (w - wr);
+    v[3] = q.ev_small ? 0.0 : lq_pwl(w * q.inv_wmax);
+  }
+  lqw::wave_totals(v, N);
+  const double tw = q.theta * q.w_max;
+  cost = v[0] + c0 + tw * tw * v[3];
+  err = sqrt(fmax(v[1] + kappa * v[2], 0.0));
+  const double w0 = __shfl(w, 0, 64);
+  price0 = q.theta * (w0 * l0[0] + (q.w_max - w0) * l0[1]) + q.q_scale * w0 * w0 * l0[2] +
+           q.theta * q.theta * w0 * w0 * lr;
+}
+
+__global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
+  // dynamic LDS: [cap][N] piece rows | [cap][8] coefficients | [cap] piece ends | cells: base,
+  // count (int2) | coverage start
+  extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
+  __shared__ double s_g[EVAL_WAVES][64 * EVAL_PASSES];            // the wave's rows: gamma, piece
+  __shared__ int s_k[EVAL_WAVES][64 * EVAL_PASSES];               //   (-1 re-solved, -2 invalid)
+  __shared__ double s_accw[EVAL_WAVES][LOMPC_MAX_N];              // per-wave row sums per stage
+  __shared__ double s_red[EVAL_WAVES][8];
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int4 info = a.blk[blockIdx.x];
+  const int s = info.x, start = info.y, end = info.z;  // thread: EVs start + tid + EVAL_EVS h
+  const int N = a.N, G = a.G;
+  const int cap = a.cap;
+  LQ_STAMPE(0);
+  double2* s_ab = s_dyn;
+  double* s_cf = reinterpret_cast<double*>(s_ab + (size_t)cap * N);
+  double* s_ge = s_cf + (size_t)cap * 8;
+  int2* s_cell = reinterpret_cast<int2*>(s_ge + cap);
+  double* s_lo = reinterpret_cast<double*>(s_cell + G);
+  // this thread's EVs (caller order), the cells and the set's piece count: one memory round
+  double gh[EVAL_PASSES];
+#pragma unroll
+  for (int h = 0; h < EVAL_PASSES; ++h) {
+    const int i = start + tid + EVAL_EVS * h;
+    gh[h] = i < end ? a.gamma[i] : 0.0;
+  }
+  const QPConst& q = a.qd[a.set_ctx[s]];
+  const double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
+  const double* __restrict__ L = a.lmbd + (size_t)s * 3 * N;
+  const double l0[3] = {L[0], L[N], L[2 * N]};  // price0 (lompc.py:164-170)
+  const double lr = a.lmbd_r[s];
+  const int np = min(a.t_np[s], cap);
+  const int cb = s * G;
+  for (int c = tid; c < G; c += EVAL_EVS) {
+    s_cell[c] = make_int2(a.t_base[cb + c], a.t_cnt[cb + c]);
+    s_lo[c] = a.t_lo[cb + c];
+  }
+  // the set's pieces (contiguous in the compact range): coalesced copies, every load of a
+  // thread issued before its first LDS store (one memory round, not one per item)
+  const size_t sb = (size_t)s * G * LQ_PPL;
+  {
+    const int nab = np * N, ncf = np * 8;
+    const double2* gab = a.t_ab + sb * N;
+    const double* gcf = a.t_cf + sb * 8;
+    constexpr int U = 8;
+    for (int b0 = tid; b0 < nab; b0 += EVAL_EVS * U) {
+      double2 v[U];
+  #pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int it = b0 + EVAL_EVS * u;
+        v[u] = it < nab ? gab[it] : make_double2(0.0, 0.0);
+      }
+  #pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int it = b0 + EVAL_EVS * u;
+        if (it < nab) s_ab[it] = v[u];
+      }
+    }
+    for (int b0 = tid; b0 < ncf + np; b0 += EVAL_EVS * U) {
+      double v[U];
+  #pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int it = b0 + EVAL_EVS * u;
+        v[u] = it < ncf ? gcf[it] : (it < ncf + np ? a.t_ge[sb + it - ncf] : 0.0);
+      }
+  #pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int it = b0 + EVAL_EVS * u;
+        if (it < ncf) s_cf[it] = v[u];
+        else if (it < ncf + np) s_ge[it - ncf] = v[u];
+      }
     }
   }
-  __syncthreads();  // pieces published to every wave (no global stores outstanding here)
-  LQ_STAMP(3);
-  // ---- the cell's EVs: wave wv takes chunks wv, wv + SOLVE_WAVES, ...
+  lq_tab_init(q);  // (its barrier publishes the staged table)
+  LQ_STAMPE(1);
+  // ---- lane = EV: piece, scalar outputs; EVs no certified piece covers listed for the
+  //      individual re-solve in k_finalize (counted as pending failures until then)
+  const double ym = q.y_max, wm = q.w_max;
+  const double tt = q.theta * q.theta;
+  const double cscale = (double)G / (whi - wlo);
   double acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
-  int n_ok = 0, n_rep = 0, n_fail = 0, n_inv = 0;
-  double rep_w = 0.0;  // lane = stage: sum of individually re-solved rows
-  if (lane < NSLOT) {
-    s_mom[wv][lane][0] = 0.0;
-    s_mom[wv][lane][1] = 0.0;
-  }
-  const int V = (N & 1) ? 1 : 2;  // stages per lane in the row stores (16-B stores for even N)
-  const int Lr = N / V;           // lanes per row
-  const int R = 64 / Lr;          // rows per store instruction
-  const int rr = lane / Lr, col = lane - rr * Lr;
-  const bool rlane = rr < R;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.w, (short)0, 0x7fffffff, 0x00020000);
-  const double wm = q.w_max;
-  const double ksc = (double)SOLVE_PATHS / (chi - clo);
-  for (int i0 = b0 + 64 * wv; i0 < b1; i0 += 64 * SOLVE_WAVES) {
-    const int j = i0 + lane;
-    const bool act = j < b1;
-    const bool first = i0 == b0 + 64 * wv;
-    const double g = first ? g_pre : (act ? a.gs[j] : 0.0);
-    const int o = first ? o_pre : (act ? (int)a.perm[j] : 0);
-    // sub-cell, then piece within it (s_ge of a sub-cell ascends)
-    const double kf = (g - clo) * ksc;
-    const int k = kf <= 0.0 ? 0 : (kf >= (double)(SOLVE_PATHS - 1) ? SOLVE_PATHS - 1 : (int)kf);
-    const int npk = s_npc[k];
-    int p = 0;
-    for (int pp = 0; pp < LQ_PPLX - 1; ++pp) p += (pp < npk - 1 && g > s_ge[k * LQ_PPLX + pp]) ? 1 : 0;
-    const int slot = k * LQ_PPLX + p;
-    const bool cov = act && !invalid_cell && npk > 0 && g >= s_cov[k][0] && g <= s_cov[k][1];
-    int tag = -1;
-    if (act && invalid_cell) {
-      tag = -2;
+  int n_ok = 0, n_fail = 0, n_inv = 0, nlist = 0;
+#pragma unroll
+  for (int h = 0; h < EVAL_PASSES; ++h) {
+    const int i = start + tid + EVAL_EVS * h;
+    const bool act = i < end;
+    const double g = gh[h];
+    const bool valid = act && g >= 0.0 && g <= ym;
+    const int c = valid ? cell_of(g, wlo, cscale, G) : 0;
+    const int2 ci = s_cell[c];
+    const int kb = ci.x, ke = ci.x + ci.y;  // the cell's pieces [kb, ke), ascending gamma
+    int key = kb;
+    for (int k = kb; k < ke - 1; ++k) key += g > s_ge[k] ? 1 : 0;
+    const bool cov = valid && ke > kb && ke <= np && g >= s_lo[c] && g <= s_ge[ke - 1];
+    if (act && !valid) {
       ++n_inv;
-      if (a.cost) st_wt8(a.cost + o, NAN);
-      if (a.w0) st_wt8(a.w0 + o, NAN);
-      if (a.status) a.status[o] = LOMPC_QP_INVALID;
+      if (a.cost) st_wt8(a.cost + i, NAN);
+      if (a.w0) st_wt8(a.w0 + i, NAN);
+      if (a.status) a.status[i] = LOMPC_QP_INVALID;
     } else if (cov) {
-      tag = slot;
-      const double4 c0 = *reinterpret_cast<const double4*>(&s_cf[slot][0]);
-      const double4 c1 = *reinterpret_cast<const double4*>(&s_cf[slot][4]);
+      const double4 c0 = *reinterpret_cast<const double4*>(s_cf + key * 8);
+      const double4 c1 = *reinterpret_cast<const double4*>(s_cf + key * 8 + 4);
       const double cst = fma(fma(c0.z, g, c0.y), g, c0.x);
       const double e2 = fma(fma(c1.y, g, c1.x), g, c0.w);
-      const double er = want_err ? sqrt(fmax(e2, 0.0)) : 0.0;
+      const double er = a.want_err ? sqrt(fmax(e2, 0.0)) : 0.0;
       const double w0v = clampw(fma(c1.w, g, c1.z), wm);
-      const double p0 = q.theta * (w0v * sd.l10 + (wm - w0v) * sd.l20) + q.q_scale * w0v * w0v * sd.l30 +
-                        tt * w0v * w0v * sd.lr;  // lompc.py:164-170
+      const double p0 = q.theta * (w0v * l0[0] + (wm - w0v) * l0[1]) + q.q_scale * w0v * w0v * l0[2] +
+                        tt * w0v * w0v * lr;  // lompc.py:164-170
       acc_cost += cst;
       acc_p0 += p0;
       acc_err = fmax(acc_err, er);
       ++n_ok;
-      if (a.cost) st_wt8(a.cost + o, cst);
-      if (a.w0) st_wt8(a.w0 + o, w0v);
-      if (a.status) a.status[o] = LOMPC_QP_OK;
+      if (a.cost) st_wt8(a.cost + i, cst);
+      if (a.w0) st_wt8(a.w0 + i, w0v);
+      if (a.status) a.status[i] = LOMPC_QP_OK;
     }
-    // per-piece moments of the covered EVs (sum w = sum over pieces of count a + b sum gamma):
-    // one masked wave total per distinct piece in the chunk, in lane order (deterministic)
-    unsigned long long rem = __ballot(cov);
-    while (rem) {
-      const int key = __builtin_amdgcn_readlane(tag, (int)__builtin_ctzll(rem));
-      const bool m = cov && tag == key;
-      rem &= ~__ballot(m);
-      double v[2] = {m ? 1.0 : 0.0, m ? g : 0.0};
-      lqw::wave_totals(v, 64);
-      if (lane == 0) {
-        s_mom[wv][key][0] += v[0];
-        s_mom[wv][key][1] += v[1];
-      }
+    s_g[wv][64 * h + lane] = g;
+    s_k[wv][64 * h + lane] = (act && !valid) ? -2 : (cov ? key : -1);
+    const unsigned long long need = __ballot(valid && !cov);
+    if (valid && !cov) {
+      a.fail_idx[(size_t)blockIdx.x * EVAL_MAXB + 64 * EVAL_PASSES * wv + nlist +
+                 __popcll(need & ((1ull << lane) - 1ull))] = i;
+      ++n_fail;
     }
-    s_g[wv][lane] = g;
-    s_p[wv][lane] = tag;
-    s_o[wv][lane] = o;
-    // ---- EVs no certified piece covers: whole-wave certified re-solve, row written here
-    unsigned long long need = __ballot(act && !invalid_cell && !cov);
-    while (need) {
-      const int l = (int)__builtin_ctzll(need);
-      need &= need - 1ull;
-      const double gl = lqw::readlane_d(g, l);
-      const int ol = __builtin_amdgcn_readlane(o, l);
-      const int kl = __builtin_amdgcn_readlane(k, l);
-      int sl = lane < N ? (int)s_sl0[kl][lane] : 0;
-      double wl = 0.0, rl = 0.0;
-      const bool okk = lqw::wave_solve(q, ws, gl, sl, wl, rl);
-      double cl, el, pl;
-      wave_ev_outputs(q, ws, sd, wr_nat, gl, wl, cl, el, pl);
-      if (!want_err) el = 0.0;
-      if (a.w && lane < N) st_wt8(a.w + (size_t)ol * N + lane, wl);
-      rep_w += lane < N ? wl : 0.0;
-      const double w0l = __shfl(wl, 0, 64);
-      if (lane == l) {
-        acc_cost += cl;
-        acc_p0 += pl;
-        acc_err = fmax(acc_err, el);
-        n_rep += okk ? 1 : 0;
-        n_fail += okk ? 0 : 1;
-        if (a.cost) st_wt8(a.cost + ol, cl);
-        if (a.w0) st_wt8(a.w0 + ol, w0l);
-        if (a.status) a.status[ol] = okk ? LOMPC_QP_REPAIRED : LOMPC_QP_FAILED;
-      }
+    nlist += __popcll(need);
+  }
+  if (lane == 0) a.fail_cnt[(size_t)blockIdx.x * EVAL_WAVES + wv] = nlist;
+  LQ_STAMPE(2);
+  __builtin_amdgcn_wave_barrier();  // this wave's own rows in LDS: in order
+  LQ_STAMPE(3);
+  // ---- rows (lane = stage pair): w_t = a_t + b_t gamma of the EV's piece -> contiguous rows
+  const int V = (N & 1) ? 1 : 2;  // stages per lane (16-B stores for even N)
+  const int Lr = N / V;           // lanes per row
+  const int R = 64 / Lr;          // rows per store instruction
+  const int rr = lane / Lr, col = lane - rr * Lr;
+  const bool rlane = rr < R;
+  // the wave's rows r: EV start + 64 wv + r (r < 64), start + EVAL_EVS + 64 wv + r - 64 (second pass)
+  const int row0 = start + 64 * wv;
+  const int n0 = max(0, min(64, end - row0));
+  const int nrow = n0 < 64 ? n0 : 64 + max(0, min(64 * (EVAL_PASSES - 1), end - row0 - EVAL_EVS));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.w, (short)0, 0x7fffffff, 0x00020000);
+  double acc0 = 0.0, acc1 = 0.0;
+  const int t0 = V * col;
+  constexpr int RU = 4;  // row instructions per batch: their LDS reads in flight together
+  for (int r0 = 0; r0 < nrow; r0 += RU * R) {
+    int kk[RU];
+    double gg[RU];
+    double2 u0[RU], u1[RU];
+  #pragma unroll
+    for (int j = 0; j < RU; ++j) {
+      const int row = r0 + j * R + rr;
+      const bool ok = rlane && row < nrow;
+      kk[j] = ok ? s_k[wv][row] : -1;
+      gg[j] = ok ? s_g[wv][row] : 0.0;
     }
-    __builtin_amdgcn_wave_barrier();  // one wave's own LDS rows: in order, no vmcnt drain
-    // ---- rows (lane = stage): w_t = a_t + b_t gamma of the EV's piece -> caller row perm[j]
-    if (a.w) {
-      const int nrow = min(64, b1 - i0);
-      for (int r0 = 0; r0 < nrow; r0 += R) {
-        const int row = r0 + rr;
-        if (rlane && row < nrow) {
-          const int pp = s_p[wv][row];
-          if (pp != -1) {
-            const double gr = s_g[wv][row];
-            const int orow = s_o[wv][row];
-            const int t0 = V * col;
-            double x0, x1 = 0.0;
-            if (pp >= 0) {
-              const double2 u = s_ab[pp][t0];
-              x0 = clampw(fma(u.y, gr, u.x), wm);
-              if (V == 2) {
-                const double2 u1 = s_ab[pp][t0 + 1];
-                x1 = clampw(fma(u1.y, gr, u1.x), wm);
-              }
-            } else {
-              x0 = x1 = NAN;  // invalid gamma
-            }
-            if (a.w_rsrc_ok) {
-              const int off = (orow * N + t0) * 8;
-              if (V == 2) st_wt16(rs, off, x0, x1);
-              else st_wt8b(rs, off, x0);
-            } else {
-              double* dst = a.w + (size_t)orow * N + t0;
-              st_wt8(dst, x0);
-              if (V == 2) st_wt8(dst + 1, x1);
-            }
+  #pragma unroll
+    for (int j = 0; j < RU; ++j) {
+      const int kx = kk[j] >= 0 ? kk[j] : 0;
+      u0[j] = s_ab[kx * N + t0];
+      u1[j] = V == 2 ? s_ab[kx * N + t0 + 1] : make_double2(0.0, 0.0);
+    }
+  #pragma unroll
+    for (int j = 0; j < RU; ++j) {
+      const int k = kk[j];
+      if (k != -1) {
+        double x0, x1 = 0.0;
+        if (k >= 0) {
+          x0 = clampw(fma(u0[j].y, gg[j], u0[j].x), wm);
+          if (V == 2) x1 = clampw(fma(u1[j].y, gg[j], u1[j].x), wm);
+          acc0 += x0;
+          acc1 += x1;
+        } else {
+          x0 = x1 = NAN;  // invalid gamma
+        }
+        if (a.w) {
+          const int rw = r0 + j * R + rr;
+          const int orow = row0 + rw + (rw >= 64 ? EVAL_EVS - 64 : 0);
+          if (a.w_rsrc_ok) {
+            const int off = (orow * N + t0) * 8;
+            if (V == 2) st_wt16(rs, off, x0, x1);
+            else st_wt8b(rs, off, x0);
+          } else {
+            double* dst = a.w + (size_t)orow * N + t0;
+            st_wt8(dst, x0);
+            if (V == 2) st_wt8(dst + 1, x1);
           }
         }
       }
-      __builtin_amdgcn_wave_barrier();
     }
   }
-  LQ_STAMP(4);
-  // ---- per-wave totals, then wave 0 combines the waves in a fixed order
+  // this wave's row sums per stage: lanes col, col + Lr, ... (fixed order)
   {
-    double tot[4] = {acc_cost, acc_p0, (double)(n_ok + n_rep), (double)n_rep};
+    double s0 = acc0, s1 = acc1;
+    for (int k = 1; k < R; ++k) {
+      s0 += __shfl(acc0, lane + k * Lr, 64);
+      s1 += __shfl(acc1, lane + k * Lr, 64);
+    }
+    if (lane < Lr) {
+      s_accw[wv][V * lane] = s0;
+      if (V == 2) s_accw[wv][V * lane + 1] = s1;
+    }
+  }
+  LQ_STAMPE(4);
+  // ---- workgroup record: per-wave totals, then a fixed-order combination
+  {
+    double tot[4] = {acc_cost, acc_p0, (double)n_ok, 0.0};
     lqw::wave_totals(tot, 64);
     const double mx = lqw::wave_max(acc_err, 64);
     double cnt[2] = {(double)n_fail, (double)n_inv};
     lqw::wave_totals(cnt, 64);
     if (lane == 0) {
-      s_red[wv][0] = tot[0];
-      s_red[wv][1] = tot[1];
-      s_red[wv][2] = mx;
-      s_red[wv][3] = tot[2];
-      s_red[wv][4] = tot[3];
-      s_red[wv][5] = cnt[0];
-      s_red[wv][6] = cnt[1];
+      s_red[wv][PX_COST] = tot[0];
+      s_red[wv][PX_PRICE0] = tot[1];
+      s_red[wv][PX_MAX_ERR] = mx;
+      s_red[wv][PX_N_OK] = tot[2];
+      s_red[wv][PX_N_REPAIRED] = tot[3];
+      s_red[wv][PX_N_FAILED] = cnt[0];
+      s_red[wv][PX_N_INVALID] = cnt[1];
     }
-    s_repw[wv][lane] = rep_w;
   }
   __syncthreads();
-  if (wv == 0) {
+  double* part = a.partial + (size_t)blockIdx.x * (N + NPX);
+  if (tid < N) {  // stage t: every wave's row sums, then the re-solved rows
     double sw = 0.0;
-    for (int kk = 0; kk < SOLVE_WAVES; ++kk) sw += s_repw[kk][lane];
-    for (int k = 0; k < SOLVE_PATHS; ++k) {
-      const int npk = s_npc[k];  // uniform
-      for (int pp = 0; pp < npk; ++pp) {
-        const int slot = k * LQ_PPLX + pp;
-        double cnt = 0.0, sg = 0.0;
-        for (int kk = 0; kk < SOLVE_WAVES; ++kk) {
-          cnt += s_mom[kk][slot][0];
-          sg += s_mom[kk][slot][1];
-        }
-        const double2 u = s_ab[slot][lane];
-        sw += (lane < N) ? fma(u.x, cnt, u.y * sg) : 0.0;
-      }
-    }
-    if (lane < N) st_wt8(part + lane, sw);
-    if (lane < NPX) {
-      double v = 0.0;
-      for (int kk = 0; kk < SOLVE_WAVES; ++kk) v = lane == PX_MAX_ERR ? fmax(v, s_red[kk][lane]) : v + s_red[kk][lane];
-      st_wt8(part + N + lane, v);
-    }
-    if (a.arrive) arrive_reduce(a, s, lane, N);
+    for (int k = 0; k < EVAL_WAVES; ++k) sw += s_accw[k][tid];
+    part[tid] = sw;
+  } else if (tid >= 64 && tid < 64 + NPX) {
+    const int x = tid - 64;
+    double v = 0.0;
+    for (int k = 0; k < EVAL_WAVES; ++k) v = x == PX_MAX_ERR ? fmax(v, s_red[k][x]) : v + s_red[k][x];
+    part[N + x] = v;
   }
-  LQ_STAMP(5);
-#ifdef LOMPC_STAMPS
-  if (threadIdx.x == 0 && blockIdx.x < 65536) {
-    int np = 0;
-    for (int k = 0; k < SOLVE_PATHS; ++k) np += s_npc[k];
-    g_stamps[blockIdx.x * 8 + 6] = np;
-    g_stamps[blockIdx.x * 8 + 7] = b1 - b0;
-  }
-#endif
+  LQ_STAMPE(5);
 }
 
-// ---------------------------------------------------------------- k_reduce
-struct ReduceArgs {
-  int G, N;
+// ---------------------------------------------------------------- k_finalize
+struct FinalArgs {
+  int N, G, want_err;
+  int* t_np;               // [S] compact piece counters of k_path, reset here for the next run
+  const QPConst* qd;
+  const uint8_t* set_ctx;
+  const int* blk_prefix;   // [S+1] k_eval workgroups of each set
   const int64_t* set_off;
+  const double* window;
+  const double* gamma;
+  const double* lmbd;
+  const double* lmbd_r;
+  const double* w_ref;
+  const uint8_t* t_sl;
+  const int* fail_cnt;
+  const int* fail_idx;
   const double* partial;
+  double* w;
+  double* cost;
+  double* w0;
+  int8_t* status;
   double* set_sum_w;
   double* set_stats;
   double* stats;
 };
 
-// One 256-thread workgroup per set: wave wv sums the cell records wv, wv+4, ... (lane =
-// column, 4 accumulators), then the 4 waves combine in a fixed order: deterministic.
-__global__ __launch_bounds__(256) void k_reduce(ReduceArgs r) {
+// One 256-thread workgroup per set.
+// (1) reduction of the set's k_eval records: wave wv sums records wv, wv+4, ... (lane =
+//     column, 4 accumulators), the 4 waves combine in a fixed order;
+// (2) if k_eval listed EVs no certified piece covers: wave wv re-solves the lists of waves
+//     (workgroup, wave) j = wv, wv+4, ... individually (wave_solve from the working set at
+//     their cell's start: fp32 search, fp64 PDAS, primal active set; KKT-certified), writes
+//     their outputs and adds them to the reduction in a fixed order.
+__global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
   __shared__ double red[4][LOMPC_MAX_N + NPX + 1];
+  __shared__ double rep[4][LOMPC_MAX_N + NPX + 1];
   const int s = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int N = r.N, W = N + NPX, G1 = r.G + 1;
-  const double* base = r.partial + (size_t)s * G1 * W;
+  const int N = r.N, W = N + NPX;
+  const int b0 = r.blk_prefix[s], b1 = r.blk_prefix[s + 1];
   for (int c = lane; c < W; c += 64) {
     const bool is_max = c == N + PX_MAX_ERR;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    constexpr int U = 8;
-    for (int b = wv; b < G1; b += 4 * U) {
+    constexpr int U = 16;
+    for (int b = b0 + wv; b < b1; b += 4 * U) {
       double v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int bb = b + 4 * u;
-        v[u] = bb < G1 ? base[(size_t)bb * W + c] : 0.0;  // 0: neutral for sums and max of errors >= 0
+        v[u] = bb < b1 ? r.partial[(size_t)bb * W + c] : 0.0;  // 0: neutral for sums and max of errors >= 0
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u & 3] = is_max ? fmax(acc[u & 3], v[u]) : acc[u & 3] + v[u];
@@ -741,6 +696,67 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs r) {
     red[0][tid] = v;
   }
   __syncthreads();
+  if (red[0][N + PX_N_FAILED] > 0.0) {  // block-uniform: individual re-solves pending
+    const QPConst& q = r.qd[r.set_ctx[s]];
+    lq_tab_init(q);
+    const double* __restrict__ L = r.lmbd + (size_t)s * 3 * N;
+    const double lr = r.lmbd_r[s];
+    lqw::WaveSet ws;
+    double l2;
+    load_set(q, L, lr, N, lane, ws, l2);
+    const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);
+    const double kappa = lr / q.delta;
+    const double l0[3] = {L[0], L[N], L[2 * N]};
+    const double wr = (r.w_ref && lane < N) ? r.w_ref[(size_t)s * N + lane] : 0.0;
+    const double wlo = r.window[2 * s], whi = r.window[2 * s + 1];
+    const int G = r.G;
+    double acc_w = 0.0, acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
+    int nrep = 0, nfail = 0;
+    for (int j = b0 * EVAL_WAVES + wv; j < b1 * EVAL_WAVES; j += 4) {  // (workgroup, wave)
+      const int nf = r.fail_cnt[j];
+      for (int k = 0; k < nf; ++k) {
+        const int i = r.fail_idx[(size_t)(j / EVAL_WAVES) * EVAL_MAXB + 64 * EVAL_PASSES * (j % EVAL_WAVES) + k];
+        const double g = r.gamma[i];
+        const int c = cell_of(g, wlo, (double)G / (whi - wlo), G);
+        int sl = lane < N ? (int)r.t_sl[((size_t)s * G + c) * 64 + lane] : 0;
+        double wl = 0.0, rl = 0.0;
+        const bool okk = lqw::wave_solve(q, ws, g, sl, wl, rl);
+        double co, eo, po;
+        wave_ev_outputs(q, ws, c0, kappa, l0, lr, wr, g, wl, co, eo, po);
+        if (!r.want_err) eo = 0.0;
+        if (r.w && lane < N) r.w[(size_t)i * N + lane] = wl;
+        if (lane == 0) {
+          if (r.cost) r.cost[i] = co;
+          if (r.w0) r.w0[i] = wl;
+          if (r.status) r.status[i] = okk ? LOMPC_QP_REPAIRED : LOMPC_QP_FAILED;
+        }
+        acc_w += lane < N ? wl : 0.0;
+        acc_cost += co;
+        acc_p0 += po;
+        acc_err = fmax(acc_err, eo);
+        nrep += okk ? 1 : 0;
+        nfail += okk ? 0 : 1;
+      }
+    }
+    if (lane < N) rep[wv][lane] = acc_w;
+    if (lane == 0) {
+      rep[wv][N + PX_COST] = acc_cost;
+      rep[wv][N + PX_PRICE0] = acc_p0;
+      rep[wv][N + PX_MAX_ERR] = acc_err;
+      rep[wv][N + PX_N_OK] = (double)nrep;
+      rep[wv][N + PX_N_REPAIRED] = (double)nrep;
+      rep[wv][N + PX_N_FAILED] = (double)nfail;
+      rep[wv][N + PX_N_INVALID] = 0.0;
+    }
+    __syncthreads();
+    if (tid < W) {
+      const bool is_max = tid == N + PX_MAX_ERR;
+      double v = (tid == N + PX_N_FAILED) ? 0.0 : red[0][tid];  // pending -> the outcome
+      for (int k = 0; k < 4; ++k) v = is_max ? fmax(v, rep[k][tid]) : v + rep[k][tid];
+      red[0][tid] = v;
+    }
+    __syncthreads();
+  }
   if (tid < N && r.set_sum_w) r.set_sum_w[(size_t)s * N + tid] = red[0][tid];
   if (tid < LOMPC_SET_STATS) {
     double v = 0.0;
@@ -757,20 +773,45 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs r) {
     if (r.set_stats) r.set_stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
     r.stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
   }
+  if (tid == 0) r.t_np[s] = 0;
 }
 
-int pick_cells(int64_t max_set, int flags) {
+int pick_cells(int64_t max_set) {
   const char* env = getenv("LOMPC_CELLS");  // diagnostics (cell-count sweeps)
   if (env) {
     const int g = atoi(env);
-    if (g >= 1 && g <= 4096) return g;
+    if (g >= 1 && g <= LQ_GMAX) return g;
   }
-  (void)flags;
-  // cells per set: the path has only a handful of breakpoints over a set's gamma window, so a
-  // cell is sized by its EVs: ~3 chunks of 64 per wave of the cell's workgroup
-  int G = 8;
-  while (G < 1024 && max_set > (int64_t)G * 64 * 3 * LQ_SOLVE_WAVES) G *= 2;
-  return G;
+  // the path of a set has a handful of breakpoints over its gamma window: the cell count trades
+  // per-wave tracking latency against more cold starts; one cell for tiny sets
+  if (max_set <= 64) return 1;
+  if (max_set <= 1024) return 8;
+  return 32;
+}
+
+int take_events(std::vector<hipEvent_t>& pool, hipEvent_t* e0, hipEvent_t* e1) {
+  for (hipEvent_t* e : {e0, e1}) {
+    if (!pool.empty()) {
+      *e = pool.back();
+      pool.pop_back();
+    } else if (hipEventCreateWithFlags(e, hipEventDisableSystemFence) != hipSuccess) {
+      return LOMPC_ERR_HIP;
+    }
+  }
+  return LOMPC_OK;
+}
+
+int plan_events_read(std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& pool, double& ms_acc, int64_t& n_acc) {
+  for (size_t k = 0; k + 1 < ev.size(); k += 2) {
+    if (hipEventSynchronize(ev[k + 1]) != hipSuccess) return LOMPC_ERR_HIP;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ev[k], ev[k + 1]) != hipSuccess) return LOMPC_ERR_HIP;
+    ms_acc += ms;
+    n_acc += 1;
+  }
+  pool.insert(pool.end(), ev.begin(), ev.end());
+  ev.clear();
+  return LOMPC_OK;
 }
 
 }  // namespace
@@ -791,7 +832,7 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   }
   if (S < 1) return fail_arg(p, "plan: at least one parameter set required");
   if (S > (1 << 20)) return fail_arg(p, "plan: too many parameter sets");
-  if (B < 0 || B >= (1ll << 31) - 64) return fail_arg(p, "plan: 0 <= B < 2^31 required");
+  if (B < 0 || B >= (1ll << 31) - EVAL_MAXB) return fail_arg(p, "plan: 0 <= B < 2^31 required");
   if (set_offsets[0] != 0 || set_offsets[S] != B) return fail_arg(p, "plan: set_offsets must run from 0 to B");
   int64_t max_set = 0;
   for (int64_t s = 0; s < S; ++s) {
@@ -802,15 +843,31 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   if (B > 0 && !gamma) return fail_arg(p, "plan: gamma required");
   const int N = ctxs[0]->N;
   HIPCHK(p, hipSetDevice(ctxs[0]->device));
-  const int G = pick_cells(max_set, flags);
-  const int64_t nbk = S * (G + 1);
-  if (nbk >= (1ll << 31)) return fail_arg(p, "plan: too many cells");
+  const int G = pick_cells(max_set);
+  const int64_t ncell = S * G;
+  // k_eval work split: every set in nb near-equal blocks of <= EVAL_MAXB EVs, the block count
+  // chosen so the workgroups fill the CUs a whole number of times (r rounds of n_cu, at most 90%
+  // of EVAL_MAXB per block) rather than spilling a few blocks into an extra round
+  if (!p->n_cu) {
+    HIPCHK(p, hipDeviceGetAttribute(&p->n_cu, hipDeviceAttributeMultiprocessorCount, ctxs[0]->device));
+    if (p->n_cu < 1) p->n_cu = 1;
+  }
+  const int64_t rounds = std::max<int64_t>(1, (10 * B + 9ll * p->n_cu * EVAL_MAXB - 1) / (9ll * p->n_cu * EVAL_MAXB));
+  const int64_t target = rounds * p->n_cu;
+  auto blocks_of = [&](int64_t m) -> int64_t {
+    if (m <= 0) return 0;
+    const int64_t lo = (m + EVAL_MAXB - 1) / EVAL_MAXB, hi = (m + 255) / 256;
+    return std::max<int64_t>(lo, std::min<int64_t>(hi, m * target / std::max<int64_t>(B, 1)));
+  };
+  int64_t nblk = 0;
+  for (int64_t s = 0; s < S; ++s) nblk += blocks_of(set_offsets[s + 1] - set_offsets[s]);
   p->device = ctxs[0]->device;
   p->N = N;
   p->nctx = nctx;
   for (int k = 0; k < nctx; ++k) p->ctx[k] = ctxs[k];
   p->flags = flags;
   p->w_ref = w_ref;
+  p->gamma = gamma;
   int rc;
   if (!p->d_q && (rc = grow(p, &p->d_q, LQ_PLAN_MAX_CTX))) return rc;
   if (!p->d_errflag) {
@@ -819,109 +876,72 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   }
   if (!p->ev_stage) HIPCHK(p, hipEventCreateWithFlags(&p->ev_stage, hipEventDisableTiming));
   if (S > p->cap_S) {
-    if ((rc = grow(p, &p->d_set_ctx, S)) || (rc = grow(p, &p->d_set_off, S + 1)) || (rc = grow(p, &p->d_arrive, S)) ||
-        (rc = grow(p, &p->d_window, 2 * S)) || (rc = grow(p, &p->d_stats_own, S * LOMPC_SET_STATS)))
+    if ((rc = grow(p, &p->d_set_ctx, S)) || (rc = grow(p, &p->d_set_off, S + 1)) ||
+        (rc = grow(p, &p->d_blk_prefix, S + 1)) || (rc = grow(p, &p->d_window, 2 * S)) ||
+        (rc = grow(p, &p->t_np, S)) ||
+        (rc = grow(p, &p->d_stats_own, S * LOMPC_SET_STATS)))
       return rc;
     p->cap_S = S;
   }
-  if (B > p->cap_B) {
-    if ((rc = grow(p, &p->d_keys, 2 * B)) || (rc = grow(p, &p->d_vals, 2 * B)) || (rc = grow(p, &p->d_gs, B)))
+  if (nblk > p->cap_blk) {
+    if ((rc = grow(p, &p->d_blk, nblk)) || (rc = grow(p, &p->d_partial, (size_t)nblk * (N + NPX))) ||
+        (rc = grow(p, &p->d_fail_cnt, (size_t)nblk * EVAL_WAVES)) || (rc = grow(p, &p->d_fail_idx, (size_t)nblk * EVAL_MAXB)))
       return rc;
-    p->cap_B = B;
+    p->cap_blk = nblk;
   }
   const bool warm = (flags & LOMPC_PLAN_WARM_START) != 0;
   bool fresh_ws = false;
-  if (nbk > p->cap_bk || (warm && !p->d_ws)) {
-    if ((rc = grow(p, &p->d_bucket_off, nbk + 1)) || (rc = grow(p, &p->d_partial, (size_t)nbk * (N + NPX))))
+  if (ncell > p->cap_cells || (warm && !p->d_ws)) {
+    if ((rc = grow(p, &p->t_cnt, ncell)) || (rc = grow(p, &p->t_base, ncell)) || (rc = grow(p, &p->t_lo, ncell)) ||
+        (rc = grow(p, &p->t_ge, ncell * LQ_PPL)) || (rc = grow(p, &p->t_cf, ncell * LQ_PPL * 8)) ||
+        (rc = grow(p, &p->t_ab, ncell * LQ_PPL * N)) || (rc = grow(p, &p->t_sl, ncell * 64)))
       return rc;
-    if (warm && (rc = grow(p, &p->d_ws, (size_t)nbk * LQ_WS_MAX * 64))) return rc;
-    p->cap_bk = nbk;
+    if (warm && (rc = grow(p, &p->d_ws, (size_t)ncell * 64))) return rc;
+    p->cap_cells = ncell;
     fresh_ws = true;
   }
-  if (warm && (fresh_ws || p->G != G || p->S != S))
-    HIPCHK(p, hipMemsetAsync(p->d_ws, 1, (size_t)nbk * LQ_WS_MAX * 64, st));
-  HIPCHK(p, hipMemsetAsync(p->d_arrive, 0, S * sizeof(unsigned), st));
+  if (warm && (fresh_ws || p->G != G || p->S != S)) HIPCHK(p, hipMemsetAsync(p->d_ws, 1, (size_t)ncell * 64, st));
+  HIPCHK(p, hipMemsetAsync(p->t_np, 0, S * sizeof(int), st));
   p->B = B;
   p->S = S;
   p->G = G;
+  p->nblk = (int)nblk;
   p->d_stats = p->d_stats_own;
-  p->d_perm = p->d_vals + B;
-  // radix-sort temporary storage
-  const unsigned end_bit = std::max(1u, (unsigned)(64 - __builtin_clzll((unsigned long long)nbk)));
-  size_t tmp = 0;
-  if (B > 0) {
-    HIPCHK(p, rocprim::radix_sort_pairs(nullptr, tmp, p->d_keys, p->d_keys + B, p->d_vals, p->d_vals + B,
-                                        (size_t)B, 0u, end_bit, st));
-    if (tmp > p->cap_tmp) {
-      if (p->d_tmp) HIPCHK(p, hipFree(p->d_tmp));
-      p->d_tmp = nullptr;
-      HIPCHK(p, hipMalloc(&p->d_tmp, tmp));
-      p->cap_tmp = tmp;
-    }
-  }
   // host arrays -> pinned staging -> device (the staging may still feed the previous prepare)
-  const size_t need_h = (size_t)(S + 1) * sizeof(int64_t) + S + LQ_PLAN_MAX_CTX * sizeof(QPConst) + 64;
+  const size_t need_h = LQ_PLAN_MAX_CTX * sizeof(QPConst) + (size_t)(S + 1) * (sizeof(int64_t) + sizeof(int)) +
+                        (size_t)nblk * sizeof(int4) + S + 64;
+  HIPCHK(p, hipEventSynchronize(p->ev_stage));
   if ((int64_t)need_h > p->cap_h) {
-    HIPCHK(p, hipEventSynchronize(p->ev_stage));
-    if (p->h_off) HIPCHK(p, hipHostFree(p->h_off));
-    p->h_off = nullptr;
-    HIPCHK(p, hipHostMalloc((void**)&p->h_off, need_h, hipHostMallocDefault));
+    if (p->h_buf) HIPCHK(p, hipHostFree(p->h_buf));
+    p->h_buf = nullptr;
+    HIPCHK(p, hipHostMalloc((void**)&p->h_buf, need_h, hipHostMallocDefault));
     p->cap_h = (int64_t)need_h;
   }
-  HIPCHK(p, hipEventSynchronize(p->ev_stage));
-  QPConst* hq = reinterpret_cast<QPConst*>(p->h_off);
+  QPConst* hq = reinterpret_cast<QPConst*>(p->h_buf);
   for (int k = 0; k < nctx; ++k) hq[k] = ctxs[k]->q;
   int64_t* hoff = reinterpret_cast<int64_t*>(hq + LQ_PLAN_MAX_CTX);
   memcpy(hoff, set_offsets, (S + 1) * sizeof(int64_t));
-  uint8_t* hctx = reinterpret_cast<uint8_t*>(hoff + S + 1);
+  int4* hblk = reinterpret_cast<int4*>(hoff + S + 1);
+  int* hpre = reinterpret_cast<int*>(hblk + nblk);
+  uint8_t* hctx = reinterpret_cast<uint8_t*>(hpre + S + 1);
+  int64_t b = 0;
+  hpre[0] = 0;
+  for (int64_t s = 0; s < S; ++s) {
+    const int64_t o = set_offsets[s], m = set_offsets[s + 1] - o, nb = blocks_of(m);
+    for (int64_t k = 0; k < nb; ++k) hblk[b++] = make_int4((int)s, (int)(o + m * k / nb), (int)(o + m * (k + 1) / nb), 0);
+    hpre[s + 1] = (int)b;
+  }
   for (int k = 0, s = 0; k < nctx; ++k)
     for (int64_t u = 0; u < sets_per_ctx[k]; ++u) hctx[s++] = (uint8_t)k;
   HIPCHK(p, hipMemcpyAsync(p->d_q, hq, nctx * sizeof(QPConst), hipMemcpyHostToDevice, st));
   HIPCHK(p, hipMemcpyAsync(p->d_set_off, hoff, (S + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
+  if (nblk) HIPCHK(p, hipMemcpyAsync(p->d_blk, hblk, nblk * sizeof(int4), hipMemcpyHostToDevice, st));
+  HIPCHK(p, hipMemcpyAsync(p->d_blk_prefix, hpre, (S + 1) * sizeof(int), hipMemcpyHostToDevice, st));
   HIPCHK(p, hipMemcpyAsync(p->d_set_ctx, hctx, S, hipMemcpyHostToDevice, st));
   HIPCHK(p, hipEventRecord(p->ev_stage, st));
-  PlanArgs a{};
-  a.S = (int)S;
-  a.G = G;
-  a.nbk = (int)nbk;
-  a.B = B;
-  a.qd = p->d_q;
-  a.set_ctx = p->d_set_ctx;
-  a.set_off = p->d_set_off;
-  a.window = p->d_window;
-  a.gamma = gamma;
-  a.keys = p->d_keys;
-  a.vals = p->d_vals;
-  a.keys_out = p->d_keys + B;
-  a.vals_out = p->d_vals + B;
-  a.bucket_off = p->d_bucket_off;
-  a.gs = p->d_gs;
-  hipLaunchKernelGGL(k_plan_window, dim3((unsigned)S), dim3(256), 0, st, a);
+  WindowArgs wa{p->d_q, p->d_set_ctx, p->d_set_off, gamma, p->d_window};
+  hipLaunchKernelGGL(k_plan_window, dim3((unsigned)S), dim3(256), 0, st, wa);
   HIPCHK(p, hipGetLastError());
-  if (B > 0) {
-    const unsigned nb = (unsigned)((B + 255) / 256);
-    hipLaunchKernelGGL(k_plan_keys, dim3(nb), dim3(256), 0, st, a);
-    HIPCHK(p, hipGetLastError());
-    size_t t2 = p->cap_tmp;
-    HIPCHK(p, rocprim::radix_sort_pairs(p->d_tmp, t2, p->d_keys, p->d_keys + B, p->d_vals, p->d_vals + B,
-                                        (size_t)B, 0u, end_bit, st));
-    hipLaunchKernelGGL(k_plan_finish, dim3(nb), dim3(256), 0, st, a);
-    HIPCHK(p, hipGetLastError());
-  } else {
-    HIPCHK(p, hipMemsetAsync(p->d_bucket_off, 0, (nbk + 1) * sizeof(int), st));
-  }
-  return LOMPC_OK;
-}
-
-static int take_events(std::vector<hipEvent_t>& pool, hipEvent_t* e0, hipEvent_t* e1) {
-  for (hipEvent_t* e : {e0, e1}) {
-    if (!pool.empty()) {
-      *e = pool.back();
-      pool.pop_back();
-    } else if (hipEventCreateWithFlags(e, hipEventDisableSystemFence) != hipSuccess) {
-      return LOMPC_ERR_HIP;
-    }
-  }
   return LOMPC_OK;
 }
 
@@ -929,64 +949,101 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
                    int8_t* status, double* set_sum_w, double* set_stats, hipStream_t st, lompc_ctx* prof_ctx) {
   if (!lmbd || !lmbd_r) return fail_arg(p, "run: lmbd and lmbd_r required");
   const int N = p->N;
-  const int64_t nbk = p->S * (p->G + 1);
-  SolveArgs a{};
-  a.S = (int)p->S;
-  a.G = p->G;
-  a.flags = p->flags;
-  a.want_err = 1;
-  a.N = N;
-  a.B = p->B;
-  a.qd = p->d_q;
-  a.set_ctx = p->d_set_ctx;
-  a.window = p->d_window;
-  a.bucket_off = p->d_bucket_off;
-  a.gs = p->d_gs;
-  a.perm = p->d_perm;
-  a.lmbd = lmbd;
-  a.lmbd_r = lmbd_r;
-  a.w_ref = p->w_ref;
-  a.ws = (p->flags & LOMPC_PLAN_WARM_START) ? p->d_ws : nullptr;
-  a.w = w;
-  a.cost = cost;
-  a.w0 = w0;
-  a.status = status;
-  a.partial = p->d_partial;
-  a.errflag = p->d_errflag;
-  a.w_rsrc_ok = (p->B * (int64_t)N * 8) < (1ll << 31) ? 1 : 0;
-  // the in-kernel per-set reduction (last-arriving workgroup) measured 4-5 us slower on the
-  // config-3 step than k_reduce (rejected designs): diagnostics only
-  static const bool fused = getenv("LOMPC_REDUCE_FUSED") != nullptr;
-  const bool separate = !fused;
-  a.arrive = separate ? nullptr : p->d_arrive;
-  a.set_off = p->d_set_off;
-  a.set_sum_w = set_sum_w;
-  a.set_stats = set_stats;
-  a.stats = p->d_stats;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  const bool prof = p->prof || (prof_ctx && prof_ctx->prof);
-  if (prof) {
-    std::vector<hipEvent_t>& pool = p->prof ? p->prof_pool : prof_ctx->prof_pool;
-    if (take_events(pool, &e0, &e1)) return fail_arg(p, "profiling events");
-  }
-  hipExtLaunchKernelGGL((k_solve<LQ_SOLVE_WAVES, LQ_SOLVE_PATHS>), dim3((unsigned)nbk), dim3(64 * LQ_SOLVE_WAVES), 0,
-                        st, e0, e1, 0, a);
+  PathArgs pa{};
+  pa.S = (int)p->S;
+  pa.G = p->G;
+  pa.N = N;
+  pa.flags = p->flags;
+  pa.qd = p->d_q;
+  pa.set_ctx = p->d_set_ctx;
+  pa.window = p->d_window;
+  pa.lmbd = lmbd;
+  pa.lmbd_r = lmbd_r;
+  pa.w_ref = p->w_ref;
+  pa.ws = (p->flags & LOMPC_PLAN_WARM_START) ? p->d_ws : nullptr;
+  pa.t_cnt = p->t_cnt;
+  pa.t_base = p->t_base;
+  pa.t_lo = p->t_lo;
+  pa.t_sl = p->t_sl;
+  pa.t_np = p->t_np;
+  pa.t_ge = p->t_ge;
+  pa.t_cf = p->t_cf;
+  pa.t_ab = p->t_ab;
+  pa.errflag = p->d_errflag;
+  hipLaunchKernelGGL(k_path, dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, pa);
   HIPCHK(p, hipGetLastError());
-  if (prof) {
-    std::vector<hipEvent_t>& ev = p->prof ? p->prof_ev : prof_ctx->prof_ev;
-    ev.push_back(e0);
-    ev.push_back(e1);
+  if (p->nblk > 0) {
+    EvalArgs a{};
+    a.S = (int)p->S;
+    a.G = p->G;
+    a.N = N;
+    a.want_err = 1;
+    a.qd = p->d_q;
+    a.set_ctx = p->d_set_ctx;
+    a.blk = p->d_blk;
+    a.set_off = p->d_set_off;
+    a.window = p->d_window;
+    a.gamma = p->gamma;
+    a.lmbd = lmbd;
+    a.lmbd_r = lmbd_r;
+    a.w_ref = p->w_ref;
+    a.t_cnt = p->t_cnt;
+    a.t_base = p->t_base;
+    a.t_lo = p->t_lo;
+    a.t_sl = p->t_sl;
+    a.t_np = p->t_np;
+    a.t_ge = p->t_ge;
+    a.t_cf = p->t_cf;
+    a.t_ab = p->t_ab;
+    a.w = w;
+    a.cost = cost;
+    a.w0 = w0;
+    a.status = status;
+    a.partial = p->d_partial;
+    a.fail_cnt = p->d_fail_cnt;
+    a.fail_idx = p->d_fail_idx;
+    a.w_rsrc_ok = (p->B * (int64_t)N * 8) < (1ll << 31) ? 1 : 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool prof = p->prof || (prof_ctx && prof_ctx->prof);
+    if (prof && take_events(p->prof ? p->prof_pool : prof_ctx->prof_pool, &e0, &e1))
+      return fail_arg(p, "profiling events");
+    // LDS: up to LQ_PIECE_CAP pieces of one set (N doubles2 + 8 + 1 doubles each) + the cells
+    a.cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
+    const size_t lds = (size_t)a.cap * (N * sizeof(double2) + 9 * sizeof(double)) + (size_t)p->G * (sizeof(int2) + sizeof(double));
+    hipExtLaunchKernelGGL(k_eval, dim3((unsigned)p->nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, a);
+    HIPCHK(p, hipGetLastError());
+    if (prof) {
+      std::vector<hipEvent_t>& ev = p->prof ? p->prof_ev : prof_ctx->prof_ev;
+      ev.push_back(e0);
+      ev.push_back(e1);
+    }
   }
-  if (!separate) return LOMPC_OK;
-  ReduceArgs r{};
-  r.G = p->G;
+  FinalArgs r{};
   r.N = N;
+  r.G = p->G;
+  r.want_err = 1;
+  r.t_np = p->t_np;
+  r.qd = p->d_q;
+  r.set_ctx = p->d_set_ctx;
+  r.blk_prefix = p->d_blk_prefix;
   r.set_off = p->d_set_off;
+  r.window = p->d_window;
+  r.gamma = p->gamma;
+  r.lmbd = lmbd;
+  r.lmbd_r = lmbd_r;
+  r.w_ref = p->w_ref;
+  r.t_sl = p->t_sl;
+  r.fail_cnt = p->d_fail_cnt;
+  r.fail_idx = p->d_fail_idx;
   r.partial = p->d_partial;
+  r.w = w;
+  r.cost = cost;
+  r.w0 = w0;
+  r.status = status;
   r.set_sum_w = set_sum_w;
   r.set_stats = set_stats;
   r.stats = p->d_stats;
-  hipLaunchKernelGGL(k_reduce, dim3((unsigned)p->S), dim3(256), 0, st, r);
+  hipLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, r);
   HIPCHK(p, hipGetLastError());
   return LOMPC_OK;
 }
@@ -995,29 +1052,17 @@ void lq_plan_free(lompc_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
   (void)hipDeviceSynchronize();
-  void* ptrs[] = {p->d_q, p->d_stats_own, p->d_set_ctx, p->d_set_off, p->d_window, p->d_keys, p->d_vals,
-                  p->d_bucket_off, p->d_gs, p->d_partial, p->d_ws, p->d_tmp, p->d_errflag, p->d_arrive};
+  void* ptrs[] = {p->d_q,     p->d_stats_own, p->d_set_ctx, p->d_set_off, p->d_blk_prefix, p->d_window,
+                  p->d_blk, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
+                  p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag, p->t_base, p->t_np,
+                  p->d_fail_cnt, p->d_fail_idx};
   for (void* x : ptrs)
     if (x) (void)hipFree(x);
-  if (p->h_off) (void)hipHostFree(p->h_off);
+  if (p->h_buf) (void)hipHostFree(p->h_buf);
   if (p->ev_stage) (void)hipEventDestroy(p->ev_stage);
   for (hipEvent_t e : p->prof_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : p->prof_pool) (void)hipEventDestroy(e);
   delete p;
-}
-
-static int plan_events_read(std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& pool, double& ms_acc,
-                            int64_t& n_acc) {
-  for (size_t k = 0; k + 1 < ev.size(); k += 2) {
-    if (hipEventSynchronize(ev[k + 1]) != hipSuccess) return LOMPC_ERR_HIP;
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, ev[k], ev[k + 1]) != hipSuccess) return LOMPC_ERR_HIP;
-    ms_acc += ms;
-    n_acc += 1;
-  }
-  pool.insert(pool.end(), ev.begin(), ev.end());
-  ev.clear();
-  return LOMPC_OK;
 }
 
 extern "C" {

@@ -81,6 +81,11 @@ __device__ __forceinline__ double* lq_tab() {
   __shared__ __attribute__((aligned(16))) double tab[LQ_NSTATE * 4];
   return tab;
 }
+// fp32 copy of the box table (the fp32 working-set search of lompc_wave.hpp)
+__device__ __forceinline__ float* lq_tabf() {
+  __shared__ __attribute__((aligned(16))) float tabf[LQ_NSTATE * 4];
+  return tabf;
+}
 // Every kernel calls this (all threads, before anything else).
 __device__ __forceinline__ void lq_tab_init(const QPConst& q) {
   double* tb = lq_tab();
@@ -103,6 +108,11 @@ __device__ __forceinline__ void lq_tab_init(const QPConst& q) {
     tb[4 * s + 1] = hi;
     tb[4 * s + 2] = slo;
     tb[4 * s + 3] = shi;
+    float* tf = lq_tabf();
+    tf[4 * s + 0] = (float)lo;
+    tf[4 * s + 1] = (float)hi;
+    tf[4 * s + 2] = (float)slo;
+    tf[4 * s + 3] = (float)shi;
   }
   __syncthreads();
 }
@@ -110,6 +120,14 @@ __device__ __forceinline__ Box lq_box(int s) {
   const double2* tb = reinterpret_cast<const double2*>(lq_tab());
   const double2 x = tb[2 * s], y = tb[2 * s + 1];
   return {x.x, x.y, y.x, y.y};
+}
+
+struct BoxF {
+  float lo, hi, slo, shi;
+};
+__device__ __forceinline__ BoxF lq_boxf(int s) {
+  const float4 x = reinterpret_cast<const float4*>(lq_tabf())[s];
+  return {x.x, x.y, x.z, x.w};
 }
 
 // Active-set move of one coordinate from (w, r): s -> s+1 / s-1 / s.

@@ -391,9 +391,140 @@ __device__ __forceinline__ double wave_kkt_point(const QPConst& q, const WaveSet
   return wave_max(res, N);
 }
 
-// Exact certified solve of one QP by the whole wave, PDAS from s, primal active set if needed.
+// ---- fp32 working-set search -------------------------------------------------
+// The PDAS iterations that only move the working set toward the optimum's run in fp32: one
+// DPP move per value instead of two, v_rcp_f32 without Newton steps.  Their result is only
+// a starting working set for the fp64 PDAS + KKT certificate below, so fp32 rounding can
+// cost iterations there, never accuracy.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dppf(float old, float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                               __builtin_bit_cast(int, x), CTRL, ROW_MASK, 0xf,
+                                                               false));
+}
+struct MobF {
+  float a, b, c, d;
+  __device__ __forceinline__ static MobF identity() { return {1.f, 0.f, 0.f, 1.f}; }
+  __device__ __forceinline__ static MobF combine(const MobF& L, const MobF& R) {
+    return {fmaf(R.a, L.a, R.b * L.c), fmaf(R.a, L.b, R.b * L.d), fmaf(R.c, L.a, R.d * L.c),
+            fmaf(R.c, L.b, R.d * L.d)};
+  }
+  template <int CTRL, int ROW_MASK>
+  __device__ __forceinline__ MobF from() const {
+    return {dppf<CTRL, ROW_MASK>(1.f, a), dppf<CTRL, ROW_MASK>(0.f, b), dppf<CTRL, ROW_MASK>(0.f, c),
+            dppf<CTRL, ROW_MASK>(1.f, d)};
+  }
+};
+struct AffF {
+  float A, B;
+  __device__ __forceinline__ static AffF identity() { return {1.f, 0.f}; }
+  __device__ __forceinline__ static AffF combine(const AffF& L, const AffF& R) { return {R.A * L.A, fmaf(R.A, L.B, R.B)}; }
+  template <int CTRL, int ROW_MASK>
+  __device__ __forceinline__ AffF from() const {
+    return {dppf<CTRL, ROW_MASK>(1.f, A), dppf<CTRL, ROW_MASK>(0.f, B)};
+  }
+};
+__device__ __forceinline__ float shr1f(float old, float x) { return dppf<0x138, 0xf>(old, x); }
+__device__ __forceinline__ float bpermf(int src_lane, float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_lane << 2, __builtin_bit_cast(int, x)));
+}
+
+// solve_stage<1> in fp32 (same recursions, see the file header)
+__device__ __forceinline__ void solve_stage_f32(const QPConst& q, const WaveSet& ws, float gamma, int s_nat,
+                                                float& w_out, float& r_out) {
+  const float c = (float)q.c;
+  const int N = ws.N;
+  const int lane = ws.lane;
+  const bool act = lane < N;
+  const int s_rev = bperm_i(ws.rsrc, s_nat);
+  const BoxF br = lq_boxf(act ? s_rev : 0);
+  const float d_rev = (float)ws.d_rev;
+  const bool fr = act && (s_rev & 1);
+  MobF f = MobF::identity();
+  if (fr) {
+    const float u = __builtin_amdgcn_rcpf(c + d_rev);
+    f = {d_rev * u, d_rev * c * u, u, 1.f};
+  } else if (act) {
+    f = {1.f, c, 0.f, 1.f};
+  }
+  const MobF T = wave_scan(f, N);
+  const float P_here = T.b * __builtin_amdgcn_rcpf(T.d);
+  const float P_next = shr1f(0.f, P_here);
+  const float Q = c + P_next;
+  const float iv = __builtin_amdgcn_rcpf(Q + d_rev);
+  const float et = (float)ws.e_rev + br.slo;
+  AffF g = AffF::identity();
+  if (fr) {
+    g.A = d_rev * iv;
+    g.B = -(c * gamma * d_rev + et * Q) * iv;
+  } else if (act) {
+    g.B = fmaf(Q, br.lo, -c * gamma);
+  }
+  const AffF Gp = wave_scan(g, N);
+  const float p_next = shr1f(0.f, Gp.B);
+  const float Kr = fr ? -Q * iv : 0.f;
+  const float kr = fr ? -(p_next - c * gamma + et) * iv : br.lo;
+  const float K = bpermf(ws.rsrc, Kr);
+  const float Pn = bpermf(ws.rsrc, P_next);
+  const float kk = bpermf(ws.rsrc, kr);
+  const float pn = bpermf(ws.rsrc, p_next);
+  AffF h = AffF::identity();
+  if (act) {
+    h.A = 1.f + K;
+    h.B = kk;
+  }
+  const AffF Y = wave_scan(h, N);
+  const float yp = shr1f(0.f, Y.B);
+  w_out = fmaf(K, yp, kk);
+  r_out = fmaf(c + Pn, Y.B, pn) + fmaf((float)ws.d_nat, w_out, (float)ws.e_nat - c * gamma);
+}
+
+// fp32 PDAS on the working set s (jump moves first, as wave_pdas), relative tolerances at fp32
+// resolution.  Returns with s at the fixed point, or after max_it iterations.
+__device__ __forceinline__ void wave_pdas_f32(const QPConst& q, const WaveSet& ws, double gamma, int& s,
+                                              int max_it) {
+  const float gf = (float)gamma;
+  const float ktol = (float)(1e-6 * q.w_max), stol = (float)(1e-6 * q.scale);
+  for (int it = 0; it < max_it; ++it) {
+    float w, r;
+    solve_stage_f32(q, ws, gf, s, w, r);
+    int ns = s;
+    if (ws.lane < ws.N) {
+      const BoxF bx = lq_boxf(s);
+      const float v = -r;
+      const bool freec = (s & 1) != 0;
+      const bool up = freec ? (w > bx.hi + ktol) : (v > bx.shi + stol);
+      const bool dn = freec ? (w < bx.lo - ktol) : (v < bx.slo - stol);
+      if (freec && it < LQ_JUMP_IT && (up || dn)) {  // jump to the knot bounding w's segment
+        if (!(w > (float)q.knots[0])) {
+          ns = 0;
+        } else if (!(w < (float)q.w_max)) {
+          ns = 2 * q.m;
+        } else {
+          int seg = 0;
+#pragma unroll
+          for (int k = 1; k < LQ_MAXSEG; ++k) seg += (k < q.m && w > (float)q.knots[k]) ? 1 : 0;
+          ns = up ? 2 * seg : 2 * seg + 2;
+        }
+      } else {
+        ns = s + (up ? 1 : 0) - (dn ? 1 : 0);
+      }
+    }
+    const bool changed = __any(ns != s);
+    s = ns;
+    if (!changed) return;
+  }
+}
+
+#ifndef LQ_F32_IT
+#define LQ_F32_IT 24  // fp32 working-set iterations before the fp64 PDAS (0 = fp64 only)
+#endif
+
+// Exact certified solve of one QP by the whole wave: fp32 working-set search, fp64 PDAS from
+// its result, primal active set if needed; KKT-certified in fp64.
 __device__ __forceinline__ bool wave_solve(const QPConst& q, const WaveSet& ws, double gamma, int& s, double& w,
                                            double& r, int* nit = nullptr) {
+  if (LQ_F32_IT > 0) wave_pdas_f32(q, ws, gamma, s, LQ_F32_IT);
   bool ok = wave_pdas(q, ws, gamma, s, w, r, min(4 * ws.N + 8, LQ_PDAS_CAP), nit);
   if (ok) ok = wave_kkt(q, ws, s, w, r) <= q.tol_cert;
   if (!ok) {

@@ -324,9 +324,10 @@ class BatchPlan:
     ``LoMPC`` or a list of them (EV types of the same horizon and device); their parameter
     sets are stacked in list order (``sets_per_ctx`` gives how many each owns) and every
     ``run`` is ONE fused launch over all of them plus the per-set reduction.
-    At construction the batch is validated, grouped by gamma cell on the device (the plan
-    keeps its own copy of gamma: a plan is built per price loop / time step, where
-    gamma_i = y_max - y0_i is fixed, price_solver.py:66-77) and the outputs are allocated.
+    At construction the batch is validated, each set's gamma window is measured on the device
+    (a plan is built per price loop / time step, where gamma_i = y_max - y0_i is fixed,
+    price_solver.py:66-77; gamma is read at every run, and values moved outside the window
+    later are still solved exactly, by the individual re-solve) and the outputs are allocated.
     ``run(lmbd, lmbd_r)`` then issues one ``lompc_plan_run`` with cached pointers; lmbd:
     contiguous fp64 device tensor (S, 3N), lmbd_r (S,) on the same device (or raw device
     pointers).  No synchronisation; ``check()`` synchronises and raises on failures.
@@ -457,7 +458,7 @@ class BatchPlan:
         return rep.value, fail.value, inv.value
 
     def profile(self, enable: bool | None = None, read: bool = False, reset: bool = False):
-        """HIP-event timing of the fused solve kernel (k_solve; DIRECT: k_direct)."""
+        """HIP-event timing of the per-EV evaluation kernel (k_eval; DIRECT: k_direct)."""
         if self.direct:
             return self.lompc.profile(enable=enable, read=read, reset=reset)
         if enable is not None:

@@ -171,12 +171,12 @@ typedef struct lompc_plan lompc_plan;
 /* Build a plan over B EVs grouped by set (S = sum of sets_per_ctx sets):
  *   ctxs         host [n_ctx]   contexts (same N and device), n_ctx <= LOMPC_PLAN_MAX_CTX
  *   sets_per_ctx host [n_ctx]   parameter sets of each context
- *   gamma        dev  [B]       gamma_i = y_max - y0_i; COPIED (the plan keeps its own grouped
- *                               copy: later changes to the caller's buffer are not seen)
+ *   gamma        dev  [B]       gamma_i = y_max - y0_i, read at every run; each set's gamma
+ *                               window is measured here (later values outside it are still
+ *                               solved exactly, by the individual re-solve: status REPAIRED)
  *   set_offsets  host [S+1]     EVs of set s are [set_offsets[s], set_offsets[s+1])
  *   w_ref        dev  [S, N]    reference w of the A_bar error, read at every run, or NULL
- * The grouping (per-set gamma window, gamma cells, a stable device radix sort) runs
- * asynchronously on ``stream``. */
+ * The window measurement runs asynchronously on ``stream``. */
 int lompc_plan_create(int n_ctx, lompc_ctx* const* ctxs, const int64_t* sets_per_ctx,
                       int64_t B, const double* gamma, const int64_t* set_offsets,
                       const double* w_ref, int flags, void* stream, lompc_plan** out);
@@ -186,8 +186,8 @@ int lompc_plan_create(int n_ctx, lompc_ctx* const* ctxs, const int64_t* sets_per
  * the caller's EV order (each may be NULL):
  *   lmbd dev [S, 3N], lmbd_r dev [S]; w dev [B, N]; cost, w0 dev [B]; status dev [B];
  *   set_sum_w dev [S, N]; set_stats dev [S, LOMPC_SET_STATS]
- * Two launches on ``stream`` (the fused per-cell solve, then the per-set reduction); no
- * synchronisation.  A plan is not re-entrant: runs are stream-ordered. */
+ * Three launches on ``stream`` (per-cell solution paths, per-EV evaluation, per-set
+ * reduction); no synchronisation.  A plan is not re-entrant: runs are stream-ordered. */
 int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, double* w,
                    double* cost, double* w0, int8_t* status, double* set_sum_w,
                    double* set_stats, void* stream);
@@ -199,7 +199,7 @@ int lompc_plan_status(lompc_plan* plan, void* stream, int64_t* n_repaired,
 /* Batch size, total parameter sets and gamma cells per set of the plan. */
 int lompc_plan_get_info(const lompc_plan* plan, int64_t* B, int64_t* S, int* cells);
 
-/* HIP-event timing of the plan's fused solve kernel (as lompc_profile_*). */
+/* HIP-event timing of the plan's per-EV evaluation kernel (as lompc_profile_*). */
 int lompc_plan_profile_enable(lompc_plan* plan, int enable);
 int lompc_plan_profile_read(lompc_plan* plan, double* total_ms, int64_t* launches, int reset);
 

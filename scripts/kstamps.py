@@ -3,8 +3,8 @@
     python scripts/kstamps.py --build     # here: builds lompc_amd/liblompc_amd_stamps.so
     python scripts/kstamps.py [N]         # on the GPU box: bench workload (both EV types, 24 sets)
 
-Per wave (= (set, gamma cell)): setup (lambda loads), exact solve at the cell start (PDAS),
-path tracking, EV phase, epilogue; shader cycles, mean / p90 / max over waves, per EV type.
+Per k_path wave (= (set, gamma cell)): setup (lambda loads), exact solve at the cell start
+(fp32 search + fp64 PDAS), path tracking; shader cycles, mean / p90 / max over waves, per EV type.
 """
 import ctypes
 import os
@@ -47,26 +47,32 @@ plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], w_ref=wr, want_w=outputs =
 for _ in range(5):
     plan.run(lm, lr)
 plan.check()
-G1 = plan.cells + 1
-nb = 2 * P * G1
+G = plan.cells
+nb = 2 * P * G
 buf = np.zeros(nb * 8, dtype=np.int64)
 assert lib.lompc_debug_stamps(buf.ctypes.data, buf.size) == 0
 st = buf.reshape(nb, 8)
-valid = st[:, 7] > 0
-cell = np.arange(nb) % G1
-valid &= cell < G1 - 1
-t = st[:, :6].astype(np.float64)
-names = ["setup", "solve@start", "tracking", "EV phase", "epilogue", "total"]
-d = np.stack([t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2], t[:, 4] - t[:, 3], t[:, 5] - t[:, 4],
-              t[:, 5] - t[:, 0]], 1)
-start0 = t[valid, 0].min()
-print(f"N={N} outputs={outputs} cells={plan.cells}  (shader cycles; s_memtime)")
+t = st[:, :4].astype(np.float64)
+names = ["setup", "solve@start", "tracking", "total"]
+d = np.stack([t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2], t[:, 3] - t[:, 0]], 1)
+print(f"N={N} cells={plan.cells} k_path waves (shader cycles; s_memtime)")
 for k, name in enumerate(("small", "large")):
-    sel = valid & (np.arange(nb) // G1 // P == k)
-    print(f"{name}: waves {sel.sum()}, EVs/wave mean {st[sel, 7].mean():.0f}, pieces mean {st[sel, 6].mean():.2f} "
-          f"max {st[sel, 6].max()}")
+    sel = np.arange(nb) // G // P == k
+    print(f"{name}: waves {sel.sum()}, pieces mean {st[sel, 6].mean():.2f} max {st[sel, 6].max()}")
     for j, nm in enumerate(names):
         x = d[sel, j]
         print(f"   {nm:12s} mean {x.mean():8.0f}  p90 {np.percentile(x, 90):8.0f}  max {x.max():8.0f}")
-    print(f"   wave start offset (vs first wave): mean {(t[sel, 0] - start0).mean():.0f} max {(t[sel, 0] - start0).max():.0f};"
-          f" end max {(t[sel, 5] - start0).max():.0f}")
+
+# k_eval workgroups (stamps at (32768 + b) * 8)
+ev = np.zeros(32768 * 8, dtype=np.int64)
+buf2 = np.zeros(65536 * 8, dtype=np.int64)
+assert lib.lompc_debug_stamps(buf2.ctypes.data, buf2.size) == 0
+e = buf2[32768 * 8:].reshape(32768, 8)[: min(32768, (B + 255) // 256)]
+e = e[e[:, 0] != 0].astype(np.float64)
+names = ["loads+stage", "lookup+outputs", "repairs", "rows", "record"]
+print(f"k_eval workgroups {len(e)} (shader cycles)")
+for j, nm in enumerate(names):
+    x = e[:, j + 1] - e[:, j]
+    print(f"   {nm:15s} mean {x.mean():8.0f}  p90 {np.percentile(x, 90):8.0f}  max {x.max():8.0f}")
+x = e[:, 5] - e[:, 0]
+print(f"   {'total':15s} mean {x.mean():8.0f}  p90 {np.percentile(x, 90):8.0f}  max {x.max():8.0f}")

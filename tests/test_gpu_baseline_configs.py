@@ -103,7 +103,6 @@ def test_config4_workload_and_sharding(gpu):
     rng = np.random.default_rng(4)
     off, g, lm, lr, wr = station_batch(B, N, P, rng)
     plan, out = run_plan(off, g, lm, lr, wr, N, P)
-    assert plan.cells >= 64
     check_all(out, off, g, lm, lr, N, P)
     sw_full = out["set_sum_w"].cpu().numpy()
     st_full = out["set_stats"].cpu().numpy()
@@ -118,7 +117,7 @@ def test_config4_workload_and_sharding(gpu):
         idx, loc = shard_sets(off, rank, world)
         _, o = run_plan(loc, g[idx], lm, lr, wr, N, P)
         dw = (o["w"] - w_full[torch.as_tensor(idx, device="cuda:0")]).abs().max().item()
-        assert dw <= 1e-12, dw  # the shard's own gamma cells: the same certified pieces
+        assert dw <= 1e-12, dw  # the shard's own gamma windows and cells: the same optimum
         sw, st = o["set_sum_w"].cpu().numpy(), o["set_stats"].cpu().numpy()
         if sw_tot is None:
             sw_tot, st_tot = sw.copy(), st.copy()

@@ -1,8 +1,8 @@
-"""GPU tests of the PATH engine behind lompc_plan_* / BatchPlan (plan: per-set gamma window,
-gamma cells, stable device radix sort; run: ONE fused k_solve over (set, cell) waves that
-computes the certified path pieces and writes every EV's outputs, then k_reduce): one call per
-price iteration, repeated runs, several EV types in one plan, ragged / empty / very large sets,
-invalid gamma, warm starts, the individual-repair path.
+"""GPU tests of the PATH engine behind lompc_plan_* / BatchPlan (plan: per-set gamma window and
+cells, the evaluation block map; run: k_path over (set, cell) waves -> certified path pieces,
+k_eval over the EVs in caller order with the set's pieces in LDS, k_reduce): one call per price
+iteration, repeated runs, several EV types in one plan, ragged / empty / very large sets,
+invalid and moved gamma, warm starts, cell counts, the individual-repair path.
 
 Tolerances as in test_gpu_parity.py (|dw| <= 1e-9, cost 1e-9 relative); reductions equal the
 sums of the per-EV outputs to 1e-11 relative (sums of up to 3e5 terms).
@@ -56,7 +56,7 @@ def oracle_check(out, g, lm, lr, off, c, N, rng, k=64):
 
 @pytest.mark.parametrize("ev", ["small", "large"])
 def test_plan_matches_solve_batch_and_oracle(gpu, ev):
-    """Ragged sets: empty, one full block, one partial block, 300k EVs (G = 2048 cells)."""
+    """Ragged sets: empty, one full block, one partial block, 300k EVs."""
     rng = np.random.default_rng(31 + (ev == "large"))
     c = O.small_consts() if ev == "small" else O.large_consts()
     N = 24
@@ -174,15 +174,15 @@ def test_two_ev_types_in_one_plan(gpu, N):
 
 
 @pytest.mark.parametrize("ev", ["small", "large"])
-def test_invalid_gamma_and_snapshot(gpu, ev):
+def test_invalid_gamma_and_moved_gamma(gpu, ev):
     """gamma outside [0, y_max] or NaN: status INVALID, NaN outputs, counted per set, the rest
-    exact; the plan keeps its own copy of gamma (later changes to the caller's buffer unseen)."""
+    exact; gamma moved in place after plan creation outside the set's window: re-solved
+    individually (status REPAIRED) and exact."""
     rng = np.random.default_rng(12 + (ev == "large"))
     c = O.small_consts() if ev == "small" else O.large_consts()
     N = 24
-    sizes = [500, 300]
     off = np.array([0, 500, 800], dtype=np.int64)
-    gn = c.y_max * rng.random(800)
+    gn = 0.3 + 0.2 * c.y_max * rng.random(800)
     bad = [3, 17, 501, 799]
     gn[bad] = [-0.1, np.nan, c.y_max + 1e-9, 5.0]
     g = torch.as_tensor(gn, device="cuda:0")
@@ -206,11 +206,20 @@ def test_invalid_gamma_and_snapshot(gpu, ev):
     for s, idx in ((0, good[good < 500][:50]), (1, good[good >= 500][:50])):
         wo, _, nf = oracle_c.solve_batch(N, c, lm[s].cpu().numpy(), 0.0, gn[idx])
         np.testing.assert_allclose(w[idx], wo, atol=TOL_W)
-    w_before = out["w"].clone()
-    g.fill_(0.0)  # the plan solved its snapshot
+    # move 10 valid EVs of set 0 far outside its window (and fix the invalid ones)
+    g2 = gn.copy()
+    g2[bad] = 0.5 * c.y_max
+    g2[:10] = 0.02 * c.y_max
+    g.copy_(torch.as_tensor(g2, device="cuda:0"))
     out2 = plan.run(lm, lr)
-    torch.cuda.synchronize()
-    assert torch.equal(torch.nan_to_num(out2["w"], nan=-1.0), torch.nan_to_num(w_before, nan=-1.0))
+    rep, fail, inv = plan.check()
+    assert fail == 0 and inv == 0 and rep >= 10
+    st2 = out2["status"].cpu().numpy()
+    assert np.all(st2[:10] == _lib.LOMPC_QP_REPAIRED)
+    w2 = out2["w"].cpu().numpy()
+    for s, idx in ((0, np.arange(0, 60)), (1, np.arange(500, 560))):
+        wo, _, nf = oracle_c.solve_batch(N, c, lm[s].cpu().numpy(), 0.0, g2[idx])
+        np.testing.assert_allclose(w2[idx], wo, atol=TOL_W)
 
 
 @pytest.mark.parametrize("ev", ["small", "large"])
@@ -244,7 +253,7 @@ def test_warm_start_and_cell_counts(gpu, ev, N):
     oracle_check(oc, g, lms[2], lr, off, c, N, rng)
     old = os.environ.get("LOMPC_CELLS")
     try:
-        for G in (16, 512):
+        for G in (1, 16, 512):
             os.environ["LOMPC_CELLS"] = str(G)
             p = BatchPlan(lompc, g, off, **kw)
             assert p.cells == G

@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--outputs", choices=["full", "cost", "set"], default="full",
                     help="diagnostics: full = w + cost + reductions (the metric's workload); cost = no w rows; "
                          "set = reductions only")
+    ap.add_argument("--split-types", action="store_true",
+                    help="path mode: one plan per EV type, each on its own stream (overlapping)")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="diagnostics: no HIP events on the per-EV kernel's dispatches in the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-station", action="store_true", help="skip the BiMPC steps/sec leg")
     ap.add_argument("--station-evs-per-gpu", type=int, default=262144, help="EVs per GPU, half per type")
@@ -106,7 +110,17 @@ def main():
         eng.append(dict(name=name, c=c, lompc=lompc, off=off, gamma=gamma, lm=lm, wr=wr, M=M))
 
     main = torch.cuda.current_stream()
-    if args.mode == "path":
+    if args.mode == "path" and args.split_types:
+        runs = []
+        for e in eng:
+            st = torch.cuda.Stream()
+            st.wait_stream(main)
+            lr = torch.zeros(P, dtype=torch.float64, device=dev)
+            plan = BatchPlan(e["lompc"], e["gamma"], e["off"], w_ref=e["wr"], want_w=args.outputs == "full",
+                             want_cost=args.outputs != "set", want_set=True, stream=st, warm_start=args.warm)
+            runs.append(dict(plan=plan, stream=st, lm_ptr=[e["lm"][k].data_ptr() for k in range(nsteps)],
+                             lr_ptr=lr.data_ptr(), qps=e["M"], keep=(lr,)))
+    elif args.mode == "path":
         # ONE plan over both EV types: their 2P parameter sets stacked (small first), every step
         # is one fused k_solve launch over all (set, gamma cell) waves + one k_reduce
         off = np.concatenate([eng[0]["off"], eng[0]["M"] + eng[1]["off"][1:]])
@@ -132,15 +146,18 @@ def main():
                              lr_ptr=lr.data_ptr(), qps=e["M"], keep=(lr,)))
     torch.cuda.synchronize()
 
+    multi = len(runs) > 1
+
     def step(k):
-        if world > 1:  # the previous step's collective reads the output buffers
+        if world > 1 or multi:  # the previous step's collective reads the output buffers
             for r in runs:
                 r["stream"].wait_stream(main)
         for r in runs:
             r["plan"].run(r["lm_ptr"][k], r["lr_ptr"])
-        if world > 1:
+        if multi:
             for r in runs:
                 main.wait_stream(r["stream"])
+        if world > 1:
             # every set's reductions (both EV types) in ONE collective
             combine_set_results([(r["plan"].out["set_sum_w"], r["plan"].out["set_stats"]) for r in runs])
 
@@ -151,7 +168,7 @@ def main():
         rep, fail, inv = r["plan"].check()
         assert fail == 0 and inv == 0, (fail, inv)
     for r in runs:
-        r["plan"].profile(enable=True)
+        r["plan"].profile(enable=("k_eval",) if not args.no_kernel_events else False)
         r["plan"].profile(read=True, reset=True)
     if world > 1:
         dist.barrier()
@@ -182,7 +199,7 @@ def main():
     avg_launch_s = (k_ms / 1e3) / max(k_n, 1)
     qp_per_launch = k_qps / max(k_n, 1)
     bytes_per_qp = 8 * (N + 2)
-    achieved_gbs = bytes_per_qp * qp_per_launch / avg_launch_s / 1e9
+    achieved_gbs = bytes_per_qp * qp_per_launch / avg_launch_s / 1e9 if k_n else 0.0
 
     total_qp = world * B * args.steps
     value = total_qp / dt

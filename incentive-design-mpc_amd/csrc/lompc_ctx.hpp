@@ -86,6 +86,8 @@ struct lompc_plan {
   int G = 0;                    // gamma cells per set (k_path waves per set)
   int nblk = 0;                 // k_eval workgroups (blocks of one set's EVs)
   int n_cu = 0;
+  int eval_occ = 1;             // k_eval workgroups resident per CU (occupancy query)
+  int64_t eval_occ_key = -1;    // (N, LDS pieces) it was queried for
   int64_t cap_S = 0, cap_blk = 0, cap_cells = 0;
   const double* gamma = nullptr;  // caller's [B] (read at every run)
   const double* w_ref = nullptr;  // caller's [S][N] (read at every run) or null
@@ -116,11 +118,11 @@ struct lompc_plan {
   char* h_buf = nullptr;
   int64_t cap_h = 0;
   hipEvent_t ev_stage = nullptr;
-  // profiling of k_eval
-  bool prof = false;
-  std::vector<hipEvent_t> prof_ev, prof_pool;
-  double prof_ms = 0.0;
-  int64_t prof_n = 0;
+  // HIP-event profiling, per kernel (LOMPC_PLAN_K_*): enabled mask, pairs since the last read
+  int prof = 0;
+  std::vector<hipEvent_t> prof_ev[LOMPC_PLAN_KERNELS], prof_pool;
+  double prof_ms[LOMPC_PLAN_KERNELS] = {0.0, 0.0, 0.0};
+  int64_t prof_n[LOMPC_PLAN_KERNELS] = {0, 0, 0};
   std::string err;
 };
 

@@ -57,7 +57,9 @@ __device__ long long g_stamps[65536 * 8];
 #define LQ_STAMPE(k)
 #endif
 
-#define EVAL_WAVES 16                      // k_eval: waves per workgroup
+#ifndef EVAL_WAVES
+#define EVAL_WAVES 8  // k_eval: waves per workgroup (16: 16.1 us, 8: 14.8 us, 4: 16.2 us at config 3)
+#endif
 #define EVAL_EVS (64 * EVAL_WAVES)         // k_eval: threads per workgroup
 #define EVAL_PASSES 2                      // k_eval: EVs per thread, at most
 #define EVAL_MAXB (EVAL_EVS * EVAL_PASSES)  // k_eval: EVs per workgroup, at most
@@ -85,6 +87,17 @@ __device__ __forceinline__ void st_wt8(double* p, double v) {
 __device__ __forceinline__ double clampw(double x, double wmax) { return fmin(fmax(x, 0.0), wmax); }
 
 // ---------------------------------------------------------------- plan kernel
+// the constants of set s's EV type: the context index made wave-uniform, so every field is a
+// scalar (constant-cache) load instead of a vector load with a full memory round trip
+// (the table is read-only for the whole launch: the constant address space lets the compiler use
+// scalar loads although the kernels store to other global memory)
+typedef const __attribute__((address_space(4))) QPConst QPConstK;
+__device__ __forceinline__ const QPConst& set_consts(const QPConst* qd, const uint8_t* set_ctx, int s) {
+  const int k = __builtin_amdgcn_readfirstlane((int)set_ctx[s]);
+  QPConstK* p = (QPConstK*)(uintptr_t)qd + k;
+  return *(const QPConst*)p;
+}
+
 struct WindowArgs {
   const QPConst* qd;
   const uint8_t* set_ctx;
@@ -98,7 +111,7 @@ struct WindowArgs {
 __global__ __launch_bounds__(256) void k_plan_window(WindowArgs a) {
   __shared__ double smin[256], smax[256];
   const int s = blockIdx.x;
-  const double ym = a.qd[a.set_ctx[s]].y_max;
+  const double ym = set_consts(a.qd, a.set_ctx, s).y_max;
   double lo = INFINITY, hi = -INFINITY;
   for (int64_t i = a.set_off[s] + threadIdx.x; i < a.set_off[s + 1]; i += 256) {
     const double g = a.gamma[i];
@@ -186,7 +199,7 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
   __shared__ double p_ge[LQ_PPL];
   const int blk = (int)blockIdx.x;
   const int G = a.G;
-  const int s = blk / G;
+  const int s = __builtin_amdgcn_readfirstlane(blk / G);
   const int cell = blk - s * G;
   const int lane = (int)threadIdx.x;
   const int N = a.N;
@@ -194,7 +207,7 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
   const double lr = a.lmbd_r[s];
   const double wr_nat = (a.w_ref && lane < N) ? a.w_ref[(size_t)s * N + lane] : 0.0;
   const double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
-  const QPConst& q = a.qd[a.set_ctx[s]];  // uniform: scalar loads, no register copy
+  const QPConst& q = set_consts(a.qd, a.set_ctx, s);  // scalar loads, no register copy
   LQ_STAMP(0);
   lq_tab_init(q);
   lqw::WaveSet ws;
@@ -224,7 +237,13 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
       sl = (lane < N && v >= 0 && v <= 2 * q.m) ? v : sl0;
     }
     double w = 0.0, r = 0.0;
+#ifdef LOMPC_STAMPS
+    int nit = 0;
+    const bool solved = lqw::wave_solve(q, ws, glo, sl, w, r, &nit);
+    if (threadIdx.x == 0 && blockIdx.x < 32768) g_stamps[blockIdx.x * 8 + 4] = nit;
+#else
     const bool solved = lqw::wave_solve(q, ws, glo, sl, w, r);
+#endif
     LQ_STAMP(2);
     if (solved) {
       sl0 = sl;
@@ -235,6 +254,9 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
       const int max_iter = 4 * LQ_PPL + 16;
       const double ee = ws.e_nat;
       for (int it = 0; it < max_iter && npc < LQ_PPL; ++it) {
+#ifdef LOMPC_STAMPS
+        if (threadIdx.x == 0 && blockIdx.x < 32768) g_stamps[blockIdx.x * 8 + 5] = it + 1;
+#endif
         const lqw::StageSol<2> sol = lqw::solve_stage<2>(q, ws, 0.0, sl);
         const double av = sol.w[0], bv = sol.w[1], r0 = sol.r[0], r1 = sol.r[1];
         double gc = INFINITY;
@@ -423,7 +445,7 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
     const int i = start + tid + EVAL_EVS * h;
     gh[h] = i < end ? a.gamma[i] : 0.0;
   }
-  const QPConst& q = a.qd[a.set_ctx[s]];
+  const QPConst& q = set_consts(a.qd, a.set_ctx, s);
   const double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
   const double* __restrict__ L = a.lmbd + (size_t)s * 3 * N;
   const double l0[3] = {L[0], L[N], L[2 * N]};  // price0 (lompc.py:164-170)
@@ -697,7 +719,7 @@ __global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
   }
   __syncthreads();
   if (red[0][N + PX_N_FAILED] > 0.0) {  // block-uniform: individual re-solves pending
-    const QPConst& q = r.qd[r.set_ctx[s]];
+    const QPConst& q = set_consts(r.qd, r.set_ctx, s);
     lq_tab_init(q);
     const double* __restrict__ L = r.lmbd + (size_t)s * 3 * N;
     const double lr = r.lmbd_r[s];
@@ -786,7 +808,7 @@ int pick_cells(int64_t max_set) {
   // per-wave tracking latency against more cold starts; one cell for tiny sets
   if (max_set <= 64) return 1;
   if (max_set <= 1024) return 8;
-  return 32;
+  return 16;  // measured flat over 12..24 at config 3 (42.1-42.4 us/step), 8 and 48+ slower
 }
 
 int take_events(std::vector<hipEvent_t>& pool, hipEvent_t* e0, hipEvent_t* e1) {
@@ -817,6 +839,22 @@ int plan_events_read(std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& pool,
 }  // namespace
 
 // ============================================================== host
+// k_eval's dynamic LDS: up to cap pieces of one set (N double2 + 8 + 1 doubles each) + the cells
+size_t eval_lds(int N, int G, int cap) {
+  return (size_t)cap * (N * sizeof(double2) + 9 * sizeof(double)) + (size_t)G * (sizeof(int2) + sizeof(double));
+}
+
+// events of one profiled dispatch (null events when kernel k is not profiled)
+int plan_prof_begin(lompc_plan* p, int k, hipEvent_t* e0, hipEvent_t* e1) {
+  *e0 = *e1 = nullptr;
+  return (p->prof >> k) & 1 ? take_events(p->prof_pool, e0, e1) : LOMPC_OK;
+}
+void plan_prof_end(lompc_plan* p, int k, hipEvent_t e0, hipEvent_t e1) {
+  if (!e0) return;
+  p->prof_ev[k].push_back(e0);
+  p->prof_ev[k].push_back(e1);
+}
+
 int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64_t* sets_per_ctx, int64_t B,
                     const double* gamma, const int64_t* set_offsets, const double* w_ref, int flags,
                     hipStream_t st) {
@@ -852,8 +890,16 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     HIPCHK(p, hipDeviceGetAttribute(&p->n_cu, hipDeviceAttributeMultiprocessorCount, ctxs[0]->device));
     if (p->n_cu < 1) p->n_cu = 1;
   }
-  const int64_t rounds = std::max<int64_t>(1, (10 * B + 9ll * p->n_cu * EVAL_MAXB - 1) / (9ll * p->n_cu * EVAL_MAXB));
-  const int64_t target = rounds * p->n_cu;
+  const int cap = std::min(LQ_PIECE_CAP, G * LQ_PPL);
+  if (p->eval_occ_key != (int64_t)N * 4096 + cap) {  // k_eval workgroups resident per CU
+    int occ = 0;
+    HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_eval, EVAL_EVS, eval_lds(N, G, cap)));
+    p->eval_occ = std::max(occ, 1);
+    p->eval_occ_key = (int64_t)N * 4096 + cap;
+  }
+  const int64_t slots = (int64_t)p->n_cu * p->eval_occ;
+  const int64_t rounds = std::max<int64_t>(1, (10 * B + 9ll * slots * EVAL_MAXB - 1) / (9ll * slots * EVAL_MAXB));
+  const int64_t target = rounds * slots;
   auto blocks_of = [&](int64_t m) -> int64_t {
     if (m <= 0) return 0;
     const int64_t lo = (m + EVAL_MAXB - 1) / EVAL_MAXB, hi = (m + 255) / 256;
@@ -970,8 +1016,13 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   pa.t_cf = p->t_cf;
   pa.t_ab = p->t_ab;
   pa.errflag = p->d_errflag;
-  hipLaunchKernelGGL(k_path, dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, pa);
-  HIPCHK(p, hipGetLastError());
+  {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
+    hipExtLaunchKernelGGL(k_path, dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa);
+    HIPCHK(p, hipGetLastError());
+    plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
+  }
   if (p->nblk > 0) {
     EvalArgs a{};
     a.S = (int)p->S;
@@ -1004,18 +1055,18 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
     a.fail_idx = p->d_fail_idx;
     a.w_rsrc_ok = (p->B * (int64_t)N * 8) < (1ll << 31) ? 1 : 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    const bool prof = p->prof || (prof_ctx && prof_ctx->prof);
-    if (prof && take_events(p->prof ? p->prof_pool : prof_ctx->prof_pool, &e0, &e1))
+    const bool cprof = prof_ctx && prof_ctx->prof;  // lompc_solve_batch: the context's k_eval timing
+    if (cprof ? take_events(prof_ctx->prof_pool, &e0, &e1) : plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1))
       return fail_arg(p, "profiling events");
-    // LDS: up to LQ_PIECE_CAP pieces of one set (N doubles2 + 8 + 1 doubles each) + the cells
     a.cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
-    const size_t lds = (size_t)a.cap * (N * sizeof(double2) + 9 * sizeof(double)) + (size_t)p->G * (sizeof(int2) + sizeof(double));
+    const size_t lds = eval_lds(N, p->G, a.cap);
     hipExtLaunchKernelGGL(k_eval, dim3((unsigned)p->nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, a);
     HIPCHK(p, hipGetLastError());
-    if (prof) {
-      std::vector<hipEvent_t>& ev = p->prof ? p->prof_ev : prof_ctx->prof_ev;
-      ev.push_back(e0);
-      ev.push_back(e1);
+    if (cprof) {
+      prof_ctx->prof_ev.push_back(e0);
+      prof_ctx->prof_ev.push_back(e1);
+    } else {
+      plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
     }
   }
   FinalArgs r{};
@@ -1043,8 +1094,11 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   r.set_sum_w = set_sum_w;
   r.set_stats = set_stats;
   r.stats = p->d_stats;
-  hipLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, r);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (plan_prof_begin(p, LOMPC_PLAN_K_FINAL, &e0, &e1)) return fail_arg(p, "profiling events");
+  hipExtLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, e0, e1, 0, r);
   HIPCHK(p, hipGetLastError());
+  plan_prof_end(p, LOMPC_PLAN_K_FINAL, e0, e1);
   return LOMPC_OK;
 }
 
@@ -1060,7 +1114,8 @@ void lq_plan_free(lompc_plan* p) {
     if (x) (void)hipFree(x);
   if (p->h_buf) (void)hipHostFree(p->h_buf);
   if (p->ev_stage) (void)hipEventDestroy(p->ev_stage);
-  for (hipEvent_t e : p->prof_ev) (void)hipEventDestroy(e);
+  for (auto& v : p->prof_ev)
+    for (hipEvent_t e : v) (void)hipEventDestroy(e);
   for (hipEvent_t e : p->prof_pool) (void)hipEventDestroy(e);
   delete p;
 }
@@ -1133,10 +1188,10 @@ int lompc_plan_get_info(const lompc_plan* p, int64_t* B, int64_t* S, int* cells)
   return LOMPC_OK;
 }
 
-int lompc_plan_profile_enable(lompc_plan* p, int enable) {
+int lompc_plan_profile_enable(lompc_plan* p, int kernel_mask) {
   if (!p) return LOMPC_ERR_INVALID_ARG;
   HIPCHK(p, hipSetDevice(p->device));
-  p->prof = enable != 0;
+  p->prof = kernel_mask & ((1 << LOMPC_PLAN_KERNELS) - 1);
   while (p->prof && p->prof_pool.size() < 512) {
     hipEvent_t e;
     HIPCHK(p, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
@@ -1145,15 +1200,17 @@ int lompc_plan_profile_enable(lompc_plan* p, int enable) {
   return LOMPC_OK;
 }
 
-int lompc_plan_profile_read(lompc_plan* p, double* total_ms, int64_t* launches, int reset) {
+int lompc_plan_profile_read(lompc_plan* p, int kernel, double* total_ms, int64_t* launches, int reset) {
   if (!p) return LOMPC_ERR_INVALID_ARG;
+  if (kernel < 0 || kernel >= LOMPC_PLAN_KERNELS) return fail_arg(p, "profile_read: kernel out of range");
   HIPCHK(p, hipSetDevice(p->device));
-  if (plan_events_read(p->prof_ev, p->prof_pool, p->prof_ms, p->prof_n)) return LOMPC_ERR_HIP;
-  if (total_ms) *total_ms = p->prof_ms;
-  if (launches) *launches = p->prof_n;
+  for (int k = 0; k < LOMPC_PLAN_KERNELS; ++k)
+    if (plan_events_read(p->prof_ev[k], p->prof_pool, p->prof_ms[k], p->prof_n[k])) return LOMPC_ERR_HIP;
+  if (total_ms) *total_ms = p->prof_ms[kernel];
+  if (launches) *launches = p->prof_n[kernel];
   if (reset) {
-    p->prof_ms = 0.0;
-    p->prof_n = 0;
+    p->prof_ms[kernel] = 0.0;
+    p->prof_n[kernel] = 0;
   }
   return LOMPC_OK;
 }

@@ -480,9 +480,9 @@ __device__ __forceinline__ void solve_stage_f32(const QPConst& q, const WaveSet&
 }
 
 // fp32 PDAS on the working set s (jump moves first, as wave_pdas), relative tolerances at fp32
-// resolution.  Returns with s at the fixed point, or after max_it iterations.
-__device__ __forceinline__ void wave_pdas_f32(const QPConst& q, const WaveSet& ws, double gamma, int& s,
-                                              int max_it) {
+// resolution.  Returns with s at the fixed point, or after max_it iterations; the iterations run.
+__device__ __forceinline__ int wave_pdas_f32(const QPConst& q, const WaveSet& ws, double gamma, int& s,
+                                             int max_it) {
   const float gf = (float)gamma;
   const float ktol = (float)(1e-6 * q.w_max), stol = (float)(1e-6 * q.scale);
   for (int it = 0; it < max_it; ++it) {
@@ -512,8 +512,9 @@ __device__ __forceinline__ void wave_pdas_f32(const QPConst& q, const WaveSet& w
     }
     const bool changed = __any(ns != s);
     s = ns;
-    if (!changed) return;
+    if (!changed) return it + 1;
   }
+  return max_it;
 }
 
 #ifndef LQ_F32_IT
@@ -521,13 +522,17 @@ __device__ __forceinline__ void wave_pdas_f32(const QPConst& q, const WaveSet& w
 #endif
 
 // Exact certified solve of one QP by the whole wave: fp32 working-set search, fp64 PDAS from
-// its result, primal active set if needed; KKT-certified in fp64.
+// its result, primal active set if needed; KKT-certified in fp64.  nit (diagnostics): fp64 PDAS
+// iterations + 256 x fp32 iterations + 65536 if the primal active set ran.
 __device__ __forceinline__ bool wave_solve(const QPConst& q, const WaveSet& ws, double gamma, int& s, double& w,
                                            double& r, int* nit = nullptr) {
-  if (LQ_F32_IT > 0) wave_pdas_f32(q, ws, gamma, s, LQ_F32_IT);
-  bool ok = wave_pdas(q, ws, gamma, s, w, r, min(4 * ws.N + 8, LQ_PDAS_CAP), nit);
+  int n32 = 0, n64 = 0;
+  if (LQ_F32_IT > 0) n32 = wave_pdas_f32(q, ws, gamma, s, LQ_F32_IT);
+  bool ok = wave_pdas(q, ws, gamma, s, w, r, min(4 * ws.N + 8, LQ_PDAS_CAP), &n64);
+  if (nit) *nit = n64 + 256 * n32;
   if (ok) ok = wave_kkt(q, ws, s, w, r) <= q.tol_cert;
   if (!ok) {
+    if (nit) *nit += 65536;
     ok = wave_primal_as(q, ws, gamma, s, w, r, 16 * ws.N + 32, true);
     if (ok) ok = wave_kkt(q, ws, s, w, r) <= q.tol_cert;
   }

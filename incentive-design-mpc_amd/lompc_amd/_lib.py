@@ -29,6 +29,10 @@ LOMPC_EV_LARGE = 1
 LOMPC_MODE_PATH = 0
 LOMPC_MODE_DIRECT = 1
 LOMPC_PLAN_MAX_CTX = 4
+LOMPC_PLAN_K_PATH = 0
+LOMPC_PLAN_K_EVAL = 1
+LOMPC_PLAN_K_FINAL = 2
+LOMPC_PLAN_KERNELS = 3
 LOMPC_PLAN_WARM_START = 1
 LOMPC_PLAN_DIAG_REPAIR = 2
 
@@ -76,7 +80,7 @@ SIGNATURES = [
     ("lompc_plan_status", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_get_info", _I, [_P, _P, _P, _P]),
     ("lompc_plan_profile_enable", _I, [_P, _I]),
-    ("lompc_plan_profile_read", _I, [_P, _P, _P, _I]),
+    ("lompc_plan_profile_read", _I, [_P, _I, _P, _P, _I]),
     ("lompc_plan_last_error", ctypes.c_char_p, [_P]),
     ("lompc_plan_destroy", _I, [_P]),
 ]

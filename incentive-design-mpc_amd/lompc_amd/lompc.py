@@ -457,15 +457,23 @@ class BatchPlan:
             raise SolverError(f"{fail.value} LoMPC QPs without a certified optimum")
         return rep.value, fail.value, inv.value
 
-    def profile(self, enable: bool | None = None, read: bool = False, reset: bool = False):
-        """HIP-event timing of the per-EV evaluation kernel (k_eval; DIRECT: k_direct)."""
+    KERNELS = ("k_path", "k_eval", "k_finalize")
+
+    def profile(self, enable=None, read: bool = False, reset: bool = False, kernel: str = "k_eval"):
+        """HIP-event timing of the plan's kernels (DIRECT: k_direct only).
+
+        enable: True (k_eval), False, or a collection of kernel names from KERNELS;
+        read: (total ms, launches) of ``kernel`` since the last reset."""
         if self.direct:
             return self.lompc.profile(enable=enable, read=read, reset=reset)
         if enable is not None:
-            self._check_rc(self._lib.lompc_plan_profile_enable(self._plan, int(bool(enable))))
+            if enable is True:
+                enable = ("k_eval",)
+            mask = 0 if enable is False else sum(1 << self.KERNELS.index(k) for k in enable)
+            self._check_rc(self._lib.lompc_plan_profile_enable(self._plan, mask))
         if read:
             ms, n = ctypes.c_double(0.0), ctypes.c_int64(0)
-            self._check_rc(self._lib.lompc_plan_profile_read(self._plan, ctypes.byref(ms), ctypes.byref(n),
-                                                             int(bool(reset))))
+            self._check_rc(self._lib.lompc_plan_profile_read(self._plan, self.KERNELS.index(kernel), ctypes.byref(ms),
+                                                             ctypes.byref(n), int(bool(reset))))
             return ms.value, n.value
         return None

@@ -199,9 +199,15 @@ int lompc_plan_status(lompc_plan* plan, void* stream, int64_t* n_repaired,
 /* Batch size, total parameter sets and gamma cells per set of the plan. */
 int lompc_plan_get_info(const lompc_plan* plan, int64_t* B, int64_t* S, int* cells);
 
-/* HIP-event timing of the plan's per-EV evaluation kernel (as lompc_profile_*). */
-int lompc_plan_profile_enable(lompc_plan* plan, int enable);
-int lompc_plan_profile_read(lompc_plan* plan, double* total_ms, int64_t* launches, int reset);
+/* HIP-event timing of the plan's kernels (hipExtLaunchKernel start/stop events on their own
+ * dispatches): enable takes a mask of (1 << LOMPC_PLAN_K_*) bits (0 = off); read synchronises
+ * and returns one kernel's accumulated milliseconds and launch count since the last reset. */
+#define LOMPC_PLAN_K_PATH 0  /* per-(set, gamma cell) solution paths */
+#define LOMPC_PLAN_K_EVAL 1  /* per-EV evaluation (the HBM-bound kernel) */
+#define LOMPC_PLAN_K_FINAL 2 /* per-set reduction + individual re-solves */
+#define LOMPC_PLAN_KERNELS 3
+int lompc_plan_profile_enable(lompc_plan* plan, int kernel_mask);
+int lompc_plan_profile_read(lompc_plan* plan, int kernel, double* total_ms, int64_t* launches, int reset);
 
 const char* lompc_plan_last_error(const lompc_plan* plan);
 int lompc_plan_destroy(lompc_plan* plan);

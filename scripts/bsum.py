@@ -3,7 +3,7 @@ import glob
 import json
 import sys
 
-for f in sorted(glob.glob(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/b*.log")):
+for f in (sys.argv[1:] or sorted(glob.glob("gpurun_out/b*.log"))):
     for x in open(f):
         if x.startswith("{"):
             d = json.loads(x)

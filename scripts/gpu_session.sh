@@ -25,12 +25,25 @@ for s in $STEPS; do
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench20q) run bench20q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-station ;;
     bench100q) run bench100q 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bsplit) run bsplit 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --split-types ;;
+    bsplitset) run bsplitset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --split-types --outputs set ;;
+    bnoev) run bnoev 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-kernel-events ;;
+    bev8) LOMPC_LIB=liblompc_amd_ev8.so run bev8 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bev4) LOMPC_LIB=liblompc_amd_ev4.so run bev4 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    qev8) LOMPC_LIB=liblompc_amd_ev8.so run qev8 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_baseline_configs.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bcost) run bcost 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs cost ;;
     bset) run bset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs set ;;
     bfused) LOMPC_REDUCE_FUSED=1 run bfused 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
     bwarm) run bwarm 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --warm ;;
     bwarmset) run bwarmset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --warm --outputs set ;;
     stampsw) KS_WARM=1 run stampsw 300 python scripts/kstamps.py && KS_WARM=1 KS_OUTPUTS=set run stampsw_set 300 python scripts/kstamps.py ;;
+    bg8) LOMPC_CELLS=8 run bg8 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bg12) LOMPC_CELLS=12 run bg12 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bg20) LOMPC_CELLS=20 run bg20 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bg24) LOMPC_CELLS=24 run bg24 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bg16) LOMPC_CELLS=16 run bg16 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bg48) LOMPC_CELLS=48 run bg48 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
+    bg64) LOMPC_CELLS=64 run bg64 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
     bg32) LOMPC_CELLS=32 run bg32 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
     bg128) LOMPC_CELLS=128 run bg128 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
     bg256) LOMPC_CELLS=256 run bg256 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
@@ -40,6 +53,7 @@ for s in $STEPS; do
     stamps) run stamps 300 python scripts/kstamps.py && KS_OUTPUTS=set run stamps_set 300 python scripts/kstamps.py && run stamps48 300 python scripts/kstamps.py 48 ;;
     fail) run fail 600 python scripts/find_failures.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-station ;;
+    profsplit) run profsplit 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profsplit -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-station --split-types ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -59,6 +59,10 @@ print(f"N={N} cells={plan.cells} k_path waves (shader cycles; s_memtime)")
 for k, name in enumerate(("small", "large")):
     sel = np.arange(nb) // G // P == k
     print(f"{name}: waves {sel.sum()}, pieces mean {st[sel, 6].mean():.2f} max {st[sel, 6].max()}")
+    nit = st[sel, 4]
+    n64, n32, pas = nit % 256, (nit // 256) % 256, nit // 65536
+    print(f"   iterations: fp32 mean {n32.mean():.2f} max {n32.max()}  fp64 mean {n64.mean():.2f} max {n64.max()}"
+          f"  primal-AS {pas.sum()}  tracking mean {st[sel, 5].mean():.2f} max {st[sel, 5].max()}")
     for j, nm in enumerate(names):
         x = d[sel, j]
         print(f"   {nm:12s} mean {x.mean():8.0f}  p90 {np.percentile(x, 90):8.0f}  max {x.max():8.0f}")
@@ -69,7 +73,7 @@ buf2 = np.zeros(65536 * 8, dtype=np.int64)
 assert lib.lompc_debug_stamps(buf2.ctypes.data, buf2.size) == 0
 e = buf2[32768 * 8:].reshape(32768, 8)[: min(32768, (B + 255) // 256)]
 e = e[e[:, 0] != 0].astype(np.float64)
-names = ["loads+stage", "lookup+outputs", "repairs", "rows", "record"]
+names = ["loads+stage", "lookup+outputs", "(lists)", "rows", "record"]
 print(f"k_eval workgroups {len(e)} (shader cycles)")
 for j, nm in enumerate(names):
     x = e[:, j + 1] - e[:, j]

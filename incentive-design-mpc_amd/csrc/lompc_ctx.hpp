@@ -75,6 +75,10 @@ struct lompc_ctx {
 
 #define LQ_PLAN_MAX_CTX LOMPC_PLAN_MAX_CTX
 
+struct CtxEnds {  // cumulative set counts of a plan's contexts (a kernel argument: no memory round)
+  int end[LQ_PLAN_MAX_CTX];
+};
+
 struct lompc_plan {
   int device = 0;
   int N = 0;
@@ -86,6 +90,7 @@ struct lompc_plan {
   int G = 0;                    // gamma cells per set (k_path waves per set)
   int nblk = 0;                 // k_eval workgroups (blocks of one set's EVs)
   int n_cu = 0;
+  CtxEnds ce{};                 // set s belongs to context #{k : ce.end[k] <= s}
   int eval_occ = 1;             // k_eval workgroups resident per CU (occupancy query)
   int64_t eval_occ_key = -1;    // (N, LDS pieces) it was queried for
   int64_t cap_S = 0, cap_blk = 0, cap_cells = 0;
@@ -94,7 +99,6 @@ struct lompc_plan {
   double* d_stats_own = nullptr;  // [S][8] when the plan owns its status rows
   double* d_stats = nullptr;      // where k_finalize writes the status rows
   // device workspaces
-  uint8_t* d_set_ctx = nullptr;   // [S]
   int64_t* d_set_off = nullptr;   // [S+1]
   int* d_blk_prefix = nullptr;    // [S+1] k_eval workgroups per set
   int4* d_blk = nullptr;          // [nblk] (set, first EV, end EV, -)

@@ -87,20 +87,24 @@ __device__ __forceinline__ void st_wt8(double* p, double v) {
 __device__ __forceinline__ double clampw(double x, double wmax) { return fmin(fmax(x, 0.0), wmax); }
 
 // ---------------------------------------------------------------- plan kernel
-// the constants of set s's EV type: the context index made wave-uniform, so every field is a
-// scalar (constant-cache) load instead of a vector load with a full memory round trip
+// the constants of set s's EV type: the context index from the kernel arguments and wave-uniform,
+// so every field is a scalar (constant-cache) load instead of a vector load with a full memory
+// round trip
 // (the table is read-only for the whole launch: the constant address space lets the compiler use
 // scalar loads although the kernels store to other global memory)
 typedef const __attribute__((address_space(4))) QPConst QPConstK;
-__device__ __forceinline__ const QPConst& set_consts(const QPConst* qd, const uint8_t* set_ctx, int s) {
-  const int k = __builtin_amdgcn_readfirstlane((int)set_ctx[s]);
+__device__ __forceinline__ const QPConst& set_consts(const QPConst* qd, const CtxEnds& ce, int s) {
+  s = __builtin_amdgcn_readfirstlane(s);
+  int k = 0;
+#pragma unroll
+  for (int j = 0; j + 1 < LQ_PLAN_MAX_CTX; ++j) k += s >= ce.end[j] ? 1 : 0;
   QPConstK* p = (QPConstK*)(uintptr_t)qd + k;
   return *(const QPConst*)p;
 }
 
 struct WindowArgs {
   const QPConst* qd;
-  const uint8_t* set_ctx;
+  CtxEnds ce;
   const int64_t* set_off;
   const double* gamma;
   double* window;
@@ -111,7 +115,7 @@ struct WindowArgs {
 __global__ __launch_bounds__(256) void k_plan_window(WindowArgs a) {
   __shared__ double smin[256], smax[256];
   const int s = blockIdx.x;
-  const double ym = set_consts(a.qd, a.set_ctx, s).y_max;
+  const double ym = set_consts(a.qd, a.ce, s).y_max;
   double lo = INFINITY, hi = -INFINITY;
   for (int64_t i = a.set_off[s] + threadIdx.x; i < a.set_off[s + 1]; i += 256) {
     const double g = a.gamma[i];
@@ -153,7 +157,7 @@ __device__ __forceinline__ int cell_of(double g, double lo, double inv_h, int G)
 struct PathArgs {
   int S, G, N, flags;
   const QPConst* qd;
-  const uint8_t* set_ctx;
+  CtxEnds ce;
   const double* window;
   const double* lmbd;    // [S][3N]
   const double* lmbd_r;  // [S]
@@ -173,16 +177,19 @@ struct PathArgs {
 };
 
 // per-stage data of set s from its prices (lompc.py:92-135 in standard form)
+// (bad: a negative or NaN price on this lane's stage)
 __device__ __forceinline__ void load_set(const QPConst& q, const double* __restrict__ L, double lr, int N,
-                                         int lane, lqw::WaveSet& ws, double& l2) {
+                                         int lane, lqw::WaveSet& ws, double& l2, bool& bad) {
   const double tt = q.theta * q.theta;
   ws.N = N;
   ws.lane = lane;
   ws.rsrc = lane < N ? N - 1 - lane : lane;
   l2 = 0.0;
+  bad = false;
   if (lane < N) {
     const double l1 = L[lane], l3 = L[2 * N + lane];
     l2 = L[N + lane];
+    bad = !(l1 >= 0.0 && l2 >= 0.0 && l3 >= 0.0);
     ws.d_nat = 2.0 * lr * tt + 2.0 * q.q_scale * l3 + q.dsmall;
     ws.e_nat = q.theta * (l1 - l2);
     const int tr = ws.rsrc;
@@ -207,14 +214,14 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
   const double lr = a.lmbd_r[s];
   const double wr_nat = (a.w_ref && lane < N) ? a.w_ref[(size_t)s * N + lane] : 0.0;
   const double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
-  const QPConst& q = set_consts(a.qd, a.set_ctx, s);  // scalar loads, no register copy
+  const QPConst& q = set_consts(a.qd, a.ce, s);  // scalar loads, no register copy
   LQ_STAMP(0);
-  lq_tab_init(q);
   lqw::WaveSet ws;
   double l2;
-  load_set(q, L, lr, N, lane, ws, l2);
-  if (lane < N && !(L[lane] >= 0.0 && l2 >= 0.0 && L[2 * N + lane] >= 0.0)) atomicOr(a.errflag, 1);
-  if (lane == 0 && !(lr >= 0.0)) atomicOr(a.errflag, 1);
+  bool bad;
+  load_set(q, L, lr, N, lane, ws, l2, bad);
+  lq_tab_init(q);
+  if (bad || (lane == 0 && !(lr >= 0.0))) atomicOr(a.errflag, 1);
   const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);  // lompc.py:128
   const double kappa = lr / q.delta;                            // price_solver.py:191
   double Ywr;
@@ -236,13 +243,14 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
       const int v = a.ws[(size_t)blk * 64 + lane];
       sl = (lane < N && v >= 0 && v <= 2 * q.m) ? v : sl0;
     }
-    double w = 0.0, r = 0.0;
+    lqw::StageSol<2> sol;
+    bool has_sol = false;
 #ifdef LOMPC_STAMPS
     int nit = 0;
-    const bool solved = lqw::wave_solve(q, ws, glo, sl, w, r, &nit);
+    const bool solved = lqw::wave_solve_path(q, ws, glo, sl, sol, has_sol, &nit);
     if (threadIdx.x == 0 && blockIdx.x < 32768) g_stamps[blockIdx.x * 8 + 4] = nit;
 #else
-    const bool solved = lqw::wave_solve(q, ws, glo, sl, w, r);
+    const bool solved = lqw::wave_solve_path(q, ws, glo, sl, sol, has_sol);
 #endif
     LQ_STAMP(2);
     if (solved) {
@@ -257,7 +265,8 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
 #ifdef LOMPC_STAMPS
         if (threadIdx.x == 0 && blockIdx.x < 32768) g_stamps[blockIdx.x * 8 + 5] = it + 1;
 #endif
-        const lqw::StageSol<2> sol = lqw::solve_stage<2>(q, ws, 0.0, sl);
+        if (!has_sol) sol = lqw::solve_stage<2>(q, ws, 0.0, sl);  // the start's solve is reused
+        has_sol = false;
         const double av = sol.w[0], bv = sol.w[1], r0 = sol.r[0], r1 = sol.r[1];
         double gc = INFINITY;
         int ns = sl;
@@ -363,7 +372,7 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
 struct EvalArgs {
   int S, G, N, want_err;
   const QPConst* qd;
-  const uint8_t* set_ctx;
+  CtxEnds ce;
   const int4* blk;        // [nblk] (set, first EV, end EV, -): <= EVAL_MAXB EVs of one set
   const int64_t* set_off; // [S+1]
   const double* window;
@@ -445,7 +454,7 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
     const int i = start + tid + EVAL_EVS * h;
     gh[h] = i < end ? a.gamma[i] : 0.0;
   }
-  const QPConst& q = set_consts(a.qd, a.set_ctx, s);
+  const QPConst& q = set_consts(a.qd, a.ce, s);
   const double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
   const double* __restrict__ L = a.lmbd + (size_t)s * 3 * N;
   const double l0[3] = {L[0], L[N], L[2 * N]};  // price0 (lompc.py:164-170)
@@ -659,7 +668,7 @@ struct FinalArgs {
   int N, G, want_err;
   int* t_np;               // [S] compact piece counters of k_path, reset here for the next run
   const QPConst* qd;
-  const uint8_t* set_ctx;
+  CtxEnds ce;
   const int* blk_prefix;   // [S+1] k_eval workgroups of each set
   const int64_t* set_off;
   const double* window;
@@ -719,13 +728,14 @@ __global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
   }
   __syncthreads();
   if (red[0][N + PX_N_FAILED] > 0.0) {  // block-uniform: individual re-solves pending
-    const QPConst& q = set_consts(r.qd, r.set_ctx, s);
+    const QPConst& q = set_consts(r.qd, r.ce, s);
     lq_tab_init(q);
     const double* __restrict__ L = r.lmbd + (size_t)s * 3 * N;
     const double lr = r.lmbd_r[s];
     lqw::WaveSet ws;
     double l2;
-    load_set(q, L, lr, N, lane, ws, l2);
+    bool bad;  // (checked by k_path)
+    load_set(q, L, lr, N, lane, ws, l2, bad);
     const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);
     const double kappa = lr / q.delta;
     const double l0[3] = {L[0], L[N], L[2 * N]};
@@ -922,7 +932,7 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   }
   if (!p->ev_stage) HIPCHK(p, hipEventCreateWithFlags(&p->ev_stage, hipEventDisableTiming));
   if (S > p->cap_S) {
-    if ((rc = grow(p, &p->d_set_ctx, S)) || (rc = grow(p, &p->d_set_off, S + 1)) ||
+    if ((rc = grow(p, &p->d_set_off, S + 1)) ||
         (rc = grow(p, &p->d_blk_prefix, S + 1)) || (rc = grow(p, &p->d_window, 2 * S)) ||
         (rc = grow(p, &p->t_np, S)) ||
         (rc = grow(p, &p->d_stats_own, S * LOMPC_SET_STATS)))
@@ -969,7 +979,6 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   memcpy(hoff, set_offsets, (S + 1) * sizeof(int64_t));
   int4* hblk = reinterpret_cast<int4*>(hoff + S + 1);
   int* hpre = reinterpret_cast<int*>(hblk + nblk);
-  uint8_t* hctx = reinterpret_cast<uint8_t*>(hpre + S + 1);
   int64_t b = 0;
   hpre[0] = 0;
   for (int64_t s = 0; s < S; ++s) {
@@ -977,15 +986,16 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     for (int64_t k = 0; k < nb; ++k) hblk[b++] = make_int4((int)s, (int)(o + m * k / nb), (int)(o + m * (k + 1) / nb), 0);
     hpre[s + 1] = (int)b;
   }
-  for (int k = 0, s = 0; k < nctx; ++k)
-    for (int64_t u = 0; u < sets_per_ctx[k]; ++u) hctx[s++] = (uint8_t)k;
+  for (int k = 0, e = 0; k < LQ_PLAN_MAX_CTX; ++k) {
+    e += k < nctx ? (int)sets_per_ctx[k] : 0;
+    p->ce.end[k] = k + 1 < nctx ? e : (int)S;  // contexts past the last: never selected
+  }
   HIPCHK(p, hipMemcpyAsync(p->d_q, hq, nctx * sizeof(QPConst), hipMemcpyHostToDevice, st));
   HIPCHK(p, hipMemcpyAsync(p->d_set_off, hoff, (S + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
   if (nblk) HIPCHK(p, hipMemcpyAsync(p->d_blk, hblk, nblk * sizeof(int4), hipMemcpyHostToDevice, st));
   HIPCHK(p, hipMemcpyAsync(p->d_blk_prefix, hpre, (S + 1) * sizeof(int), hipMemcpyHostToDevice, st));
-  HIPCHK(p, hipMemcpyAsync(p->d_set_ctx, hctx, S, hipMemcpyHostToDevice, st));
   HIPCHK(p, hipEventRecord(p->ev_stage, st));
-  WindowArgs wa{p->d_q, p->d_set_ctx, p->d_set_off, gamma, p->d_window};
+  WindowArgs wa{p->d_q, p->ce, p->d_set_off, gamma, p->d_window};
   hipLaunchKernelGGL(k_plan_window, dim3((unsigned)S), dim3(256), 0, st, wa);
   HIPCHK(p, hipGetLastError());
   return LOMPC_OK;
@@ -1001,7 +1011,7 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   pa.N = N;
   pa.flags = p->flags;
   pa.qd = p->d_q;
-  pa.set_ctx = p->d_set_ctx;
+  pa.ce = p->ce;
   pa.window = p->d_window;
   pa.lmbd = lmbd;
   pa.lmbd_r = lmbd_r;
@@ -1030,7 +1040,7 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
     a.N = N;
     a.want_err = 1;
     a.qd = p->d_q;
-    a.set_ctx = p->d_set_ctx;
+    a.ce = p->ce;
     a.blk = p->d_blk;
     a.set_off = p->d_set_off;
     a.window = p->d_window;
@@ -1075,7 +1085,7 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   r.want_err = 1;
   r.t_np = p->t_np;
   r.qd = p->d_q;
-  r.set_ctx = p->d_set_ctx;
+  r.ce = p->ce;
   r.blk_prefix = p->d_blk_prefix;
   r.set_off = p->d_set_off;
   r.window = p->d_window;
@@ -1106,7 +1116,7 @@ void lq_plan_free(lompc_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
   (void)hipDeviceSynchronize();
-  void* ptrs[] = {p->d_q,     p->d_stats_own, p->d_set_ctx, p->d_set_off, p->d_blk_prefix, p->d_window,
+  void* ptrs[] = {p->d_q,     p->d_stats_own, p->d_set_off, p->d_blk_prefix, p->d_window,
                   p->d_blk, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
                   p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag, p->t_base, p->t_np,
                   p->d_fail_cnt, p->d_fail_idx};

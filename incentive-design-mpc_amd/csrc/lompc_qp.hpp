@@ -91,18 +91,30 @@ __device__ __forceinline__ void lq_tab_init(const QPConst& q) {
   double* tb = lq_tab();
   const int s = threadIdx.x;
   if (s < LQ_NSTATE) {
+    // knots / slopes as opaque uniform values (scalar loads + readfirstlane), selected per lane by
+    // compares: a lane-indexed load from q would be a vector memory round at every kernel start
+    auto u = [](double x) {
+      const long long b = __builtin_bit_cast(long long, x);
+      const int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+      return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+    };
+    const double k0 = u(q.knots[0]), k1 = u(q.knots[1]), k2 = u(q.knots[2]), k3 = u(q.knots[3]), k4 = u(q.knots[4]);
+    const double s0 = u(q.slopes[0]), s1 = u(q.slopes[1]), s2 = u(q.slopes[2]), s3 = u(q.slopes[3]);
+    static_assert(LQ_MAXSEG == 4, "knot selection written for 4 segments");
+    auto pick_k = [&](int i) { return i <= 0 ? k0 : i == 1 ? k1 : i == 2 ? k2 : i == 3 ? k3 : k4; };
+    auto pick_s = [&](int i) { return i <= 0 ? s0 : i == 1 ? s1 : i == 2 ? s2 : s3; };
     const int k = s >> 1;
     double lo, hi, slo, shi;
     if (s & 1) {
       const int kk = k < q.m ? k : q.m - 1;
-      lo = q.knots[kk];
-      hi = q.knots[kk + 1];
-      slo = shi = q.slopes[kk];
+      lo = pick_k(kk);
+      hi = pick_k(kk + 1);
+      slo = shi = pick_s(kk);
     } else {
       const int kk = k <= q.m ? k : q.m;
-      lo = hi = q.knots[kk];
-      slo = kk > 0 ? q.slopes[kk - 1] : -INFINITY;
-      shi = kk < q.m ? q.slopes[kk] : INFINITY;
+      lo = hi = pick_k(kk);
+      slo = kk > 0 ? pick_s(kk - 1) : -INFINITY;
+      shi = kk < q.m ? pick_s(kk) : INFINITY;
     }
     tb[4 * s + 0] = lo;
     tb[4 * s + 1] = hi;

@@ -541,4 +541,41 @@ __device__ __forceinline__ bool wave_solve(const QPConst& q, const WaveSet& ws, 
   return ok;
 }
 
+// wave_solve for the start of a parametric path: the fp64 PDAS iterations solve the sub-problem
+// as an affine function of gamma (solve_stage<2>, evaluated at gamma), so on convergence `sol`
+// already holds w(g) = a + b g and r(g) of the final working set for the path tracking (one
+// sub-problem solve fewer per path).  has_sol is false when the primal active set had to take
+// over (the caller then solves the final working set itself).
+__device__ __forceinline__ bool wave_solve_path(const QPConst& q, const WaveSet& ws, double gamma, int& s,
+                                                StageSol<2>& sol, bool& has_sol, int* nit = nullptr) {
+  int n32 = 0, n64 = 0;
+  if (LQ_F32_IT > 0) n32 = wave_pdas_f32(q, ws, gamma, s, LQ_F32_IT);
+  const int max_it = min(4 * ws.N + 8, LQ_PDAS_CAP);
+  bool ok = false;
+  double w = 0.0, r = 0.0;
+  for (int it = 0; it < max_it; ++it) {
+    sol = solve_stage<2>(q, ws, 0.0, s);
+    w = fma(sol.w[1], gamma, sol.w[0]);
+    r = fma(sol.r[1], gamma, sol.r[0]);
+    const Box bx = lq_box(s);
+    const int ns = ws.lane < ws.N ? (it < LQ_JUMP_IT ? lq_move_jump(q, s, bx, w, r) : lq_move(q, s, bx, w, r)) : s;
+    const bool changed = __any(ns != s);
+    s = ns;
+    n64 = it + 1;
+    if (!changed) {
+      ok = true;
+      break;
+    }
+  }
+  if (nit) *nit = n64 + 256 * n32;
+  if (ok) ok = wave_kkt(q, ws, s, w, r) <= q.tol_cert;
+  has_sol = ok;
+  if (!ok) {
+    if (nit) *nit += 65536;
+    ok = wave_primal_as(q, ws, gamma, s, w, r, 16 * ws.N + 32, true);
+    if (ok) ok = wave_kkt(q, ws, s, w, r) <= q.tol_cert;
+  }
+  return ok;
+}
+
 }  // namespace lqw

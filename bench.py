@@ -12,11 +12,18 @@ reductions of price_solver.py:203-214; with N > 1 ranks the per-partition
 reductions are combined by one RCCL sum + one max all-reduce.  Weak scaling:
 262 144 EVs per GPU (config 3; at 8 GPUs this is config 4's 2 097 152).
 
-Rank 0 prints ONE JSON line.  ``roofline`` prices the per-EV kernel (k_eval in
-PATH mode, the only kernel whose work scales with the EV count) by its
-algorithmic bytes per QP (gamma in 8 B, w out 8N B, cost out 8 B) over its
-launch duration from HIP events attached to its dispatch; ``cpu_baseline`` times the C
-oracle (oracle/, dense active set) on a bounded sample of the same workload.
+Every step is one plan run = three launches on one stream: k_path (per (set, gamma cell)
+solution paths), k_eval (per-EV evaluation + rows) and k_finalize (per-set reductions).
+
+Rank 0 prints ONE JSON line.  ``roofline`` prices the per-EV kernel (k_eval, the only
+kernel whose work scales with the EV count) by its algorithmic bytes per QP (gamma in 8 B,
+w out 8N B, cost out 8 B) over its launch duration from HIP events attached to its dispatch
+in the timed region; ``kernels`` gives every kernel's average duration from a separate
+20-step pass with events on all three (after the timed region, so the timed steps carry
+one event pair only) and k_path's latency roof (PMC figures from profiles/, when they match
+this configuration); ``cpu_baseline`` times the C oracle (oracle/, dense active set) on a
+bounded sample of the same workload: all host threads, one thread, and the lmbd_r > 0
+variant; ``direct_mode`` times the per-EV DIRECT mode on the same batch.
 """
 from __future__ import annotations
 
@@ -60,8 +67,9 @@ def parse():
     ap.add_argument("--no-station", action="store_true", help="skip the BiMPC steps/sec leg")
     ap.add_argument("--station-evs-per-gpu", type=int, default=262144, help="EVs per GPU, half per type")
     ap.add_argument("--station-horizon", type=int, default=48)
-    ap.add_argument("--station-steps", type=int, default=3)
-    ap.add_argument("--station-warmup", type=int, default=1)
+    ap.add_argument("--station-steps", type=int, default=20)
+    ap.add_argument("--station-warmup", type=int, default=3)
+    ap.add_argument("--no-direct", action="store_true", help="skip the DIRECT-mode comparison leg")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (the product path); gloo only to rehearse world > 1 on one GPU")
     return ap.parse_args()
@@ -189,7 +197,7 @@ def main():
         rep, fail, inv = r["plan"].check()
         assert fail == 0 and inv == 0
         repaired += rep
-    # per-EV kernel (k_solve / k_direct) timing: HIP events on its own dispatch (hipExtLaunchKernel)
+    # the per-EV kernel's timing over the timed region: HIP events on its own dispatches
     k_ms, k_n, k_qps = 0.0, 0, 0
     for r in runs:
         ms, n = r["plan"].profile(read=True)
@@ -203,6 +211,7 @@ def main():
 
     total_qp = world * B * args.steps
     value = total_qp / dt
+    path = args.mode == "path"
     line = {
         "metric": "LoMPC QP solves/sec",
         "value": value,
@@ -227,7 +236,7 @@ def main():
             "outputs": args.outputs,
             "warm_start": bool(args.warm),
             "parallelism": f"dp{world} (EV shards, one RCCL all-gather of both types' per-set reductions per step)",
-            "launches_per_step": 2 if args.mode == "path" else 6,
+            "launches_per_step": 3 * len(runs),
         },
         "roofline": {
             "bound": "hbm",
@@ -236,24 +245,23 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": None,
-            "kernel": "k_solve" if args.mode == "path" else "k_direct",
+            "kernel": "k_eval" if path else "k_direct",
             "bytes_per_qp": bytes_per_qp,
             "qp_per_launch": qp_per_launch,
             "avg_launch_us": avg_launch_s * 1e6,
         },
         "repaired_qps": repaired,
     }
-    traffic_file = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(traffic_file):
-        try:
-            tr = json.load(open(traffic_file))
-            if tr.get("mode") == args.mode and tr.get("horizon") == N and tr.get("qp_per_launch") == qp_per_launch:
-                line["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
-                line["roofline"]["traffic_source"] = tr.get("source")
-        except Exception:
-            pass
+    pmc = load_pmc(args, N, qp_per_launch)
+    if pmc and "k_eval" in pmc:
+        line["roofline"]["traffic"] = pmc["k_eval"]["hbm_bytes_per_launch"]
+        line["roofline"]["traffic_source"] = pmc["source"]
+    if path and world == 1 and len(runs) == 1:
+        line["kernels"] = kernel_breakdown(runs[0], step, args, nsteps, pmc, torch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(eng, N, args.cpu_seconds)
+    if path and world == 1 and not args.no_direct:
+        line["direct_mode"] = direct_leg(eng, N, P, args, nsteps, dev, torch)
     if not args.no_station:
         del eng, runs
         line["bimpc"] = station_leg(args, world, dev)
@@ -261,6 +269,88 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if "error" in line.get("bimpc", {}):
+        sys.exit(1)  # the QP/s line is printed; a failed station leg still fails the run
+
+
+def load_pmc(args, N, qp_per_launch):
+    """profiles/pmc.json (scripts/make_traffic.py over a rocprofv3 --pmc session of this bench):
+    per-kernel counters, used only when it was collected on this configuration."""
+    f = os.path.join(ROOT, "profiles", "pmc.json")
+    try:
+        d = json.load(open(f))
+    except (OSError, ValueError):
+        return None
+    ok = d.get("mode") == args.mode and d.get("horizon") == N and d.get("qp_per_launch") == qp_per_launch
+    return d if ok else None
+
+
+def kernel_breakdown(run, step, args, nsteps, pmc, torch):
+    """Average duration of each of the plan's kernels over 20 more steps with HIP events on
+    all three dispatches (outside the timed region), and k_path's roof: it is latency-bound
+    (one wave per (set, gamma cell), a chain of dependent DPP scans; far fewer waves than
+    SIMDs), so it is priced by the fraction of its waves' cycles that issue VALU work (PMC)."""
+    plan = run["plan"]
+    kernels = ("k_path", "k_eval", "k_finalize")
+    plan.profile(enable=kernels)
+    for k in kernels:
+        plan.profile(read=True, reset=True, kernel=k)
+    n = 20
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(n):
+        step(args.warmup + j % max(nsteps - args.warmup, 1))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"steps": n, "ms_per_step_with_events": dt / n * 1e3}
+    for k in kernels:
+        ms, cnt = plan.profile(read=True, kernel=k)
+        out[k] = {"avg_us": ms / max(cnt, 1) * 1e3, "launches": cnt}
+    plan.profile(enable=False)
+    info = plan.info()
+    out["k_path"].update({"waves": info["sets"] * info["cells"], "cells_per_set": info["cells"],
+                          "bound": "latency (dependent DPP-scan chains, one wave per SIMD at most)"})
+    out["k_eval"]["workgroups"] = info["workgroups"]
+    if pmc:
+        for k in kernels:
+            if k in pmc:
+                out[k]["pmc"] = {x: pmc[k][x] for x in pmc[k] if x != "hbm_bytes_per_launch"}
+        if "k_path" in pmc and "valu_issue_frac" in pmc["k_path"]:
+            out["k_path"]["valu_issue_frac"] = pmc["k_path"]["valu_issue_frac"]
+    return out
+
+
+def direct_leg(eng, N, P, args, nsteps, dev, torch):
+    """The same batch in DIRECT mode (every EV solved by its own lane from a per-set working
+    set, no gamma paths): QP/s over 20 steps, for comparison with the PATH plan above."""
+    from lompc_amd import BatchPlan, LoMPC
+
+    runs = []
+    for e in eng:
+        lo = LoMPC(N, e["c"], device=dev.index, mode="direct")
+        lr = torch.zeros(P, dtype=torch.float64, device=dev)
+        plan = BatchPlan(lo, e["gamma"], e["off"], w_ref=e["wr"], gamma_ref=torch.full(
+            (P,), e["c"].y_max - 0.4, dtype=torch.float64, device=dev), want_w=True, want_cost=True,
+            want_set=True)
+        runs.append((plan, lo, [e["lm"][k].data_ptr() for k in range(nsteps)], lr))
+    n = 20
+    for plan, _, lm, lr in runs:
+        plan.run(lm[0], lr.data_ptr())
+        plan.check()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(n):
+        for plan, _, lm, lr in runs:
+            plan.run(lm[args.warmup + j % max(nsteps - args.warmup, 1)], lr.data_ptr())
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    rep = 0
+    for plan, _, _, _ in runs:
+        r_, f_, i_ = plan.check()
+        assert f_ == 0 and i_ == 0
+        rep += r_
+    B = sum(e["M"] for e in eng)
+    return {"value": B * n / dt, "unit": "QP/s", "ms_per_step": dt / n * 1e3, "steps": n, "repaired_qps": rep}
 
 
 def station_leg(args, world, dev):
@@ -308,10 +398,14 @@ def station_leg(args, world, dev):
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        per_step = []
         t0 = time.perf_counter()
         for _ in range(steps):
+            ts = time.perf_counter()
             st._step()
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            per_step.append(time.perf_counter() - ts)
+            check_station_state(st, consts)
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
@@ -320,15 +414,43 @@ def station_leg(args, world, dev):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         stats = st.logs["statistics"]
-        it = np.concatenate([stats["niter_s"][:, warm:].ravel(), stats["niter_l"][:, warm:].ravel()])
+        it = np.concatenate([stats["niter_s"][:, warm:warm + steps].ravel(), stats["niter_l"][:, warm:warm + steps].ravel()])
         ncalls = calls() - c0
+        ms = np.asarray(per_step) * 1e3
+        info = st.bimpc.last_info or {}
         out.update({"value": steps / dt, "ms_per_step": dt / steps * 1e3,
+                    "ms_per_step_median": float(np.median(ms)), "ms_per_step_min": float(ms.min()),
+                    "ms_per_step_max": float(ms.max()),
                     "price_iterations_per_step": float(np.sum(it[it >= 0])) / steps,
                     "engine_calls_per_step": ncalls / steps,
-                    "lompc_qps_per_sec_est": (ncalls + 2 * P * steps) * M_2 / P / dt})
+                    "lompc_qps_per_sec_est": (ncalls + 2 * P * steps) * M_2 / P / dt,
+                    "checks": {"storage_x_final": float(st.x), "x_max": float(consts.bimpc_consts.x_max),
+                               "bimpc_iterations_last": info.get("iterations"),
+                               "bimpc_primal_residual_last": info.get("primal_residual"),
+                               "bimpc_dual_residual_last": info.get("dual_residual"),
+                               "evs_per_type_counted": int(stats["Mp_s"][:, warm + steps - 1].sum())}})
     except Exception as e:  # reported, never hides the QP/s line
         out["error"] = f"{type(e).__name__}: {e}"
     return out
+
+
+def check_station_state(st, consts):
+    """Invariants of a closed-loop step (raise -> the leg reports "error" and the run fails):
+    storage state within [0, x_max] up to the BiMPC's robustness margin, the planner converged
+    with small residuals, every EV counted in exactly one partition."""
+    x_max = consts.bimpc_consts.x_max
+    tol = 1e-6 + 0.05 * x_max
+    if not (-tol <= st.x <= x_max + tol):
+        raise AssertionError(f"storage state {st.x} outside [0, {x_max}]")
+    info = st.bimpc.last_info or {}
+    scale = 1.0 + abs(info.get("objective", 0.0))
+    for k in ("primal_residual", "dual_residual"):
+        if not (info.get(k, 0.0) <= 1e-6 * scale):
+            raise AssertionError(f"BiMPC {k} {info.get(k)} (objective {info.get('objective')})")
+    t = st.t - 1
+    for key in ("Mp_s", "Mp_l"):
+        if int(st.logs["statistics"][key][:, t].sum()) != st.M_2:
+            raise AssertionError(f"{key} does not count every EV once")
 
 
 def cpu_baseline(eng, N, seconds):

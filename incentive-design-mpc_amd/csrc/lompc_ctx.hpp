@@ -106,11 +106,8 @@ struct lompc_plan {
   double* d_partial = nullptr;    // [nblk][N+NPX] k_eval workgroup records
   int* d_fail_cnt = nullptr;      // [nblk][waves] EVs listed for k_finalize's individual re-solve
   int* d_fail_idx = nullptr;      // [nblk][EVs]
-  // path table: per cell count / first piece / coverage start / working set; per set a compact
-  // range of G*LQ_PPL piece slots and its fill counter
+  // path table: per cell piece count / coverage start / working set and LQ_PPL piece slots
   int* t_cnt = nullptr;
-  int* t_base = nullptr;
-  int* t_np = nullptr;
   double* t_lo = nullptr;
   double* t_ge = nullptr;
   double* t_cf = nullptr;

@@ -63,7 +63,7 @@ __device__ long long g_stamps[65536 * 8];
 #define EVAL_EVS (64 * EVAL_WAVES)         // k_eval: threads per workgroup
 #define EVAL_PASSES 2                      // k_eval: EVs per thread, at most
 #define EVAL_MAXB (EVAL_EVS * EVAL_PASSES)  // k_eval: EVs per workgroup, at most
-#define LQ_PIECE_CAP 96                    // k_eval: max pieces of one set staged in LDS (more: re-solved)
+#define LQ_PIECE_CAP 128                   // k_eval: piece slots of one set staged in LDS (more: re-solved)
 #define LQ_GMAX 1024                       // max cells per set
 
 namespace {
@@ -165,11 +165,9 @@ struct PathArgs {
   uint8_t* ws;           // [S*G][64] warm-start working sets or null
   // per cell
   int* t_cnt;            // [S*G]             certified pieces of the cell (0: none)
-  int* t_base;           // [S*G]             its first piece in the set's compact range
   double* t_lo;          // [S*G]             coverage start
   uint8_t* t_sl;         // [S*G][64]         working set at the cell start (repairs)
-  // per set: pieces in a compact range [0, t_np[s]) of G*PPL slots, cells in arrival order
-  int* t_np;             // [S]               pieces of the set (k_reduce resets it to 0)
+  // per cell LQ_PPL piece slots, the first t_cnt used (ascending gamma)
   double* t_ge;          // [S][G*PPL]        gamma at each piece's end
   double* t_cf;          // [S][G*PPL][8]     K0 K1 K2 (cost) F0 F1 F2 (err^2) a_0 b_0
   double2* t_ab;         // [S][G*PPL][N]     (a_t, b_t)
@@ -344,13 +342,8 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
       }
     }
   }
-  // reserve the cell's pieces in the set's compact range (one agent-scope add per cell; the
-  // order of the cells in it does not change any output), then write them
-  int base = 0;
-  if (lane == 0 && npc > 0) base = atomicAdd(a.t_np + s, npc);
-  base = __shfl(base, 0, 64);
-  __builtin_amdgcn_wave_barrier();
-  const size_t sb = (size_t)s * G * LQ_PPL + base;
+  // the cell's pieces in its fixed slots [blk * LQ_PPL, + npc)
+  const size_t sb = (size_t)blk * LQ_PPL;
   for (int k = 0; k < npc; ++k) {  // npc is wave-uniform
     if (lane < N) a.t_ab[(sb + k) * N + lane] = p_ab[k][lane];
     if (lane < 8) a.t_cf[(sb + k) * 8 + lane] = p_cf[k][lane];
@@ -359,7 +352,6 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
   a.t_sl[(size_t)blk * 64 + lane] = (uint8_t)sl0;
   if (lane == 0) {
     a.t_cnt[blk] = npc;
-    a.t_base[blk] = base;
     a.t_lo[blk] = glo;
   }
   LQ_STAMP(3);
@@ -381,10 +373,8 @@ struct EvalArgs {
   const double* lmbd_r;
   const double* w_ref;
   const int* t_cnt;
-  const int* t_base;
   const double* t_lo;
   const uint8_t* t_sl;
-  const int* t_np;
   const double* t_ge;
   const double* t_cf;
   const double2* t_ab;
@@ -429,8 +419,8 @@ __device__ __forceinline__ void wave_ev_outputs(const QPConst& q, const lqw::Wav
 }
 
 __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
-  // dynamic LDS: [cap][N] piece rows | [cap][8] coefficients | [cap] piece ends | cells: base,
-  // count (int2) | coverage start
+  // dynamic LDS: [cap][N] piece rows | [cap][8] coefficients | [cap] piece ends | cells:
+  // coverage start | piece count
   extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
   __shared__ double s_g[EVAL_WAVES][64 * EVAL_PASSES];            // the wave's rows: gamma, piece
   __shared__ int s_k[EVAL_WAVES][64 * EVAL_PASSES];               //   (-1 re-solved, -2 invalid)
@@ -445,8 +435,8 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
   double2* s_ab = s_dyn;
   double* s_cf = reinterpret_cast<double*>(s_ab + (size_t)cap * N);
   double* s_ge = s_cf + (size_t)cap * 8;
-  int2* s_cell = reinterpret_cast<int2*>(s_ge + cap);
-  double* s_lo = reinterpret_cast<double*>(s_cell + G);
+  double* s_lo = s_ge + cap;
+  int* s_cnt = reinterpret_cast<int*>(s_lo + G);
   // this thread's EVs (caller order), the cells and the set's piece count: one memory round
   double gh[EVAL_PASSES];
 #pragma unroll
@@ -459,15 +449,16 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
   const double* __restrict__ L = a.lmbd + (size_t)s * 3 * N;
   const double l0[3] = {L[0], L[N], L[2 * N]};  // price0 (lompc.py:164-170)
   const double lr = a.lmbd_r[s];
-  const int np = min(a.t_np[s], cap);
   const int cb = s * G;
   for (int c = tid; c < G; c += EVAL_EVS) {
-    s_cell[c] = make_int2(a.t_base[cb + c], a.t_cnt[cb + c]);
+    s_cnt[c] = a.t_cnt[cb + c];
     s_lo[c] = a.t_lo[cb + c];
   }
-  // the set's pieces (contiguous in the compact range): coalesced copies, every load of a
-  // thread issued before its first LDS store (one memory round, not one per item)
+  // the set's piece slots (the first `cap`: cells past them are re-solved individually), all
+  // of them whatever the cells' counts, so every load of the staging is in one memory round:
+  // coalesced copies, each thread's loads issued before its first LDS store
   const size_t sb = (size_t)s * G * LQ_PPL;
+  const int np = min(G * LQ_PPL, cap);
   {
     const int nab = np * N, ncf = np * 8;
     const double2* gab = a.t_ab + sb * N;
@@ -475,12 +466,12 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
     constexpr int U = 8;
     for (int b0 = tid; b0 < nab; b0 += EVAL_EVS * U) {
       double2 v[U];
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < U; ++u) {
         const int it = b0 + EVAL_EVS * u;
         v[u] = it < nab ? gab[it] : make_double2(0.0, 0.0);
       }
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < U; ++u) {
         const int it = b0 + EVAL_EVS * u;
         if (it < nab) s_ab[it] = v[u];
@@ -488,12 +479,12 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
     }
     for (int b0 = tid; b0 < ncf + np; b0 += EVAL_EVS * U) {
       double v[U];
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < U; ++u) {
         const int it = b0 + EVAL_EVS * u;
         v[u] = it < ncf ? gcf[it] : (it < ncf + np ? a.t_ge[sb + it - ncf] : 0.0);
       }
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < U; ++u) {
         const int it = b0 + EVAL_EVS * u;
         if (it < ncf) s_cf[it] = v[u];
@@ -517,8 +508,7 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
     const double g = gh[h];
     const bool valid = act && g >= 0.0 && g <= ym;
     const int c = valid ? cell_of(g, wlo, cscale, G) : 0;
-    const int2 ci = s_cell[c];
-    const int kb = ci.x, ke = ci.x + ci.y;  // the cell's pieces [kb, ke), ascending gamma
+    const int kb = c * LQ_PPL, ke = kb + s_cnt[c];  // the cell's pieces [kb, ke), ascending gamma
     int key = kb;
     for (int k = kb; k < ke - 1; ++k) key += g > s_ge[k] ? 1 : 0;
     const bool cov = valid && ke > kb && ke <= np && g >= s_lo[c] && g <= s_ge[ke - 1];
@@ -666,7 +656,6 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
 // ---------------------------------------------------------------- k_finalize
 struct FinalArgs {
   int N, G, want_err;
-  int* t_np;               // [S] compact piece counters of k_path, reset here for the next run
   const QPConst* qd;
   CtxEnds ce;
   const int* blk_prefix;   // [S+1] k_eval workgroups of each set
@@ -805,7 +794,6 @@ __global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
     if (r.set_stats) r.set_stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
     r.stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
   }
-  if (tid == 0) r.t_np[s] = 0;
 }
 
 int pick_cells(int64_t max_set) {
@@ -851,7 +839,7 @@ int plan_events_read(std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& pool,
 // ============================================================== host
 // k_eval's dynamic LDS: up to cap pieces of one set (N double2 + 8 + 1 doubles each) + the cells
 size_t eval_lds(int N, int G, int cap) {
-  return (size_t)cap * (N * sizeof(double2) + 9 * sizeof(double)) + (size_t)G * (sizeof(int2) + sizeof(double));
+  return (size_t)cap * (N * sizeof(double2) + 9 * sizeof(double)) + (size_t)G * (sizeof(int) + sizeof(double));
 }
 
 // events of one profiled dispatch (null events when kernel k is not profiled)
@@ -934,7 +922,6 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   if (S > p->cap_S) {
     if ((rc = grow(p, &p->d_set_off, S + 1)) ||
         (rc = grow(p, &p->d_blk_prefix, S + 1)) || (rc = grow(p, &p->d_window, 2 * S)) ||
-        (rc = grow(p, &p->t_np, S)) ||
         (rc = grow(p, &p->d_stats_own, S * LOMPC_SET_STATS)))
       return rc;
     p->cap_S = S;
@@ -948,7 +935,7 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   const bool warm = (flags & LOMPC_PLAN_WARM_START) != 0;
   bool fresh_ws = false;
   if (ncell > p->cap_cells || (warm && !p->d_ws)) {
-    if ((rc = grow(p, &p->t_cnt, ncell)) || (rc = grow(p, &p->t_base, ncell)) || (rc = grow(p, &p->t_lo, ncell)) ||
+    if ((rc = grow(p, &p->t_cnt, ncell)) || (rc = grow(p, &p->t_lo, ncell)) ||
         (rc = grow(p, &p->t_ge, ncell * LQ_PPL)) || (rc = grow(p, &p->t_cf, ncell * LQ_PPL * 8)) ||
         (rc = grow(p, &p->t_ab, ncell * LQ_PPL * N)) || (rc = grow(p, &p->t_sl, ncell * 64)))
       return rc;
@@ -957,7 +944,6 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     fresh_ws = true;
   }
   if (warm && (fresh_ws || p->G != G || p->S != S)) HIPCHK(p, hipMemsetAsync(p->d_ws, 1, (size_t)ncell * 64, st));
-  HIPCHK(p, hipMemsetAsync(p->t_np, 0, S * sizeof(int), st));
   p->B = B;
   p->S = S;
   p->G = G;
@@ -1018,10 +1004,8 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   pa.w_ref = p->w_ref;
   pa.ws = (p->flags & LOMPC_PLAN_WARM_START) ? p->d_ws : nullptr;
   pa.t_cnt = p->t_cnt;
-  pa.t_base = p->t_base;
   pa.t_lo = p->t_lo;
   pa.t_sl = p->t_sl;
-  pa.t_np = p->t_np;
   pa.t_ge = p->t_ge;
   pa.t_cf = p->t_cf;
   pa.t_ab = p->t_ab;
@@ -1049,10 +1033,8 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
     a.lmbd_r = lmbd_r;
     a.w_ref = p->w_ref;
     a.t_cnt = p->t_cnt;
-    a.t_base = p->t_base;
     a.t_lo = p->t_lo;
     a.t_sl = p->t_sl;
-    a.t_np = p->t_np;
     a.t_ge = p->t_ge;
     a.t_cf = p->t_cf;
     a.t_ab = p->t_ab;
@@ -1083,7 +1065,6 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   r.N = N;
   r.G = p->G;
   r.want_err = 1;
-  r.t_np = p->t_np;
   r.qd = p->d_q;
   r.ce = p->ce;
   r.blk_prefix = p->d_blk_prefix;
@@ -1118,7 +1099,7 @@ void lq_plan_free(lompc_plan* p) {
   (void)hipDeviceSynchronize();
   void* ptrs[] = {p->d_q,     p->d_stats_own, p->d_set_off, p->d_blk_prefix, p->d_window,
                   p->d_blk, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
-                  p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag, p->t_base, p->t_np,
+                  p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag,
                   p->d_fail_cnt, p->d_fail_idx};
   for (void* x : ptrs)
     if (x) (void)hipFree(x);
@@ -1190,11 +1171,12 @@ int lompc_plan_status(lompc_plan* p, void* stream, int64_t* n_repaired, int64_t*
   return LOMPC_OK;
 }
 
-int lompc_plan_get_info(const lompc_plan* p, int64_t* B, int64_t* S, int* cells) {
+int lompc_plan_get_info(const lompc_plan* p, int64_t* B, int64_t* S, int* cells, int* eval_workgroups) {
   if (!p) return LOMPC_ERR_INVALID_ARG;
   if (B) *B = p->B;
   if (S) *S = p->S;
   if (cells) *cells = p->G;
+  if (eval_workgroups) *eval_workgroups = p->nblk;
   return LOMPC_OK;
 }
 

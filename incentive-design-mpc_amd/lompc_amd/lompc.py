@@ -403,9 +403,16 @@ class BatchPlan:
         if rc != _lib.LOMPC_OK:
             lo._check_rc(rc)
         self._plan = plan
-        cells = ctypes.c_int(0)
-        self._lib.lompc_plan_get_info(plan, None, None, ctypes.byref(cells))
-        self.cells = cells.value
+        self.cells = self.info()["cells"]
+
+    def info(self) -> dict:
+        """Batch size, parameter sets, gamma cells per set and k_eval workgroups of the plan."""
+        if self.direct:
+            return {"B": self.B, "sets": self.S, "cells": 0, "workgroups": 0}
+        B, S, cells, wg = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int(0), ctypes.c_int(0)
+        self._check_rc(self._lib.lompc_plan_get_info(self._plan, ctypes.byref(B), ctypes.byref(S), ctypes.byref(cells),
+                                                     ctypes.byref(wg)))
+        return {"B": B.value, "sets": S.value, "cells": cells.value, "workgroups": wg.value}
 
     def __del__(self):
         if getattr(self, "_plan", None) is not None:

@@ -196,8 +196,9 @@ int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, d
 int lompc_plan_status(lompc_plan* plan, void* stream, int64_t* n_repaired,
                       int64_t* n_failed, int64_t* n_invalid);
 
-/* Batch size, total parameter sets and gamma cells per set of the plan. */
-int lompc_plan_get_info(const lompc_plan* plan, int64_t* B, int64_t* S, int* cells);
+/* Batch size, total parameter sets, gamma cells per set and k_eval workgroups of the plan
+ * (any pointer may be null). */
+int lompc_plan_get_info(const lompc_plan* plan, int64_t* B, int64_t* S, int* cells, int* eval_workgroups);
 
 /* HIP-event timing of the plan's kernels (hipExtLaunchKernel start/stop events on their own
  * dispatches): enable takes a mask of (1 << LOMPC_PLAN_K_*) bits (0 = off); read synchronises

@@ -52,7 +52,7 @@ for s in $STEPS; do
     host) run host 300 python scripts/host_overhead.py ;;
     stamps) run stamps 300 python scripts/kstamps.py && KS_OUTPUTS=set run stamps_set 300 python scripts/kstamps.py && run stamps48 300 python scripts/kstamps.py 48 ;;
     fail) run fail 600 python scripts/find_failures.py ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-station ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-station --no-direct ;;
     profsplit) run profsplit 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profsplit -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-station --split-types ;;
     *) echo "unknown step $s" ;;
   esac

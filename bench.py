@@ -9,7 +9,8 @@ partition price vectors (lambda ~ theta U[0,1]^{3N}, test_lompc.py:34) and
 solve every EV's LoMPC QP (gamma_i = y_max - y0_i, y0 ~ U[0.3, 0.5],
 settings.py:27-28) with full outputs (w, cost) plus the fused per-partition
 reductions of price_solver.py:203-214; with N > 1 ranks the per-partition
-reductions are combined by one RCCL sum + one max all-reduce.  Weak scaling:
+reductions of both types are combined by ONE RCCL all-gather (lompc_amd.dist.
+combine_set_results, rank-ordered local sum / max).  Weak scaling:
 262 144 EVs per GPU (config 3; at 8 GPUs this is config 4's 2 097 152).
 
 Every step is one plan run = three launches on one stream: k_path (per (set, gamma cell)
@@ -259,7 +260,7 @@ def main():
     if path and world == 1 and len(runs) == 1:
         line["kernels"] = kernel_breakdown(runs[0], step, args, nsteps, pmc, torch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(eng, N, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(eng, N, args.cpu_seconds, args.seed)
     if path and world == 1 and not args.no_direct:
         line["direct_mode"] = direct_leg(eng, N, P, args, nsteps, dev, torch)
     if not args.no_station:
@@ -453,41 +454,55 @@ def check_station_state(st, consts):
             raise AssertionError(f"{key} does not count every EV once")
 
 
-def cpu_baseline(eng, N, seconds):
-    """C oracle (dense primal active set, oracle/lompc_oracle.c) on this host's
-    cores over a bounded sample of the same workload (both EV types, the
-    last step's partition prices)."""
+def cpu_baseline(eng, N, seconds, seed=0):
+    """C oracle (dense primal active set, oracle/lompc_oracle.c) on this host's cores over a
+    bounded sample of the same workload (both EV types, the last step's partition-0 prices):
+    the headline figure on every host thread, plus one thread (the reference's per-EV loop on
+    one core) and the lmbd_r = 3 N delta U variant (test_lompc.py:35) on every thread."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_c  # checker / baseline only
 
     oracle_c.build()
     threads = oracle_c.max_threads()
-    # calibrate, then size the sample to ~`seconds` of CPU work
+    rng = np.random.default_rng(seed + 7)
     samples = []
     for e in eng:
         g = e["gamma"].cpu().numpy()
         lm = e["lm"][-1, 0].cpu().numpy()
-        samples.append((e["c"], lm, g))
-    t0 = time.perf_counter()
-    n_cal = 256 * threads
-    for c, lm, g in samples:
-        oracle_c.solve_batch(N, c, lm, 0.0, g[:n_cal], nthreads=threads)
-    rate = 2 * n_cal / (time.perf_counter() - t0)
-    n = int(min(len(samples[0][2]), max(n_cal, rate * seconds / 2)))
-    # the batch holds fewer QPs than `seconds` of CPU work: repeat it (the same QPs, solved
-    # from scratch each pass, as the reference's per-EV loop would at every price iteration)
-    reps = max(1, int(round(rate * seconds / (2 * n))))
-    t0 = time.perf_counter()
-    done = 0
-    for _ in range(reps):
-        for c, lm, g in samples:
-            _, _, nf = oracle_c.solve_batch(N, c, lm, 0.0, g[:n], nthreads=threads)
-            assert nf == 0
-            done += n
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "QP/s", "cores": threads, "kind": "port",
+        samples.append((e["c"], lm, g, 3 * N * e["c"].delta * rng.random()))
+
+    def timed(nthreads, budget, lr_on):
+        for c, lm, g, lr in samples:  # warm-up (page-in, thread pool) before the calibration
+            oracle_c.solve_batch(N, c, lm, lr if lr_on else 0.0, g[:64 * nthreads], nthreads=nthreads)
+        n_cal = 256 * nthreads
+        t0 = time.perf_counter()
+        for c, lm, g, lr in samples:
+            oracle_c.solve_batch(N, c, lm, lr if lr_on else 0.0, g[:n_cal], nthreads=nthreads)
+        rate = 2 * n_cal / (time.perf_counter() - t0)
+        n = int(min(len(samples[0][2]), max(n_cal, rate * budget / 2)))
+        # a batch smaller than `budget` of CPU work is repeated (the same QPs solved from scratch
+        # each pass, as the reference's per-EV loop does at every price iteration)
+        reps = max(1, int(round(rate * budget / (2 * n))))
+        t0 = time.perf_counter()
+        done = 0
+        for _ in range(reps):
+            for c, lm, g, lr in samples:
+                _, _, nf = oracle_c.solve_batch(N, c, lm, lr if lr_on else 0.0, g[:n], nthreads=nthreads)
+                assert nf == 0
+                done += n
+        dt = time.perf_counter() - t0
+        return done / dt, done, reps, n, dt
+
+    v, done, reps, n, dt = timed(threads, seconds, False)
+    v1, done1, _, n1, dt1 = timed(1, seconds / 3, False)
+    vr, doner, _, nr, dtr = timed(threads, seconds / 3, True)
+    return {"value": v, "unit": "QP/s", "cores": threads, "kind": "port",
             "sample": f"{done} QPs ({reps} passes over {n} small + {n} large EVs, horizon {N}, partition-0 "
-                      f"prices) in {dt:.1f} s, C oracle dense active set, OpenMP {threads} threads"}
+                      f"prices, lmbd_r = 0) in {dt:.1f} s, C oracle dense active set, OpenMP {threads} threads",
+            "host_cpus": os.cpu_count(), "seed": seed,
+            "single_thread": {"value": v1, "sample": f"{done1} QPs in {dt1:.1f} s, 1 thread"},
+            "lmbd_r_random": {"value": vr, "sample": f"{doner} QPs in {dtr:.1f} s, {threads} threads, "
+                                                     "lmbd_r = 3 N delta U[0,1] per type"}}
 
 
 if __name__ == "__main__":

@@ -18,7 +18,6 @@ import numpy as np
 from . import _lib
 
 
-
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     """Contiguous block [lo, hi) of n items owned by ``rank``."""
     base, rem = divmod(n, world)
@@ -62,14 +61,10 @@ def combine_set_results(pairs, group=None):
     flat = [torch.cat([sw.reshape(-1), st.reshape(-1)]) for sw, st in pairs]
     packed = torch.cat(flat) if len(flat) > 1 else flat[0]
     L = packed.numel()
-    if dist.get_backend(group) == "nccl":
-        out = torch.empty(world * L, dtype=packed.dtype, device=packed.device)
-        dist.all_gather_into_tensor(out, packed, group=group)
-        rows = out.view(world, L)
-    else:  # gloo (CPU tests, one-GPU rehearsals)
-        parts = [torch.empty_like(packed) for _ in range(world)]
-        dist.all_gather(parts, packed, group=group)
-        rows = torch.stack(parts)
+    # the same collective on every backend (RCCL on the GPUs; gloo in the CPU tests)
+    out = torch.empty(world * L, dtype=packed.dtype, device=packed.device)
+    dist.all_gather_into_tensor(out, packed, group=group)
+    rows = out.view(world, L)
     tot = rows[0].clone()
     for r in range(1, world):  # fixed rank order
         tot += rows[r]
@@ -85,3 +80,25 @@ def combine_set_results(pairs, group=None):
         st.copy_(sums)
         st[:, _lib.LOMPC_STAT_MAX_ERR] = maxes[:, _lib.LOMPC_STAT_MAX_ERR]
         off += S * K
+
+
+def global_levels(y, y_max: float, group=None) -> tuple[float, float, float, int, int]:
+    """(max, min, mean, count, out-of-range count) of a sharded charge-level vector y (any
+    device) over all ranks: ONE all-gather of a 5-value record per rank and ONE host sync
+    (the reference's per-partition statistics, price_solver.py:66-77, over a sharded batch)."""
+    import torch
+    import torch.distributed as dist
+
+    n = y.numel()
+    inf = torch.tensor(float("inf"), dtype=torch.float64, device=y.device)
+    rec = torch.stack([y.max() if n else -inf, -y.min() if n else -inf, y.sum(),
+                       torch.tensor(float(n), dtype=torch.float64, device=y.device),
+                       torch.logical_not((y >= 0) & (y <= y_max)).sum().to(torch.float64)])
+    world = dist.get_world_size(group)
+    out = torch.empty(world * 5, dtype=torch.float64, device=y.device)
+    dist.all_gather_into_tensor(out, rec, group=group)
+    rows = out.view(world, 5).cpu().numpy()  # the one host sync
+    mx = rows[:, :2].max(axis=0)
+    sm = rows[:, 2:].sum(axis=0)
+    count = int(sm[1])
+    return float(mx[0]), float(-mx[1]), float(sm[0] / count) if count else float("nan"), count, int(sm[2])

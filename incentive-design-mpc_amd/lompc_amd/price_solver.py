@@ -143,21 +143,13 @@ class PriceSolver:
         self._build_plans(gamma)
 
     def _global_levels(self, y0d):
-        """Global max / min / mean / count of a sharded y0 (one MAX + one SUM all-reduce)."""
-        torch = _torch()
-        import torch.distributed as dist
+        """Global max / min / mean / count of a sharded y0: one all-gather, one host sync."""
+        from .dist import global_levels
 
-        n = y0d.numel()
-        assert bool(((y0d >= 0) & (y0d <= self.consts.y_max)).all())
-        inf = float("inf")
-        mx = torch.tensor([y0d.max().item() if n else -inf, -(y0d.min().item()) if n else -inf],
-                          dtype=torch.float64, device=self._dev)
-        sm = torch.tensor([y0d.sum().item() if n else 0.0, float(n)], dtype=torch.float64, device=self._dev)
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=self.group)
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM, group=self.group)
-        mx, sm = mx.cpu().numpy(), sm.cpu().numpy()
-        self.nEVs = int(sm[1])
-        return float(mx[0]), float(-mx[1]), float(sm[0] / sm[1])
+        y_hi, y_lo, y_mean, n, bad = global_levels(y0d, self.consts.y_max, self.group)
+        assert bad == 0  # price_solver.py:71 (0 <= y0 <= y_max on every rank)
+        self.nEVs = n
+        return y_hi, y_lo, y_mean
 
     def _build_plans(self, gamma) -> None:
         """Batch layout of one price iteration: set 0 = this rank's EVs, set 1 = the central QP."""

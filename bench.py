@@ -185,6 +185,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.warmup, nsteps):
         step(k)
+    t_issue = time.perf_counter() - t0  # host time to enqueue the K steps (GPU-bound if << dt)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -252,6 +253,7 @@ def main():
             "avg_launch_us": avg_launch_s * 1e6,
         },
         "repaired_qps": repaired,
+        "host_issue_us_per_step": t_issue / args.steps * 1e6,
     }
     pmc = load_pmc(args, N, qp_per_launch)
     if pmc and "k_eval" in pmc:

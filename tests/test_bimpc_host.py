@@ -59,7 +59,7 @@ def solve(N, P, bi, params):
 
 
 @pytest.mark.parametrize("N,P,ct,tol", [(24, 12, 2, 1e-5), (16, 12, 2, 1e-7), (24, 12, 1, 1e-7), (12, 4, 0, 1e-7),
-                                        (12, 4, 1, 1e-7)])
+                                        (12, 4, 1, 1e-7), (48, 12, 2, 1e-5), (48, 12, 1, 1e-7)])
 def test_kkt_certificate(N, P, ct, tol):
     bi, params, lit = instance(N, P, seed=N * 10 + ct, cost_type=ct)
     b, ws, wl, ug = solve(N, P, bi, params)

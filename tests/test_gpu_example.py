@@ -34,3 +34,28 @@ def test_paper_experiment_runs_and_keeps_storage_bounds(gpu, monkeypatch, seed):
     it = np.concatenate([st["niter_s"].ravel(), st["niter_l"].ravel()])
     assert np.all(it < settings.MAX_PRICE_SOLVER_ITERATIONS)
     assert np.all(np.isfinite(logs["inputs"]["u_g"])) and np.all(logs["inputs"]["u_g"] >= -1e-9)
+
+
+def test_paper_experiment_as_shipped(gpu, monkeypatch):
+    """Config 1 exactly as the example ships it: 49 hours, 500 EVs per type, horizons 12 / 16,
+    12 partitions, linear-convex prices, BiMPC EXP_UNWEIGHTED (real_time_price_control.py:11-78);
+    the same properties over the whole run, plus every EV charged at most once per step and the
+    price logs finite where a partition is populated."""
+    monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
+    consts = station_consts()
+    assert consts.simulation_length == 49 and consts.nEVs_per_EV_type == 500
+    np.random.seed(0)
+    cs = ChargingStation(consts, device=0)
+    logs = cs.simulate()
+    x = logs["states"]["x"]
+    x_max = consts.bimpc_consts.x_max
+    assert np.all(x >= -1e-6) and np.all(x <= x_max + 1e-6), x
+    st = logs["statistics"]
+    np.testing.assert_array_equal(st["Mp_s"].sum(axis=0), NUM_EVS_PER_EV_TYPE)
+    np.testing.assert_array_equal(st["Mp_l"].sum(axis=0), NUM_EVS_PER_EV_TYPE)
+    it = np.concatenate([st["niter_s"].ravel(), st["niter_l"].ravel()])
+    assert np.all(it < settings.MAX_PRICE_SOLVER_ITERATIONS)
+    pop = st["Mp_s"] > 0
+    assert np.all(np.isfinite(logs["prices"]["avg_price_s"][pop]))
+    assert np.all(np.isfinite(logs["inputs"]["u_g"])) and np.all(logs["inputs"]["u_g"] >= -1e-9)
+    assert 0 <= st["ncharged_s"] and 0 <= st["ncharged_l"]

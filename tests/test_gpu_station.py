@@ -27,7 +27,7 @@ pytestmark = pytest.mark.gpu
 TF, N_LO, N_BI, P = 3, 12, 16, 12
 
 
-def consts(M_2, Tf=TF, cost=BiMPCChargingCostType.UNWEIGHTED):
+def consts(M_2, Tf=TF, cost=BiMPCChargingCostType.UNWEIGHTED, n_lo=N_LO, n_bi=N_BI, storage=0.3):
     """The example's constants (real_time_price_control.py:26-52) with the BiMPC charging
     cost UNWEIGHTED by default: with EXP_UNWEIGHTED (rate 5) the first steps of w_hat carry
     weight 5^(t-N+1) ~ 3e-11, so they are determined only to the solvers' tolerance and two
@@ -35,9 +35,9 @@ def consts(M_2, Tf=TF, cost=BiMPCChargingCostType.UNWEIGHTED):
     BiMPC whose optimum both solvers resolve to ~1e-10."""
     cs = LoMPCConstants(0.05, 10, 0.9, 0.25, "small")
     cl = LoMPCConstants(0.025, 50, 0.9, 0.15, "large")
-    bi = BiMPCConstants(1e3, 1, 1, 0.3, 0.3, cost, 5)
-    demand = medium_term_demand_forecast(Tf + N_BI + 1, 1 / 4 * M_2 / 500, interpolate=False)  # scaled to M_2
-    return ChargingStationConstants(Tf, N_BI, N_LO, M_2, P, demand, bi, cs, cl, "linear-convex")
+    bi = BiMPCConstants(1e3, 1, 1, storage, storage, cost, 5)
+    demand = medium_term_demand_forecast(Tf + n_bi + 1, 1 / 4 * M_2 / 500, interpolate=False)  # scaled to M_2
+    return ChargingStationConstants(Tf, n_bi, n_lo, M_2, P, demand, bi, cs, cl, "linear-convex")
 
 
 def compare_logs(logs, ol):
@@ -52,18 +52,22 @@ def compare_logs(logs, ol):
         np.testing.assert_allclose(a, b, rtol=0, atol=1e-6 * scale, err_msg=k)
 
 
-def test_closed_loop_matches_oracle(gpu, monkeypatch):
+@pytest.mark.parametrize("n_lo,n_bi,storage", [(N_LO, N_BI, 0.3), (48, 48, 0.5)], ids=["example", "config5_N48"])
+def test_closed_loop_matches_oracle(gpu, monkeypatch, n_lo, n_bi, storage):
+    """The example's horizons (12 / 16) and config 5's (48 / 48; storage rate and capacity 0.5,
+    as bench.py's station leg: at horizon 48 the example's 0.3 / 0.3 leaves the first BiMPC
+    infeasible)."""
     import station_oracle as SO
 
     monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
     M_2 = 60
-    c = consts(M_2)
+    c = consts(M_2, n_lo=n_lo, n_bi=n_bi, storage=storage)
     np.random.seed(1)
     cs = ChargingStation(c, device=0)
     logs = cs.simulate()
     np.random.seed(1)
-    bi = dict(delta=1e3, c_g=1, u_g_max=1, u_b_max=0.3, x_max=0.3, cost_type=1, exp_rate=5)
-    so = SO.OracleStation(N_BI, N_LO, M_2, P, c.demand, bi, O.small_consts(), O.large_consts(), "linear-convex", TF)
+    bi = dict(delta=1e3, c_g=1, u_g_max=1, u_b_max=storage, x_max=storage, cost_type=1, exp_rate=5)
+    so = SO.OracleStation(n_bi, n_lo, M_2, P, c.demand, bi, O.small_consts(), O.large_consts(), "linear-convex", TF)
     for _ in range(TF):
         so.step()
     compare_logs(logs, so.logs)

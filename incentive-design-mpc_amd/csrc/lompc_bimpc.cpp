@@ -17,9 +17,10 @@
 // feasible (slack = distance to the bound), the 4N coupling rows carry explicit slacks.  The
 // Newton matrix is
 //     M = blockdiag(H_k + D_k, D_u) + L'QL,   H_k = 2 delta A'Omega_k A,  Q = E'D_g E (N x N),
-// with L z = u_g + sum_k c_k W_k the aggregate storage input.  It is solved through the N x N
-// Schur complement (I + T Q) y = L Hb^-1 rhs, T = sum_k c_k^2 (H_k + D_k)^-1 + D_u^-1:
-// O(2P N^3) per iteration instead of O(((2P+1) N)^3).
+// with L z = u_g + sum_k c_k W_k the aggregate storage input.  It is solved by Woodbury in the
+// coupling rows (Newton::factor): tridiagonal block factors (O(N) each, O(N^2) for the explicit
+// inverses) and one 2N x 2N Cholesky, O(2P N^2 + N^3) per iteration instead of
+// O(((2P+1) N)^3).
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -244,53 +245,87 @@ static bool chol_blocked(double* a, int m) {
 
 struct Newton {
   int N = 0, nb = 0, n = 0;
-  std::vector<double> Hf;   // [nb][N*N] Cholesky factors of H_k + D_k
   std::vector<double> Du;   // [N]
   std::vector<double> Q;    // [N*N]
-  std::vector<double> W;    // [4N*4N] Cholesky of D_g^-1 + E T E'
+  std::vector<double> W;    // [2N*2N] Cholesky of D2^-1 + F T F'
   std::vector<double> ck;
-  std::vector<double> Xk;   // [nb][N*N] H_k^-1
+  std::vector<double> Xk;   // [nb][N*N] T_k^-1 (H_k^-1 = A^-1 T_k^-1 A^-T)
+  std::vector<double> Lf, Df;  // [N][nb] LDL' factors of the T_k, stage-major (hb_solve)
   mutable std::vector<double> hb_tmp;
 
-  // factor M for the current iterate; dk: [n] box barrier diagonal, dg: [4N] coupling D_g
+  // factor M for the current iterate; dbox: [n] box barrier diagonal, dg: [4N] coupling D_g.
+  //
+  // Block k: H_k = 2 delta A'Omega_k A + D_k = A' (Omega'_k + A^-T D_k A^-1) A with A^-1 the
+  // difference operator, so the middle factor T_k is TRIDIAGONAL (diagonal Omega'_t + D_t +
+  // D_{t+1}, off-diagonal -D_{t+1}): an O(N) LDL' and H_k^-1 = A^-1 T_k^-1 A^-T in O(N^2),
+  // instead of a dense Cholesky and inverse (O(N^3)) per block.
+  //
+  // Coupling rows: the 4N rows come in +/- pairs on the same linear forms (v_t and (A v)_t), so
+  // E'D_g E = F'D_2 F with F = [I; A] and D_2 = the pairwise sums of D_g: the Woodbury matrix
+  // is W = D_2^-1 + F T F' (2N x 2N) — the same Newton step as the 4N form at 1/8 of its
+  // Cholesky.  An active row (D_g -> inf) keeps F T F'; inactive rows become a large diagonal.
   bool factor(const Bimpc& B, const double* z, const double* dbox, const double* dg) {
     N = B.N;
     nb = B.nb;
     n = B.n;
     ck = B.ck;
-    Hf.assign((size_t)nb * N * N, 0.0);
     Xk.resize((size_t)nb * N * N);
+    Lf.resize((size_t)nb * N);
+    Df.resize((size_t)nb * N);
     std::vector<double> T((size_t)N * N, 0.0);
     std::vector<char> okk(nb, 1);
     BlockPool::get().run(nb, [&](int k) {
-      double* H = &Hf[(size_t)k * N * N];
-      // 2 delta A'Omega A: (i,j) -> 2 delta sum_{t >= max(i,j)} omega_t
-      double s = 0.0;
-      std::vector<double> suf(N), work((size_t)N * N);
-      for (int t = N - 1; t >= 0; --t) {
-        s += B.omega[k * N + t];
-        suf[t] = 2.0 * B.delta * s;
-      }
-      for (int i = 0; i < N; ++i)
-        for (int j = 0; j < N; ++j) H[i * N + j] = suf[std::max(i, j)];
-      for (int i = 0; i < N; ++i) H[i * N + i] += dbox[k * N + i];
+      double* X = &Xk[(size_t)k * N * N];
+      std::vector<double> dd(N), l(N);
       // static regularisation (the EXP weights 5^(t-N+1) leave early steps with almost no
       // curvature); iterative refinement against the exact matrix removes its bias
-      const double rho = 1e-11 * (1.0 + suf[0]);  // relative to the charging curvature, not the barrier
-      for (int i = 0; i < N; ++i) H[i * N + i] += rho;
-      if (!lqd::chol(H, N)) {
-        okk[k] = 0;
-        return;
+      double s = 0.0;
+      for (int t = 0; t < N; ++t) s += B.omega[k * N + t];
+      const double rho = 1e-11 * (1.0 + 2.0 * B.delta * s);  // relative to the charging curvature
+      // LDL' of the tridiagonal T_k: diag a_t, sub-diagonal c_t = -D_{t+1} (rows t+1, t)
+      double prev_l = 0.0, prev_d = 0.0;
+      for (int t = 0; t < N; ++t) {
+        const double Dt = dbox[k * N + t] + rho;
+        const double Dn = t + 1 < N ? dbox[k * N + t + 1] + rho : 0.0;
+        double a = 2.0 * B.delta * B.omega[k * N + t] + Dt + Dn;
+        if (t > 0) a -= prev_l * prev_l * prev_d;
+        if (!(a > 0.0)) {
+          okk[k] = 0;
+          return;
+        }
+        dd[t] = a;
+        l[t] = t + 1 < N ? -Dn / a : 0.0;  // L_{t+1,t}
+        Df[(size_t)t * nb + k] = a;
+        Lf[(size_t)t * nb + k] = l[t];
+        prev_l = l[t];
+        prev_d = a;
       }
-      lqd::chol_inverse(H, N, &Xk[(size_t)k * N * N], work.data());  // H_k^-1 (T and hb_solve)
+      // X = T_k^-1 from the LDL' factors: X_jj = 1/d_j + l_j^2 X_{j+1,j+1} and, above the
+      // diagonal, row i = -l_i x row i+1 (L'X = D^-1 L^-1 is lower triangular); rows are
+      // independent vector operations, no per-column substitution chains
+      X[(size_t)(N - 1) * N + N - 1] = 1.0 / dd[N - 1];
+      for (int i = N - 2; i >= 0; --i) {
+        double* xi = X + (size_t)i * N;
+        const double* x1 = xi + N;
+        const double li = l[i];
+        for (int j = i + 1; j < N; ++j) xi[j] = -li * x1[j];
+        xi[i] = 1.0 / dd[i] + li * li * x1[i + 1];
+      }
+      for (int i = 1; i < N; ++i)  // lower triangle by symmetry
+        for (int j = 0; j < i; ++j) X[(size_t)i * N + j] = X[(size_t)j * N + i];
     });
     for (int k = 0; k < nb; ++k) {
       if (!okk[k]) return false;
       if (ck[k] == 0.0) continue;
-      const double c2 = ck[k] * ck[k];  // T += c_k^2 H_k^-1, in block order
+      const double c2 = ck[k] * ck[k];  // sum c_k^2 T_k^-1, in block order
       const double* X = &Xk[(size_t)k * N * N];
       for (size_t e = 0; e < (size_t)N * N; ++e) T[e] += c2 * X[e];
     }
+    // T = A^-1 (sum c_k^2 T_k^-1) A^-T: differences along the columns, then along the rows
+    for (int i = N - 1; i > 0; --i)
+      for (int j = 0; j < N; ++j) T[(size_t)i * N + j] -= T[(size_t)(i - 1) * N + j];
+    for (int i = 0; i < N; ++i)
+      for (int j = N - 1; j > 0; --j) T[(size_t)i * N + j] -= T[(size_t)i * N + j - 1];
     Du.assign(N, 0.0);
     for (int t = 0; t < N; ++t) {
       const double u = z[nb * N + t];
@@ -298,7 +333,7 @@ struct Newton {
       if (!(Du[t] > 0.0)) return false;
       T[t * N + t] += 1.0 / Du[t];
     }
-    // Q = E' D_g E = diag(d0 + d1) + A' diag(d2 + d3) A
+    // Q = E' D_g E = diag(d0 + d1) + A' diag(d2 + d3) A  (apply() uses the exact matrix)
     Q.assign((size_t)N * N, 0.0);
     {
       double s = 0.0;
@@ -311,49 +346,55 @@ struct Newton {
         for (int j = 0; j < N; ++j) Q[i * N + j] = suf[std::max(i, j)];
       for (int i = 0; i < N; ++i) Q[i * N + i] += dg[i] + dg[N + i];
     }
-    // Woodbury in the coupling rows: M^-1 = Hb^-1 - Hb^-1 L'E' W^-1 E L Hb^-1 with the SPD
-    // W = D_g^-1 + E T E' (4N x 4N).  Unlike a solve with I + T Q, W stays well scaled as the
-    // interior point converges: active rows (D_g -> inf) keep E T E', inactive rows become a
-    // large diagonal.
-    const int m = 4 * N;
-    std::vector<double> ET((size_t)m * N);  // rows of E T: -T, T, -A T, A T
-    for (int t = 0; t < N; ++t)
-      for (int j = 0; j < N; ++j) {
-        const double v = T[t * N + j];
-        const double pv = (t ? ET[(size_t)(3 * N + t - 1) * N + j] : 0.0) + v;  // (A T)_t = sum_{u<=t} T_u
-        ET[(size_t)t * N + j] = -v;
-        ET[(size_t)(N + t) * N + j] = v;
-        ET[(size_t)(2 * N + t) * N + j] = -pv;
-        ET[(size_t)(3 * N + t) * N + j] = pv;
-      }
+    // W = D_2^-1 + F T F' with F = [I; A]: blocks T, T A', A T, A T A'
+    const int m = 2 * N;
+    std::vector<double> AT((size_t)N * N);  // (A T)_ij = sum_{u <= i} T_uj
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) AT[(size_t)i * N + j] = T[(size_t)i * N + j] + (i ? AT[(size_t)(i - 1) * N + j] : 0.0);
     W.assign((size_t)m * m, 0.0);
-    std::vector<double> ps(N);
-    for (int a = 0; a < m; ++a) {
-      const double* e = &ET[(size_t)a * N];
+    for (int i = 0; i < N; ++i) {
       double acc = 0.0;
-      for (int t = 0; t < N; ++t) ps[t] = (acc += e[t]);
-      for (int t = 0; t < N; ++t) {  // (E T E')_{a,b} for the four row blocks b of E
-        W[(size_t)a * m + t] = -e[t];
-        W[(size_t)a * m + N + t] = e[t];
-        W[(size_t)a * m + 2 * N + t] = -ps[t];
-        W[(size_t)a * m + 3 * N + t] = ps[t];
+      for (int j = 0; j < N; ++j) {
+        W[(size_t)i * m + j] = T[(size_t)i * N + j];
+        W[(size_t)i * m + N + j] = AT[(size_t)j * N + i];          // (T A')_ij = (A T)_ji
+        W[(size_t)(N + i) * m + j] = AT[(size_t)i * N + j];
+        acc += AT[(size_t)i * N + j];                              // (A T A')_ij = sum_{u<=j} (A T)_iu
+        W[(size_t)(N + i) * m + N + j] = acc;
       }
-      W[(size_t)a * m + a] += 1.0 / dg[a];
+    }
+    for (int t = 0; t < N; ++t) {
+      W[(size_t)t * m + t] += 1.0 / (dg[t] + dg[N + t]);
+      W[(size_t)(N + t) * m + N + t] += 1.0 / (dg[2 * N + t] + dg[3 * N + t]);
     }
     return chol_blocked(W.data(), m);
   }
 
   void hb_solve(double* x) const {  // Hb^-1 in place
-    // products with the explicit block inverses (independent row dots, no substitution chain:
-    // ~3x faster than two triangular solves at N = 48; the refinement in solve() runs against
-    // the exact matrix).  Sequential: below the pool's dispatch cost (measured on the GPU box).
-    hb_tmp.resize(N);
-    double* tmp = hb_tmp.data();
+    // H_k^-1 x = A^-1 T_k^-1 A^-T x with the tridiagonal LDL' factors: differences and
+    // bidiagonal substitutions, O(N) per block; the blocks are interleaved (stage-major) so
+    // their independent recurrences overlap instead of running as one long chain
+    hb_tmp.resize((size_t)N * nb);
+    double* v = hb_tmp.data();  // [t][k]
     for (int k = 0; k < nb; ++k) {
-      const double* X = &Xk[(size_t)k * N * N];
+      const double* xk = x + (size_t)k * N;
+      for (int t = 0; t < N; ++t) v[(size_t)t * nb + k] = xk[t] - (t + 1 < N ? xk[t + 1] : 0.0);  // A^-T
+    }
+    for (int t = 1; t < N; ++t) {  // L w = v
+      double* vt = v + (size_t)t * nb;
+      const double* vp = vt - nb;
+      const double* lp = &Lf[(size_t)(t - 1) * nb];
+      for (int k = 0; k < nb; ++k) vt[k] -= lp[k] * vp[k];
+    }
+    for (size_t e = 0; e < (size_t)N * nb; ++e) v[e] /= Df[e];
+    for (int t = N - 2; t >= 0; --t) {  // L' u = D^-1 w
+      double* vt = v + (size_t)t * nb;
+      const double* vn = vt + nb;
+      const double* lt = &Lf[(size_t)t * nb];
+      for (int k = 0; k < nb; ++k) vt[k] -= lt[k] * vn[k];
+    }
+    for (int k = 0; k < nb; ++k) {
       double* xk = x + (size_t)k * N;
-      for (int i = 0; i < N; ++i) tmp[i] = lqd::dot(X + (size_t)i * N, xk, N);
-      std::copy(tmp, tmp + N, xk);
+      for (int t = 0; t < N; ++t) xk[t] = v[(size_t)t * nb + k] - (t ? v[(size_t)(t - 1) * nb + k] : 0.0);  // A^-1
     }
     for (int t = 0; t < N; ++t) x[nb * N + t] /= Du[t];
   }
@@ -411,12 +452,20 @@ struct Newton {
   }
 
   void solve_reg(const Bimpc& B, const double* rhs, double* dz) const {
-    std::vector<double> t1(rhs, rhs + n), y(N), ey(4 * N), g(N), tmp(n);
+    std::vector<double> t1(rhs, rhs + n), y(N), fy(2 * N), g(N), tmp(n);
     hb_solve(t1.data());
     mulL(B, t1.data(), y.data());
-    mulE(N, y.data(), ey.data());
-    lqd::chol_solve(W.data(), 4 * N, ey.data());
-    mulEt(N, ey.data(), g.data());
+    double acc = 0.0;
+    for (int t = 0; t < N; ++t) {  // F y = [y; A y]
+      fy[t] = y[t];
+      fy[N + t] = (acc += y[t]);
+    }
+    lqd::chol_solve(W.data(), 2 * N, fy.data());
+    acc = 0.0;
+    for (int t = N - 1; t >= 0; --t) {  // F' v = v_0 + A' v_1
+      acc += fy[N + t];
+      g[t] = fy[t] + acc;
+    }
     mulLt(B, g.data(), tmp.data());
     hb_solve(tmp.data());
     for (int i = 0; i < n; ++i) dz[i] = t1[i] - tmp[i];

@@ -1139,6 +1139,19 @@ int lompc_plan_create(int n_ctx, lompc_ctx* const* ctxs, const int64_t* sets_per
   return LOMPC_OK;
 }
 
+int lompc_plan_update(lompc_plan* p, int64_t B, const double* gamma, const int64_t* set_offsets,
+                      const double* w_ref, void* stream) {
+  if (!p) return LOMPC_ERR_INVALID_ARG;
+  HIPCHK(p, hipSetDevice(p->device));
+  int64_t spc[LQ_PLAN_MAX_CTX];
+  for (int k = 0, prev = 0; k < p->nctx; ++k) {  // the plan's set counts per context
+    const int e = k + 1 < p->nctx ? p->ce.end[k] : (int)p->S;
+    spc[k] = e - prev;
+    prev = e;
+  }
+  return lq_plan_prepare(p, p->nctx, p->ctx, spc, B, gamma, set_offsets, w_ref, p->flags, (hipStream_t)stream);
+}
+
 int lompc_plan_run(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
                    int8_t* status, double* set_sum_w, double* set_stats, void* stream) {
   if (!p) return LOMPC_ERR_INVALID_ARG;

@@ -79,6 +79,7 @@ SIGNATURES = [
     ("lompc_plan_run", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_plan_status", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_get_info", _I, [_P, _P, _P, _P, _P]),
+    ("lompc_plan_update", _I, [_P, _L, _P, _P, _P, _P]),
     ("lompc_plan_profile_enable", _I, [_P, _I]),
     ("lompc_plan_profile_read", _I, [_P, _I, _P, _P, _I]),
     ("lompc_plan_last_error", ctypes.c_char_p, [_P]),

@@ -350,12 +350,7 @@ class BatchPlan:
             raise ValueError("BatchPlan: every LoMPC must have the same horizon and device")
         if len(lompcs) > _lib.LOMPC_PLAN_MAX_CTX:
             raise ValueError(f"BatchPlan: at most {_lib.LOMPC_PLAN_MAX_CTX} contexts")
-        self.gamma = lo._dev(gamma).reshape(-1)
-        B = self.gamma.numel()
-        self.off = np.ascontiguousarray(np.asarray(set_offsets, dtype=np.int64))
-        S = self.off.shape[0] - 1
-        if S < 1 or self.off[0] != 0 or self.off[-1] != B or np.any(np.diff(self.off) < 0):
-            raise ValueError("set_offsets must be non-decreasing from 0 to B")
+        S = np.asarray(set_offsets).shape[0] - 1
         if sets_per_ctx is None:
             if len(lompcs) != 1:
                 raise ValueError("sets_per_ctx required with several contexts")
@@ -363,47 +358,68 @@ class BatchPlan:
         self.sets_per_ctx = np.ascontiguousarray(np.asarray(sets_per_ctx, dtype=np.int64))
         if self.sets_per_ctx.shape != (len(lompcs),) or int(self.sets_per_ctx.sum()) != S:
             raise ValueError("sets_per_ctx must give one count per context, summing to S")
-        if validate:  # (callers that already checked 0 <= gamma <= y_max skip two host syncs)
-            ym = np.repeat([x.y_max for x in lompcs], self.sets_per_ctx)
-            ymax_ev = torch.as_tensor(np.repeat(ym, np.diff(self.off)), device=self.gamma.device)
-            if bool((self.gamma > ymax_ev).any()):
-                raise AssertionError("gamma <= y_max required")
-            if bool(torch.logical_not(self.gamma >= 0).any()):
-                raise ValueError("Parameter value must be nonnegative.")
-        self.S, self.B, self.N = S, B, N
-        dev = f"cuda:{lo.device}"
-        self.w_ref = None if w_ref is None else lo._dev(w_ref).reshape(S, N)
-        self.gamma_ref = None if gamma_ref is None else lo._dev(gamma_ref).reshape(S)
-        e = lambda shape, dt=torch.float64: torch.empty(shape, dtype=dt, device=dev)
-        self.out = {
-            "w": e((B, N)) if want_w else None,
-            "cost": e((B,)) if want_cost else None,
-            "w0": e((B,)) if want_w0 else None,
-            "status": e((B,), torch.int8) if want_status else None,
-            "set_sum_w": e((S, N)) if want_set else None,
-            "set_stats": e((S, _lib.LOMPC_SET_STATS)) if want_set else None,
-        }
+        self.N = N
+        self._want = dict(w=want_w, cost=want_cost, w0=want_w0, status=want_status, set=want_set)
         self._stream = (stream if stream is not None else torch.cuda.current_stream(lo.device)).cuda_stream
-        self._outs = [_ptr(self.out[k]) for k in ("w", "cost", "w0", "status", "set_sum_w", "set_stats")]
         self._lib = lo._lib
         self._plan = None
         self.direct = any(x.mode == "direct" for x in lompcs)
+        if self.direct and len(lompcs) != 1:
+            raise ValueError("DIRECT mode plans hold one context")
+        self.gamma_ref = None if gamma_ref is None else lo._dev(gamma_ref).reshape(S)
+        self._layout(gamma, set_offsets, w_ref, validate)
         if self.direct:
-            if len(lompcs) != 1:
-                raise ValueError("DIRECT mode plans hold one context")
-            self._args = [_ptr(self.w_ref), _ptr(self.gamma_ref), B, _ptr(self.gamma), self.off.ctypes.data] + \
-                self._outs + [self._stream]
             return
         ctxs = (ctypes.c_void_p * len(lompcs))(*[x._ctx.value for x in lompcs])
         plan = ctypes.c_void_p()
         flags = (_lib.LOMPC_PLAN_WARM_START if warm_start else 0) | (_lib.LOMPC_PLAN_DIAG_REPAIR if diag_repair else 0)
         rc = self._lib.lompc_plan_create(len(lompcs), ctypes.cast(ctxs, ctypes.c_void_p), self.sets_per_ctx.ctypes.data,
-                                         B, _ptr(self.gamma), self.off.ctypes.data, _ptr(self.w_ref), flags,
+                                         self.B, _ptr(self.gamma), self.off.ctypes.data, _ptr(self.w_ref), flags,
                                          self._stream, ctypes.byref(plan))
         if rc != _lib.LOMPC_OK:
             lo._check_rc(rc)
         self._plan = plan
         self.cells = self.info()["cells"]
+
+    def _layout(self, gamma, set_offsets, w_ref, validate) -> None:
+        """Validate and take a batch (gamma, set_offsets, w_ref); (re)allocate the outputs when
+        the batch size changed."""
+        torch = _torch()
+        lo, N = self.lompc, self.N
+        gamma = lo._dev(gamma).reshape(-1)
+        B = gamma.numel()
+        off = np.ascontiguousarray(np.asarray(set_offsets, dtype=np.int64))
+        S = off.shape[0] - 1
+        if S < 1 or off[0] != 0 or off[-1] != B or np.any(np.diff(off) < 0):
+            raise ValueError("set_offsets must be non-decreasing from 0 to B")
+        if S != int(self.sets_per_ctx.sum()):
+            raise ValueError("the number of parameter sets is fixed for a plan")
+        if validate:  # (callers that already checked 0 <= gamma <= y_max skip two host syncs)
+            ym = np.repeat([x.y_max for x in self.lompcs], self.sets_per_ctx)
+            ymax_ev = torch.as_tensor(np.repeat(ym, np.diff(off)), device=gamma.device)
+            if bool((gamma > ymax_ev).any()):
+                raise AssertionError("gamma <= y_max required")
+            if bool(torch.logical_not(gamma >= 0).any()):
+                raise ValueError("Parameter value must be nonnegative.")
+        self.gamma, self.off = gamma, off
+        self.w_ref = None if w_ref is None else lo._dev(w_ref).reshape(S, N)
+        if getattr(self, "B", None) != B or getattr(self, "S", None) != S:
+            dev = f"cuda:{lo.device}"
+            e = lambda shape, dt=torch.float64: torch.empty(shape, dtype=dt, device=dev)
+            wt = self._want
+            self.out = {
+                "w": e((B, N)) if wt["w"] else None,
+                "cost": e((B,)) if wt["cost"] else None,
+                "w0": e((B,)) if wt["w0"] else None,
+                "status": e((B,), torch.int8) if wt["status"] else None,
+                "set_sum_w": e((S, N)) if wt["set"] else None,
+                "set_stats": e((S, _lib.LOMPC_SET_STATS)) if wt["set"] else None,
+            }
+            self._outs = [_ptr(self.out[k]) for k in ("w", "cost", "w0", "status", "set_sum_w", "set_stats")]
+        self.S, self.B = S, B
+        if self.direct:
+            self._args = [_ptr(self.w_ref), _ptr(self.gamma_ref), B, _ptr(self.gamma), self.off.ctypes.data] + \
+                self._outs + [self._stream]
 
     def info(self) -> dict:
         """Batch size, parameter sets, gamma cells per set and k_eval workgroups of the plan."""
@@ -413,6 +429,17 @@ class BatchPlan:
         self._check_rc(self._lib.lompc_plan_get_info(self._plan, ctypes.byref(B), ctypes.byref(S), ctypes.byref(cells),
                                                      ctypes.byref(wg)))
         return {"B": B.value, "sets": S.value, "cells": cells.value, "workgroups": wg.value}
+
+    def update(self, gamma, set_offsets, w_ref=None, validate=True) -> "BatchPlan":
+        """Re-target the plan at a new batch with the same contexts and set counts (e.g. the
+        next partition of a price loop): device buffers, events and pinned staging are reused,
+        the outputs are reallocated only when the batch size changes."""
+        self._layout(gamma, set_offsets, w_ref, validate)
+        if not self.direct:
+            rc = self._lib.lompc_plan_update(self._plan, self.B, _ptr(self.gamma), self.off.ctypes.data,
+                                             _ptr(self.w_ref), self._stream)
+            self._check_rc(rc)
+        return self
 
     def __del__(self):
         if getattr(self, "_plan", None) is not None:

@@ -75,6 +75,7 @@ class PriceSolver:
         self._h_st = torch.zeros((2, _lib.LOMPC_SET_STATS), dtype=torch.float64).pin_memory()
         self._plan = None
         self._plan_w0 = None
+        self._w0_live = False
         self._A_bar_inv = None
         self._kappa = None
         self.n_batched_calls = 0
@@ -164,11 +165,22 @@ class PriceSolver:
         off = np.array([0, B, B + central], dtype=np.int64)
         # gamma = y_max - y0 with 0 <= y0 <= y_max asserted in set_charge_levels.  The price
         # iterations change the prices a little at a time: each gamma cell's exact solve starts
-        # from the working set the previous iteration ended with there.
-        self._plan = BatchPlan(self.lompc, self._gam, off, w_ref=self._wr2, want_w=False, want_cost=False,
-                               want_set=True, validate=False, warm_start=True)
-        self._plan_w0 = BatchPlan(self.lompc, self._gam[:B], np.array([0, B], dtype=np.int64), want_w=False,
-                                  want_cost=False, want_w0=True, want_set=True, validate=False) if B else None
+        # from the working set the previous iteration ended with there.  The plans are built once
+        # and re-targeted at every partition (lompc_plan_update: no allocation, no device sync).
+        if self._plan is None:
+            self._plan = BatchPlan(self.lompc, self._gam, off, w_ref=self._wr2, want_w=False, want_cost=False,
+                                   want_set=True, validate=False, warm_start=True)
+        else:
+            self._plan.update(self._gam, off, w_ref=self._wr2, validate=False)
+        if not B:
+            self._w0_live = False
+        elif self._plan_w0 is None:
+            self._plan_w0 = BatchPlan(self.lompc, self._gam[:B], np.array([0, B], dtype=np.int64), want_w=False,
+                                      want_cost=False, want_w0=True, want_set=True, validate=False)
+            self._w0_live = True
+        else:
+            self._plan_w0.update(self._gam[:B], np.array([0, B], dtype=np.int64), validate=False)
+            self._w0_live = True
         self._B = B
 
     def compute_optimal_prices(self, w_ref: np.ndarray, lmbd_r: float) -> tuple[np.ndarray, dict]:
@@ -374,7 +386,7 @@ class PriceSolver:
         h[: self.r] = lmbd
         h[2 * N3:2 * N3 + 2] = float(lmbd_r)
         self._in.copy_(self._h_in, non_blocking=True)
-        if self._plan_w0 is not None:
+        if self._plan_w0 is not None and self._w0_live:
             out = self._plan_w0.run(self._lm2[:1], self._lr2[:1])
             st = out["set_stats"]
             w0 = out["w0"]

@@ -181,6 +181,13 @@ int lompc_plan_create(int n_ctx, lompc_ctx* const* ctxs, const int64_t* sets_per
                       int64_t B, const double* gamma, const int64_t* set_offsets,
                       const double* w_ref, int flags, void* stream, lompc_plan** out);
 
+/* Re-target a plan at a new batch of the same contexts and set counts (B, gamma,
+ * set_offsets, w_ref as in lompc_plan_create): device workspaces, events and the pinned
+ * staging are reused (grown when needed), the gamma windows re-measured on `stream`.  The
+ * cheap way to move a price loop from one partition to the next. */
+int lompc_plan_update(lompc_plan* plan, int64_t B, const double* gamma, const int64_t* set_offsets,
+                      const double* w_ref, void* stream);
+
 /* One price iteration of the whole batch: the exact LoMPC optimum of every EV at the
  * prices of its set plus the fused per-set reductions.  Outputs as lompc_solve_batch, in
  * the caller's EV order (each may be NULL):

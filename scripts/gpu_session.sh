@@ -33,6 +33,8 @@ for s in $STEPS; do
     qev8) LOMPC_LIB=liblompc_amd_ev8.so run qev8 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_baseline_configs.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     station5) run station5 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-direct --station-evs-per-gpu 2097152 --station-steps 5 --station-warmup 1 ;;
     qnew) run qnew 600 python -u -m pytest tests/test_gpu_example.py tests/test_gpu_station.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    sprof) run sprof 300 python scripts/station_profile.py ;;
+    bimpc) run bimpc 300 python scripts/bimpc_timing.py ;;
     bcost) run bcost 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs cost ;;
     bset) run bset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs set ;;
     bfused) LOMPC_REDUCE_FUSED=1 run bfused 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;

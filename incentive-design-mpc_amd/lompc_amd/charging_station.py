@@ -78,8 +78,8 @@ def shard_bounds(n: int, rank: int, world: int) -> tuple[int, int]:
 
 def partition_stats(y, idx, P: int, group=None) -> np.ndarray:
     """Per partition (count, max, min, sum) of y over the EVs with idx == p, combined over
-    ranks (one MAX and one SUM all-reduce).  Returns a host (P, 4) array; empty partitions
-    have count 0."""
+    ranks (one all-gather of the per-rank records, reduced locally in rank order).  Returns a
+    host (P, 4) array; empty partitions have count 0."""
     torch = _torch()
     # masked column reductions over an (n, P) view: P is small, and scatter/atomic forms
     # (bincount, index_add_, scatter_reduce) serialise n updates on P addresses
@@ -89,15 +89,22 @@ def partition_stats(y, idx, P: int, group=None) -> np.ndarray:
     sm = torch.where(onehot, yy, 0.0).sum(0)
     mx = torch.where(onehot, yy, -float("inf")).amax(0)
     mn = torch.where(onehot, yy, float("inf")).amin(0)
-    if group is not None:
-        import torch.distributed as dist
+    rec = torch.stack([cnt, mx, mn, sm], dim=1)
+    if group is None:
+        return rec.cpu().numpy()
+    import torch.distributed as dist
 
-        a = torch.cat([cnt, sm])
-        b = torch.cat([mx, -mn])
-        dist.all_reduce(a, op=dist.ReduceOp.SUM, group=group)
-        dist.all_reduce(b, op=dist.ReduceOp.MAX, group=group)
-        cnt, sm, mx, mn = a[:P], a[P:], b[:P], -b[P:]
-    return torch.stack([cnt, mx, mn, sm], dim=1).cpu().numpy()
+    world = dist.get_world_size(group)
+    out = torch.empty((world * P, 4), dtype=torch.float64, device=y.device)
+    dist.all_gather_into_tensor(out, rec.contiguous(), group=group)
+    rows = out.view(world, P, 4).cpu().numpy()  # the one host sync
+    tot = rows[0].copy()
+    for r in range(1, world):  # fixed rank order
+        tot[:, 0] += rows[r, :, 0]
+        tot[:, 3] += rows[r, :, 3]
+    tot[:, 1] = rows[:, :, 1].max(axis=0)
+    tot[:, 2] = rows[:, :, 2].min(axis=0)
+    return tot
 
 
 def redraw_full(y, mask, lo_val: float, hi_val: float, rng_random, group=None) -> int:
@@ -203,11 +210,10 @@ class ChargingStation:
 
     def _update_indices(self) -> None:
         # charging_station.py:111-116 (later partitions win on shared edges, as there)
-        for p in range(self.P):
-            mask_s = (self.y_s >= self.y0_s_rng[p]) & (self.y_s <= self.y0_s_rng[p + 1])
-            self.idx_s[mask_s] = p
-            mask_l = (self.y_l >= self.y0_l_rng[p]) & (self.y_l <= self.y0_l_rng[p + 1])
-            self.idx_l[mask_l] = p
+        for p in range(self.P):  # masked_fill_: no host sync (boolean-index assignment would)
+            self.idx_s.masked_fill_((self.y_s >= self.y0_s_rng[p]) & (self.y_s <= self.y0_s_rng[p + 1]), p)
+            self.idx_l.masked_fill_((self.y_l >= self.y0_l_rng[p]) & (self.y_l <= self.y0_l_rng[p + 1]), p)
+        self._layout = {}
 
     def _init_logs(self, consts: ChargingStationConstants) -> None:
         # charging_station.py:118-149
@@ -333,7 +339,8 @@ class ChargingStation:
                     ("Small", self.price_solver_s, self.y_s, self.idx_s, st_s, w_hat_s_opt, prices_s, stats_s),
                     ("Large", self.price_solver_l, self.y_l, self.idx_l, st_l, w_hat_l_opt, prices_l, stats_l)):
                 if st[p, 0] > 0:
-                    solver.set_charge_levels(y[idx == p])
+                    ys, off = self._partition_layout(kind, y, idx)
+                    solver.set_charge_levels_stats(ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3])
                     if PRINT_LEVEL >= 1 and self._rank0():
                         print(f"{kind} EVs, partition {p:2d}: ", end="")
                         if PRINT_LEVEL >= 2:
@@ -347,15 +354,27 @@ class ChargingStation:
                     stats.append({})
         return prices_s, prices_l, stats_s, stats_l
 
-    def _w0_batched(self, solver: PriceSolver, y, idx, prices, lmbd_r):
+    def _partition_layout(self, kind, y, idx):
+        """This rank's EVs of one type grouped by partition (stable), once per step: (charge
+        levels in that order, host offsets [P+1]) — per-partition slices without boolean
+        indexing (one host sync per type and step instead of one per partition)."""
+        torch = _torch()
+        if kind not in self._layout:
+            perm = torch.argsort(idx, stable=True)
+            counts = torch.bincount(idx, minlength=self.P)[: self.P].cpu().numpy()
+            off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+            self._layout[kind] = (perm, off, y[perm])
+        perm, off, ys = self._layout[kind]
+        return ys, off
+
+    def _w0_batched(self, kind, solver: PriceSolver, y, idx, prices, lmbd_r):
         """All partitions of one EV type in ONE engine call (price_solver.py:272-285 per partition).
         Returns (w0 in EV order, per-partition (sum w0, sum price0, count) combined over ranks)."""
         torch = _torch()
         N, P = self.N_lo, self.P
-        perm = torch.argsort(idx, stable=True)
-        counts = (idx.unsqueeze(1) == torch.arange(P, device=idx.device).unsqueeze(0)).sum(0)
-        off = np.concatenate([[0], np.cumsum(counts.cpu().numpy())]).astype(np.int64)
-        gamma = (solver.consts.y_max - y)[perm].contiguous()
+        ys, off = self._partition_layout(kind, y, idx)
+        perm = self._layout[kind][0]
+        gamma = (solver.consts.y_max - ys).contiguous()
         lm = np.zeros((P, 3 * N))
         lm[:, : self.r] = prices
         lompc = solver.lompc
@@ -380,8 +399,8 @@ class ChargingStation:
 
     def _get_w0_price0(self, prices_s, prices_l, lmbd_r: float):
         # charging_station.py:310-329
-        w0_s, red_s = self._w0_batched(self.price_solver_s, self.y_s, self.idx_s, prices_s, lmbd_r)
-        w0_l, red_l = self._w0_batched(self.price_solver_l, self.y_l, self.idx_l, prices_l, lmbd_r)
+        w0_s, red_s = self._w0_batched("Small", self.price_solver_s, self.y_s, self.idx_s, prices_s, lmbd_r)
+        w0_l, red_l = self._w0_batched("Large", self.price_solver_l, self.y_l, self.idx_l, prices_l, lmbd_r)
         price0_s, price0_l = np.zeros((self.P,)), np.zeros((self.P,))
         for p in range(self.P):
             if red_s[p, 2] > 0:

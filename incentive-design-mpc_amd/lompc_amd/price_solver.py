@@ -76,6 +76,7 @@ class PriceSolver:
         self._plan = None
         self._plan_w0 = None
         self._w0_live = False
+        self._A_bar = None
         self._A_bar_inv = None
         self._kappa = None
         self.n_batched_calls = 0
@@ -142,6 +143,20 @@ class PriceSolver:
         self.gamma_sc = self.consts.y_max - (y_hi + y_lo) / 2
         self.gamma_sm = self.consts.y_max - y_mean
         self._build_plans(gamma)
+
+    def set_charge_levels_stats(self, y0d, n: int, y_hi: float, y_lo: float, y_sum: float) -> None:
+        """set_charge_levels for a device slice of charge levels whose (global) count / max /
+        min / sum the caller already has (ChargingStation computes every partition's in one pass
+        per step, charging_station.py:187-266): no host sync, no collective."""
+        if not (n > 0 and 0.0 <= y_lo <= y_hi <= self.consts.y_max):
+            raise AssertionError("0 <= y0 <= y_max required (price_solver.py:71)")
+        self.y0 = y0d
+        self.nEVs = int(n)
+        self._y_hi, self._y_lo = float(y_hi), float(y_lo)
+        self.y0_rng = (y_hi - y_lo) / 2  # = \bar{\Gamma}
+        self.gamma_sc = self.consts.y_max - (y_hi + y_lo) / 2
+        self.gamma_sm = self.consts.y_max - y_sum / n
+        self._build_plans(self.consts.y_max - y0d)
 
     def _global_levels(self, y0d):
         """Global max / min / mean / count of a sharded y0: one all-gather, one host sync."""
@@ -277,9 +292,11 @@ class PriceSolver:
     def _get_w_inner_product_metric(self, lmbd_r: float) -> tuple[np.ndarray, np.ndarray]:
         """price_solver.py:188-194."""
         kappa = lmbd_r / self.consts.delta
+        if self._kappa == kappa and self._A_bar_inv is not None:  # every partition of a step: same metric
+            return self._A_bar, self._A_bar_inv
         A_bar = self.A.T @ self.A + kappa * np.eye(self.N)
         A_bar_inv = np.linalg.inv(A_bar)
-        self._A_bar_inv, self._kappa = A_bar_inv, kappa
+        self._A_bar, self._A_bar_inv, self._kappa = A_bar, A_bar_inv, kappa
         return A_bar, A_bar_inv
 
     # ------------------------------------------------------------ engine calls

@@ -37,6 +37,22 @@ for name in ("_get_bimpc_solution", "_get_optimal_prices", "_get_w0_price0", "_u
         return r
 
     setattr(st, name, wrap)
+for obj, name, label in ((st.bimpc, "solve_bimpc", "  bimpc.solve_bimpc"),
+                         (st.price_solver_s, "_iterate", "  price._iterate (s)"),
+                         (st.price_solver_l, "_iterate", "  price._iterate (l)"),
+                         (st.price_solver_s, "_price_gradient_descent_step", "  price step (s)"),
+                         (st.price_solver_l, "_price_gradient_descent_step", "  price step (l)"),
+                         (st.price_solver_s, "set_charge_levels", "  set_charge_levels (s)"),
+                         (st.price_solver_l, "set_charge_levels", "  set_charge_levels (l)")):
+    f = getattr(obj, name)
+
+    def wrap2(*a, _f=f, _n=label, **k):
+        t0 = time.perf_counter()
+        r = _f(*a, **k)
+        phases[_n] = phases.get(_n, 0.0) + time.perf_counter() - t0
+        return r
+
+    setattr(obj, name, wrap2)
 orig_step = st.price_solver_s._price_gradient_descent_step
 st._step()
 phases.clear()
@@ -51,5 +67,6 @@ print(f"step {dt * 1e3:.1f} ms")
 for k, v in phases.items():
     print(f"  {k:22s} {v / 2 * 1e3:8.2f} ms")
 it = st.logs["statistics"]
+print("bimpc last info:", st.bimpc.last_info)
 print("price iterations per (type, partition):", it["niter_s"][:, 1:3].tolist(), it["niter_l"][:, 1:3].tolist())
 pstats.Stats(pr).sort_stats("tottime").print_stats(25)

@@ -85,6 +85,7 @@ struct lompc_plan {
   int nctx = 0;
   int flags = 0;
   lompc_ctx* ctx[LQ_PLAN_MAX_CTX] = {};
+  char* d_meta = nullptr;       // host-built metadata, one block (the four views below)
   QPConst* d_q = nullptr;       // [nctx]
   int64_t B = 0, S = 0;
   int G = 0;                    // gamma cells per set (k_path waves per set)
@@ -99,9 +100,9 @@ struct lompc_plan {
   double* d_stats_own = nullptr;  // [S][8] when the plan owns its status rows
   double* d_stats = nullptr;      // where k_finalize writes the status rows
   // device workspaces
-  int64_t* d_set_off = nullptr;   // [S+1]
-  int* d_blk_prefix = nullptr;    // [S+1] k_eval workgroups per set
-  int4* d_blk = nullptr;          // [nblk] (set, first EV, end EV, -)
+  int64_t* d_set_off = nullptr;   // [S+1]                          (view of d_meta)
+  int* d_blk_prefix = nullptr;    // [S+1] k_eval workgroups per set (view of d_meta)
+  int4* d_blk = nullptr;          // [nblk] (set, first EV, end EV, -) (view of d_meta)
   double* d_window = nullptr;     // [S][2] (lo, hi) of the set's valid gamma, widened
   double* d_partial = nullptr;    // [nblk][N+NPX] k_eval workgroup records
   int* d_fail_cnt = nullptr;      // [nblk][waves] EVs listed for k_finalize's individual re-solve

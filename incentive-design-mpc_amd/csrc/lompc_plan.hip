@@ -913,21 +913,19 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   p->w_ref = w_ref;
   p->gamma = gamma;
   int rc;
-  if (!p->d_q && (rc = grow(p, &p->d_q, LQ_PLAN_MAX_CTX))) return rc;
   if (!p->d_errflag) {
     if ((rc = grow(p, &p->d_errflag, 1))) return rc;
     HIPCHK(p, hipMemset(p->d_errflag, 0, sizeof(int)));
   }
   if (!p->ev_stage) HIPCHK(p, hipEventCreateWithFlags(&p->ev_stage, hipEventDisableTiming));
   if (S > p->cap_S) {
-    if ((rc = grow(p, &p->d_set_off, S + 1)) ||
-        (rc = grow(p, &p->d_blk_prefix, S + 1)) || (rc = grow(p, &p->d_window, 2 * S)) ||
+    if ((rc = grow(p, &p->d_window, 2 * S)) ||
         (rc = grow(p, &p->d_stats_own, S * LOMPC_SET_STATS)))
       return rc;
     p->cap_S = S;
   }
   if (nblk > p->cap_blk) {
-    if ((rc = grow(p, &p->d_blk, nblk)) || (rc = grow(p, &p->d_partial, (size_t)nblk * (N + NPX))) ||
+    if ((rc = grow(p, &p->d_partial, (size_t)nblk * (N + NPX))) ||
         (rc = grow(p, &p->d_fail_cnt, (size_t)nblk * EVAL_WAVES)) || (rc = grow(p, &p->d_fail_idx, (size_t)nblk * EVAL_MAXB)))
       return rc;
     p->cap_blk = nblk;
@@ -950,21 +948,27 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   p->nblk = (int)nblk;
   p->d_stats = p->d_stats_own;
   // host arrays -> pinned staging -> device (the staging may still feed the previous prepare)
-  const size_t need_h = LQ_PLAN_MAX_CTX * sizeof(QPConst) + (size_t)(S + 1) * (sizeof(int64_t) + sizeof(int)) +
-                        (size_t)nblk * sizeof(int4) + S + 64;
-  HIPCHK(p, hipEventSynchronize(p->ev_stage));
+  // the plan's host-built metadata, one block in pinned memory and one copy to its device
+  // mirror: [QPConst x LQ_PLAN_MAX_CTX | int4 blocks | int64 set offsets | int block prefix]
+  auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t o_blk = up16(LQ_PLAN_MAX_CTX * sizeof(QPConst));
+  const size_t o_off = o_blk + up16((size_t)nblk * sizeof(int4));
+  const size_t o_pre = o_off + up16((size_t)(S + 1) * sizeof(int64_t));
+  const size_t need_h = o_pre + up16((size_t)(S + 1) * sizeof(int));
+  HIPCHK(p, hipEventSynchronize(p->ev_stage));  // (the staging may still feed the previous copy)
   if ((int64_t)need_h > p->cap_h) {
     if (p->h_buf) HIPCHK(p, hipHostFree(p->h_buf));
     p->h_buf = nullptr;
     HIPCHK(p, hipHostMalloc((void**)&p->h_buf, need_h, hipHostMallocDefault));
+    if ((rc = grow(p, &p->d_meta, need_h))) return rc;
     p->cap_h = (int64_t)need_h;
   }
   QPConst* hq = reinterpret_cast<QPConst*>(p->h_buf);
   for (int k = 0; k < nctx; ++k) hq[k] = ctxs[k]->q;
-  int64_t* hoff = reinterpret_cast<int64_t*>(hq + LQ_PLAN_MAX_CTX);
+  int4* hblk = reinterpret_cast<int4*>(p->h_buf + o_blk);
+  int64_t* hoff = reinterpret_cast<int64_t*>(p->h_buf + o_off);
+  int* hpre = reinterpret_cast<int*>(p->h_buf + o_pre);
   memcpy(hoff, set_offsets, (S + 1) * sizeof(int64_t));
-  int4* hblk = reinterpret_cast<int4*>(hoff + S + 1);
-  int* hpre = reinterpret_cast<int*>(hblk + nblk);
   int64_t b = 0;
   hpre[0] = 0;
   for (int64_t s = 0; s < S; ++s) {
@@ -976,10 +980,11 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     e += k < nctx ? (int)sets_per_ctx[k] : 0;
     p->ce.end[k] = k + 1 < nctx ? e : (int)S;  // contexts past the last: never selected
   }
-  HIPCHK(p, hipMemcpyAsync(p->d_q, hq, nctx * sizeof(QPConst), hipMemcpyHostToDevice, st));
-  HIPCHK(p, hipMemcpyAsync(p->d_set_off, hoff, (S + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
-  if (nblk) HIPCHK(p, hipMemcpyAsync(p->d_blk, hblk, nblk * sizeof(int4), hipMemcpyHostToDevice, st));
-  HIPCHK(p, hipMemcpyAsync(p->d_blk_prefix, hpre, (S + 1) * sizeof(int), hipMemcpyHostToDevice, st));
+  p->d_q = reinterpret_cast<QPConst*>(p->d_meta);
+  p->d_blk = reinterpret_cast<int4*>(p->d_meta + o_blk);
+  p->d_set_off = reinterpret_cast<int64_t*>(p->d_meta + o_off);
+  p->d_blk_prefix = reinterpret_cast<int*>(p->d_meta + o_pre);
+  HIPCHK(p, hipMemcpyAsync(p->d_meta, p->h_buf, need_h, hipMemcpyHostToDevice, st));
   HIPCHK(p, hipEventRecord(p->ev_stage, st));
   WindowArgs wa{p->d_q, p->ce, p->d_set_off, gamma, p->d_window};
   hipLaunchKernelGGL(k_plan_window, dim3((unsigned)S), dim3(256), 0, st, wa);
@@ -1097,8 +1102,7 @@ void lq_plan_free(lompc_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
   (void)hipDeviceSynchronize();
-  void* ptrs[] = {p->d_q,     p->d_stats_own, p->d_set_off, p->d_blk_prefix, p->d_window,
-                  p->d_blk, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
+  void* ptrs[] = {p->d_meta,  p->d_stats_own, p->d_window, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
                   p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag,
                   p->d_fail_cnt, p->d_fail_idx};
   for (void* x : ptrs)

@@ -187,15 +187,7 @@ class PriceSolver:
                                    want_set=True, validate=False, warm_start=True)
         else:
             self._plan.update(self._gam, off, w_ref=self._wr2, validate=False)
-        if not B:
-            self._w0_live = False
-        elif self._plan_w0 is None:
-            self._plan_w0 = BatchPlan(self.lompc, self._gam[:B], np.array([0, B], dtype=np.int64), want_w=False,
-                                      want_cost=False, want_w0=True, want_set=True, validate=False)
-            self._w0_live = True
-        else:
-            self._plan_w0.update(self._gam[:B], np.array([0, B], dtype=np.int64), validate=False)
-            self._w0_live = True
+        self._w0_live = False  # the w0 plan follows lazily (get_w0_price0_device)
         self._B = B
 
     def compute_optimal_prices(self, w_ref: np.ndarray, lmbd_r: float) -> tuple[np.ndarray, dict]:
@@ -403,7 +395,15 @@ class PriceSolver:
         h[: self.r] = lmbd
         h[2 * N3:2 * N3 + 2] = float(lmbd_r)
         self._in.copy_(self._h_in, non_blocking=True)
-        if self._plan_w0 is not None and self._w0_live:
+        B = self._B
+        if B and not self._w0_live:
+            if self._plan_w0 is None:
+                self._plan_w0 = BatchPlan(self.lompc, self._gam[:B], np.array([0, B], dtype=np.int64), want_w=False,
+                                          want_cost=False, want_w0=True, want_set=True, validate=False)
+            else:
+                self._plan_w0.update(self._gam[:B], np.array([0, B], dtype=np.int64), validate=False)
+            self._w0_live = True
+        if B:
             out = self._plan_w0.run(self._lm2[:1], self._lr2[:1])
             st = out["set_stats"]
             w0 = out["w0"]

@@ -247,4 +247,116 @@ int lompc_lp_separable(int n_rows, int n_cols, const double* A, const double* b,
   return LOMPC_OK;
 }
 
+// General LP  min c'x  s.t.  A x = b, x >= 0  (the reference's PriceRegularizer accepts any
+// such LP, price_regularizer.py:62-85): dense two-phase tableau simplex with Bland's rule (no
+// cycling), artificial basis for phase 1, redundant rows dropped.  Sizes here are the price
+// vector's (r <= 3N columns, N rows), so a dense tableau is the simple exact choice.
+int lompc_lp_solve(int n_rows, int n_cols, const double* A, const double* b, const double* c, double* x,
+                   double* objective) {
+  if (n_rows < 0 || n_cols < 0) return LOMPC_ERR_INVALID_ARG;
+  if ((n_cols > 0 && (!c || !x)) || (n_rows > 0 && !b) || ((int64_t)n_rows * n_cols > 0 && !A))
+    return LOMPC_ERR_INVALID_ARG;
+  const int m = n_rows, n = n_cols, W = n + m + 1;  // columns: x | artificials | rhs
+  std::vector<double> T((size_t)(m + 1) * W, 0.0);
+  std::vector<int> basis(m);
+  double scale = 1.0;
+  for (int i = 0; i < m; ++i) {
+    const double sg = b[i] < 0.0 ? -1.0 : 1.0;  // rows with b >= 0
+    for (int j = 0; j < n; ++j) {
+      T[(size_t)i * W + j] = sg * A[(size_t)i * n + j];
+      scale = std::max(scale, std::fabs(A[(size_t)i * n + j]));
+    }
+    T[(size_t)i * W + n + i] = 1.0;
+    T[(size_t)i * W + W - 1] = sg * b[i];
+    scale = std::max(scale, std::fabs(b[i]));
+    basis[i] = n + i;
+  }
+  const double eps = 1e-11 * scale;
+  std::vector<char> live(m, 1);  // rows not removed as redundant
+  double* obj = &T[(size_t)m * W];
+  auto pivot = [&](int pr, int pc) {
+    double* rp = &T[(size_t)pr * W];
+    const double inv = 1.0 / rp[pc];
+    for (int j = 0; j < W; ++j) rp[j] *= inv;
+    rp[pc] = 1.0;
+    for (int i = 0; i <= m; ++i) {
+      if (i == pr) continue;
+      double* ri = &T[(size_t)i * W];
+      const double f = ri[pc];
+      if (f == 0.0) continue;
+      for (int j = 0; j < W; ++j) ri[j] -= f * rp[j];
+      ri[pc] = 0.0;
+    }
+    basis[pr] = pc;
+  };
+  // simplex on the objective row `obj` over columns [0, ncol): Bland's rule
+  auto run = [&](int ncol) -> int {
+    for (int it = 0; it < 50 * (m + n) + 100; ++it) {
+      int pc = -1;
+      for (int j = 0; j < ncol; ++j)
+        if (obj[j] < -eps) {
+          pc = j;
+          break;
+        }
+      if (pc < 0) return LOMPC_OK;
+      int pr = -1;
+      double best = INFINITY;
+      for (int i = 0; i < m; ++i) {
+        if (!live[i]) continue;
+        const double a = T[(size_t)i * W + pc];
+        if (a > eps) {
+          const double ratio = T[(size_t)i * W + W - 1] / a;
+          if (pr < 0 || ratio < best - 1e-15 * best || (ratio <= best && basis[i] < basis[pr])) {
+            best = ratio;
+            pr = i;
+          }
+        }
+      }
+      if (pr < 0) return LOMPC_ERR_UNSUPPORTED;  // unbounded
+      pivot(pr, pc);
+    }
+    return LOMPC_ERR_NOT_CONVERGED;
+  };
+  // phase 1: minimise the sum of the artificials (objective row = -sum of the rows)
+  for (int j = 0; j < W; ++j) {
+    double sacc = 0.0;
+    for (int i = 0; i < m; ++i) sacc += T[(size_t)i * W + j];
+    obj[j] = (j >= n && j < n + m) ? 0.0 : -sacc;
+  }
+  int rc = run(n + m);
+  if (rc == LOMPC_ERR_NOT_CONVERGED) return rc;
+  if (-obj[W - 1] > 1e-9 * scale) return LOMPC_ERR_NOT_CONVERGED;  // infeasible
+  for (int i = 0; i < m; ++i) {  // drive the artificials out of the basis
+    if (basis[i] < n) continue;
+    int pc = -1;
+    for (int j = 0; j < n; ++j)
+      if (std::fabs(T[(size_t)i * W + j]) > eps) {
+        pc = j;
+        break;
+      }
+    if (pc >= 0) pivot(i, pc);
+    else live[i] = 0;  // redundant row
+  }
+  // phase 2: the original costs, reduced by the basis
+  for (int j = 0; j < W; ++j) obj[j] = j < n ? c[j] : 0.0;
+  for (int i = 0; i < m; ++i) {
+    if (!live[i]) continue;
+    const int k = basis[i];
+    const double f = obj[k];
+    if (f == 0.0) continue;
+    for (int j = 0; j < W; ++j) obj[j] -= f * T[(size_t)i * W + j];
+  }
+  rc = run(n);
+  if (rc != LOMPC_OK) return rc;
+  for (int j = 0; j < n; ++j) x[j] = 0.0;
+  for (int i = 0; i < m; ++i)
+    if (live[i] && basis[i] < n) x[basis[i]] = std::max(0.0, T[(size_t)i * W + W - 1]);
+  if (objective) {
+    double f = 0.0;
+    for (int j = 0; j < n; ++j) f += c[j] * x[j];
+    *objective = f;
+  }
+  return LOMPC_OK;
+}
+
 }  // extern "C"

@@ -18,6 +18,9 @@
 #pragma once
 #include "lompc_qp.hpp"
 
+#ifndef LQ_JUMP_FREE
+#define LQ_JUMP_FREE 0  // fp32 search jumps: 0 = to the knot bounding w's segment, 1 = free inside it
+#endif
 #ifndef LQ_JUMP_IT
 #define LQ_JUMP_IT 3  // PDAS iterations that may jump across segments
 #endif
@@ -504,7 +507,11 @@ __device__ __forceinline__ int wave_pdas_f32(const QPConst& q, const WaveSet& ws
           int seg = 0;
 #pragma unroll
           for (int k = 1; k < LQ_MAXSEG; ++k) seg += (k < q.m && w > (float)q.knots[k]) ? 1 : 0;
+#if LQ_JUMP_FREE
+          ns = 2 * seg + 1;  // free in the segment that contains w
+#else
           ns = up ? 2 * seg : 2 * seg + 2;
+#endif
         }
       } else {
         ns = s + (up ? 1 : 0) - (dn ? 1 : 0);

@@ -74,6 +74,7 @@ SIGNATURES = [
     ("lompc_abi_version", _I, []),
     ("lompc_price_step", _I, [_I, _I, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P]),
     ("lompc_lp_separable", _I, [_I, _I, _P, _P, _P, _P]),
+    ("lompc_lp_solve", _I, [_I, _I, _P, _P, _P, _P, _P]),
     ("lompc_bimpc_solve", _I, [_I, _I, _I] + [_D] * 10 + [_P] * 6 + [_D] + [_P] * 6),
     ("lompc_plan_create", _I, [_I, _P, _P, _L, _P, _P, _P, _I, _P, ctypes.POINTER(_P)]),
     ("lompc_plan_run", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -4,8 +4,9 @@ The reference solves  min c'x  s.t.  A x = b, x >= 0  with CVXPY's default LP
 solver (price_regularizer.py:45,83).  Its only caller passes A = Dphi(w)',
 b = Dphi(w)' lmbd, c = phi(w) (price_solver.py:248-255), and every column of
 Dphi(w)' has one nonzero (lompc.py:179-187), so the LP separates into one-row
-LPs solved in closed form by ``lompc_lp_separable`` in the C-ABI library.
-Same constructor (N, r) and method signature as the reference.
+LPs solved in closed form by ``lompc_lp_separable`` in the C-ABI library; any other
+LP (the reference's class accepts every A, b, c) goes to ``lompc_lp_solve``, a dense
+two-phase simplex.  Same constructor (N, r) and method signature as the reference.
 """
 from __future__ import annotations
 
@@ -15,8 +16,8 @@ from . import _lib
 
 
 class PriceRegularizerError(Exception):
-    """The LP is infeasible or not column-separable (the reference would raise SolverError
-    or return None from CVXPY)."""
+    """The LP is infeasible or unbounded (the reference would raise SolverError or return
+    None from CVXPY)."""
 
 
 class PriceRegularizer:
@@ -46,8 +47,11 @@ class PriceRegularizer:
         x = np.empty(self.r)
         rc = self._lib.lompc_lp_separable(self.N, self.r, A.ctypes.data, b.ctypes.data, c.ctypes.data,
                                           x.ctypes.data)
-        if rc == _lib.LOMPC_ERR_UNSUPPORTED:
-            raise PriceRegularizerError("LP is not column-separable (or has negative costs)")
+        if rc == _lib.LOMPC_ERR_UNSUPPORTED:  # not column-separable: the general LP
+            rc = self._lib.lompc_lp_solve(self.N, self.r, A.ctypes.data, b.ctypes.data, c.ctypes.data,
+                                          x.ctypes.data, None)
+            if rc == _lib.LOMPC_ERR_UNSUPPORTED:
+                raise PriceRegularizerError("LP unbounded")
         if rc != _lib.LOMPC_OK:
             raise PriceRegularizerError("LP infeasible: " + _lib.status_text(self._lib, None, rc))
         return x

@@ -253,6 +253,13 @@ int lompc_price_step(int N, int r, double theta, double w_max, double m, double 
 int lompc_lp_separable(int n_rows, int n_cols, const double* A, const double* b,
                        const double* c, double* x);
 
+/* General LP: min c'x s.t. A x = b, x >= 0 (row-major A [n_rows, n_cols]): the
+ * reference's PriceRegularizer accepts any such LP (price_regularizer.py:62-85).  Dense
+ * two-phase simplex, Bland's rule; *objective (may be NULL) = c'x.
+ * LOMPC_ERR_NOT_CONVERGED if infeasible, LOMPC_ERR_UNSUPPORTED if unbounded. */
+int lompc_lp_solve(int n_rows, int n_cols, const double* A, const double* b, const double* c,
+                   double* x, double* objective);
+
 /* BiMPC charging cost types (bimpc.py:12-15, BiMPCChargingCostType) */
 #define LOMPC_BIMPC_WEIGHTED       0
 #define LOMPC_BIMPC_UNWEIGHTED     1

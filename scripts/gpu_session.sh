@@ -35,6 +35,7 @@ for s in $STEPS; do
     qnew) run qnew 600 python -u -m pytest tests/test_gpu_example.py tests/test_gpu_station.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sprof) run sprof 300 python scripts/station_profile.py ;;
     bimpc) run bimpc 300 python scripts/bimpc_timing.py ;;
+    stampsvar) for v in ${KS_VARIANTS}; do KS_VARIANT=$v run stamps_$v 300 python scripts/kstamps.py || exit $?; done ;;
     bcost) run bcost 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs cost ;;
     bset) run bset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs set ;;
     bfused) LOMPC_REDUCE_FUSED=1 run bfused 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;

@@ -16,9 +16,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "incentive-design-mpc_amd"))
 from lompc_amd import _lib, build  # noqa: E402
 
-DBG = os.path.join(ROOT, "incentive-design-mpc_amd", "lompc_amd", "liblompc_amd_stamps.so")
+# KS_VARIANT=name: lompc_amd/liblompc_amd_stamps_<name>.so built with KS_DEFINES (comma list)
+VAR = os.environ.get("KS_VARIANT")
+DBG = os.path.join(ROOT, "incentive-design-mpc_amd", "lompc_amd",
+                   f"liblompc_amd_stamps_{VAR}.so" if VAR else "liblompc_amd_stamps.so")
 if "--build" in sys.argv:
-    print(build.build(force=True, verbose=True, out=DBG, defines=("LOMPC_STAMPS",)))
+    extra = tuple(d for d in os.environ.get("KS_DEFINES", "").split(",") if d)
+    print(build.build(force=True, verbose=True, out=DBG, defines=("LOMPC_STAMPS",) + extra))
     sys.exit(0)
 
 import torch  # noqa: E402

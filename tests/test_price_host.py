@@ -131,9 +131,44 @@ def test_regularizer_reference_invariants():
         assert x[:N] @ x[N:] == 0.0
 
 
-def test_regularizer_rejects_non_separable():
+def test_regularizer_general_lp_matches_highs():
+    """The reference's PriceRegularizer accepts any LP (price_regularizer.py:62-85): dense,
+    non-separable instances go to lompc_lp_solve (two-phase simplex) — same optimal value as
+    scipy's HiGHS, feasible, non-negative."""
+    from scipy.optimize import linprog
+
+    rng = np.random.default_rng(11)
+    for trial in range(40):
+        m, n = int(rng.integers(2, 20)), int(rng.integers(20, 60))
+        A = rng.standard_normal((m, n))
+        x0 = rng.random(n) * (rng.random(n) < 0.5)  # a feasible point: b = A x0, x0 >= 0
+        b = A @ x0
+        c = rng.random(n) + 0.1  # positive costs: bounded
+        if trial % 4 == 0:
+            A[-1] = A[0]  # a redundant row
+            b[-1] = b[0]
+        reg = PriceRegularizer(m, n)
+        x = reg.solve_price_regularization(A, b, c)
+        ref = linprog(c, A_eq=A, b_eq=b, bounds=(0, None), method="highs")
+        assert ref.status == 0
+        assert np.all(x >= 0.0)
+        np.testing.assert_allclose(A @ x, b, rtol=0, atol=1e-9 * (1 + np.abs(b).max()))
+        assert abs(c @ x - ref.fun) <= 1e-9 * (1 + abs(ref.fun)), (trial, c @ x, ref.fun)
+
+
+def test_regularizer_general_lp_infeasible_and_unbounded():
     reg = PriceRegularizer(2, 3)
-    with pytest.raises(PriceRegularizerError):
-        reg.solve_price_regularization(np.ones((2, 3)), np.ones(2), np.ones(3))
+    A = np.array([[1.0, 1.0, 0.0], [1.0, 1.0, 0.0]])
+    with pytest.raises(PriceRegularizerError):  # x1 + x2 = 1 and = 2
+        reg.solve_price_regularization(A, np.array([1.0, 2.0]), np.ones(3))
+    A = np.array([[1.0, -1.0, 0.0], [0.0, 0.0, 1.0]])
+    with pytest.raises(PriceRegularizerError):  # x1 - x2 = 1 with cost -x1: unbounded
+        reg.solve_price_regularization(A, np.array([1.0, 1.0]), np.array([-1.0, 0.0, 1.0]))
+
+
+def test_regularizer_rejects_bad_shapes():
+    reg = PriceRegularizer(2, 3)
+    x = reg.solve_price_regularization(np.ones((2, 3)), np.ones(2), np.ones(3))  # general LP now
+    np.testing.assert_allclose(np.ones((2, 3)) @ x, np.ones(2))
     with pytest.raises(ValueError):
         reg.solve_price_regularization(np.ones((3, 3)), np.ones(2), np.ones(3))

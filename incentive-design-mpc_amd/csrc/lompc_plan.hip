@@ -1156,6 +1156,95 @@ int lompc_plan_update(lompc_plan* p, int64_t B, const double* gamma, const int64
   return lq_plan_prepare(p, p->nctx, p->ctx, spc, B, gamma, set_offsets, w_ref, p->flags, (hipStream_t)stream);
 }
 
+int lompc_price_loop(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd, double* w_k, double* dual_cost,
+                     double* dec_actual, double* dec_pred, int* iterations, double* errs, void* stream) {
+  if (!p || !a || !lmbd || !w_k || !iterations || !a->A_bar || !a->w_ref || !a->dev_in || !a->host_in ||
+      !a->dev_sw || !a->dev_st || !a->host_sw || !a->host_st || a->max_iter < 1 || !(a->n_evs > 0.0))
+    return LOMPC_ERR_INVALID_ARG;
+  const int N = a->N, r = a->r, N3 = 3 * N;
+  if (N != p->N || p->S != 2 || (r != 2 * N && r != 3 * N)) return fail_arg(p, "price loop: a plan of 2 sets of horizon N");
+  HIPCHK(p, hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t n_in = (size_t)6 * N + 2 + 2 * N;
+  // one engine call at prices x: the batch errors and the central solve (price_solver.py:106/:132)
+  double e[3] = {0.0, 0.0, 0.0};
+  double cost_c = 0.0;
+  auto iterate = [&](const double* x) -> int {
+    double* h = a->host_in;
+    memcpy(h, x, N3 * sizeof(double));
+    memcpy(h + N3, x, N3 * sizeof(double));
+    h[2 * N3] = h[2 * N3 + 1] = a->lmbd_r;
+    memcpy(h + 2 * N3 + 2, a->w_ref, N * sizeof(double));
+    memcpy(h + 2 * N3 + 2 + N, a->w_ref, N * sizeof(double));
+    HIPCHK(p, hipMemcpyAsync(a->dev_in, h, n_in * sizeof(double), hipMemcpyHostToDevice, st));
+    const int rc = lq_plan_launch(p, a->dev_in, a->dev_in + 2 * N3, nullptr, nullptr, nullptr, nullptr,
+                                  const_cast<double*>(a->dev_sw), const_cast<double*>(a->dev_st), st, nullptr);
+    if (rc) return rc;
+    HIPCHK(p, hipMemcpyAsync(a->host_sw, a->dev_sw, 2 * N * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(p, hipMemcpyAsync(a->host_st, a->dev_st, 2 * LOMPC_SET_STATS * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(p, hipStreamSynchronize(st));
+    const double* sw = a->host_sw;
+    const double* sst = a->host_st;
+    for (int s = 0; s < 2; ++s) {
+      if (sst[s * LOMPC_SET_STATS + LOMPC_STAT_N_INVALID] > 0) return fail_arg(p, "gamma outside [0, y_max]");
+      if (sst[s * LOMPC_SET_STATS + LOMPC_STAT_N_FAILED] > 0) {
+        p->err = "LoMPC QPs without a certified optimum";
+        return LOMPC_ERR_NOT_CONVERGED;
+      }
+    }
+    double qf = 0.0;  // (w_avg - w_ref)' A_bar (w_avg - w_ref)  (price_solver.py:210-214)
+    for (int i = 0; i < N; ++i) {
+      const double di = sw[i] / a->n_evs - a->w_ref[i];
+      double acc = 0.0;
+      for (int j = 0; j < N; ++j) acc += a->A_bar[(size_t)i * N + j] * (sw[j] / a->n_evs - a->w_ref[j]);
+      qf += di * acc;
+    }
+    e[0] = sst[LOMPC_STAT_MAX_ERR];
+    e[1] = std::fabs(sw[0] / a->n_evs - a->w_ref[0]);
+    e[2] = std::sqrt(qf);
+    memcpy(w_k, sw + N, N * sizeof(double));
+    cost_c = sst[LOMPC_SET_STATS + LOMPC_STAT_SUM_COST];
+    return LOMPC_OK;
+  };
+  // phi(w_ref) (lompc.py:172-177)
+  std::vector<double> phi_ref(N3), lm(lmbd, lmbd + N3), lm_new(N3, 0.0);
+  const double q_s = 3.0 * a->theta / (4.0 * a->w_max);
+  for (int t = 0; t < N; ++t) {
+    phi_ref[t] = a->theta * a->w_ref[t];
+    phi_ref[N + t] = a->theta * (a->w_max - a->w_ref[t]);
+    phi_ref[2 * N + t] = q_s * a->w_ref[t] * a->w_ref[t];
+  }
+  int rc = iterate(lm.data());
+  if (rc) return rc;
+  double dc = cost_c;
+  int it = 0;
+  for (it = 0; it < a->max_iter; ++it) {
+    if ((a->tol_avg ? e[2] : e[0]) <= a->tol) break;
+    double dec = 0.0;
+    int qit = 0;
+    rc = lompc_price_step(N, r, a->theta, a->w_max, a->m, a->kappa, a->eps_reg, a->w_ref, w_k, lm.data(),
+                          lm_new.data(), &dec, &qit);
+    if (rc) {
+      p->err = "price-gradient QP: no certified optimum";
+      return rc;
+    }
+    rc = iterate(lm_new.data());
+    if (rc) return rc;
+    double dterm = 0.0;  // (lmbd_k - lmbd_k_new) @ phi(w_ref): the reference's two arrays alias
+    if (it == 0)         // after the first iteration (lmbd_k = lmbd_k_new), so the term is 0 then
+      for (int i = 0; i < N3; ++i) dterm += (lm[i] - lm_new[i]) * phi_ref[i];
+    if (dec_actual) dec_actual[it] = cost_c - dc + dterm;
+    if (dec_pred) dec_pred[it] = dec;
+    dc = cost_c;
+    lm = lm_new;
+  }
+  *iterations = it;  // steps taken (= the reference's `iter` unless the cap was hit: then max_iter)
+  memcpy(lmbd, lm.data(), N3 * sizeof(double));
+  if (dual_cost) *dual_cost = dc;
+  if (errs) memcpy(errs, e, sizeof(e));
+  return LOMPC_OK;
+}
+
 int lompc_plan_run(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
                    int8_t* status, double* set_sum_w, double* set_stats, void* stream) {
   if (!p) return LOMPC_ERR_INVALID_ARG;

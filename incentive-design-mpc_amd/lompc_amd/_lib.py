@@ -81,6 +81,7 @@ SIGNATURES = [
     ("lompc_plan_status", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_get_info", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_update", _I, [_P, _L, _P, _P, _P, _P]),
+    ("lompc_price_loop", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_plan_profile_enable", _I, [_P, _I]),
     ("lompc_plan_profile_read", _I, [_P, _I, _P, _P, _I]),
     ("lompc_plan_last_error", ctypes.c_char_p, [_P]),
@@ -91,6 +92,17 @@ LOMPC_BIMPC_UNWEIGHTED = 1
 LOMPC_BIMPC_EXP_UNWEIGHTED = 2
 LOMPC_BIMPC_INFO = 5
 ABI_VERSION = 2
+
+
+class PriceLoopArgs(ctypes.Structure):
+    """include/lompc_amd.h lompc_price_loop_args."""
+    _fields_ = [("N", ctypes.c_int), ("r", ctypes.c_int), ("max_iter", ctypes.c_int), ("tol_avg", ctypes.c_int),
+                ("theta", ctypes.c_double), ("w_max", ctypes.c_double), ("m", ctypes.c_double),
+                ("kappa", ctypes.c_double), ("eps_reg", ctypes.c_double), ("tol", ctypes.c_double),
+                ("n_evs", ctypes.c_double), ("lmbd_r", ctypes.c_double),
+                ("A_bar", ctypes.c_void_p), ("w_ref", ctypes.c_void_p), ("dev_in", ctypes.c_void_p),
+                ("host_in", ctypes.c_void_p), ("dev_sw", ctypes.c_void_p), ("dev_st", ctypes.c_void_p),
+                ("host_sw", ctypes.c_void_p), ("host_st", ctypes.c_void_p)]
 
 _lock = threading.Lock()
 _lib = None

@@ -24,6 +24,8 @@ redundantly on identical inputs; the re-draw replays the global random stream.
 """
 from __future__ import annotations
 
+import concurrent.futures
+
 from dataclasses import dataclass
 
 import numpy as np
@@ -143,6 +145,7 @@ class ChargingStation:
             consts.demand.shape[0] >= consts.simulation_length + consts.horizon_bimpc + 1)
         torch = _torch()
         self.group = group
+        self._pool = None  # one worker thread: the large-EV price chain beside the small one
         self.device = torch.cuda.current_device() if device is None else int(device)
         self._dev = f"cuda:{self.device}"
         # Set constants, initialize PriceSolvers and BiMPC.
@@ -328,30 +331,62 @@ class ChargingStation:
 
     # ------------------------------------------------------------------ prices
     def _get_optimal_prices(self, w_hat_s, w_hat_l, lmbd_r: float):
-        # charging_station.py:268-308 (sequential: prev_prices chains the partitions)
+        # charging_station.py:268-308.  Within one EV type the partitions are sequential
+        # (prev_prices chains them); the two types are independent, so without printing (whose
+        # order is the reference's interleaving) and on one rank their chains run side by side:
+        # one host thread each (the price loops spend their time in C-ABI calls, outside the
+        # GIL) on each solver's own stream.
         PRINT_LEVEL = _settings.PRINT_LEVEL
         w_hat_s_opt, w_hat_l_opt = w_hat_s[:, : self.N_lo], w_hat_l[:, : self.N_lo]
         prices_s, prices_l = np.zeros((self.P, self.r)), np.zeros((self.P, self.r))
         stats_s, stats_l = [], []
         st_s, st_l = self._pstats
-        for p in range(self.P):
-            for kind, solver, y, idx, st, w_hat, prices, stats in (
-                    ("Small", self.price_solver_s, self.y_s, self.idx_s, st_s, w_hat_s_opt, prices_s, stats_s),
-                    ("Large", self.price_solver_l, self.y_l, self.idx_l, st_l, w_hat_l_opt, prices_l, stats_l)):
-                if st[p, 0] > 0:
-                    ys, off = self._partition_layout(kind, y, idx)
-                    solver.set_charge_levels_stats(ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3])
-                    if PRINT_LEVEL >= 1 and self._rank0():
-                        print(f"{kind} EVs, partition {p:2d}: ", end="")
-                        if PRINT_LEVEL >= 2:
-                            print("\n" + "-" * 27)
-                    lmbd_, stats_ = solver.compute_optimal_prices(w_hat[p, :], lmbd_r)
-                    prices[p, :] = lmbd_[: self.r]
-                    stats.append(stats_)
+        chains = (("Small", self.price_solver_s, self.y_s, self.idx_s, st_s, w_hat_s_opt, prices_s, stats_s),
+                  ("Large", self.price_solver_l, self.y_l, self.idx_l, st_l, w_hat_l_opt, prices_l, stats_l))
+        for kind, _, y, idx, *_ in chains:  # (on this thread: the layouts' host sync)
+            self._partition_layout(kind, y, idx)
+
+        def one(chain, p):
+            kind, solver, y, idx, st, w_hat, prices, stats = chain
+            if st[p, 0] > 0:
+                ys, off = self._partition_layout(kind, y, idx)
+                solver.set_charge_levels_stats(ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3])
+                if PRINT_LEVEL >= 1 and self._rank0():
+                    print(f"{kind} EVs, partition {p:2d}: ", end="")
                     if PRINT_LEVEL >= 2:
-                        print("")
-                else:
-                    stats.append({})
+                        print("\n" + "-" * 27)
+                lmbd_, stats_ = solver.compute_optimal_prices(w_hat[p, :], lmbd_r)
+                prices[p, :] = lmbd_[: self.r]
+                stats.append(stats_)
+                if PRINT_LEVEL >= 2:
+                    print("")
+            else:
+                stats.append({})
+
+        if PRINT_LEVEL == 0 and self.group is None:
+            torch = _torch()
+            main = torch.cuda.current_stream(self.device)
+
+            def run_chain(chain):
+                solver = chain[1]
+                # the chain's thread works on its solver's stream (no waits through a shared one)
+                with torch.cuda.device(self.device), torch.cuda.stream(solver._stream):
+                    for p in range(self.P):
+                        one(chain, p)
+
+            for chain in chains:
+                chain[1]._stream.wait_stream(main)  # the layouts were made on the main stream
+            if self._pool is None:
+                self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=1)
+            fut = self._pool.submit(run_chain, chains[1])
+            run_chain(chains[0])
+            fut.result()
+            for chain in chains:
+                main.wait_stream(chain[1]._stream)
+        else:
+            for p in range(self.P):
+                for chain in chains:
+                    one(chain, p)
         return prices_s, prices_l, stats_s, stats_l
 
     def _partition_layout(self, kind, y, idx):

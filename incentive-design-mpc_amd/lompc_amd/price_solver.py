@@ -24,6 +24,7 @@ step runs redundantly on every rank with identical inputs.
 """
 from __future__ import annotations
 
+import functools
 import ctypes
 
 import numpy as np
@@ -39,6 +40,26 @@ def _torch():
     import torch
 
     return torch
+
+
+def _solver_stream(fn):
+    """Run a PriceSolver method on the solver's own stream, ordered after the caller's stream
+    (its inputs) and before it (its outputs), so two solvers' loops can run side by side."""
+
+    @functools.wraps(fn)
+    def wrapped(self, *args, **kwargs):
+        torch = _torch()
+        caller = torch.cuda.current_stream(self.lompc.device)
+        if caller == self._stream:
+            return fn(self, *args, **kwargs)
+        self._stream.wait_stream(caller)
+        try:
+            with torch.cuda.stream(self._stream):
+                return fn(self, *args, **kwargs)
+        finally:
+            caller.wait_stream(self._stream)
+
+    return wrapped
 
 
 class PriceSolver:
@@ -79,6 +100,8 @@ class PriceSolver:
         self._A_bar = None
         self._A_bar_inv = None
         self._kappa = None
+        # the solver's own stream: its loop can run beside the other EV type's (charging_station)
+        self._stream = torch.cuda.Stream(device=self.lompc.device)
         self.n_batched_calls = 0
 
     # ------------------------------------------------------------ price_solver.py
@@ -108,6 +131,8 @@ class PriceSolver:
 
         return dist.get_rank(self.group)
 
+
+    @_solver_stream
     def set_charge_levels(self, y0) -> None:
         """price_solver.py:66-77.  y0: (nEVs,) ndarray or device tensor (this rank's shard
         in sharded mode)."""
@@ -144,6 +169,8 @@ class PriceSolver:
         self.gamma_sm = self.consts.y_max - y_mean
         self._build_plans(gamma)
 
+
+    @_solver_stream
     def set_charge_levels_stats(self, y0d, n: int, y_hi: float, y_lo: float, y_sum: float) -> None:
         """set_charge_levels for a device slice of charge levels whose (global) count / max /
         min / sum the caller already has (ChargingStation computes every partition's in one pass
@@ -190,6 +217,8 @@ class PriceSolver:
         self._w0_live = False  # the w0 plan follows lazily (get_w0_price0_device)
         self._B = B
 
+
+    @_solver_stream
     def compute_optimal_prices(self, w_ref: np.ndarray, lmbd_r: float) -> tuple[np.ndarray, dict]:
         """
         Inputs:
@@ -209,6 +238,9 @@ class PriceSolver:
         # Initialize price iterate from previous prices.
         lmbd_k, lmbd_k_new = np.zeros((3 * self.N)), np.zeros((3 * self.N))
         lmbd_k[: self.r] = self.prev_prices
+        if self.group is None and PRINT_LEVEL < 2:  # the whole loop in one C-ABI call
+            return self._finish_prices(*self._native_loop(lmbd_k, lmbd_r, w_ref, A_bar, tol), lmbd_r, w_ref, A_bar,
+                                       tol, w0_err_bound)
         phi_w_ref = self.lompc.phi(w_ref)
         # one engine call: the batch error at lmbd_k and the central solve (price_solver.py:106)
         errs, (w_k, dual_cost) = self._iterate(lmbd_k, lmbd_r, w_ref, A_bar)
@@ -244,6 +276,45 @@ class PriceSolver:
             dual_cost_decrease_pred.append(dual_cost_derease)
             dual_cost = dual_cost_new
             lmbd_k = lmbd_k_new
+        return self._finish_prices(lmbd_k, w_k, iter, dual_cost_decrease_ac, dual_cost_decrease_pred, lmbd_r, w_ref,
+                                   A_bar, tol, w0_err_bound)
+
+    def _native_loop(self, lmbd_k, lmbd_r, w_ref, A_bar, tol):
+        """price_solver.py:106-140 in ONE call (lompc_price_loop): plan runs, copies, syncs and
+        price steps stay in C++ until convergence."""
+        if self._plan is None:
+            raise RuntimeError("set_charge_levels first")
+        MAX = _settings.MAX_PRICE_SOLVER_ITERATIONS
+        A_bar = np.ascontiguousarray(A_bar, dtype=np.float64)
+        w_ref = np.ascontiguousarray(w_ref, dtype=np.float64)
+        args = _lib.PriceLoopArgs(
+            self.N, self.r, MAX, 1 if _settings.PRICE_SOLVER_TOL_TYPE != "max" else 0, float(self.consts.theta),
+            float(self.consts.w_max), float(self.m), float(self._kappa_of(self._A_bar_inv)), float(self.eps_reg),
+            float(tol), float(self.nEVs), float(lmbd_r), A_bar.ctypes.data, w_ref.ctypes.data, self._in.data_ptr(),
+            self._h_in.data_ptr(), self._plan.out["set_sum_w"].data_ptr(), self._plan.out["set_stats"].data_ptr(),
+            self._h_sw.data_ptr(), self._h_st.data_ptr())
+        lm = np.ascontiguousarray(lmbd_k, dtype=np.float64).copy()
+        w_k = np.empty(self.N)
+        dec_ac, dec_pred = np.empty(MAX), np.empty(MAX)
+        dual_cost, it = ctypes.c_double(0.0), ctypes.c_int(0)
+        errs = np.empty(3)
+        rc = self._lib.lompc_price_loop(self._plan._plan, ctypes.byref(args), lm.ctypes.data, w_k.ctypes.data,
+                                        ctypes.byref(dual_cost), dec_ac.ctypes.data, dec_pred.ctypes.data,
+                                        ctypes.byref(it), errs.ctypes.data, self._plan._stream)
+        if rc != _lib.LOMPC_OK:
+            text = self._lib.lompc_plan_last_error(self._plan._plan).decode(errors="replace")
+            if rc == _lib.LOMPC_ERR_NOT_CONVERGED:
+                raise SolverError(text)
+            if "gamma" in text:
+                raise AssertionError(text)
+            raise ValueError(text)
+        n = it.value
+        self.n_batched_calls += n + 1
+        return lm, w_k, min(n, MAX - 1), list(dec_ac[:n]), list(dec_pred[:n])
+
+    def _finish_prices(self, lmbd_k, w_k, iter, dual_cost_decrease_ac, dual_cost_decrease_pred, lmbd_r, w_ref,
+                       A_bar, tol, w0_err_bound):
+        PRINT_LEVEL = _settings.PRINT_LEVEL
         # Regularize prices (price_solver.py:145-147).
         price_pre = self.lompc.phi(w_k) @ lmbd_k
         lmbd_k[: self.r] = self._regularize_prices(w_k, lmbd_k[: self.r])
@@ -315,7 +386,7 @@ class PriceSolver:
             allreduce_set_results(sw, st, group=self.group)
         self._h_sw.copy_(sw, non_blocking=True)
         self._h_st.copy_(st, non_blocking=True)
-        torch.cuda.current_stream(self.lompc.device).synchronize()
+        self._stream.synchronize()
         sw, st = self._h_sw.numpy(), self._h_st.numpy()
         self._check_stats(st)
         # price_solver.py:210-214 from the fused sums
@@ -333,6 +404,8 @@ class PriceSolver:
         if np.any(st[:, _lib.LOMPC_STAT_N_FAILED] > 0):
             raise SolverError("LoMPC QPs without a certified optimum")
 
+
+    @_solver_stream
     def _get_w_err(self, lmbd: np.ndarray, lmbd_r: float, w_ref: np.ndarray,
                    A_bar: np.ndarray) -> tuple[float, float, float]:
         """price_solver.py:196-214: (w_err_max, w0_err, w_avg_err) with the per-EV loop batched."""
@@ -386,6 +459,8 @@ class PriceSolver:
         w0, price0_sum = self.get_w0_price0_device(lmbd, lmbd_r)
         return (w0.cpu().numpy() if w0 is not None else np.zeros(0)), price0_sum / self.nEVs
 
+
+    @_solver_stream
     def get_w0_price0_device(self, lmbd: np.ndarray, lmbd_r: float):
         """(w0 device tensor of this rank's EVs, global sum of price0) — no host copy of w0."""
         torch = _torch()

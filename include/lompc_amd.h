@@ -220,6 +220,33 @@ int lompc_plan_profile_read(lompc_plan* plan, int kernel, double* total_ms, int6
 const char* lompc_plan_last_error(const lompc_plan* plan);
 int lompc_plan_destroy(lompc_plan* plan);
 
+/* The price loop of one (EV type, partition) on a plan holding [this partition's EVs | the
+ * central QP] (PriceSolver.compute_optimal_prices, price_solver.py:106-140): repeated
+ * {lompc_plan_run at lmbd_k, one D2H copy + stream sync, convergence test, lompc_price_step}
+ * without returning to the caller until convergence.  Single-rank only (the sharded loop
+ * combines the reductions across ranks between iterations).  Buffers:
+ *   dev_in / host_in  [2*3N | 2 | 2N] = both sets' prices, lmbd_r, w_ref (the plan reads
+ *                     dev_in; host_in is pinned staging), dev_sw [2,N] / dev_st [2,8] the
+ *                     plan's set outputs, host_sw / host_st pinned copies.
+ * In/out: lmbd [3N] (prev prices in, converged out), w_k [N] (central solve at lmbd).
+ * Out: dual_cost (last), dec_actual / dec_pred [max_iter] (price_solver.py:133-138, with the
+ * reference's lmbd_k / lmbd_k_new aliasing: the actual decrease drops the price term after
+ * the first iteration), *iterations = price steps taken (the reference's `iter` at the break;
+ * max_iter when the cap was hit, where the reference's `iter` is max_iter - 1),
+ * errs [3] = (w_err_max, w0_err, w_avg_err) at the final prices. */
+typedef struct lompc_price_loop_args {
+  int N, r, max_iter, tol_avg;          /* tol_avg: 1 = PRICE_SOLVER_TOL_TYPE "avg", 0 = "max" */
+  double theta, w_max, m, kappa, eps_reg, tol, n_evs, lmbd_r;
+  const double* A_bar;                  /* host [N, N] */
+  const double* w_ref;                  /* host [N]    */
+  double* dev_in; double* host_in;
+  const double* dev_sw; const double* dev_st;
+  double* host_sw; double* host_st;
+} lompc_price_loop_args;
+int lompc_price_loop(lompc_plan* plan, const lompc_price_loop_args* args, double* lmbd, double* w_k,
+                     double* dual_cost, double* dec_actual, double* dec_pred, int* iterations,
+                     double* errs, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Host-side solvers of the price iteration (no device, no context).  They run
  * once per price iteration / per partition next to the convergence test, like

@@ -91,6 +91,9 @@ struct lompc_plan {
   int G = 0;                    // gamma cells per set (k_path waves per set)
   int nblk = 0;                 // k_eval workgroups (blocks of one set's EVs)
   int n_cu = 0;
+  bool fused = false;           // k_path + k_eval as one launch (k_fused)
+  int* d_fused = nullptr;       // [1 + S] k_fused's ticket + per-set published-cell counters
+  int64_t cap_fused = 0;
   CtxEnds ce{};                 // set s belongs to context #{k : ce.end[k] <= s}
   int eval_occ = 1;             // k_eval workgroups resident per CU (occupancy query)
   int64_t eval_occ_key = -1;    // (N, LDS pieces) it was queried for

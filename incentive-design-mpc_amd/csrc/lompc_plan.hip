@@ -50,7 +50,7 @@ __device__ long long g_stamps[65536 * 8];
 #define LQ_STAMP(k)                                                                         \
   do {                                                                                      \
     const long long t__ = __builtin_amdgcn_s_memtime();                                     \
-    if (threadIdx.x == 0 && blockIdx.x < 65536) g_stamps[blockIdx.x * 8 + (k)] = t__;      \
+    if ((threadIdx.x & 63) == 0 && blk < 65536) g_stamps[blk * 8 + (k)] = t__;              \
   } while (0)
 #else
 #define LQ_STAMP(k)
@@ -198,15 +198,14 @@ __device__ __forceinline__ void load_set(const QPConst& q, const double* __restr
   }
 }
 
-__global__ __launch_bounds__(64) void k_path(PathArgs a) {
-  __shared__ double2 p_ab[LQ_PPL][64];
-  __shared__ double p_cf[LQ_PPL][8];
-  __shared__ double p_ge[LQ_PPL];
-  const int blk = (int)blockIdx.x;
+// One (set, gamma cell) path by one wave (blk = s * G + cell); the wave's workgroup has
+// initialised the box table for the set's constants (lq_tab_init).  Every piece goes straight
+// to the cell's fixed slots with write-through stores (visible to any XCD once they complete).
+__device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
   const int G = a.G;
   const int s = __builtin_amdgcn_readfirstlane(blk / G);
   const int cell = blk - s * G;
-  const int lane = (int)threadIdx.x;
+  const int lane = (int)threadIdx.x & 63;
   const int N = a.N;
   const double* __restrict__ L = a.lmbd + (size_t)s * 3 * N;
   const double lr = a.lmbd_r[s];
@@ -218,7 +217,6 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
   double l2;
   bool bad;
   load_set(q, L, lr, N, lane, ws, l2, bad);
-  lq_tab_init(q);
   if (bad || (lane == 0 && !(lr >= 0.0))) atomicOr(a.errflag, 1);
   const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);  // lompc.py:128
   const double kappa = lr / q.delta;                            // price_solver.py:191
@@ -246,7 +244,7 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
 #ifdef LOMPC_STAMPS
     int nit = 0;
     const bool solved = lqw::wave_solve_path(q, ws, glo, sl, sol, has_sol, &nit);
-    if (threadIdx.x == 0 && blockIdx.x < 32768) g_stamps[blockIdx.x * 8 + 4] = nit;
+    if (lane == 0 && blk < 32768) g_stamps[blk * 8 + 4] = nit;
 #else
     const bool solved = lqw::wave_solve_path(q, ws, glo, sl, sol, has_sol);
 #endif
@@ -254,6 +252,7 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
     if (solved) {
       sl0 = sl;
       if (a.ws) a.ws[(size_t)blk * 64 + lane] = (uint8_t)sl;
+      const size_t sb = (size_t)blk * LQ_PPL;  // the cell's fixed piece slots
       // ---- parametric active-set tracking of w*(gamma) on [glo, ghi]
       double gcur = glo;
       int last = -1;
@@ -261,7 +260,7 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
       const double ee = ws.e_nat;
       for (int it = 0; it < max_iter && npc < LQ_PPL; ++it) {
 #ifdef LOMPC_STAMPS
-        if (threadIdx.x == 0 && blockIdx.x < 32768) g_stamps[blockIdx.x * 8 + 5] = it + 1;
+        if (lane == 0 && blk < 32768) g_stamps[blk * 8 + 5] = it + 1;
 #endif
         if (!has_sol) sol = lqw::solve_stage<2>(q, ws, 0.0, sl);  // the start's solve is reused
         has_sol = false;
@@ -322,16 +321,20 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
 #pragma unroll
           for (int k = 0; k < 6; ++k) t[k] = act ? t[k] : 0.0;
           lqw::wave_totals(t, N);
-          p_ab[npc][lane] = make_double2(av, bv);
+          if (lane < N) {
+            double* dst = reinterpret_cast<double*>(a.t_ab + (sb + npc) * N + lane);
+            st_wt8(dst, av);
+            st_wt8(dst + 1, bv);
+          }
           const double a0 = __shfl(av, 0, 64), b0v = __shfl(bv, 0, 64);
           if (lane < 8) {
             double v = t[0] + c0;
 #pragma unroll
             for (int k = 1; k < 6; ++k) v = lane == k ? t[k] : v;
             v = lane == 6 ? a0 : (lane == 7 ? b0v : v);
-            p_cf[npc][lane] = v;
+            st_wt8(a.t_cf + (sb + npc) * 8 + lane, v);
           }
-          if (lane == 0) p_ge[npc] = best;
+          if (lane == 0) st_wt8(a.t_ge + sb + npc, best);
           ++npc;
         }
         if (bj < 0) break;
@@ -342,22 +345,22 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
       }
     }
   }
-  // the cell's pieces in its fixed slots [blk * LQ_PPL, + npc)
-  const size_t sb = (size_t)blk * LQ_PPL;
-  for (int k = 0; k < npc; ++k) {  // npc is wave-uniform
-    if (lane < N) a.t_ab[(sb + k) * N + lane] = p_ab[k][lane];
-    if (lane < 8) a.t_cf[(sb + k) * 8 + lane] = p_cf[k][lane];
-  }
-  if (lane < npc) a.t_ge[sb + lane] = p_ge[lane];
   a.t_sl[(size_t)blk * 64 + lane] = (uint8_t)sl0;
   if (lane == 0) {
-    a.t_cnt[blk] = npc;
-    a.t_lo[blk] = glo;
+    __hip_atomic_store(a.t_cnt + blk, npc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_wt8(a.t_lo + blk, glo);
   }
   LQ_STAMP(3);
 #ifdef LOMPC_STAMPS
-  if (threadIdx.x == 0 && blockIdx.x < 65536) g_stamps[blockIdx.x * 8 + 6] = npc;
+  if (lane == 0 && blk < 65536) g_stamps[blk * 8 + 6] = npc;
 #endif
+}
+
+__global__ __launch_bounds__(64) void k_path(PathArgs a) {
+  const int blk = (int)blockIdx.x;
+  const int s = __builtin_amdgcn_readfirstlane(blk / a.G);
+  lq_tab_init(set_consts(a.qd, a.ce, s));
+  path_cell(a, blk);
 }
 
 // ---------------------------------------------------------------- k_eval
@@ -418,7 +421,31 @@ __device__ __forceinline__ void wave_ev_outputs(const QPConst& q, const lqw::Wav
            q.theta * q.theta * w0 * w0 * lr;
 }
 
-__global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
+// loads of the path table: plain after a kernel boundary, device-coherent (sc1, past any stale
+// L2 line of this XCD) when k_path's waves published them inside the same launch (k_fused)
+template <bool COH>
+__device__ __forceinline__ double ld_t(const double* p) {
+  if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool COH>
+__device__ __forceinline__ int ld_t(const int* p) {
+  if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool COH>
+__device__ __forceinline__ double2 ld_t(const double2* p) {
+  if constexpr (COH) {
+    const double* d = reinterpret_cast<const double*>(p);
+    return make_double2(ld_t<true>(d), ld_t<true>(d + 1));
+  } else {
+    return *p;
+  }
+}
+
+// One k_eval block (EVs [start, end) of one set, <= EVAL_MAXB) by the whole workgroup.
+template <bool COH>
+__device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
   // dynamic LDS: [cap][N] piece rows | [cap][8] coefficients | [cap] piece ends | cells:
   // coverage start | piece count
   extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
@@ -427,7 +454,7 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
   __shared__ double s_accw[EVAL_WAVES][LOMPC_MAX_N];              // per-wave row sums per stage
   __shared__ double s_red[EVAL_WAVES][8];
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int4 info = a.blk[blockIdx.x];
+  const int4 info = a.blk[blk];
   const int s = info.x, start = info.y, end = info.z;  // thread: EVs start + tid + EVAL_EVS h
   const int N = a.N, G = a.G;
   const int cap = a.cap;
@@ -451,8 +478,8 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
   const double lr = a.lmbd_r[s];
   const int cb = s * G;
   for (int c = tid; c < G; c += EVAL_EVS) {
-    s_cnt[c] = a.t_cnt[cb + c];
-    s_lo[c] = a.t_lo[cb + c];
+    s_cnt[c] = ld_t<COH>(a.t_cnt + cb + c);
+    s_lo[c] = ld_t<COH>(a.t_lo + cb + c);
   }
   // the set's piece slots (the first `cap`: cells past them are re-solved individually), all
   // of them whatever the cells' counts, so every load of the staging is in one memory round:
@@ -469,7 +496,7 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int it = b0 + EVAL_EVS * u;
-        v[u] = it < nab ? gab[it] : make_double2(0.0, 0.0);
+        v[u] = it < nab ? ld_t<COH>(gab + it) : make_double2(0.0, 0.0);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -482,7 +509,7 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int it = b0 + EVAL_EVS * u;
-        v[u] = it < ncf ? gcf[it] : (it < ncf + np ? a.t_ge[sb + it - ncf] : 0.0);
+        v[u] = it < ncf ? ld_t<COH>(gcf + it) : (it < ncf + np ? ld_t<COH>(a.t_ge + sb + it - ncf) : 0.0);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -538,13 +565,13 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
     s_k[wv][64 * h + lane] = (act && !valid) ? -2 : (cov ? key : -1);
     const unsigned long long need = __ballot(valid && !cov);
     if (valid && !cov) {
-      a.fail_idx[(size_t)blockIdx.x * EVAL_MAXB + 64 * EVAL_PASSES * wv + nlist +
+      a.fail_idx[(size_t)blk * EVAL_MAXB + 64 * EVAL_PASSES * wv + nlist +
                  __popcll(need & ((1ull << lane) - 1ull))] = i;
       ++n_fail;
     }
     nlist += __popcll(need);
   }
-  if (lane == 0) a.fail_cnt[(size_t)blockIdx.x * EVAL_WAVES + wv] = nlist;
+  if (lane == 0) a.fail_cnt[(size_t)blk * EVAL_WAVES + wv] = nlist;
   LQ_STAMPE(2);
   __builtin_amdgcn_wave_barrier();  // this wave's own rows in LDS: in order
   LQ_STAMPE(3);
@@ -639,7 +666,7 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
     }
   }
   __syncthreads();
-  double* part = a.partial + (size_t)blockIdx.x * (N + NPX);
+  double* part = a.partial + (size_t)blk * (N + NPX);
   if (tid < N) {  // stage t: every wave's row sums, then the re-solved rows
     double sw = 0.0;
     for (int k = 0; k < EVAL_WAVES; ++k) sw += s_accw[k][tid];
@@ -653,9 +680,73 @@ __global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) {
   LQ_STAMPE(5);
 }
 
+__global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) { eval_block<false>(a, (int)blockIdx.x); }
+
+// ---------------------------------------------------------------- k_fused
+// k_path and k_eval in ONE launch (plan option): grid = the k_eval blocks.  Phase A: every
+// workgroup takes path tickets (EVAL_WAVES consecutive cells of one set, one wave each) until
+// none are left, and publishes each cell (write-through stores, then a per-set count).  Phase B:
+// the workgroup evaluates its own block once its set's G cells are counted, reading the path
+// table with device-coherent loads.  A workgroup only ever waits for cells claimed by running
+// workgroups (it reaches phase B after the ticket counter ran out), so the launch cannot
+// deadlock whatever the dispatch order; the bounded spin is a guard, never expected to fire.
+// The early sets' evaluation overlaps the late sets' paths, and one launch boundary goes.
+struct FusedArgs {
+  int* tickets;   // [1] path tickets taken (k_finalize resets it)
+  int* set_done;  // [S] published cells per set (k_finalize resets them)
+  int* errflag;   // |= 2 if a workgroup gave up waiting
+  int n_tickets;  // S * G / EVAL_WAVES
+  int nblk;
+  int spin_max;
+};
+
+__global__ __launch_bounds__(EVAL_EVS) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_fused(PathArgs pa, EvalArgs ea, FusedArgs f) {
+  __shared__ int s_tk;
+  const int tid = (int)threadIdx.x, wv = tid >> 6;
+  for (;;) {  // phase A
+    if (tid == 0) s_tk = atomicAdd(f.tickets, 1);
+    __syncthreads();
+    const int t = s_tk;
+    __syncthreads();
+    if (t >= f.n_tickets) break;
+    const int c0 = t * EVAL_WAVES;
+    const int s = __builtin_amdgcn_readfirstlane(c0 / pa.G);
+    lq_tab_init(set_consts(pa.qd, pa.ce, s));
+    path_cell(pa, c0 + wv);
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's write-through stores have completed
+    if ((tid & 63) == 0) __hip_atomic_fetch_add(f.set_done + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // (the box table is rewritten by the next ticket)
+  }
+  const int b = (int)blockIdx.x;  // phase B
+  if (b >= f.nblk) return;
+  const int4 info = ea.blk[b];
+  if (tid == 0) {
+    int n = 0;
+    while (__hip_atomic_load(f.set_done + info.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pa.G &&
+           n < f.spin_max) {
+      __builtin_amdgcn_s_sleep(2);
+      ++n;
+    }
+    s_tk = n < f.spin_max;
+  }
+  __syncthreads();
+  if (s_tk) {
+    eval_block<true>(ea, b);
+  } else {  // guard: the block's EVs reported failed, the run flagged
+    const int W = ea.N + NPX;
+    double* part = ea.partial + (size_t)b * W;
+    if (tid < W) part[tid] = tid == ea.N + PX_N_FAILED ? (double)(info.z - info.y) : 0.0;
+    if (tid < EVAL_WAVES) ea.fail_cnt[(size_t)b * EVAL_WAVES + tid] = 0;
+    if (tid == 0) atomicOr(f.errflag, 2);
+  }
+}
+
+
 // ---------------------------------------------------------------- k_finalize
 struct FinalArgs {
   int N, G, want_err;
+  int* fused_tickets;      // k_fused's counters, reset here for the next run (or null)
+  int* fused_done;
   const QPConst* qd;
   CtxEnds ce;
   const int* blk_prefix;   // [S+1] k_eval workgroups of each set
@@ -777,6 +868,10 @@ __global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
       red[0][tid] = v;
     }
     __syncthreads();
+  }
+  if (tid == 0 && r.fused_done) {
+    r.fused_done[s] = 0;
+    if (s == 0) r.fused_tickets[0] = 0;
   }
   if (tid < N && r.set_sum_w) r.set_sum_w[(size_t)s * N + tid] = red[0][tid];
   if (tid < LOMPC_SET_STATS) {
@@ -942,6 +1037,17 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     fresh_ws = true;
   }
   if (warm && (fresh_ws || p->G != G || p->S != S)) HIPCHK(p, hipMemsetAsync(p->d_ws, 1, (size_t)ncell * 64, st));
+  // k_fused (k_path + k_eval in one launch): its ticket and per-set counters, zero between runs
+  if (S + 1 > p->cap_fused) {
+    if ((rc = grow(p, &p->d_fused, S + 1))) return rc;
+    HIPCHK(p, hipMemsetAsync(p->d_fused, 0, (S + 1) * sizeof(int), st));
+    p->cap_fused = S + 1;
+  }
+  {
+    const char* env = getenv("LOMPC_FUSED");  // diagnostics: force the split / fused launches
+    const bool want = env ? atoi(env) != 0 : (flags & LOMPC_PLAN_FUSED) != 0;
+    p->fused = want && G % EVAL_WAVES == 0;
+  }
   p->B = B;
   p->S = S;
   p->G = G;
@@ -1015,7 +1121,39 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   pa.t_cf = p->t_cf;
   pa.t_ab = p->t_ab;
   pa.errflag = p->d_errflag;
-  {
+  EvalArgs a{};
+  a.S = (int)p->S;
+  a.G = p->G;
+  a.N = N;
+  a.want_err = 1;
+  a.qd = p->d_q;
+  a.ce = p->ce;
+  a.blk = p->d_blk;
+  a.set_off = p->d_set_off;
+  a.window = p->d_window;
+  a.gamma = p->gamma;
+  a.lmbd = lmbd;
+  a.lmbd_r = lmbd_r;
+  a.w_ref = p->w_ref;
+  a.t_cnt = p->t_cnt;
+  a.t_lo = p->t_lo;
+  a.t_sl = p->t_sl;
+  a.t_ge = p->t_ge;
+  a.t_cf = p->t_cf;
+  a.t_ab = p->t_ab;
+  a.w = w;
+  a.cost = cost;
+  a.w0 = w0;
+  a.status = status;
+  a.partial = p->d_partial;
+  a.fail_cnt = p->d_fail_cnt;
+  a.fail_idx = p->d_fail_idx;
+  a.w_rsrc_ok = (p->B * (int64_t)N * 8) < (1ll << 31) ? 1 : 0;
+  a.cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
+  const size_t lds = eval_lds(N, p->G, a.cap);
+  const bool cprof = prof_ctx && prof_ctx->prof;  // lompc_solve_batch: the context's k_eval timing
+  const bool fused = p->fused && p->nblk > 0;
+  if (!fused) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
     hipExtLaunchKernelGGL(k_path, dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa);
@@ -1023,41 +1161,15 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
     plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
   }
   if (p->nblk > 0) {
-    EvalArgs a{};
-    a.S = (int)p->S;
-    a.G = p->G;
-    a.N = N;
-    a.want_err = 1;
-    a.qd = p->d_q;
-    a.ce = p->ce;
-    a.blk = p->d_blk;
-    a.set_off = p->d_set_off;
-    a.window = p->d_window;
-    a.gamma = p->gamma;
-    a.lmbd = lmbd;
-    a.lmbd_r = lmbd_r;
-    a.w_ref = p->w_ref;
-    a.t_cnt = p->t_cnt;
-    a.t_lo = p->t_lo;
-    a.t_sl = p->t_sl;
-    a.t_ge = p->t_ge;
-    a.t_cf = p->t_cf;
-    a.t_ab = p->t_ab;
-    a.w = w;
-    a.cost = cost;
-    a.w0 = w0;
-    a.status = status;
-    a.partial = p->d_partial;
-    a.fail_cnt = p->d_fail_cnt;
-    a.fail_idx = p->d_fail_idx;
-    a.w_rsrc_ok = (p->B * (int64_t)N * 8) < (1ll << 31) ? 1 : 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    const bool cprof = prof_ctx && prof_ctx->prof;  // lompc_solve_batch: the context's k_eval timing
     if (cprof ? take_events(prof_ctx->prof_pool, &e0, &e1) : plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1))
       return fail_arg(p, "profiling events");
-    a.cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
-    const size_t lds = eval_lds(N, p->G, a.cap);
-    hipExtLaunchKernelGGL(k_eval, dim3((unsigned)p->nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, a);
+    if (fused) {  // k_path + k_eval in one launch (timed as k_eval)
+      FusedArgs f{p->d_fused, p->d_fused + 1, p->d_errflag, (int)(p->S * p->G / EVAL_WAVES), p->nblk, 1 << 24};
+      hipExtLaunchKernelGGL(k_fused, dim3((unsigned)p->nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, pa, a, f);
+    } else {
+      hipExtLaunchKernelGGL(k_eval, dim3((unsigned)p->nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, a);
+    }
     HIPCHK(p, hipGetLastError());
     if (cprof) {
       prof_ctx->prof_ev.push_back(e0);
@@ -1090,6 +1202,8 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   r.set_sum_w = set_sum_w;
   r.set_stats = set_stats;
   r.stats = p->d_stats;
+  r.fused_tickets = p->d_fused;
+  r.fused_done = p->d_fused ? p->d_fused + 1 : nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (plan_prof_begin(p, LOMPC_PLAN_K_FINAL, &e0, &e1)) return fail_arg(p, "profiling events");
   hipExtLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, e0, e1, 0, r);
@@ -1104,7 +1218,7 @@ void lq_plan_free(lompc_plan* p) {
   (void)hipDeviceSynchronize();
   void* ptrs[] = {p->d_meta,  p->d_stats_own, p->d_window, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
                   p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag,
-                  p->d_fail_cnt, p->d_fail_idx};
+                  p->d_fail_cnt, p->d_fail_idx, p->d_fused};
   for (void* x : ptrs)
     if (x) (void)hipFree(x);
   if (p->h_buf) (void)hipHostFree(p->h_buf);
@@ -1180,8 +1294,11 @@ int lompc_price_loop(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd
     const int rc = lq_plan_launch(p, a->dev_in, a->dev_in + 2 * N3, nullptr, nullptr, nullptr, nullptr,
                                   const_cast<double*>(a->dev_sw), const_cast<double*>(a->dev_st), st, nullptr);
     if (rc) return rc;
-    HIPCHK(p, hipMemcpyAsync(a->host_sw, a->dev_sw, 2 * N * sizeof(double), hipMemcpyDeviceToHost, st));
-    HIPCHK(p, hipMemcpyAsync(a->host_st, a->dev_st, 2 * LOMPC_SET_STATS * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (a->dev_sw != a->host_sw)  // (pinned outputs written by the kernel itself need no copy)
+      HIPCHK(p, hipMemcpyAsync(a->host_sw, a->dev_sw, 2 * N * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (a->dev_st != a->host_st)
+      HIPCHK(p, hipMemcpyAsync(a->host_st, a->dev_st, 2 * LOMPC_SET_STATS * sizeof(double), hipMemcpyDeviceToHost,
+                               st));
     HIPCHK(p, hipStreamSynchronize(st));
     const double* sw = a->host_sw;
     const double* sst = a->host_st;

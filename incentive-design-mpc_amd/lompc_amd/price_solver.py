@@ -291,8 +291,7 @@ class PriceSolver:
             self.N, self.r, MAX, 1 if _settings.PRICE_SOLVER_TOL_TYPE != "max" else 0, float(self.consts.theta),
             float(self.consts.w_max), float(self.m), float(self._kappa_of(self._A_bar_inv)), float(self.eps_reg),
             float(tol), float(self.nEVs), float(lmbd_r), A_bar.ctypes.data, w_ref.ctypes.data, self._in.data_ptr(),
-            self._h_in.data_ptr(), self._plan.out["set_sum_w"].data_ptr(), self._plan.out["set_stats"].data_ptr(),
-            self._h_sw.data_ptr(), self._h_st.data_ptr())
+            self._h_in.data_ptr(), *self._loop_outs(), self._h_sw.data_ptr(), self._h_st.data_ptr())
         lm = np.ascontiguousarray(lmbd_k, dtype=np.float64).copy()
         w_k = np.empty(self.N)
         dec_ac, dec_pred = np.empty(MAX), np.empty(MAX)
@@ -311,6 +310,15 @@ class PriceSolver:
         n = it.value
         self.n_batched_calls += n + 1
         return lm, w_k, min(n, MAX - 1), list(dec_ac[:n]), list(dec_pred[:n])
+
+    def _loop_outs(self):
+        """Where the native loop's plan runs write the two sets' reductions: straight into the
+        pinned host buffers (zero copy; LOMPC_ZERO_COPY=0: the plan's device outputs + copies)."""
+        import os
+
+        if os.environ.get("LOMPC_ZERO_COPY", "1") != "0":
+            return self._h_sw.data_ptr(), self._h_st.data_ptr()
+        return self._plan.out["set_sum_w"].data_ptr(), self._plan.out["set_stats"].data_ptr()
 
     def _finish_prices(self, lmbd_k, w_k, iter, dual_cost_decrease_ac, dual_cost_decrease_pred, lmbd_r, w_ref,
                        A_bar, tol, w0_err_bound):

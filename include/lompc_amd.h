@@ -165,7 +165,8 @@ typedef struct lompc_plan lompc_plan;
 #define LOMPC_PLAN_WARM_START 1 /* flag: start each gamma cell's exact solve from the working
                                    set the previous run of the plan ended with there (prices
                                    that change little between price iterations) */
-#define LOMPC_PLAN_DIAG_REPAIR 2 /* diagnostics: no solution path, every EV takes the individual
+#define LOMPC_PLAN_DIAG_REPAIR 2
+#define LOMPC_PLAN_FUSED 4       /* k_path and k_eval as one launch */ /* diagnostics: no solution path, every EV takes the individual
                                     whole-wave re-solve (status REPAIRED) */
 
 /* Build a plan over B EVs grouped by set (S = sum of sets_per_ctx sets):
@@ -227,7 +228,8 @@ int lompc_plan_destroy(lompc_plan* plan);
  * combines the reductions across ranks between iterations).  Buffers:
  *   dev_in / host_in  [2*3N | 2 | 2N] = both sets' prices, lmbd_r, w_ref (the plan reads
  *                     dev_in; host_in is pinned staging), dev_sw [2,N] / dev_st [2,8] the
- *                     plan's set outputs, host_sw / host_st pinned copies.
+ *                     plan's set outputs, host_sw / host_st pinned copies (dev_* == host_*:
+ *                     the kernels write the pinned buffers directly, no copy).
  * In/out: lmbd [3N] (prev prices in, converged out), w_k [N] (central solve at lmbd).
  * Out: dual_cost (last), dec_actual / dec_pred [max_iter] (price_solver.py:133-138, with the
  * reference's lmbd_k / lmbd_k_new aliasing: the actual decrease drops the price term after

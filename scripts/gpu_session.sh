@@ -36,9 +36,12 @@ for s in $STEPS; do
     sprof) run sprof 300 python scripts/station_profile.py ;;
     bimpc) run bimpc 300 python scripts/bimpc_timing.py ;;
     stampsvar) for v in ${KS_VARIANTS}; do KS_VARIANT=$v run stamps_$v 300 python scripts/kstamps.py || exit $?; done ;;
+    qfused) LOMPC_FUSED=1 run qfused 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_parity.py tests/test_gpu_baseline_configs.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    bfused) LOMPC_FUSED=1 run bfused 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct ;;
+    bfusednoev) LOMPC_FUSED=1 run bfusednoev 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct --no-kernel-events ;;
+    sprofcopy) LOMPC_ZERO_COPY=0 run sprofcopy 300 python scripts/station_profile.py ;;
     bcost) run bcost 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs cost ;;
     bset) run bset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs set ;;
-    bfused) LOMPC_REDUCE_FUSED=1 run bfused 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
     bwarm) run bwarm 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --warm ;;
     bwarmset) run bwarmset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --warm --outputs set ;;
     stampsw) KS_WARM=1 run stampsw 300 python scripts/kstamps.py && KS_WARM=1 KS_OUTPUTS=set run stampsw_set 300 python scripts/kstamps.py ;;

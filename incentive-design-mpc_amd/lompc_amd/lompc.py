@@ -333,13 +333,14 @@ class BatchPlan:
     pointers).  No synchronisation; ``check()`` synchronises and raises on failures.
     w_ref (S, N) is read at every run (update it in place).  ``warm_start``: every gamma
     cell's exact solve starts from the working set the previous run ended with.  ``diag_repair``
-    (diagnostics): no solution path, every EV is re-solved individually.
+    (diagnostics): no solution path, every EV is re-solved individually.  ``fused``: k_path and
+    k_eval as one launch (k_fused; needs cells per set divisible by 8).
     DIRECT-mode contexts fall back to ``lompc_run`` (one context only).
     """
 
     def __init__(self, lompc, gamma, set_offsets, *, sets_per_ctx=None, w_ref=None, gamma_ref=None, want_w=True,
                  want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None, validate=True,
-                 warm_start=False, diag_repair=False):
+                 warm_start=False, diag_repair=False, fused=False):
         torch = _torch()
         lompcs = list(lompc) if isinstance(lompc, (list, tuple)) else [lompc]
         self.lompcs = lompcs
@@ -372,7 +373,8 @@ class BatchPlan:
             return
         ctxs = (ctypes.c_void_p * len(lompcs))(*[x._ctx.value for x in lompcs])
         plan = ctypes.c_void_p()
-        flags = (_lib.LOMPC_PLAN_WARM_START if warm_start else 0) | (_lib.LOMPC_PLAN_DIAG_REPAIR if diag_repair else 0)
+        flags = ((_lib.LOMPC_PLAN_WARM_START if warm_start else 0) | (_lib.LOMPC_PLAN_DIAG_REPAIR if diag_repair else 0)
+                 | (_lib.LOMPC_PLAN_FUSED if fused else 0))
         rc = self._lib.lompc_plan_create(len(lompcs), ctypes.cast(ctxs, ctypes.c_void_p), self.sets_per_ctx.ctypes.data,
                                          self.B, _ptr(self.gamma), self.off.ctypes.data, _ptr(self.w_ref), flags,
                                          self._stream, ctypes.byref(plan))

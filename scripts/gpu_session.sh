@@ -39,7 +39,7 @@ for s in $STEPS; do
     qfused) LOMPC_FUSED=1 run qfused 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_parity.py tests/test_gpu_baseline_configs.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bfused) LOMPC_FUSED=1 run bfused 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct ;;
     bfusednoev) LOMPC_FUSED=1 run bfusednoev 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct --no-kernel-events ;;
-    sprofcopy) LOMPC_ZERO_COPY=0 run sprofcopy 300 python scripts/station_profile.py ;;
+    sprofzc) LOMPC_ZERO_COPY=1 run sprofzc 300 python scripts/station_profile.py ;;
     bcost) run bcost 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs cost ;;
     bset) run bset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs set ;;
     bwarm) run bwarm 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --warm ;;

@@ -267,3 +267,35 @@ def test_warm_start_and_cell_counts(gpu, ev, N):
             os.environ.pop("LOMPC_CELLS", None)
         else:
             os.environ["LOMPC_CELLS"] = old
+
+
+def test_fused_plan_matches_split(gpu):
+    """LOMPC_PLAN_FUSED (k_path + k_eval in one launch, k_fused) gives bitwise the split
+    launches' outputs: same path and evaluation code, the path table read coherently; repeated
+    runs check that the fused counters are reset between runs."""
+    N, P = 24, 12
+    rng = np.random.default_rng(21)
+    cs = [O.small_consts(), O.large_consts()]
+    lompcs = [LoMPC(N, LoMPCConstants(c.delta, c.theta, c.y_max, c.w_max, c.ev_type), device=0) for c in cs]
+    M = [30000, 30001]
+    off1 = [np.array([(m * p) // P for p in range(P + 1)], dtype=np.int64) for m in M]
+    off = np.concatenate([off1[0], M[0] + off1[1][1:]])
+    g = torch.as_tensor(np.concatenate([c.y_max - (0.3 + 0.2 * rng.random(m)) for c, m in zip(cs, M)]), device="cuda:0")
+    wr = torch.as_tensor(np.concatenate([c.w_max * rng.random((P, N)) for c in cs]), device="cuda:0")
+    lms = [torch.as_tensor(np.concatenate([c.theta * rng.random((P, 3 * N)) for c in cs]), device="cuda:0")
+           for _ in range(3)]
+    lr = torch.zeros(2 * P, dtype=torch.float64, device="cuda:0")
+    outs = []
+    for fused in (False, True):
+        plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], w_ref=wr, want_status=True, fused=fused)
+        assert plan.cells % 8 == 0
+        res = []
+        for lm in lms:
+            out = plan.run(lm, lr)
+            rep, fail, inv = plan.check()
+            assert fail == 0 and inv == 0
+            res.append({k: v.clone() for k, v in out.items() if v is not None})
+        outs.append(res)
+    for a, b in zip(*outs):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k

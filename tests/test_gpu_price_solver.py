@@ -44,13 +44,17 @@ def compare(lm, st, lmo, sto, theta):
         np.testing.assert_allclose(st[k], sto[k], rtol=1e-6, atol=1e-6 * np.max(np.abs(sto[k]), initial=1.0))
 
 
+@pytest.mark.parametrize("native", [True, False], ids=["native_loop", "python_loop"])
 @pytest.mark.parametrize("case", SWEEP, ids=lambda c: f"{c[0]}-{c[3]}-{c[4]}-N{c[2]}-lr{c[5]}")
-def test_compute_optimal_prices_matches_oracle(gpu, case, monkeypatch):
+def test_compute_optimal_prices_matches_oracle(gpu, case, native, monkeypatch):
+    """Both loops: the single-rank C++ loop (lompc_price_loop) and the Python restatement (used
+    with PRINT_LEVEL >= 2 and on sharded ranks)."""
     name, nev, N, ev, price_type, lmbd_r, spread = case
     monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
     c, lc = consts(ev)
     rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
     ps = PriceSolver(N, lc, price_type, device=0)
+    ps.native_loop = native
     po = PO.OraclePriceSolver(N, c, price_type)
     for call in range(2):  # the second call starts from prev_prices (price_solver.py:104, :166)
         y0 = spread * c.y_max * rng.random(nev)  # test_price_solver.py:32

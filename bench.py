@@ -64,6 +64,9 @@ def parse():
                     help="path mode: one plan per EV type, each on its own stream (overlapping)")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostics: no HIP events on the per-EV kernel's dispatches in the timed region")
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="HIP events on the per-EV kernel's dispatch of every E-th timed step (the "
+                         "events' own cost, ~2 us per pair, stays out of the other steps)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-station", action="store_true", help="skip the BiMPC steps/sec leg")
     ap.add_argument("--station-evs-per-gpu", type=int, default=262144, help="EVs per GPU, half per type")
@@ -182,8 +185,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev_every = max(1, args.event_every)
     t0 = time.perf_counter()
     for k in range(args.warmup, nsteps):
+        sample = not args.no_kernel_events and (k - args.warmup) % ev_every == 0
+        if ev_every > 1 and not args.no_kernel_events:
+            for r in runs:
+                r["plan"].profile(enable=("k_eval",) if sample else False)
         step(k)
     t_issue = time.perf_counter() - t0  # host time to enqueue the K steps (GPU-bound if << dt)
     torch.cuda.synchronize()
@@ -239,6 +247,7 @@ def main():
             "warm_start": bool(args.warm),
             "parallelism": f"dp{world} (EV shards, one RCCL all-gather of both types' per-set reductions per step)",
             "launches_per_step": 3 * len(runs),
+            "kernel_events": "none" if args.no_kernel_events else f"k_eval, 1 in {ev_every} timed steps",
         },
         "roofline": {
             "bound": "hbm",

@@ -302,7 +302,8 @@ struct Newton {
       }
       // X = T_k^-1 from the LDL' factors: X_jj = 1/d_j + l_j^2 X_{j+1,j+1} and, above the
       // diagonal, row i = -l_i x row i+1 (L'X = D^-1 L^-1 is lower triangular); rows are
-      // independent vector operations, no per-column substitution chains
+      // independent vector operations, no per-column substitution chains.  Upper triangle only:
+      // the sum below mirrors it once.
       X[(size_t)(N - 1) * N + N - 1] = 1.0 / dd[N - 1];
       for (int i = N - 2; i >= 0; --i) {
         double* xi = X + (size_t)i * N;
@@ -311,16 +312,17 @@ struct Newton {
         for (int j = i + 1; j < N; ++j) xi[j] = -li * x1[j];
         xi[i] = 1.0 / dd[i] + li * li * x1[i + 1];
       }
-      for (int i = 1; i < N; ++i)  // lower triangle by symmetry
-        for (int j = 0; j < i; ++j) X[(size_t)i * N + j] = X[(size_t)j * N + i];
     });
     for (int k = 0; k < nb; ++k) {
       if (!okk[k]) return false;
       if (ck[k] == 0.0) continue;
       const double c2 = ck[k] * ck[k];  // sum c_k^2 T_k^-1, in block order
       const double* X = &Xk[(size_t)k * N * N];
-      for (size_t e = 0; e < (size_t)N * N; ++e) T[e] += c2 * X[e];
+      for (int i = 0; i < N; ++i)
+        for (int j = i; j < N; ++j) T[(size_t)i * N + j] += c2 * X[(size_t)i * N + j];
     }
+    for (int i = 1; i < N; ++i)  // lower triangle by symmetry
+      for (int j = 0; j < i; ++j) T[(size_t)i * N + j] = T[(size_t)j * N + i];
     // T = A^-1 (sum c_k^2 T_k^-1) A^-T: differences along the columns, then along the rows
     for (int i = N - 1; i > 0; --i)
       for (int j = 0; j < N; ++j) T[(size_t)i * N + j] -= T[(size_t)(i - 1) * N + j];
@@ -919,6 +921,11 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
       bf = fval;
       since_best = 0;
     } else if (++since_best >= 15) {
+      break;
+    } else if (best_merit < 1e-6 && merit > 1e3 * best_merit) {
+      // breakdown next to the optimum (the exp weights' flat directions: the Newton steps lose
+      // accuracy, the step length collapses and the residuals blow up): the iterates do not
+      // come back, the best one is returned as below
       break;
     }
     if (pres <= 1e-10 * (1.0 + hmax) && dres <= 1e-9 * (1.0 + gmax) && gap <= 1e-10 * (1.0 + std::fabs(fval))) {

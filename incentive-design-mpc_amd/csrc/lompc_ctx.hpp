@@ -107,6 +107,8 @@ struct lompc_plan {
   int* d_blk_prefix = nullptr;    // [S+1] k_eval workgroups per set (view of d_meta)
   int4* d_blk = nullptr;          // [nblk] (set, first EV, end EV, -) (view of d_meta)
   double* d_window = nullptr;     // [S][2] (lo, hi) of the set's valid gamma, widened
+  unsigned long long* d_wacc = nullptr;  // [S][3] k_plan_window accumulators (~lo bits, hi bits,
+                                         // blocks done), zero between launches
   double* d_partial = nullptr;    // [nblk][N+NPX] k_eval workgroup records
   int* d_fail_cnt = nullptr;      // [nblk][waves] EVs listed for k_finalize's individual re-solve
   int* d_fail_idx = nullptr;      // [nblk][EVs]

@@ -105,46 +105,82 @@ __device__ __forceinline__ const QPConst& set_consts(const QPConst* qd, const Ct
 struct WindowArgs {
   const QPConst* qd;
   CtxEnds ce;
-  const int64_t* set_off;
+  const int4* blk;         // k_eval's block map: (set, begin, end)
+  const int* blk_prefix;   // [S+1] first block of each set
   const double* gamma;
+  unsigned long long* acc; // [S][3], zero on entry and on exit
   double* window;
+  int S, nblk;
 };
 
 // per set: [lo, hi] = range of its valid gamma, widened by 1e-7 y_max (a zero-width set still
-// gets cells of positive width), clipped to [0, y_max]; no valid EV -> [0, y_max]
+// gets cells of positive width), clipped to [0, y_max]; no valid EV -> [0, y_max].
+// One workgroup per k_eval block (>= one per CU): a block folds its EVs, then merges into its
+// set's accumulators with integer atomics (the bits of a non-negative double order like the
+// double, so min/max are exact and the result does not depend on the order); the set's last
+// block writes the window and zeroes the accumulators for the next launch.  One extra workgroup
+// (the last) writes the windows of the empty sets, which have no blocks.
 __global__ __launch_bounds__(256) void k_plan_window(WindowArgs a) {
-  __shared__ double smin[256], smax[256];
-  const int s = blockIdx.x;
+  __shared__ double smin[4], smax[4];
+  __shared__ int last;
+  if ((int)blockIdx.x == a.nblk) {
+    for (int s = threadIdx.x; s < a.S; s += 256)
+      if (a.blk_prefix[s + 1] == a.blk_prefix[s]) {
+        int k = 0;  // (s differs per lane: no scalar set_consts)
+        for (int j = 0; j + 1 < LQ_PLAN_MAX_CTX; ++j) k += s >= a.ce.end[j] ? 1 : 0;
+        a.window[2 * s] = 0.0;
+        a.window[2 * s + 1] = a.qd[k].y_max;
+      }
+    return;
+  }
+  const int4 bk = a.blk[blockIdx.x];
+  const int s = bk.x;
   const double ym = set_consts(a.qd, a.ce, s).y_max;
   double lo = INFINITY, hi = -INFINITY;
-  for (int64_t i = a.set_off[s] + threadIdx.x; i < a.set_off[s + 1]; i += 256) {
+  for (int i = bk.y + (int)threadIdx.x; i < bk.z; i += 256) {
     const double g = a.gamma[i];
     if (g >= 0.0 && g <= ym) {
       lo = fmin(lo, g);
       hi = fmax(hi, g);
     }
   }
-  smin[threadIdx.x] = lo;
-  smax[threadIdx.x] = hi;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o));
+    hi = fmax(hi, __shfl_xor(hi, o));
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    smin[wv] = lo;
+    smax[wv] = hi;
+  }
   __syncthreads();
-  for (int k = 128; k > 0; k >>= 1) {
-    if ((int)threadIdx.x < k) {
-      smin[threadIdx.x] = fmin(smin[threadIdx.x], smin[threadIdx.x + k]);
-      smax[threadIdx.x] = fmax(smax[threadIdx.x], smax[threadIdx.x + k]);
-    }
-    __syncthreads();
-  }
+  unsigned long long* acc = a.acc + 3 * s;
   if (threadIdx.x == 0) {
-    const double mg = 1e-7 * ym;
-    double wlo = 0.0, whi = ym;
-    if (smin[0] <= smax[0]) {
-      wlo = fmin(fmax(smin[0] - mg, 0.0), ym);
-      whi = fmin(fmax(smax[0] + mg, wlo + mg), ym);
-      if (!(whi > wlo)) wlo = fmax(whi - 2.0 * mg, 0.0);
+    lo = fmin(fmin(smin[0], smin[1]), fmin(smin[2], smin[3]));
+    hi = fmax(fmax(smax[0], smax[1]), fmax(smax[2], smax[3]));
+    if (lo <= hi) {  // + 0.0: -0.0 -> +0.0, whose bits order with the positive doubles
+      atomicMax(&acc[0], ~(unsigned long long)__double_as_longlong(lo + 0.0));
+      atomicMax(&acc[1], (unsigned long long)__double_as_longlong(hi + 0.0));
     }
-    a.window[2 * s] = wlo;
-    a.window[2 * s + 1] = whi;
+    __threadfence();
+    const unsigned long long nb = (unsigned long long)(a.blk_prefix[s + 1] - a.blk_prefix[s]);
+    last = atomicAdd(&acc[2], 1ull) == nb - 1;
   }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __threadfence();
+  const unsigned long long blo = atomicExch(&acc[0], 0ull), bhi = atomicExch(&acc[1], 0ull);
+  atomicExch(&acc[2], 0ull);
+  const double mg = 1e-7 * ym;
+  double wlo = 0.0, whi = ym;
+  if (blo != 0) {  // some valid gamma
+    wlo = fmin(fmax(__longlong_as_double((long long)~blo) - mg, 0.0), ym);
+    whi = fmin(fmax(__longlong_as_double((long long)bhi) + mg, wlo + mg), ym);
+    if (!(whi > wlo)) wlo = fmax(whi - 2.0 * mg, 0.0);
+  }
+  a.window[2 * s] = wlo;
+  a.window[2 * s + 1] = whi;
 }
 
 // cell of a valid gamma in a set's window (k_eval), the same arithmetic as k_path's cell bounds
@@ -1014,9 +1050,10 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   }
   if (!p->ev_stage) HIPCHK(p, hipEventCreateWithFlags(&p->ev_stage, hipEventDisableTiming));
   if (S > p->cap_S) {
-    if ((rc = grow(p, &p->d_window, 2 * S)) ||
+    if ((rc = grow(p, &p->d_window, 2 * S)) || (rc = grow(p, &p->d_wacc, 3 * S)) ||
         (rc = grow(p, &p->d_stats_own, S * LOMPC_SET_STATS)))
       return rc;
+    HIPCHK(p, hipMemsetAsync(p->d_wacc, 0, 3 * S * sizeof(unsigned long long), st));
     p->cap_S = S;
   }
   if (nblk > p->cap_blk) {
@@ -1092,8 +1129,8 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   p->d_blk_prefix = reinterpret_cast<int*>(p->d_meta + o_pre);
   HIPCHK(p, hipMemcpyAsync(p->d_meta, p->h_buf, need_h, hipMemcpyHostToDevice, st));
   HIPCHK(p, hipEventRecord(p->ev_stage, st));
-  WindowArgs wa{p->d_q, p->ce, p->d_set_off, gamma, p->d_window};
-  hipLaunchKernelGGL(k_plan_window, dim3((unsigned)S), dim3(256), 0, st, wa);
+  WindowArgs wa{p->d_q, p->ce, p->d_blk, p->d_blk_prefix, gamma, p->d_wacc, p->d_window, (int)S, (int)nblk};
+  hipLaunchKernelGGL(k_plan_window, dim3((unsigned)nblk + 1), dim3(256), 0, st, wa);
   HIPCHK(p, hipGetLastError());
   return LOMPC_OK;
 }
@@ -1218,7 +1255,7 @@ void lq_plan_free(lompc_plan* p) {
   (void)hipDeviceSynchronize();
   void* ptrs[] = {p->d_meta,  p->d_stats_own, p->d_window, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
                   p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag,
-                  p->d_fail_cnt, p->d_fail_idx, p->d_fused};
+                  p->d_fail_cnt, p->d_fail_idx, p->d_fused, p->d_wacc};
   for (void* x : ptrs)
     if (x) (void)hipFree(x);
   if (p->h_buf) (void)hipHostFree(p->h_buf);

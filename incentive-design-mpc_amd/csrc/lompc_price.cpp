@@ -11,8 +11,9 @@
 // modelling layer:
 //   * Dphi = [theta I; -theta I; 2 q_s diag(w)] (lompc.py:179-187): every row of Dphi touches ONE
 //     time step, so for any free set F the reduced Hessian 2P_FF = 2 eps I + U_F A_bar^-1 U_F' / m
-//     has U_F'U_F diagonal.  Woodbury turns each reduced solve into one N x N Cholesky of
-//     G = 2 eps m A_bar + diag(d_F) (N^3/3 flops instead of |F|^3/3).  Primal-dual active-set
+//     has U_F'U_F diagonal.  Woodbury turns each reduced solve into one solve with
+//     G = 2 eps m A_bar + diag(d_F), and A_bar = A'A + kappa I makes every such matrix
+//     A' (tridiagonal) A: O(N) per solve (TriSolve) instead of an N x N Cholesky.  Primal-dual active-set
 //     (PDAS) iterations from the previous free set, a finite primal active-set method as the
 //     fallback; the result is KKT-certified (LOMPC_ERR_NOT_CONVERGED otherwise).
 //   * an LP whose every column touches one row separates into one-row LPs; the optimum of each is
@@ -29,54 +30,89 @@
 
 namespace {
 
+// Solves with c A'A + diag(E) (A = tril(ones), c > 0, E >= 0) in O(N): since A^-1 is the
+// difference operator, c A'A + E = A' T A with T = c I + A^-T E A^-1 TRIDIAGONAL (diagonal
+// c + E_t + E_{t+1}, off-diagonal -E_{t+1}); x = A^-1 T^-1 A^-T b by two differences and one
+// tridiagonal LDL' solve (SPD: c > 0).
+struct TriSolve {
+  int N = 0;
+  std::vector<double> d, l;  // LDL' of T: inverse pivots, sub-diagonal multipliers
+  bool factor(int N_, double c, const double* E) {
+    N = N_;
+    d.resize(N);
+    l.resize(N);
+    for (int t = 0; t < N; ++t) {
+      const double En = t + 1 < N ? E[t + 1] : 0.0;
+      double a = c + E[t] + En;
+      if (t > 0) a += l[t - 1] * E[t];  // - l_{t-1}^2 p_{t-1} with l_{t-1} = -E_t / p_{t-1}
+      if (!(a > 0.0)) return false;
+      d[t] = 1.0 / a;
+      l[t] = -En * d[t];
+    }
+    return true;
+  }
+  void solve(double* x) const {  // in place: x <- (c A'A + E)^-1 x
+    for (int t = 0; t + 1 < N; ++t) x[t] -= x[t + 1];   // A^-T
+    for (int t = 1; t < N; ++t) x[t] -= l[t - 1] * x[t - 1];
+    for (int t = 0; t < N; ++t) x[t] *= d[t];
+    for (int t = N - 2; t >= 0; --t) x[t] -= l[t] * x[t + 1];
+    for (int t = N - 1; t > 0; --t) x[t] -= x[t - 1];    // A^-1
+  }
+};
+
 // Q = 2P = 2 eps I + U A_bar^-1 U' / m ;  row i of U is u[i] e_{i mod N}'.
+// A_bar = A'A + kappa I (price_solver.py:191-192).
 struct PriceQP {
   int N = 0, r = 0;
-  double eps = 0.0, m = 0.0;
-  std::vector<double> u, Abar, LA, G, s, v;
+  double eps = 0.0, m = 0.0, kappa = 0.0;
+  std::vector<double> u, E, s, v;
+  std::vector<int> st;  // stage of row i (i mod N, precomputed: integer division dominated the loops)
+  TriSolve Ab, Gf;
 
-  bool init(int N_, int r_, double theta, double w_max, double m_, double kappa, double eps_, const double* w) {
+  bool init(int N_, int r_, double theta, double w_max, double m_, double kappa_, double eps_, const double* w) {
     N = N_;
     r = r_;
     eps = eps_;
     m = m_;
+    kappa = kappa_;
     const double q_s = 3.0 * theta / (4.0 * w_max);  // lompc.py:67
     u.assign(r, 0.0);
+    st.resize(r);
     for (int i = 0; i < r; ++i) {
       const int b = i / N, j = i % N;
+      st[i] = j;
       u[i] = b == 0 ? theta : (b == 1 ? -theta : 2.0 * q_s * w[j]);  // Dphi rows, lompc.py:179-187
     }
-    Abar.assign((size_t)N * N, 0.0);  // A'A + kappa I, (A'A)_jk = N - max(j,k)   (price_solver.py:191-192)
-    for (int j = 0; j < N; ++j)
-      for (int k = 0; k < N; ++k) Abar[j * N + k] = (double)(N - std::max(j, k)) + (j == k ? kappa : 0.0);
-    LA = Abar;
-    G.assign((size_t)N * N, 0.0);
+    E.assign(N, kappa);
     s.assign(N, 0.0);
     v.assign(N, 0.0);
-    return lqd::chol(LA.data(), N);
+    return Ab.factor(N, 1.0, E.data());
   }
 
   void mulQ(const double* x, double* y) {
     std::fill(v.begin(), v.end(), 0.0);
-    for (int i = 0; i < r; ++i) v[i % N] += u[i] * x[i];
-    lqd::chol_solve(LA.data(), N, v.data());
-    for (int i = 0; i < r; ++i) y[i] = 2.0 * eps * x[i] + u[i] * v[i % N] / m;
+    for (int i = 0; i < r; ++i) v[st[i]] += u[i] * x[i];
+    Ab.solve(v.data());
+    const double im = 1.0 / m;
+    for (int i = 0; i < r; ++i) y[i] = 2.0 * eps * x[i] + u[i] * v[st[i]] * im;
   }
 
-  // z = argmin 1/2 z'Qz + q'z over {z : z_i = 0 for i not in F}
+  // z = argmin 1/2 z'Qz + q'z over {z : z_i = 0 for i not in F}:  Woodbury in the free rows,
+  // (a A_bar + D_F) s = U_F'q with a = 2 eps m, D_F = sum of u_i^2 over the free rows of a stage
   bool solveF(const std::vector<char>& F, const double* q, double* z) {
     const double a = 2.0 * eps * m;
-    for (size_t k = 0; k < G.size(); ++k) G[k] = a * Abar[k];
     std::fill(s.begin(), s.end(), 0.0);
+    for (int j = 0; j < N; ++j) E[j] = a * kappa;
     for (int i = 0; i < r; ++i)
       if (F[i]) {
-        const int j = i % N;
-        G[j * N + j] += u[i] * u[i];
+        const int j = st[i];
+        E[j] += u[i] * u[i];
         s[j] += u[i] * q[i];
       }
-    if (!lqd::chol(G.data(), N)) return false;
-    lqd::chol_solve(G.data(), N, s.data());
-    for (int i = 0; i < r; ++i) z[i] = F[i] ? -(q[i] - u[i] * s[i % N]) / (2.0 * eps) : 0.0;
+    if (!Gf.factor(N, a, E.data())) return false;
+    Gf.solve(s.data());
+    const double h = -0.5 / eps;
+    for (int i = 0; i < r; ++i) z[i] = F[i] ? h * (q[i] - u[i] * s[st[i]]) : 0.0;
     return true;
   }
 };

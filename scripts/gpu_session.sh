@@ -40,6 +40,7 @@ for s in $STEPS; do
     bfused) LOMPC_FUSED=1 run bfused 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct ;;
     bfusednoev) LOMPC_FUSED=1 run bfusednoev 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct --no-kernel-events ;;
     sprofzc) LOMPC_ZERO_COPY=1 run sprofzc 300 python scripts/station_profile.py ;;
+    sproftrace) run sproftrace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/sproft -o run --output-format csv -- python scripts/station_profile.py ;;
     bcost) run bcost 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs cost ;;
     bset) run bset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs set ;;
     bwarm) run bwarm 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --warm ;;

@@ -14,7 +14,8 @@ combine_set_results, rank-ordered local sum / max).  Weak scaling:
 262 144 EVs per GPU (config 3; at 8 GPUs this is config 4's 2 097 152).
 
 Every step is one plan run = three launches on one stream: k_path (per (set, gamma cell)
-solution paths), k_eval (per-EV evaluation + rows) and k_finalize (per-set reductions).
+solution paths), k_eval (per-EV evaluation + rows) and k_finalize (per-set reductions and any
+individual re-solve).
 
 Rank 0 prints ONE JSON line.  ``roofline`` prices the per-EV kernel (k_eval, the only
 kernel whose work scales with the EV count) by its algorithmic bytes per QP (gamma in 8 B,
@@ -246,7 +247,7 @@ def main():
             "outputs": args.outputs,
             "warm_start": bool(args.warm),
             "parallelism": f"dp{world} (EV shards, one RCCL all-gather of both types' per-set reductions per step)",
-            "launches_per_step": 3 * len(runs),
+            "launches_per_step": sum(r["plan"].launches_per_run() for r in runs),
             "kernel_events": "none" if args.no_kernel_events else f"k_eval, 1 in {ev_every} timed steps",
         },
         "roofline": {
@@ -317,7 +318,8 @@ def kernel_breakdown(run, step, args, nsteps, pmc, torch):
     out = {"steps": n, "ms_per_step_with_events": dt / n * 1e3}
     for k in kernels:
         ms, cnt = plan.profile(read=True, kernel=k)
-        out[k] = {"avg_us": ms / max(cnt, 1) * 1e3, "launches": cnt}
+        if cnt:  # (no k_finalize launches when the sets close inside k_eval)
+            out[k] = {"avg_us": ms / cnt * 1e3, "launches": cnt}
     plan.profile(enable=False)
     info = plan.info()
     out["k_path"].update({"waves": info["sets"] * info["cells"], "cells_per_set": info["cells"],
@@ -325,7 +327,7 @@ def kernel_breakdown(run, step, args, nsteps, pmc, torch):
     out["k_eval"]["workgroups"] = info["workgroups"]
     if pmc:
         for k in kernels:
-            if k in pmc:
+            if k in pmc and k in out:
                 out[k]["pmc"] = {x: pmc[k][x] for x in pmc[k] if x != "hbm_bytes_per_launch"}
         if "k_path" in pmc and "valu_issue_frac" in pmc["k_path"]:
             out["k_path"]["valu_issue_frac"] = pmc["k_path"]["valu_issue_frac"]

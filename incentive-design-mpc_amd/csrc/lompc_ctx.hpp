@@ -94,6 +94,9 @@ struct lompc_plan {
   bool fused = false;           // k_path + k_eval as one launch (k_fused)
   int* d_fused = nullptr;       // [1 + S] k_fused's ticket + per-set published-cell counters
   int64_t cap_fused = 0;
+  bool close = false;           // the sets' closing inside k_eval (no k_finalize launch)
+  int* d_arrive = nullptr;      // [S] k_eval's per-set arrival counters (close mode)
+  int n_empty = 0;              // sets without EVs (closed by one extra k_eval workgroup)
   CtxEnds ce{};                 // set s belongs to context #{k : ce.end[k] <= s}
   int eval_occ = 1;             // k_eval workgroups resident per CU (occupancy query)
   int64_t eval_occ_key = -1;    // (N, LDS pieces) it was queried for

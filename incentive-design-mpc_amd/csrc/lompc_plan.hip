@@ -34,6 +34,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "lompc_ctx.hpp"
 #include "lompc_wave.hpp"
@@ -65,6 +66,7 @@ __device__ long long g_stamps[65536 * 8];
 #define EVAL_MAXB (EVAL_EVS * EVAL_PASSES)  // k_eval: EVs per workgroup, at most
 #define LQ_PIECE_CAP 128                   // k_eval: piece slots of one set staged in LDS (more: re-solved)
 #define LQ_GMAX 1024                       // max cells per set
+#define LQ_DROP_OFF 0x7fff0000             // k_eval: a store offset past any w descriptor's range (dropped)
 
 namespace {
 
@@ -82,6 +84,10 @@ __device__ __forceinline__ void st_wt8b(__amdgpu_buffer_rsrc_t rs, int off, doub
 __device__ __forceinline__ void st_wt8(double* p, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void st_wt4(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ double clampw(double x, double wmax) { return fmin(fmax(x, 0.0), wmax); }
@@ -424,8 +430,10 @@ struct EvalArgs {
   double* partial;        // [nblk][N + NPX]
   int* fail_cnt;          // [nblk][EVAL_WAVES]  EVs left for the individual re-solve (k_finalize)
   int* fail_idx;          // [nblk][EVAL_MAXB]   their indices, per wave in row order
-  int w_rsrc_ok;          // B*N*8 fits a buffer descriptor's 31-bit offsets
+  int w_rsrc_ok;          // B*N*8 <= LQ_DROP_OFF: w through a buffer descriptor (offsets from 0)
+  int w_bytes;            // B*N*8 when w_rsrc_ok (the descriptor's range)
   int cap;                // pieces staged in LDS (a set with more re-solves the rest individually)
+  int nblk;               // workgroups of EVs (close mode: workgroup nblk closes the empty sets)
 };
 
 // cost / A_bar error / price0 of a QP solved by the whole wave (lane t = w_t), valid on every lane
@@ -479,8 +487,167 @@ __device__ __forceinline__ double2 ld_t(const double2* p) {
   }
 }
 
+struct FinalArgs {
+  int N, G, want_err;
+  int* fused_tickets;      // k_fused's counters, reset here for the next run (or null)
+  int* fused_done;
+  int* arrive;             // [S] k_eval (close mode): arrived workgroups per set, zero between runs
+  const QPConst* qd;
+  CtxEnds ce;
+  const int* blk_prefix;   // [S+1] k_eval workgroups of each set
+  const int64_t* set_off;
+  const double* window;
+  const double* gamma;
+  const double* lmbd;
+  const double* lmbd_r;
+  const double* w_ref;
+  const uint8_t* t_sl;
+  const int* fail_cnt;
+  const int* fail_idx;
+  const double* partial;
+  double* w;
+  double* cost;
+  double* w0;
+  int8_t* status;
+  double* set_sum_w;
+  double* set_stats;
+  double* stats;
+};
+
+constexpr int FIN_W = LOMPC_MAX_N + NPX + 1;
+
+// Closing of set s by one workgroup of NW waves (k_finalize: one 4-wave workgroup per set; k_eval
+// in close mode: the set's last-arriving workgroup, COH = its records read with sc1 loads).
+// (1) reduction of the set's k_eval records: wave wv sums records wv, wv+NW, ... (lane =
+//     column, 4 accumulators), the NW waves combine in a fixed order;
+// (2) if k_eval listed EVs no certified piece covers: wave wv re-solves the lists of waves
+//     (workgroup, wave) j = wv, wv+NW, ... individually (wave_solve from the working set at
+//     their cell's start: fp32 search, fp64 PDAS, primal active set; KKT-certified), writes
+//     their outputs and adds them to the reduction in a fixed order.
+template <int NW, bool COH>
+__device__ __forceinline__ void finalize_set(const FinalArgs& r, const int s, double (*red)[FIN_W], double (*rep)[FIN_W]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int N = r.N, W = N + NPX;
+  const int b0 = r.blk_prefix[s], b1 = r.blk_prefix[s + 1];
+  for (int c = lane; c < W; c += 64) {
+    const bool is_max = c == N + PX_MAX_ERR;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    constexpr int U = 16;
+    for (int b = b0 + wv; b < b1; b += NW * U) {
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int bb = b + NW * u;
+        v[u] = bb < b1 ? ld_t<COH>(r.partial + (size_t)bb * W + c) : 0.0;  // 0: neutral for sums and max of errors >= 0
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u & 3] = is_max ? fmax(acc[u & 3], v[u]) : acc[u & 3] + v[u];
+    }
+    red[wv][c] = is_max ? fmax(fmax(acc[0], acc[1]), fmax(acc[2], acc[3])) : (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  }
+  __syncthreads();
+  if (tid < W) {
+    const bool is_max = tid == N + PX_MAX_ERR;
+    double v = red[0][tid];
+    for (int k = 1; k < NW; ++k) v = is_max ? fmax(v, red[k][tid]) : v + red[k][tid];
+    red[0][tid] = v;
+  }
+  __syncthreads();
+  if (red[0][N + PX_N_FAILED] > 0.0) {  // block-uniform: individual re-solves pending
+    const QPConst& q = set_consts(r.qd, r.ce, s);
+    lq_tab_init(q);
+    const double* __restrict__ L = r.lmbd + (size_t)s * 3 * N;
+    const double lr = r.lmbd_r[s];
+    lqw::WaveSet ws;
+    double l2;
+    bool bad;  // (checked by k_path)
+    load_set(q, L, lr, N, lane, ws, l2, bad);
+    const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);
+    const double kappa = lr / q.delta;
+    const double l0[3] = {L[0], L[N], L[2 * N]};
+    const double wr = (r.w_ref && lane < N) ? r.w_ref[(size_t)s * N + lane] : 0.0;
+    const double wlo = r.window[2 * s], whi = r.window[2 * s + 1];
+    const int G = r.G;
+    double acc_w = 0.0, acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
+    int nrep = 0, nfail = 0;
+    for (int j = b0 * EVAL_WAVES + wv; j < b1 * EVAL_WAVES; j += NW) {  // (workgroup, wave)
+      const int nf = ld_t<COH>(r.fail_cnt + j);
+      for (int k = 0; k < nf; ++k) {
+        const int i = ld_t<COH>(r.fail_idx + (size_t)(j / EVAL_WAVES) * EVAL_MAXB + 64 * EVAL_PASSES * (j % EVAL_WAVES) + k);
+        const double g = r.gamma[i];
+        const int c = cell_of(g, wlo, (double)G / (whi - wlo), G);
+        int sl = lane < N ? (int)r.t_sl[((size_t)s * G + c) * 64 + lane] : 0;
+        double wl = 0.0, rl = 0.0;
+        const bool okk = lqw::wave_solve(q, ws, g, sl, wl, rl);
+        double co, eo, po;
+        wave_ev_outputs(q, ws, c0, kappa, l0, lr, wr, g, wl, co, eo, po);
+        if (!r.want_err) eo = 0.0;
+        if (r.w && lane < N) r.w[(size_t)i * N + lane] = wl;
+        if (lane == 0) {
+          if (r.cost) r.cost[i] = co;
+          if (r.w0) r.w0[i] = wl;
+          if (r.status) r.status[i] = okk ? LOMPC_QP_REPAIRED : LOMPC_QP_FAILED;
+        }
+        acc_w += lane < N ? wl : 0.0;
+        acc_cost += co;
+        acc_p0 += po;
+        acc_err = fmax(acc_err, eo);
+        nrep += okk ? 1 : 0;
+        nfail += okk ? 0 : 1;
+      }
+    }
+    if (lane < N) rep[wv][lane] = acc_w;
+    if (lane == 0) {
+      rep[wv][N + PX_COST] = acc_cost;
+      rep[wv][N + PX_PRICE0] = acc_p0;
+      rep[wv][N + PX_MAX_ERR] = acc_err;
+      rep[wv][N + PX_N_OK] = (double)nrep;
+      rep[wv][N + PX_N_REPAIRED] = (double)nrep;
+      rep[wv][N + PX_N_FAILED] = (double)nfail;
+      rep[wv][N + PX_N_INVALID] = 0.0;
+    }
+    __syncthreads();
+    if (tid < W) {
+      const bool is_max = tid == N + PX_MAX_ERR;
+      double v = (tid == N + PX_N_FAILED) ? 0.0 : red[0][tid];  // pending -> the outcome
+      for (int k = 0; k < NW; ++k) v = is_max ? fmax(v, rep[k][tid]) : v + rep[k][tid];
+      red[0][tid] = v;
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && r.fused_done) {
+    r.fused_done[s] = 0;
+    if (s == 0) r.fused_tickets[0] = 0;
+  }
+  if (tid < N && r.set_sum_w) r.set_sum_w[(size_t)s * N + tid] = red[0][tid];
+  if (tid < LOMPC_SET_STATS) {
+    double v = 0.0;
+    switch (tid) {
+      case LOMPC_STAT_COUNT: v = (double)(r.set_off[s + 1] - r.set_off[s]); break;
+      case LOMPC_STAT_SUM_W0: v = red[0][0]; break;
+      case LOMPC_STAT_SUM_PRICE0: v = red[0][N + PX_PRICE0]; break;
+      case LOMPC_STAT_MAX_ERR: v = red[0][N + PX_MAX_ERR]; break;
+      case LOMPC_STAT_SUM_COST: v = red[0][N + PX_COST]; break;
+      case LOMPC_STAT_N_REPAIRED: v = red[0][N + PX_N_REPAIRED]; break;
+      case LOMPC_STAT_N_FAILED: v = red[0][N + PX_N_FAILED]; break;
+      default: v = red[0][N + PX_N_INVALID]; break;
+    }
+    if (r.set_stats) r.set_stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
+    r.stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
+  }
+}
+
+
+__global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
+  __shared__ double red[4][FIN_W];
+  __shared__ double rep[4][FIN_W];
+  finalize_set<4, false>(r, (int)blockIdx.x, red, rep);
+}
+
 // One k_eval block (EVs [start, end) of one set, <= EVAL_MAXB) by the whole workgroup.
-template <bool COH>
+// NT: the horizon as a compile-time constant (0: a.N at run time) — the row loop's lane map
+// (stages per lane, rows per store instruction) and its address arithmetic become constants.
+template <bool COH, int NT = 0>
 __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
   // dynamic LDS: [cap][N] piece rows | [cap][8] coefficients | [cap] piece ends | cells:
   // coverage start | piece count
@@ -492,11 +659,13 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int4 info = a.blk[blk];
   const int s = info.x, start = info.y, end = info.z;  // thread: EVs start + tid + EVAL_EVS h
-  const int N = a.N, G = a.G;
+  const int N = NT ? NT : a.N, G = a.G;
   const int cap = a.cap;
+  const int ZK = cap;  // the zero piece (a = b = 0): rows of re-solved and invalid EVs, which
+                       // then add exactly 0 to the row sums and need no branch in the row loop
   LQ_STAMPE(0);
   double2* s_ab = s_dyn;
-  double* s_cf = reinterpret_cast<double*>(s_ab + (size_t)cap * N);
+  double* s_cf = reinterpret_cast<double*>(s_ab + (size_t)(cap + 1) * N);  // (row cap: the zero piece)
   double* s_ge = s_cf + (size_t)cap * 8;
   double* s_lo = s_ge + cap;
   int* s_cnt = reinterpret_cast<int*>(s_lo + G);
@@ -513,46 +682,55 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
   const double l0[3] = {L[0], L[N], L[2 * N]};  // price0 (lompc.py:164-170)
   const double lr = a.lmbd_r[s];
   const int cb = s * G;
-  for (int c = tid; c < G; c += EVAL_EVS) {
-    s_cnt[c] = ld_t<COH>(a.t_cnt + cb + c);
-    s_lo[c] = ld_t<COH>(a.t_lo + cb + c);
-  }
   // the set's piece slots (the first `cap`: cells past them are re-solved individually), all
-  // of them whatever the cells' counts, so every load of the staging is in one memory round:
-  // coalesced copies, each thread's loads issued before its first LDS store
+  // of them whatever the cells' counts, and the cells' counts / coverage starts: ONE memory
+  // round — every thread issues all its staging loads (behind its gamma loads) before its first
+  // LDS store; only N > 32 or more than EVAL_EVS cells leave a remainder for a second round
   const size_t sb = (size_t)s * G * LQ_PPL;
   const int np = min(G * LQ_PPL, cap);
   {
     const int nab = np * N, ncf = np * 8;
     const double2* gab = a.t_ab + sb * N;
     const double* gcf = a.t_cf + sb * 8;
-    constexpr int U = 8;
-    for (int b0 = tid; b0 < nab; b0 += EVAL_EVS * U) {
-      double2 v[U];
+    constexpr int U = 8, UC = (LQ_PIECE_CAP * 9 + EVAL_EVS - 1) / EVAL_EVS;
+    double2 v[U];
+    double vc[UC];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int it = b0 + EVAL_EVS * u;
-        v[u] = it < nab ? ld_t<COH>(gab + it) : make_double2(0.0, 0.0);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int it = b0 + EVAL_EVS * u;
-        if (it < nab) s_ab[it] = v[u];
-      }
+    for (int u = 0; u < U; ++u) {
+      const int it = tid + EVAL_EVS * u;
+      v[u] = it < nab ? ld_t<COH>(gab + it) : make_double2(0.0, 0.0);
     }
-    for (int b0 = tid; b0 < ncf + np; b0 += EVAL_EVS * U) {
-      double v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int it = b0 + EVAL_EVS * u;
-        v[u] = it < ncf ? ld_t<COH>(gcf + it) : (it < ncf + np ? ld_t<COH>(a.t_ge + sb + it - ncf) : 0.0);
-      }
+    for (int u = 0; u < UC; ++u) {
+      const int it = tid + EVAL_EVS * u;
+      vc[u] = it < ncf ? ld_t<COH>(gcf + it) : (it < ncf + np ? ld_t<COH>(a.t_ge + sb + it - ncf) : 0.0);
+    }
+    int vn = 0;
+    double vl = 0.0;
+    if (tid < G) {
+      vn = ld_t<COH>(a.t_cnt + cb + tid);
+      vl = ld_t<COH>(a.t_lo + cb + tid);
+    }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int it = b0 + EVAL_EVS * u;
-        if (it < ncf) s_cf[it] = v[u];
-        else if (it < ncf + np) s_ge[it - ncf] = v[u];
-      }
+    for (int u = 0; u < U; ++u) {
+      const int it = tid + EVAL_EVS * u;
+      if (it < nab) s_ab[it] = v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < UC; ++u) {
+      const int it = tid + EVAL_EVS * u;
+      if (it < ncf) s_cf[it] = vc[u];
+      else if (it < ncf + np) s_ge[it - ncf] = vc[u];
+    }
+    if (tid < G) {
+      s_cnt[tid] = vn;
+      s_lo[tid] = vl;
+    }
+    if (tid < N) s_ab[ZK * N + tid] = make_double2(0.0, 0.0);
+    for (int it = tid + EVAL_EVS * U; it < nab; it += EVAL_EVS) s_ab[it] = ld_t<COH>(gab + it);
+    for (int c = tid + EVAL_EVS; c < G; c += EVAL_EVS) {
+      s_cnt[c] = ld_t<COH>(a.t_cnt + cb + c);
+      s_lo[c] = ld_t<COH>(a.t_lo + cb + c);
     }
   }
   lq_tab_init(q);  // (its barrier publishes the staged table)
@@ -564,6 +742,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
   const double cscale = (double)G / (whi - wlo);
   double acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
   int n_ok = 0, n_fail = 0, n_inv = 0, nlist = 0;
+  bool inv_rows = false;  // (wave-uniform) some row of this wave has an invalid gamma
 #pragma unroll
   for (int h = 0; h < EVAL_PASSES; ++h) {
     const int i = start + tid + EVAL_EVS * h;
@@ -598,16 +777,17 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
       if (a.status) a.status[i] = LOMPC_QP_OK;
     }
     s_g[wv][64 * h + lane] = g;
-    s_k[wv][64 * h + lane] = (act && !valid) ? -2 : (cov ? key : -1);
+    s_k[wv][64 * h + lane] = cov ? key : ZK;
+    inv_rows |= __ballot(act && !valid) != 0ull;
     const unsigned long long need = __ballot(valid && !cov);
     if (valid && !cov) {
-      a.fail_idx[(size_t)blk * EVAL_MAXB + 64 * EVAL_PASSES * wv + nlist +
-                 __popcll(need & ((1ull << lane) - 1ull))] = i;
+      st_wt4(a.fail_idx + (size_t)blk * EVAL_MAXB + 64 * EVAL_PASSES * wv + nlist +
+                 __popcll(need & ((1ull << lane) - 1ull)), i);
       ++n_fail;
     }
     nlist += __popcll(need);
   }
-  if (lane == 0) a.fail_cnt[(size_t)blk * EVAL_WAVES + wv] = nlist;
+  if (lane == 0) st_wt4(a.fail_cnt + (size_t)blk * EVAL_WAVES + wv, nlist);
   LQ_STAMPE(2);
   __builtin_amdgcn_wave_barrier();  // this wave's own rows in LDS: in order
   LQ_STAMPE(3);
@@ -617,57 +797,99 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
   const int R = 64 / Lr;          // rows per store instruction
   const int rr = lane / Lr, col = lane - rr * Lr;
   const bool rlane = rr < R;
-  // the wave's rows r: EV start + 64 wv + r (r < 64), start + EVAL_EVS + 64 wv + r - 64 (second pass)
-  const int row0 = start + 64 * wv;
-  const int n0 = max(0, min(64, end - row0));
-  const int nrow = n0 < 64 ? n0 : 64 + max(0, min(64 * (EVAL_PASSES - 1), end - row0 - EVAL_EVS));
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.w, (short)0, 0x7fffffff, 0x00020000);
-  double acc0 = 0.0, acc1 = 0.0;
   const int t0 = V * col;
   constexpr int RU = 4;  // row instructions per batch: their LDS reads in flight together
-  for (int r0 = 0; r0 < nrow; r0 += RU * R) {
+  double acc0 = 0.0, acc1 = 0.0;
+  // one pass per EV of a thread: the wave's rows of pass h are EVs rbase .. rbase + nh - 1
+  // (contiguous in w), LDS rows 64 h ...; every row is a plain piece lookup (re-solved and
+  // invalid EVs read the zero piece), so the loop has no per-row branch: the stores of a full
+  // batch use one address register and immediate offsets; lanes past the row width (rlane
+  // false) store out of the descriptor's range, which drops them
+  const bool fast = a.w && a.w_rsrc_ok;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(a.w, (short)0, a.w ? a.w_bytes : 0, 0x00020000);
+#pragma unroll
+  for (int h = 0; h < EVAL_PASSES; ++h) {
+    const int rbase = start + EVAL_EVS * h + 64 * wv;
+    const int nh = max(0, min(64, end - rbase));  // wave-uniform
+    if (nh == 0) continue;
+    const int* sk = &s_k[wv][64 * h];
+    const double* sg = &s_g[wv][64 * h];
+    const int vb = rlane ? ((rbase + rr) * N + t0) * 8 : LQ_DROP_OFF;  // row rr of the pass
     int kk[RU];
     double gg[RU];
-    double2 u0[RU], u1[RU];
-  #pragma unroll
+#pragma unroll
     for (int j = 0; j < RU; ++j) {
-      const int row = r0 + j * R + rr;
-      const bool ok = rlane && row < nrow;
-      kk[j] = ok ? s_k[wv][row] : -1;
-      gg[j] = ok ? s_g[wv][row] : 0.0;
+      const int rc = min(j * R + rr, 63);
+      kk[j] = sk[rc];
+      gg[j] = sg[rc];
     }
-  #pragma unroll
-    for (int j = 0; j < RU; ++j) {
-      const int kx = kk[j] >= 0 ? kk[j] : 0;
-      u0[j] = s_ab[kx * N + t0];
-      u1[j] = V == 2 ? s_ab[kx * N + t0 + 1] : make_double2(0.0, 0.0);
-    }
-  #pragma unroll
-    for (int j = 0; j < RU; ++j) {
-      const int k = kk[j];
-      if (k != -1) {
-        double x0, x1 = 0.0;
-        if (k >= 0) {
-          x0 = clampw(fma(u0[j].y, gg[j], u0[j].x), wm);
-          if (V == 2) x1 = clampw(fma(u1[j].y, gg[j], u1[j].x), wm);
-          acc0 += x0;
-          acc1 += x1;
-        } else {
-          x0 = x1 = NAN;  // invalid gamma
-        }
-        if (a.w) {
-          const int rw = r0 + j * R + rr;
-          const int orow = row0 + rw + (rw >= 64 ? EVAL_EVS - 64 : 0);
-          if (a.w_rsrc_ok) {
-            const int off = (orow * N + t0) * 8;
-            if (V == 2) st_wt16(rs, off, x0, x1);
-            else st_wt8b(rs, off, x0);
-          } else {
-            double* dst = a.w + (size_t)orow * N + t0;
-            st_wt8(dst, x0);
-            if (V == 2) st_wt8(dst + 1, x1);
+    for (int r0 = 0; r0 < nh; r0 += RU * R) {
+      double2 u0[RU], u1[RU];
+#pragma unroll
+      for (int j = 0; j < RU; ++j) {
+        u0[j] = s_ab[kk[j] * N + t0];
+        u1[j] = V == 2 ? s_ab[kk[j] * N + t0 + 1] : make_double2(0.0, 0.0);
+      }
+      int kn[RU];  // the next batch's keys and gammas (software pipeline: one LDS round per batch)
+      double gn[RU];
+#pragma unroll
+      for (int j = 0; j < RU; ++j) {
+        const int rc = min(r0 + (RU + j) * R + rr, 63);
+        kn[j] = sk[rc];
+        gn[j] = sg[rc];
+      }
+      // a batch's row math and stores; FULL (every row of the batch exists: no per-row masks)
+      // and FAST (w through the descriptor: one address register, immediate offsets) are
+      // wave-uniform and specialised so the common case has no exec-mask change per row
+      auto rows = [&](auto full_t, auto fast_t) {
+        constexpr bool FULL = decltype(full_t)::value, FAST = decltype(fast_t)::value;
+#pragma unroll
+        for (int j = 0; j < RU; ++j) {
+          const double x0 = clampw(fma(u0[j].y, gg[j], u0[j].x), wm);
+          const double x1 = V == 2 ? clampw(fma(u1[j].y, gg[j], u1[j].x), wm) : 0.0;
+          if (FULL || (rlane && r0 + j * R + rr < nh)) {  // (FULL: lanes past the row width add 0 below)
+            acc0 += x0;
+            acc1 += x1;
+            if (FAST) {
+              const int off = vb + (r0 + j * R) * N * 8;
+              if (V == 2) st_wt16(rs, off, x0, x1);
+              else st_wt8b(rs, off, x0);
+            } else if (a.w) {
+              double* dst = a.w + (size_t)(rbase + r0 + j * R + rr) * N + t0;
+              st_wt8(dst, x0);
+              if (V == 2) st_wt8(dst + 1, x1);
+            }
           }
         }
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      if (r0 + RU * R <= nh) {  // wave-uniform
+        if (fast) rows(T_{}, T_{});
+        else rows(T_{}, F_{});
+      } else {
+        if (fast) rows(F_{}, T_{});
+        else rows(F_{}, F_{});
+      }
+#pragma unroll
+      for (int j = 0; j < RU; ++j) {
+        kk[j] = kn[j];
+        gg[j] = gn[j];
+      }
+    }
+  }
+  if (!rlane) acc0 = acc1 = 0.0;  // (lanes past the row width read real rows in full batches)
+  // rows of invalid EVs (gamma outside [0, y_max] or NaN): NaN, written after the loop's
+  // zeros of the same rows (rare; ordered by the wait)
+  if (inv_rows && a.w) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int h = 0; h < EVAL_PASSES; ++h) {
+      const int rbase = start + EVAL_EVS * h + 64 * wv;
+      const int nh = max(0, min(64, end - rbase));
+      for (int r = 0; r < nh; ++r) {
+        const double g = s_g[wv][64 * h + r];
+        if (!(g >= 0.0 && g <= ym) && lane < N) st_wt8(a.w + (size_t)(rbase + r) * N + lane, NAN);
       }
     }
   }
@@ -706,17 +928,65 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
   if (tid < N) {  // stage t: every wave's row sums, then the re-solved rows
     double sw = 0.0;
     for (int k = 0; k < EVAL_WAVES; ++k) sw += s_accw[k][tid];
-    part[tid] = sw;
+    st_wt8(part + tid, sw);
   } else if (tid >= 64 && tid < 64 + NPX) {
     const int x = tid - 64;
     double v = 0.0;
     for (int k = 0; k < EVAL_WAVES; ++k) v = x == PX_MAX_ERR ? fmax(v, s_red[k][x]) : v + s_red[k][x];
-    part[N + x] = v;
+    st_wt8(part + N + x, v);
   }
   LQ_STAMPE(5);
 }
 
-__global__ __launch_bounds__(EVAL_EVS) void k_eval(EvalArgs a) { eval_block<false>(a, (int)blockIdx.x); }
+// k_eval.  CLOSE: the set's closing (finalize_set) runs inside the launch, by the workgroup of the
+// set that arrives last (an agent-scope counter per set; its records and re-solve lists are
+// write-through stores drained before the arrival, read back with sc1 loads), so no k_finalize
+// launch and no kernel boundary follow; workgroup nblk closes the sets that have no EVs.
+template <bool CLOSE, int NT>
+__global__ __launch_bounds__(EVAL_EVS, 4) void k_eval(EvalArgs a, FinalArgs r) {  // (4 waves per SIMD: two workgroups per CU)
+  extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
+  double (*red)[FIN_W] = reinterpret_cast<double (*)[FIN_W]>(s_dyn);
+  double (*rep)[FIN_W] = red + EVAL_WAVES;
+  const int b = (int)blockIdx.x;
+  if constexpr (CLOSE) {
+    if (b == a.nblk) {
+      for (int s = 0; s < a.S; ++s)
+        if (r.blk_prefix[s + 1] == r.blk_prefix[s]) {
+          finalize_set<EVAL_WAVES, true>(r, s, red, rep);
+          __syncthreads();  // (red / rep are rewritten for the next set)
+        }
+      return;
+    }
+  }
+  eval_block<false, NT>(a, b);
+  if constexpr (CLOSE) {
+    __shared__ int s_last;
+    const int s = __builtin_amdgcn_readfirstlane(a.blk[b].x);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record / list stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int nb = r.blk_prefix[s + 1] - r.blk_prefix[s];
+      const int old = __hip_atomic_fetch_add(r.arrive + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == nb - 1;
+      if (old == nb - 1) __hip_atomic_store(r.arrive + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (s_last) finalize_set<EVAL_WAVES, true>(r, s, red, rep);
+  }
+}
+
+// k_eval for horizon N: exact-N instantiations for the shipped horizons, run-time N otherwise
+typedef void (*EvalKernel)(EvalArgs, FinalArgs);
+template <bool CLOSE>
+EvalKernel eval_kernel(int N) {
+  switch (N) {
+    case 12: return k_eval<CLOSE, 12>;
+    case 16: return k_eval<CLOSE, 16>;
+    case 24: return k_eval<CLOSE, 24>;
+    case 48: return k_eval<CLOSE, 48>;
+    default: return k_eval<CLOSE, 0>;
+  }
+}
 
 // ---------------------------------------------------------------- k_fused
 // k_path and k_eval in ONE launch (plan option): grid = the k_eval blocks.  Phase A: every
@@ -779,153 +1049,6 @@ __global__ __launch_bounds__(EVAL_EVS) __attribute__((amdgpu_waves_per_eu(4, 8))
 
 
 // ---------------------------------------------------------------- k_finalize
-struct FinalArgs {
-  int N, G, want_err;
-  int* fused_tickets;      // k_fused's counters, reset here for the next run (or null)
-  int* fused_done;
-  const QPConst* qd;
-  CtxEnds ce;
-  const int* blk_prefix;   // [S+1] k_eval workgroups of each set
-  const int64_t* set_off;
-  const double* window;
-  const double* gamma;
-  const double* lmbd;
-  const double* lmbd_r;
-  const double* w_ref;
-  const uint8_t* t_sl;
-  const int* fail_cnt;
-  const int* fail_idx;
-  const double* partial;
-  double* w;
-  double* cost;
-  double* w0;
-  int8_t* status;
-  double* set_sum_w;
-  double* set_stats;
-  double* stats;
-};
-
-// One 256-thread workgroup per set.
-// (1) reduction of the set's k_eval records: wave wv sums records wv, wv+4, ... (lane =
-//     column, 4 accumulators), the 4 waves combine in a fixed order;
-// (2) if k_eval listed EVs no certified piece covers: wave wv re-solves the lists of waves
-//     (workgroup, wave) j = wv, wv+4, ... individually (wave_solve from the working set at
-//     their cell's start: fp32 search, fp64 PDAS, primal active set; KKT-certified), writes
-//     their outputs and adds them to the reduction in a fixed order.
-__global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
-  __shared__ double red[4][LOMPC_MAX_N + NPX + 1];
-  __shared__ double rep[4][LOMPC_MAX_N + NPX + 1];
-  const int s = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int N = r.N, W = N + NPX;
-  const int b0 = r.blk_prefix[s], b1 = r.blk_prefix[s + 1];
-  for (int c = lane; c < W; c += 64) {
-    const bool is_max = c == N + PX_MAX_ERR;
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    constexpr int U = 16;
-    for (int b = b0 + wv; b < b1; b += 4 * U) {
-      double v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int bb = b + 4 * u;
-        v[u] = bb < b1 ? r.partial[(size_t)bb * W + c] : 0.0;  // 0: neutral for sums and max of errors >= 0
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) acc[u & 3] = is_max ? fmax(acc[u & 3], v[u]) : acc[u & 3] + v[u];
-    }
-    red[wv][c] = is_max ? fmax(fmax(acc[0], acc[1]), fmax(acc[2], acc[3])) : (acc[0] + acc[1]) + (acc[2] + acc[3]);
-  }
-  __syncthreads();
-  if (tid < W) {
-    const bool is_max = tid == N + PX_MAX_ERR;
-    double v = red[0][tid];
-    for (int k = 1; k < 4; ++k) v = is_max ? fmax(v, red[k][tid]) : v + red[k][tid];
-    red[0][tid] = v;
-  }
-  __syncthreads();
-  if (red[0][N + PX_N_FAILED] > 0.0) {  // block-uniform: individual re-solves pending
-    const QPConst& q = set_consts(r.qd, r.ce, s);
-    lq_tab_init(q);
-    const double* __restrict__ L = r.lmbd + (size_t)s * 3 * N;
-    const double lr = r.lmbd_r[s];
-    lqw::WaveSet ws;
-    double l2;
-    bool bad;  // (checked by k_path)
-    load_set(q, L, lr, N, lane, ws, l2, bad);
-    const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);
-    const double kappa = lr / q.delta;
-    const double l0[3] = {L[0], L[N], L[2 * N]};
-    const double wr = (r.w_ref && lane < N) ? r.w_ref[(size_t)s * N + lane] : 0.0;
-    const double wlo = r.window[2 * s], whi = r.window[2 * s + 1];
-    const int G = r.G;
-    double acc_w = 0.0, acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
-    int nrep = 0, nfail = 0;
-    for (int j = b0 * EVAL_WAVES + wv; j < b1 * EVAL_WAVES; j += 4) {  // (workgroup, wave)
-      const int nf = r.fail_cnt[j];
-      for (int k = 0; k < nf; ++k) {
-        const int i = r.fail_idx[(size_t)(j / EVAL_WAVES) * EVAL_MAXB + 64 * EVAL_PASSES * (j % EVAL_WAVES) + k];
-        const double g = r.gamma[i];
-        const int c = cell_of(g, wlo, (double)G / (whi - wlo), G);
-        int sl = lane < N ? (int)r.t_sl[((size_t)s * G + c) * 64 + lane] : 0;
-        double wl = 0.0, rl = 0.0;
-        const bool okk = lqw::wave_solve(q, ws, g, sl, wl, rl);
-        double co, eo, po;
-        wave_ev_outputs(q, ws, c0, kappa, l0, lr, wr, g, wl, co, eo, po);
-        if (!r.want_err) eo = 0.0;
-        if (r.w && lane < N) r.w[(size_t)i * N + lane] = wl;
-        if (lane == 0) {
-          if (r.cost) r.cost[i] = co;
-          if (r.w0) r.w0[i] = wl;
-          if (r.status) r.status[i] = okk ? LOMPC_QP_REPAIRED : LOMPC_QP_FAILED;
-        }
-        acc_w += lane < N ? wl : 0.0;
-        acc_cost += co;
-        acc_p0 += po;
-        acc_err = fmax(acc_err, eo);
-        nrep += okk ? 1 : 0;
-        nfail += okk ? 0 : 1;
-      }
-    }
-    if (lane < N) rep[wv][lane] = acc_w;
-    if (lane == 0) {
-      rep[wv][N + PX_COST] = acc_cost;
-      rep[wv][N + PX_PRICE0] = acc_p0;
-      rep[wv][N + PX_MAX_ERR] = acc_err;
-      rep[wv][N + PX_N_OK] = (double)nrep;
-      rep[wv][N + PX_N_REPAIRED] = (double)nrep;
-      rep[wv][N + PX_N_FAILED] = (double)nfail;
-      rep[wv][N + PX_N_INVALID] = 0.0;
-    }
-    __syncthreads();
-    if (tid < W) {
-      const bool is_max = tid == N + PX_MAX_ERR;
-      double v = (tid == N + PX_N_FAILED) ? 0.0 : red[0][tid];  // pending -> the outcome
-      for (int k = 0; k < 4; ++k) v = is_max ? fmax(v, rep[k][tid]) : v + rep[k][tid];
-      red[0][tid] = v;
-    }
-    __syncthreads();
-  }
-  if (tid == 0 && r.fused_done) {
-    r.fused_done[s] = 0;
-    if (s == 0) r.fused_tickets[0] = 0;
-  }
-  if (tid < N && r.set_sum_w) r.set_sum_w[(size_t)s * N + tid] = red[0][tid];
-  if (tid < LOMPC_SET_STATS) {
-    double v = 0.0;
-    switch (tid) {
-      case LOMPC_STAT_COUNT: v = (double)(r.set_off[s + 1] - r.set_off[s]); break;
-      case LOMPC_STAT_SUM_W0: v = red[0][0]; break;
-      case LOMPC_STAT_SUM_PRICE0: v = red[0][N + PX_PRICE0]; break;
-      case LOMPC_STAT_MAX_ERR: v = red[0][N + PX_MAX_ERR]; break;
-      case LOMPC_STAT_SUM_COST: v = red[0][N + PX_COST]; break;
-      case LOMPC_STAT_N_REPAIRED: v = red[0][N + PX_N_REPAIRED]; break;
-      case LOMPC_STAT_N_FAILED: v = red[0][N + PX_N_FAILED]; break;
-      default: v = red[0][N + PX_N_INVALID]; break;
-    }
-    if (r.set_stats) r.set_stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
-    r.stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
-  }
-}
 
 int pick_cells(int64_t max_set) {
   const char* env = getenv("LOMPC_CELLS");  // diagnostics (cell-count sweeps)
@@ -970,7 +1093,9 @@ int plan_events_read(std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& pool,
 // ============================================================== host
 // k_eval's dynamic LDS: up to cap pieces of one set (N double2 + 8 + 1 doubles each) + the cells
 size_t eval_lds(int N, int G, int cap) {
-  return (size_t)cap * (N * sizeof(double2) + 9 * sizeof(double)) + (size_t)G * (sizeof(int) + sizeof(double));
+  const size_t stage = (size_t)cap * (N * sizeof(double2) + 9 * sizeof(double)) + (size_t)N * sizeof(double2) +
+                       (size_t)G * (sizeof(int) + sizeof(double));
+  return std::max(stage, (size_t)2 * EVAL_WAVES * FIN_W * sizeof(double));  // (close mode: red / rep)
 }
 
 // events of one profiled dispatch (null events when kernel k is not profiled)
@@ -1022,7 +1147,7 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   const int cap = std::min(LQ_PIECE_CAP, G * LQ_PPL);
   if (p->eval_occ_key != (int64_t)N * 4096 + cap) {  // k_eval workgroups resident per CU
     int occ = 0;
-    HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_eval, EVAL_EVS, eval_lds(N, G, cap)));
+    HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, eval_kernel<true>(N), EVAL_EVS, eval_lds(N, G, cap)));
     p->eval_occ = std::max(occ, 1);
     p->eval_occ_key = (int64_t)N * 4096 + cap;
   }
@@ -1035,7 +1160,12 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     return std::max<int64_t>(lo, std::min<int64_t>(hi, m * target / std::max<int64_t>(B, 1)));
   };
   int64_t nblk = 0;
-  for (int64_t s = 0; s < S; ++s) nblk += blocks_of(set_offsets[s + 1] - set_offsets[s]);
+  int64_t n_empty = 0;
+  for (int64_t s = 0; s < S; ++s) {
+    const int64_t nb = blocks_of(set_offsets[s + 1] - set_offsets[s]);
+    nblk += nb;
+    n_empty += nb == 0 ? 1 : 0;
+  }
   p->device = ctxs[0]->device;
   p->N = N;
   p->nctx = nctx;
@@ -1051,9 +1181,10 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   if (!p->ev_stage) HIPCHK(p, hipEventCreateWithFlags(&p->ev_stage, hipEventDisableTiming));
   if (S > p->cap_S) {
     if ((rc = grow(p, &p->d_window, 2 * S)) || (rc = grow(p, &p->d_wacc, 3 * S)) ||
-        (rc = grow(p, &p->d_stats_own, S * LOMPC_SET_STATS)))
+        (rc = grow(p, &p->d_stats_own, S * LOMPC_SET_STATS)) || (rc = grow(p, &p->d_arrive, S)))
       return rc;
     HIPCHK(p, hipMemsetAsync(p->d_wacc, 0, 3 * S * sizeof(unsigned long long), st));
+    HIPCHK(p, hipMemsetAsync(p->d_arrive, 0, S * sizeof(int), st));
     p->cap_S = S;
   }
   if (nblk > p->cap_blk) {
@@ -1084,11 +1215,14 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     const char* env = getenv("LOMPC_FUSED");  // diagnostics: force the split / fused launches
     const bool want = env ? atoi(env) != 0 : (flags & LOMPC_PLAN_FUSED) != 0;
     p->fused = want && G % EVAL_WAVES == 0;
+    const char* ce = getenv("LOMPC_CLOSE");  // diagnostics: 1 = close the sets inside k_eval
+    p->close = !p->fused && (ce ? atoi(ce) != 0 : (flags & LOMPC_PLAN_CLOSE_IN_EVAL) != 0);
   }
   p->B = B;
   p->S = S;
   p->G = G;
   p->nblk = (int)nblk;
+  p->n_empty = (int)n_empty;
   p->d_stats = p->d_stats_own;
   // host arrays -> pinned staging -> device (the staging may still feed the previous prepare)
   // the plan's host-built metadata, one block in pinned memory and one copy to its device
@@ -1185,36 +1319,11 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   a.partial = p->d_partial;
   a.fail_cnt = p->d_fail_cnt;
   a.fail_idx = p->d_fail_idx;
-  a.w_rsrc_ok = (p->B * (int64_t)N * 8) < (1ll << 31) ? 1 : 0;
+  a.w_rsrc_ok = (p->B * (int64_t)N * 8) <= LQ_DROP_OFF ? 1 : 0;
+  a.w_bytes = a.w_rsrc_ok ? (int)(p->B * (int64_t)N * 8) : 0;
   a.cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
+  a.nblk = p->nblk;
   const size_t lds = eval_lds(N, p->G, a.cap);
-  const bool cprof = prof_ctx && prof_ctx->prof;  // lompc_solve_batch: the context's k_eval timing
-  const bool fused = p->fused && p->nblk > 0;
-  if (!fused) {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
-    hipExtLaunchKernelGGL(k_path, dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa);
-    HIPCHK(p, hipGetLastError());
-    plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
-  }
-  if (p->nblk > 0) {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (cprof ? take_events(prof_ctx->prof_pool, &e0, &e1) : plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1))
-      return fail_arg(p, "profiling events");
-    if (fused) {  // k_path + k_eval in one launch (timed as k_eval)
-      FusedArgs f{p->d_fused, p->d_fused + 1, p->d_errflag, (int)(p->S * p->G / EVAL_WAVES), p->nblk, 1 << 24};
-      hipExtLaunchKernelGGL(k_fused, dim3((unsigned)p->nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, pa, a, f);
-    } else {
-      hipExtLaunchKernelGGL(k_eval, dim3((unsigned)p->nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, a);
-    }
-    HIPCHK(p, hipGetLastError());
-    if (cprof) {
-      prof_ctx->prof_ev.push_back(e0);
-      prof_ctx->prof_ev.push_back(e1);
-    } else {
-      plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
-    }
-  }
   FinalArgs r{};
   r.N = N;
   r.G = p->G;
@@ -1241,6 +1350,39 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   r.stats = p->d_stats;
   r.fused_tickets = p->d_fused;
   r.fused_done = p->d_fused ? p->d_fused + 1 : nullptr;
+  r.arrive = p->d_arrive;
+  const bool close = p->close && !p->fused && p->nblk > 0;
+  const bool cprof = prof_ctx && prof_ctx->prof;  // lompc_solve_batch: the context's k_eval timing
+  const bool fused = p->fused && p->nblk > 0;
+  if (!fused) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
+    hipExtLaunchKernelGGL(k_path, dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa);
+    HIPCHK(p, hipGetLastError());
+    plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
+  }
+  if (p->nblk > 0) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (cprof ? take_events(prof_ctx->prof_pool, &e0, &e1) : plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1))
+      return fail_arg(p, "profiling events");
+    if (fused) {  // k_path + k_eval in one launch (timed as k_eval)
+      FusedArgs f{p->d_fused, p->d_fused + 1, p->d_errflag, (int)(p->S * p->G / EVAL_WAVES), p->nblk, 1 << 24};
+      hipExtLaunchKernelGGL(k_fused, dim3((unsigned)p->nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, pa, a, f);
+    } else if (close) {  // + one workgroup for the sets without EVs
+      hipExtLaunchKernelGGL(eval_kernel<true>(N), dim3((unsigned)(p->nblk + (p->n_empty > 0 ? 1 : 0))), dim3(EVAL_EVS), lds, st,
+                            e0, e1, 0, a, r);
+    } else {
+      hipExtLaunchKernelGGL(eval_kernel<false>(N), dim3((unsigned)p->nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, a, r);
+    }
+    HIPCHK(p, hipGetLastError());
+    if (cprof) {
+      prof_ctx->prof_ev.push_back(e0);
+      prof_ctx->prof_ev.push_back(e1);
+    } else {
+      plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
+    }
+  }
+  if (close) return LOMPC_OK;  // the sets were closed inside k_eval
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (plan_prof_begin(p, LOMPC_PLAN_K_FINAL, &e0, &e1)) return fail_arg(p, "profiling events");
   hipExtLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, e0, e1, 0, r);
@@ -1255,7 +1397,7 @@ void lq_plan_free(lompc_plan* p) {
   (void)hipDeviceSynchronize();
   void* ptrs[] = {p->d_meta,  p->d_stats_own, p->d_window, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
                   p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag,
-                  p->d_fail_cnt, p->d_fail_idx, p->d_fused, p->d_wacc};
+                  p->d_fail_cnt, p->d_fail_idx, p->d_fused, p->d_wacc, p->d_arrive};
   for (void* x : ptrs)
     if (x) (void)hipFree(x);
   if (p->h_buf) (void)hipHostFree(p->h_buf);

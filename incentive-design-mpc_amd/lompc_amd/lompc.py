@@ -334,13 +334,15 @@ class BatchPlan:
     w_ref (S, N) is read at every run (update it in place).  ``warm_start``: every gamma
     cell's exact solve starts from the working set the previous run ended with.  ``diag_repair``
     (diagnostics): no solution path, every EV is re-solved individually.  ``fused``: k_path and
-    k_eval as one launch (k_fused; needs cells per set divisible by 8).
+    k_eval as one launch (k_fused; needs cells per set divisible by 8).  ``close_in_eval``: the per-set
+    reductions and re-solves inside k_eval (each set's last-arriving workgroup) instead of the
+    k_finalize launch (measured slower: DESIGN.md §10).
     DIRECT-mode contexts fall back to ``lompc_run`` (one context only).
     """
 
     def __init__(self, lompc, gamma, set_offsets, *, sets_per_ctx=None, w_ref=None, gamma_ref=None, want_w=True,
                  want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None, validate=True,
-                 warm_start=False, diag_repair=False, fused=False):
+                 warm_start=False, diag_repair=False, fused=False, close_in_eval=False):
         torch = _torch()
         lompcs = list(lompc) if isinstance(lompc, (list, tuple)) else [lompc]
         self.lompcs = lompcs
@@ -374,7 +376,8 @@ class BatchPlan:
         ctxs = (ctypes.c_void_p * len(lompcs))(*[x._ctx.value for x in lompcs])
         plan = ctypes.c_void_p()
         flags = ((_lib.LOMPC_PLAN_WARM_START if warm_start else 0) | (_lib.LOMPC_PLAN_DIAG_REPAIR if diag_repair else 0)
-                 | (_lib.LOMPC_PLAN_FUSED if fused else 0))
+                 | (_lib.LOMPC_PLAN_FUSED if fused else 0) | (_lib.LOMPC_PLAN_CLOSE_IN_EVAL if close_in_eval else 0))
+        self._flags = flags
         rc = self._lib.lompc_plan_create(len(lompcs), ctypes.cast(ctxs, ctypes.c_void_p), self.sets_per_ctx.ctypes.data,
                                          self.B, _ptr(self.gamma), self.off.ctypes.data, _ptr(self.w_ref), flags,
                                          self._stream, ctypes.byref(plan))
@@ -422,6 +425,19 @@ class BatchPlan:
         if self.direct:
             self._args = [_ptr(self.w_ref), _ptr(self.gamma_ref), B, _ptr(self.gamma), self.off.ctypes.data] + \
                 self._outs + [self._stream]
+
+    def launches_per_run(self) -> int:
+        """Kernel launches of one run: k_path + k_eval + k_finalize; two when the sets close inside
+        k_eval (LOMPC_PLAN_CLOSE_IN_EVAL / LOMPC_CLOSE=1) or with k_fused + k_finalize."""
+        import os
+
+        if self.direct:
+            return 2
+        if self._flags & _lib.LOMPC_PLAN_FUSED:
+            return 2
+        env = os.environ.get("LOMPC_CLOSE")
+        close = (env == "1") if env is not None else bool(self._flags & _lib.LOMPC_PLAN_CLOSE_IN_EVAL)
+        return 2 if close else 3
 
     def info(self) -> dict:
         """Batch size, parameter sets, gamma cells per set and k_eval workgroups of the plan."""

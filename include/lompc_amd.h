@@ -165,9 +165,12 @@ typedef struct lompc_plan lompc_plan;
 #define LOMPC_PLAN_WARM_START 1 /* flag: start each gamma cell's exact solve from the working
                                    set the previous run of the plan ended with there (prices
                                    that change little between price iterations) */
-#define LOMPC_PLAN_DIAG_REPAIR 2
-#define LOMPC_PLAN_FUSED 4       /* k_path and k_eval as one launch */ /* diagnostics: no solution path, every EV takes the individual
+#define LOMPC_PLAN_DIAG_REPAIR 2 /* diagnostics: no solution path, every EV takes the individual
                                     whole-wave re-solve (status REPAIRED) */
+#define LOMPC_PLAN_FUSED 4       /* k_path and k_eval as one launch */
+#define LOMPC_PLAN_CLOSE_IN_EVAL 8 /* the per-set reductions and re-solves inside k_eval, by each
+                                      set's last-arriving workgroup, instead of the k_finalize
+                                      launch (measured slower) */
 
 /* Build a plan over B EVs grouped by set (S = sum of sets_per_ctx sets):
  *   ctxs         host [n_ctx]   contexts (same N and device), n_ctx <= LOMPC_PLAN_MAX_CTX

@@ -286,7 +286,7 @@ def test_fused_plan_matches_split(gpu):
            for _ in range(3)]
     lr = torch.zeros(2 * P, dtype=torch.float64, device="cuda:0")
     outs = []
-    for fused in (False, True):
+    for fused in (False, True):  # both close the sets with k_finalize
         plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], w_ref=wr, want_status=True, fused=fused)
         assert plan.cells % 8 == 0
         res = []
@@ -299,3 +299,46 @@ def test_fused_plan_matches_split(gpu):
     for a, b in zip(*outs):
         for k in a:
             assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("diag_repair", [False, True])
+def test_close_in_eval_matches_k_finalize(gpu, diag_repair):
+    """LOMPC_PLAN_CLOSE_IN_EVAL closes each set inside k_eval (its last-arriving workgroup reduces
+    the set's records and re-solves the listed EVs); default plans run the same closing as the
+    k_finalize launch.  Per-EV outputs are bitwise equal, the set reductions equal up to the
+    summation order (8 vs 4 waves).  Empty sets (closed by the extra workgroup), sets of one EV,
+    every EV re-solved (diag_repair), and repeated runs (the arrival counters reset)."""
+    N, P = 24, 5
+    rng = np.random.default_rng(33)
+    cs = [O.small_consts(), O.large_consts()]
+    lompcs = [LoMPC(N, LoMPCConstants(c.delta, c.theta, c.y_max, c.w_max, c.ev_type), device=0) for c in cs]
+    sizes = [[700, 0, 333, 1, 0], [0, 512, 1, 0, 900]] if diag_repair else [[9000, 0, 4321, 1, 0], [0, 7000, 1, 0, 12000]]
+    off = np.concatenate([[0], np.cumsum(np.concatenate(sizes))]).astype(np.int64)
+    B = int(off[-1])
+    ctx_of = np.repeat(np.arange(2 * P) // P, np.diff(off))
+    g = torch.as_tensor(np.array([cs[k].y_max for k in ctx_of]) - (0.3 + 0.2 * rng.random(B)), device="cuda:0")
+    wr = torch.as_tensor(np.concatenate([c.w_max * rng.random((P, N)) for c in cs]), device="cuda:0")
+    lms = [torch.as_tensor(np.concatenate([c.theta * rng.random((P, 3 * N)) for c in cs]), device="cuda:0")
+           for _ in range(3)]
+    lr = torch.as_tensor(np.concatenate([[0.0, 0.1, 0.0, 0.2, 0.0]] * 2), device="cuda:0")
+    outs = []
+    for close in (True, False):
+        plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], w_ref=wr, want_status=True, want_w0=True,
+                         diag_repair=diag_repair, close_in_eval=close)
+        res = []
+        for lm in lms:
+            out = plan.run(lm, lr)
+            rep, fail, inv = plan.check()
+            assert fail == 0 and inv == 0
+            if diag_repair:
+                assert rep == B
+            res.append({k: v.clone() for k, v in out.items() if v is not None})
+        outs.append(res)
+    for a, b in zip(*outs):
+        for k in a:
+            if k in ("set_sum_w", "set_stats"):
+                np.testing.assert_allclose(a[k].cpu().numpy(), b[k].cpu().numpy(), rtol=1e-12, atol=1e-12, err_msg=k)
+            else:
+                assert torch.equal(a[k], b[k]), k
+        st = a["set_stats"].cpu().numpy()
+        np.testing.assert_array_equal(st[:, 0], np.diff(off))  # LOMPC_STAT_COUNT, empty sets included

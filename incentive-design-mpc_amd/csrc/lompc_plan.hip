@@ -750,10 +750,12 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
     const double g = gh[h];
     const bool valid = act && g >= 0.0 && g <= ym;
     const int c = valid ? cell_of(g, wlo, cscale, G) : 0;
-    const int kb = c * LQ_PPL, ke = kb + s_cnt[c];  // the cell's pieces [kb, ke), ascending gamma
-    int key = kb;
-    for (int k = kb; k < ke - 1; ++k) key += g > s_ge[k] ? 1 : 0;
-    const bool cov = valid && ke > kb && ke <= np && g >= s_lo[c] && g <= s_ge[ke - 1];
+    const int nc = s_cnt[c];
+    const int kb = c * LQ_PPL, ke = kb + nc;  // the cell's pieces [kb, ke), ascending gamma
+    int key = kb;  // piece = number of piece ends below g: every end read at once (no loop)
+#pragma unroll
+    for (int k = 0; k + 1 < LQ_PPL; ++k) key += (k + 1 < nc && g > s_ge[min(kb + k, cap - 1)]) ? 1 : 0;
+    const bool cov = valid && ke > kb && ke <= np && g >= s_lo[c] && g <= s_ge[max(ke - 1, 0)];
     if (act && !valid) {
       ++n_inv;
       if (a.cost) st_wt8(a.cost + i, NAN);
@@ -764,7 +766,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
       const double4 c1 = *reinterpret_cast<const double4*>(s_cf + key * 8 + 4);
       const double cst = fma(fma(c0.z, g, c0.y), g, c0.x);
       const double e2 = fma(fma(c1.y, g, c1.x), g, c0.w);
-      const double er = a.want_err ? sqrt(fmax(e2, 0.0)) : 0.0;
+      const double er = a.want_err ? fmax(e2, 0.0) : 0.0;  // squared: sqrt of the max at the record
       const double w0v = clampw(fma(c1.w, g, c1.z), wm);
       const double p0 = q.theta * (w0v * l0[0] + (wm - w0v) * l0[1]) + q.q_scale * w0v * w0v * l0[2] +
                         tt * w0v * w0v * lr;  // lompc.py:164-170
@@ -910,7 +912,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
   {
     double tot[4] = {acc_cost, acc_p0, (double)n_ok, 0.0};
     lqw::wave_totals(tot, 64);
-    const double mx = lqw::wave_max(acc_err, 64);
+    const double mx = sqrt(lqw::wave_max(acc_err, 64));  // (sqrt is monotone: max of the roots)
     double cnt[2] = {(double)n_fail, (double)n_inv};
     lqw::wave_totals(cnt, 64);
     if (lane == 0) {

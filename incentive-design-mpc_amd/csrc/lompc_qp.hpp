@@ -33,7 +33,9 @@
 #ifndef LQ_G
 #define LQ_G 64                         // path cells per parameter set (one wave each)
 #endif
+#ifndef LQ_PPL
 #define LQ_PPL 8                        // max affine pieces stored per cell
+#endif
 #define LQ_STB 64                       // state bytes per stored working set (N <= 64)
 
 struct QPConst {

@@ -24,6 +24,7 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py ;;
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench20q) run bench20q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-station ;;
+    bqtag) run "bq_${TAG}" 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct ;;
     bench100q) run bench100q 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
     bsplit) run bsplit 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --split-types ;;
     bsplitset) run bsplitset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --split-types --outputs set ;;

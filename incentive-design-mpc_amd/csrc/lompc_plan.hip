@@ -243,12 +243,15 @@ __device__ __forceinline__ void load_set(const QPConst& q, const double* __restr
 // One (set, gamma cell) path by one wave (blk = s * G + cell); the wave's workgroup has
 // initialised the box table for the set's constants (lq_tab_init).  Every piece goes straight
 // to the cell's fixed slots with write-through stores (visible to any XCD once they complete).
+// NT: the horizon as a compile-time constant (0: a.N at run time) — the scans' row / bank steps
+// become straight-line code, so independent chains can be interleaved
+template <int NT = 0>
 __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
   const int G = a.G;
   const int s = __builtin_amdgcn_readfirstlane(blk / G);
   const int cell = blk - s * G;
   const int lane = (int)threadIdx.x & 63;
-  const int N = a.N;
+  const int N = NT ? NT : a.N;
   const double* __restrict__ L = a.lmbd + (size_t)s * 3 * N;
   const double lr = a.lmbd_r[s];
   const double wr_nat = (a.w_ref && lane < N) ? a.w_ref[(size_t)s * N + lane] : 0.0;
@@ -300,12 +303,11 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
       int last = -1;
       const int max_iter = 4 * LQ_PPL + 16;
       const double ee = ws.e_nat;
+      if (!has_sol) sol = lqw::solve_stage<2>(q, ws, 0.0, sl);  // (else the start's solve is reused)
       for (int it = 0; it < max_iter && npc < LQ_PPL; ++it) {
 #ifdef LOMPC_STAMPS
         if (lane == 0 && blk < 32768) g_stamps[blk * 8 + 5] = it + 1;
 #endif
-        if (!has_sol) sol = lqw::solve_stage<2>(q, ws, 0.0, sl);  // the start's solve is reused
-        has_sol = false;
         const double av = sol.w[0], bv = sol.w[1], r0 = sol.r[0], r1 = sol.r[1];
         double gc = INFINITY;
         int ns = sl;
@@ -330,15 +332,24 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
           bj = -1;
         }
         const bool final_piece = (bj < 0) || (npc == LQ_PPL - 1);
-        if (best > gcur || final_piece) {
+        const bool emit = best > gcur || final_piece;  // (wave-uniform)
+        // The next working set (the switch at the breakpoint) and its sub-problem solve do not
+        // depend on this piece's certificate and quadratics: all of them in one basic block, so
+        // the scheduler interleaves the independent DPP-scan chains (the next solve is wasted
+        // work, not latency, when this piece is the last).
+        const int bns = __shfl(ns, bj < 0 ? 0 : bj, 64);
+        const int sln = lane == bj ? bns : sl;
+        lqw::StageSol<2> nsol;
+        double res;
+        double t[6];
+        const bool act = lane < N;
+        const Box bx = lq_box(act ? sl : 0);
+        auto piece = [&]() {
           // KKT certificate at the piece's end; its start is the previous certified end (same w
           // and r, only the switched coordinate's box changed and it contains the value)
-          const Box bx = lq_box(lane < N ? sl : 0);
           const double wz = fmin(fmax(fma(bv, best, av), bx.lo), bx.hi);
-          const double res = lqw::wave_kkt_point(q, ws, best, sl, wz);
-          if (!(res <= q.tol_cert)) break;  // coverage ends at gcur
+          res = lqw::wave_kkt_point(q, ws, best, sl, wz);
           // cost and err^2 are quadratics in gamma on the piece
-          const bool act = lane < N;
           lqw::Sums<2> pf;
           pf.v[0] = act ? av : 0.0;
           pf.v[1] = act ? bv : 0.0;
@@ -347,13 +358,10 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
           const double Ea = Ya - Ywr, da = av - wr_nat;
           const double dd = ws.d_nat, cc = q.c;
           const double sg = (sl & 1) ? bx.slo : 0.0;  // PWL slope of a free coordinate
-          double icpt = 0.0;                          // PWL value at w = 0 of its linear piece
-          if (!q.ev_small) {
-            const double wm = fma(bv, 0.5 * (gcur + best), av);
-            const double tw = q.theta * q.w_max;
-            icpt = fma(-sg, wm, tw * tw * lq_pwl(wm * q.inv_wmax));
-          }
-          double t[6];
+          const double wmid = fma(bv, 0.5 * (gcur + best), av);
+          const double tw = q.theta * q.w_max;
+          // PWL value at w = 0 of its linear piece (large EVs; small EVs have no PWL term)
+          const double icpt = q.ev_small ? 0.0 : fma(-sg, wmid, tw * tw * lq_pwl(wmid * q.inv_wmax));
           t[0] = fma(0.5 * cc, Ya * Ya, fma(av, fma(0.5 * dd, av, ee + sg), icpt));
           t[1] = fma(cc, fma(Ya, Yb, -Ya), bv * fma(dd, av, ee + sg));
           t[2] = fma(0.5 * cc, Yb * Yb, fma(-cc, Yb, 0.5 * dd * bv * bv));
@@ -363,6 +371,15 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
 #pragma unroll
           for (int k = 0; k < 6; ++k) t[k] = act ? t[k] : 0.0;
           lqw::wave_totals(t, N);
+        };
+        if (bj >= 0) {  // (wave-uniform) the next solve beside this piece's certificate
+          nsol = lqw::solve_stage<2>(q, ws, 0.0, sln);
+          piece();
+        } else {
+          piece();
+        }
+        if (emit) {
+          if (!(res <= q.tol_cert)) break;  // coverage ends at gcur
           if (lane < N) {
             double* dst = reinterpret_cast<double*>(a.t_ab + (sb + npc) * N + lane);
             st_wt8(dst, av);
@@ -380,8 +397,8 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
           ++npc;
         }
         if (bj < 0) break;
-        const int bns = __shfl(ns, bj, 64);
-        if (lane == bj) sl = bns;
+        sl = sln;
+        sol = nsol;
         gcur = best;
         last = bj;
       }
@@ -398,11 +415,23 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
 #endif
 }
 
+template <int NT>
 __global__ __launch_bounds__(64) void k_path(PathArgs a) {
   const int blk = (int)blockIdx.x;
   const int s = __builtin_amdgcn_readfirstlane(blk / a.G);
   lq_tab_init(set_consts(a.qd, a.ce, s));
-  path_cell(a, blk);
+  path_cell<NT>(a, blk);
+}
+
+typedef void (*PathKernel)(PathArgs);
+PathKernel path_kernel(int N) {
+  switch (N) {
+    case 12: return k_path<12>;
+    case 16: return k_path<16>;
+    case 24: return k_path<24>;
+    case 48: return k_path<48>;
+    default: return k_path<0>;
+  }
 }
 
 // ---------------------------------------------------------------- k_eval
@@ -1359,7 +1388,7 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   if (!fused) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
-    hipExtLaunchKernelGGL(k_path, dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa);
+    hipExtLaunchKernelGGL(path_kernel(N), dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa);
     HIPCHK(p, hipGetLastError());
     plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
   }

@@ -61,6 +61,7 @@ __device__ long long g_stamps[65536 * 8];
 #ifndef EVAL_WAVES
 #define EVAL_WAVES 8  // k_eval: waves per workgroup (16: 16.1 us, 8: 14.8 us, 4: 16.2 us at config 3)
 #endif
+#define EVAL_MIN_WAVES ((2 * EVAL_WAVES + 3) / 4)  // k_eval: waves per SIMD for two workgroups per CU
 #define EVAL_EVS (64 * EVAL_WAVES)         // k_eval: threads per workgroup
 #define EVAL_PASSES 2                      // k_eval: EVs per thread, at most
 #define EVAL_MAXB (EVAL_EVS * EVAL_PASSES)  // k_eval: EVs per workgroup, at most
@@ -974,7 +975,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
 // write-through stores drained before the arrival, read back with sc1 loads), so no k_finalize
 // launch and no kernel boundary follow; workgroup nblk closes the sets that have no EVs.
 template <bool CLOSE, int NT>
-__global__ __launch_bounds__(EVAL_EVS, 4) void k_eval(EvalArgs a, FinalArgs r) {  // (4 waves per SIMD: two workgroups per CU)
+__global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_eval(EvalArgs a, FinalArgs r) {  // (4 waves per SIMD: two workgroups per CU)
   extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
   double (*red)[FIN_W] = reinterpret_cast<double (*)[FIN_W]>(s_dyn);
   double (*rep)[FIN_W] = red + EVAL_WAVES;
@@ -1176,11 +1177,14 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     if (p->n_cu < 1) p->n_cu = 1;
   }
   const int cap = std::min(LQ_PIECE_CAP, G * LQ_PPL);
-  if (p->eval_occ_key != (int64_t)N * 4096 + cap) {  // k_eval workgroups resident per CU
+  const bool close_mode = (flags & LOMPC_PLAN_CLOSE_IN_EVAL) != 0 || (getenv("LOMPC_CLOSE") && atoi(getenv("LOMPC_CLOSE")) != 0);
+  const int64_t occ_key = ((int64_t)N * 4096 + cap) * 2 + (close_mode ? 1 : 0);
+  if (p->eval_occ_key != occ_key) {  // k_eval workgroups resident per CU (of the kernel launched)
     int occ = 0;
-    HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, eval_kernel<true>(N), EVAL_EVS, eval_lds(N, G, cap)));
+    HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, close_mode ? eval_kernel<true>(N) : eval_kernel<false>(N),
+                                                           EVAL_EVS, eval_lds(N, G, cap)));
     p->eval_occ = std::max(occ, 1);
-    p->eval_occ_key = (int64_t)N * 4096 + cap;
+    p->eval_occ_key = occ_key;
   }
   const int64_t slots = (int64_t)p->n_cu * p->eval_occ;
   const int64_t rounds = std::max<int64_t>(1, (10 * B + 9ll * slots * EVAL_MAXB - 1) / (9ll * slots * EVAL_MAXB));

@@ -95,6 +95,7 @@ struct lompc_plan {
   int* d_fused = nullptr;       // [1 + S] k_fused's ticket + per-set published-cell counters
   int64_t cap_fused = 0;
   bool close = false;           // the sets' closing inside k_eval (no k_finalize launch)
+  bool close_no_w = true;       // ... in runs without w output
   int* d_arrive = nullptr;      // [S] k_eval's per-set arrival counters (close mode)
   int n_empty = 0;              // sets without EVs (closed by one extra k_eval workgroup)
   CtxEnds ce{};                 // set s belongs to context #{k : ce.end[k] <= s}

@@ -1177,13 +1177,12 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     if (p->n_cu < 1) p->n_cu = 1;
   }
   const int cap = std::min(LQ_PIECE_CAP, G * LQ_PPL);
-  const bool close_mode = (flags & LOMPC_PLAN_CLOSE_IN_EVAL) != 0 || (getenv("LOMPC_CLOSE") && atoi(getenv("LOMPC_CLOSE")) != 0);
-  const int64_t occ_key = ((int64_t)N * 4096 + cap) * 2 + (close_mode ? 1 : 0);
-  if (p->eval_occ_key != occ_key) {  // k_eval workgroups resident per CU (of the kernel launched)
-    int occ = 0;
-    HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, close_mode ? eval_kernel<true>(N) : eval_kernel<false>(N),
-                                                           EVAL_EVS, eval_lds(N, G, cap)));
-    p->eval_occ = std::max(occ, 1);
+  const int64_t occ_key = (int64_t)N * 4096 + cap;
+  if (p->eval_occ_key != occ_key) {  // k_eval workgroups resident per CU (either variant may run)
+    int occ0 = 0, occ1 = 0;
+    HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, eval_kernel<false>(N), EVAL_EVS, eval_lds(N, G, cap)));
+    HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, eval_kernel<true>(N), EVAL_EVS, eval_lds(N, G, cap)));
+    p->eval_occ = std::max(std::min(occ0, occ1), 1);
     p->eval_occ_key = occ_key;
   }
   const int64_t slots = (int64_t)p->n_cu * p->eval_occ;
@@ -1250,8 +1249,13 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     const char* env = getenv("LOMPC_FUSED");  // diagnostics: force the split / fused launches
     const bool want = env ? atoi(env) != 0 : (flags & LOMPC_PLAN_FUSED) != 0;
     p->fused = want && G % EVAL_WAVES == 0;
-    const char* ce = getenv("LOMPC_CLOSE");  // diagnostics: 1 = close the sets inside k_eval
-    p->close = !p->fused && (ce ? atoi(ce) != 0 : (flags & LOMPC_PLAN_CLOSE_IN_EVAL) != 0);
+    // the sets close inside k_eval when the plan asks for it, and by default in runs that write
+    // no w rows (a price loop's reductions-only runs): nothing then makes the arriving
+    // workgroups wait for row stores, and the k_finalize launch and its boundary go
+    // (LOMPC_CLOSE: 1 = always, 0 = never, diagnostics)
+    const char* ce = getenv("LOMPC_CLOSE");
+    p->close = !p->fused && (ce ? atoi(ce) == 1 : (flags & LOMPC_PLAN_CLOSE_IN_EVAL) != 0);
+    p->close_no_w = !p->fused && (ce ? atoi(ce) == 1 : true);
   }
   p->B = B;
   p->S = S;
@@ -1386,7 +1390,7 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   r.fused_tickets = p->d_fused;
   r.fused_done = p->d_fused ? p->d_fused + 1 : nullptr;
   r.arrive = p->d_arrive;
-  const bool close = p->close && !p->fused && p->nblk > 0;
+  const bool close = (p->close || (p->close_no_w && !w)) && !p->fused && p->nblk > 0;
   const bool cprof = prof_ctx && prof_ctx->prof;  // lompc_solve_batch: the context's k_eval timing
   const bool fused = p->fused && p->nblk > 0;
   if (!fused) {

@@ -428,7 +428,8 @@ class BatchPlan:
 
     def launches_per_run(self) -> int:
         """Kernel launches of one run: k_path + k_eval + k_finalize; two when the sets close inside
-        k_eval (LOMPC_PLAN_CLOSE_IN_EVAL / LOMPC_CLOSE=1) or with k_fused + k_finalize."""
+        k_eval (runs without w output, LOMPC_PLAN_CLOSE_IN_EVAL, LOMPC_CLOSE=1) or with k_fused +
+        k_finalize."""
         import os
 
         if self.direct:
@@ -436,7 +437,10 @@ class BatchPlan:
         if self._flags & _lib.LOMPC_PLAN_FUSED:
             return 2
         env = os.environ.get("LOMPC_CLOSE")
-        close = (env == "1") if env is not None else bool(self._flags & _lib.LOMPC_PLAN_CLOSE_IN_EVAL)
+        if env is not None:
+            close = env == "1"
+        else:
+            close = bool(self._flags & _lib.LOMPC_PLAN_CLOSE_IN_EVAL) or not self._want["w"]
         return 2 if close else 3
 
     def info(self) -> dict:

@@ -170,7 +170,8 @@ typedef struct lompc_plan lompc_plan;
 #define LOMPC_PLAN_FUSED 4       /* k_path and k_eval as one launch */
 #define LOMPC_PLAN_CLOSE_IN_EVAL 8 /* the per-set reductions and re-solves inside k_eval, by each
                                       set's last-arriving workgroup, instead of the k_finalize
-                                      launch (measured slower) */
+                                      launch, also in runs that write w rows (slower there, see
+                                      DESIGN.md); runs without w output always close this way */
 
 /* Build a plan over B EVs grouped by set (S = sum of sets_per_ctx sets):
  *   ctxs         host [n_ctx]   contexts (same N and device), n_ctx <= LOMPC_PLAN_MAX_CTX

@@ -25,7 +25,7 @@ for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
         for k in KERNELS:
-            if name.startswith(k + "("):
+            if name.startswith(k + "(") or name.startswith(k + "<"):  # (exact-N template instances)
                 vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 
 

@@ -342,3 +342,43 @@ def test_close_in_eval_matches_k_finalize(gpu, diag_repair):
                 assert torch.equal(a[k], b[k]), k
         st = a["set_stats"].cpu().numpy()
         np.testing.assert_array_equal(st[:, 0], np.diff(off))  # LOMPC_STAT_COUNT, empty sets included
+
+
+def test_reductions_only_runs_close_in_eval(gpu):
+    """Runs without w output (a price loop's) close their sets inside k_eval by default; the
+    same plan with LOMPC_CLOSE=0 (k_finalize launch) gives the same costs bitwise and the same
+    set reductions up to the summation order (an empty set and a set of one EV included)."""
+    N, P = 48, 3
+    rng = np.random.default_rng(5)
+    c = O.large_consts()
+    lo = LoMPC(N, LoMPCConstants(c.delta, c.theta, c.y_max, c.w_max, c.ev_type), device=0)
+    off = np.array([0, 5000, 5000, 5001], dtype=np.int64)
+    g = torch.as_tensor(c.y_max - (0.3 + 0.2 * rng.random(5001)), device="cuda:0")
+    wr = torch.as_tensor(c.w_max * rng.random((P, N)), device="cuda:0")
+    lm = torch.as_tensor(c.theta * rng.random((P, 3 * N)), device="cuda:0")
+    lr = torch.as_tensor([0.0, 0.3, 0.1], dtype=torch.float64, device="cuda:0")
+    outs = []
+    old = os.environ.get("LOMPC_CLOSE")
+    try:
+        for env in (None, "0"):
+            if env is None:
+                os.environ.pop("LOMPC_CLOSE", None)
+            else:
+                os.environ["LOMPC_CLOSE"] = env
+            plan = BatchPlan(lo, g, off, w_ref=wr, want_w=False, want_cost=True, warm_start=True)
+            assert plan.launches_per_run() == (2 if env is None else 3)
+            res = []
+            for _ in range(3):
+                out = plan.run(lm, lr)
+                assert plan.check()[1:] == (0, 0)
+                res.append({k: v.clone() for k, v in out.items() if v is not None})
+            outs.append(res)
+    finally:
+        if old is None:
+            os.environ.pop("LOMPC_CLOSE", None)
+        else:
+            os.environ["LOMPC_CLOSE"] = old
+    for a, b in zip(*outs):
+        assert torch.equal(a["cost"], b["cost"])
+        for k in ("set_sum_w", "set_stats"):
+            np.testing.assert_allclose(a[k].cpu().numpy(), b[k].cpu().numpy(), rtol=1e-12, atol=1e-12, err_msg=k)

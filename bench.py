@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--event-every", type=int, default=4,
                     help="HIP events on the per-EV kernel's dispatch of every E-th timed step (the "
                          "events' own cost, ~2 us per pair, stays out of the other steps)")
+    ap.add_argument("--per-step-issue", action="store_true",
+                    help="diagnostics: issue each timed step from Python (one lompc_plan_run per step)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-station", action="store_true", help="skip the BiMPC steps/sec leg")
     ap.add_argument("--station-evs-per-gpu", type=int, default=262144, help="EVs per GPU, half per type")
@@ -144,6 +146,7 @@ def main():
         runs = [dict(plan=BatchPlan([e["lompc"] for e in eng], gamma, off, sets_per_ctx=[P, P], w_ref=wr,
                                     want_w=args.outputs == "full", want_cost=args.outputs != "set", want_set=True,
                                     stream=main, warm_start=args.warm), stream=main, lm_ptr=[lm[k].data_ptr() for k in range(nsteps)], lr_ptr=lr.data_ptr(),
+                     lm_stride=int(lm[0].numel()),
                      qps=B, keep=(gamma, lm, wr, lr))]
     else:
         # DIRECT mode: one context per EV type, each on its own stream
@@ -187,13 +190,22 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     ev_every = max(1, args.event_every)
+    # one rank, one plan: the K timed steps are issued by ONE C-ABI call (lompc_plan_run_steps:
+    # the same three launches per step at that step's prices, the HIP events on every E-th
+    # step's k_eval), so host issue stays far below the GPU time even on a slow host CPU
+    batched = world == 1 and len(runs) == 1 and "lm_stride" in runs[0] and not args.per_step_issue
     t0 = time.perf_counter()
-    for k in range(args.warmup, nsteps):
-        sample = not args.no_kernel_events and (k - args.warmup) % ev_every == 0
-        if ev_every > 1 and not args.no_kernel_events:
-            for r in runs:
-                r["plan"].profile(enable=("k_eval",) if sample else False)
-        step(k)
+    if batched:
+        r = runs[0]
+        r["plan"].run_steps(r["lm_ptr"][args.warmup], r["lr_ptr"], args.steps, r["lm_stride"], 0,
+                            profile_every=0 if args.no_kernel_events else ev_every)
+    else:
+        for k in range(args.warmup, nsteps):
+            sample = not args.no_kernel_events and (k - args.warmup) % ev_every == 0
+            if ev_every > 1 and not args.no_kernel_events:
+                for r in runs:
+                    r["plan"].profile(enable=("k_eval",) if sample else False)
+            step(k)
     t_issue = time.perf_counter() - t0  # host time to enqueue the K steps (GPU-bound if << dt)
     torch.cuda.synchronize()
     if world > 1:
@@ -249,6 +261,8 @@ def main():
             "parallelism": f"dp{world} (EV shards, one RCCL all-gather of both types' per-set reductions per step)",
             "launches_per_step": sum(r["plan"].launches_per_run() for r in runs),
             "kernel_events": "none" if args.no_kernel_events else f"k_eval, 1 in {ev_every} timed steps",
+            "issue": "per-step lompc_plan_run" if (world > 1 or args.per_step_issue or args.mode != "path" or args.split_types)
+                     else "one lompc_plan_run_steps call for the K timed steps",
         },
         "roofline": {
             "bound": "hbm",

@@ -677,28 +677,41 @@ __global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
 // One k_eval block (EVs [start, end) of one set, <= EVAL_MAXB) by the whole workgroup.
 // NT: the horizon as a compile-time constant (0: a.N at run time) — the row loop's lane map
 // (stages per lane, rows per store instruction) and its address arithmetic become constants.
-template <bool COH, int NT = 0>
-__device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
-  // dynamic LDS: [cap][N] piece rows | [cap][8] coefficients | [cap] piece ends | cells:
-  // coverage start | piece count
+// CLOSE: the set is closed inside the launch (no k_finalize).  The workgroup record is built
+// BEFORE the rows: the per-stage sums come from per-piece aggregates (EV count and gamma sum of
+// each piece, fixed-point integer LDS atomics: exact and order-free), so wave 0 publishes the
+// record and arrives on the set's counter while no row store is in flight, and the other waves
+// write all the rows; the set's last arriver closes it (finalize_set) after its rows.  Rows of
+// EVs left to the individual re-solve are not written here (key ZD), the closing workgroup writes
+// them, so no two writes of a row race.
+template <bool COH, int NT = 0, bool CLOSE = false>
+__device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, const FinalArgs* fr = nullptr) {
+  // dynamic LDS: [cap + 2][N] piece rows (rows cap, cap + 1: zero pieces) | [cap][8] coefficients |
+  // [cap] piece ends | cells: coverage start | piece count | (CLOSE) per piece: gamma sum, EV count
   extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
-  __shared__ double s_g[EVAL_WAVES][64 * EVAL_PASSES];            // the wave's rows: gamma, piece
-  __shared__ int s_k[EVAL_WAVES][64 * EVAL_PASSES];               //   (-1 re-solved, -2 invalid)
-  __shared__ double s_accw[EVAL_WAVES][LOMPC_MAX_N];              // per-wave row sums per stage
+  __shared__ double s_g[EVAL_MAXB];  // block row r = EV start + r: gamma
+  __shared__ int s_k[EVAL_MAXB];     //   its piece (ZK / ZD: zero pieces)
+  __shared__ double s_accw[EVAL_WAVES][LOMPC_MAX_N];  // per-wave row sums per stage
   __shared__ double s_red[EVAL_WAVES][8];
+  __shared__ int s_fc[EVAL_WAVES];  // (CLOSE) re-solve list lengths
+  __shared__ int s_last;            // (CLOSE) this workgroup closes the set
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int4 info = a.blk[blk];
   const int s = info.x, start = info.y, end = info.z;  // thread: EVs start + tid + EVAL_EVS h
   const int N = NT ? NT : a.N, G = a.G;
   const int cap = a.cap;
-  const int ZK = cap;  // the zero piece (a = b = 0): rows of re-solved and invalid EVs, which
-                       // then add exactly 0 to the row sums and need no branch in the row loop
+  const int ZK = cap;      // the zero piece (a = b = 0): rows of invalid (and, without CLOSE,
+                           // re-solved) EVs, which then add exactly 0 to the row sums and need no
+                           // branch in the row loop
+  const int ZD = cap + 1;  // (CLOSE) zero piece whose row is not written: re-solved EVs
   LQ_STAMPE(0);
   double2* s_ab = s_dyn;
-  double* s_cf = reinterpret_cast<double*>(s_ab + (size_t)(cap + 1) * N);  // (row cap: the zero piece)
+  double* s_cf = reinterpret_cast<double*>(s_ab + (size_t)(cap + 2) * N);
   double* s_ge = s_cf + (size_t)cap * 8;
   double* s_lo = s_ge + cap;
   int* s_cnt = reinterpret_cast<int*>(s_lo + G);
+  unsigned long long* s_pf = reinterpret_cast<unsigned long long*>(s_cnt + ((G + 1) & ~1));
+  int* s_pn = reinterpret_cast<int*>(s_pf + cap + 2);
   // this thread's EVs (caller order), the cells and the set's piece count: one memory round
   double gh[EVAL_PASSES];
 #pragma unroll
@@ -756,7 +769,11 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
       s_cnt[tid] = vn;
       s_lo[tid] = vl;
     }
-    if (tid < N) s_ab[ZK * N + tid] = make_double2(0.0, 0.0);
+    if (tid < 2 * N) s_ab[ZK * N + tid] = make_double2(0.0, 0.0);  // both zero pieces
+    if (CLOSE && tid < cap + 2) {
+      s_pf[tid] = 0ull;
+      s_pn[tid] = 0;
+    }
     for (int it = tid + EVAL_EVS * U; it < nab; it += EVAL_EVS) s_ab[it] = ld_t<COH>(gab + it);
     for (int c = tid + EVAL_EVS; c < G; c += EVAL_EVS) {
       s_cnt[c] = ld_t<COH>(a.t_cnt + cb + c);
@@ -766,10 +783,11 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
   lq_tab_init(q);  // (its barrier publishes the staged table)
   LQ_STAMPE(1);
   // ---- lane = EV: piece, scalar outputs; EVs no certified piece covers listed for the
-  //      individual re-solve in k_finalize (counted as pending failures until then)
+  //      individual re-solve (counted as pending failures until then)
   const double ym = q.y_max, wm = q.w_max;
   const double tt = q.theta * q.theta;
   const double cscale = (double)G / (whi - wlo);
+  const double fxs = 0x1p40 / (whi - wlo);  // (CLOSE) gamma - wlo in units of the window / 2^40
   double acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
   int n_ok = 0, n_fail = 0, n_inv = 0, nlist = 0;
   bool inv_rows = false;  // (wave-uniform) some row of this wave has an invalid gamma
@@ -807,9 +825,13 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
       if (a.cost) st_wt8(a.cost + i, cst);
       if (a.w0) st_wt8(a.w0 + i, w0v);
       if (a.status) a.status[i] = LOMPC_QP_OK;
+      if (CLOSE) {
+        atomicAdd(s_pn + key, 1);
+        atomicAdd(s_pf + key, (unsigned long long)rint(fmax(g - wlo, 0.0) * fxs));
+      }
     }
-    s_g[wv][64 * h + lane] = g;
-    s_k[wv][64 * h + lane] = cov ? key : ZK;
+    s_g[tid + EVAL_EVS * h] = g;
+    s_k[tid + EVAL_EVS * h] = cov ? key : ((CLOSE && valid) ? ZD : ZK);
     inv_rows |= __ballot(act && !valid) != 0ull;
     const unsigned long long need = __ballot(valid && !cov);
     if (valid && !cov) {
@@ -819,127 +841,8 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
     }
     nlist += __popcll(need);
   }
-  if (lane == 0) st_wt4(a.fail_cnt + (size_t)blk * EVAL_WAVES + wv, nlist);
-  LQ_STAMPE(2);
-  __builtin_amdgcn_wave_barrier();  // this wave's own rows in LDS: in order
-  LQ_STAMPE(3);
-  // ---- rows (lane = stage pair): w_t = a_t + b_t gamma of the EV's piece -> contiguous rows
-  const int V = (N & 1) ? 1 : 2;  // stages per lane (16-B stores for even N)
-  const int Lr = N / V;           // lanes per row
-  const int R = 64 / Lr;          // rows per store instruction
-  const int rr = lane / Lr, col = lane - rr * Lr;
-  const bool rlane = rr < R;
-  const int t0 = V * col;
-  constexpr int RU = 4;  // row instructions per batch: their LDS reads in flight together
-  double acc0 = 0.0, acc1 = 0.0;
-  // one pass per EV of a thread: the wave's rows of pass h are EVs rbase .. rbase + nh - 1
-  // (contiguous in w), LDS rows 64 h ...; every row is a plain piece lookup (re-solved and
-  // invalid EVs read the zero piece), so the loop has no per-row branch: the stores of a full
-  // batch use one address register and immediate offsets; lanes past the row width (rlane
-  // false) store out of the descriptor's range, which drops them
-  const bool fast = a.w && a.w_rsrc_ok;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(a.w, (short)0, a.w ? a.w_bytes : 0, 0x00020000);
-#pragma unroll
-  for (int h = 0; h < EVAL_PASSES; ++h) {
-    const int rbase = start + EVAL_EVS * h + 64 * wv;
-    const int nh = max(0, min(64, end - rbase));  // wave-uniform
-    if (nh == 0) continue;
-    const int* sk = &s_k[wv][64 * h];
-    const double* sg = &s_g[wv][64 * h];
-    const int vb = rlane ? ((rbase + rr) * N + t0) * 8 : LQ_DROP_OFF;  // row rr of the pass
-    int kk[RU];
-    double gg[RU];
-#pragma unroll
-    for (int j = 0; j < RU; ++j) {
-      const int rc = min(j * R + rr, 63);
-      kk[j] = sk[rc];
-      gg[j] = sg[rc];
-    }
-    for (int r0 = 0; r0 < nh; r0 += RU * R) {
-      double2 u0[RU], u1[RU];
-#pragma unroll
-      for (int j = 0; j < RU; ++j) {
-        u0[j] = s_ab[kk[j] * N + t0];
-        u1[j] = V == 2 ? s_ab[kk[j] * N + t0 + 1] : make_double2(0.0, 0.0);
-      }
-      int kn[RU];  // the next batch's keys and gammas (software pipeline: one LDS round per batch)
-      double gn[RU];
-#pragma unroll
-      for (int j = 0; j < RU; ++j) {
-        const int rc = min(r0 + (RU + j) * R + rr, 63);
-        kn[j] = sk[rc];
-        gn[j] = sg[rc];
-      }
-      // a batch's row math and stores; FULL (every row of the batch exists: no per-row masks)
-      // and FAST (w through the descriptor: one address register, immediate offsets) are
-      // wave-uniform and specialised so the common case has no exec-mask change per row
-      auto rows = [&](auto full_t, auto fast_t) {
-        constexpr bool FULL = decltype(full_t)::value, FAST = decltype(fast_t)::value;
-#pragma unroll
-        for (int j = 0; j < RU; ++j) {
-          const double x0 = clampw(fma(u0[j].y, gg[j], u0[j].x), wm);
-          const double x1 = V == 2 ? clampw(fma(u1[j].y, gg[j], u1[j].x), wm) : 0.0;
-          if (FULL || (rlane && r0 + j * R + rr < nh)) {  // (FULL: lanes past the row width add 0 below)
-            acc0 += x0;
-            acc1 += x1;
-            if (FAST) {
-              const int off = vb + (r0 + j * R) * N * 8;
-              if (V == 2) st_wt16(rs, off, x0, x1);
-              else st_wt8b(rs, off, x0);
-            } else if (a.w) {
-              double* dst = a.w + (size_t)(rbase + r0 + j * R + rr) * N + t0;
-              st_wt8(dst, x0);
-              if (V == 2) st_wt8(dst + 1, x1);
-            }
-          }
-        }
-      };
-      using T_ = std::true_type;
-      using F_ = std::false_type;
-      if (r0 + RU * R <= nh) {  // wave-uniform
-        if (fast) rows(T_{}, T_{});
-        else rows(T_{}, F_{});
-      } else {
-        if (fast) rows(F_{}, T_{});
-        else rows(F_{}, F_{});
-      }
-#pragma unroll
-      for (int j = 0; j < RU; ++j) {
-        kk[j] = kn[j];
-        gg[j] = gn[j];
-      }
-    }
-  }
-  if (!rlane) acc0 = acc1 = 0.0;  // (lanes past the row width read real rows in full batches)
-  // rows of invalid EVs (gamma outside [0, y_max] or NaN): NaN, written after the loop's
-  // zeros of the same rows (rare; ordered by the wait)
-  if (inv_rows && a.w) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int h = 0; h < EVAL_PASSES; ++h) {
-      const int rbase = start + EVAL_EVS * h + 64 * wv;
-      const int nh = max(0, min(64, end - rbase));
-      for (int r = 0; r < nh; ++r) {
-        const double g = s_g[wv][64 * h + r];
-        if (!(g >= 0.0 && g <= ym) && lane < N) st_wt8(a.w + (size_t)(rbase + r) * N + lane, NAN);
-      }
-    }
-  }
-  // this wave's row sums per stage: lanes col, col + Lr, ... (fixed order)
-  {
-    double s0 = acc0, s1 = acc1;
-    for (int k = 1; k < R; ++k) {
-      s0 += __shfl(acc0, lane + k * Lr, 64);
-      s1 += __shfl(acc1, lane + k * Lr, 64);
-    }
-    if (lane < Lr) {
-      s_accw[wv][V * lane] = s0;
-      if (V == 2) s_accw[wv][V * lane + 1] = s1;
-    }
-  }
-  LQ_STAMPE(4);
-  // ---- workgroup record: per-wave totals, then a fixed-order combination
-  {
+  // per-wave totals of the scalar outputs
+  auto wave_record = [&]() {
     double tot[4] = {acc_cost, acc_p0, (double)n_ok, 0.0};
     lqw::wave_totals(tot, 64);
     const double mx = sqrt(lqw::wave_max(acc_err, 64));  // (sqrt is monotone: max of the roots)
@@ -954,57 +857,236 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk) {
       s_red[wv][PX_N_FAILED] = cnt[0];
       s_red[wv][PX_N_INVALID] = cnt[1];
     }
+  };
+  // the workgroup record (fixed-order combination of the waves'), by the threads of `lanes`
+  auto store_record = [&](int t, int nthreads) {
+    double* part = a.partial + (size_t)blk * (N + NPX);
+    for (int c = t; c < N + NPX; c += nthreads) {
+      double v = 0.0;
+      if (c < N) {
+        for (int k = 0; k < EVAL_WAVES; ++k) v += s_accw[k][c];
+      } else {
+        const int x = c - N;
+        for (int k = 0; k < EVAL_WAVES; ++k) v = x == PX_MAX_ERR ? fmax(v, s_red[k][x]) : v + s_red[k][x];
+      }
+      st_wt8(part + c, v);
+    }
+  };
+  bool any_inv = inv_rows;  // (CLOSE: the block's; else this wave's own rows)
+  if constexpr (CLOSE) {
+    if (lane == 0) s_fc[wv] = nlist;
+    if (nlist > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's re-solve list has landed
+    __syncthreads();  // every row's key, the piece aggregates and the list lengths complete
+    // per-stage sums of the block's rows: sum over pieces p of n_p a_t + Gamma_p b_t, pieces
+    // p = wv, wv + W, ... by wave wv (lane = stage), the waves combined in a fixed order
+    const double fxi = (whi - wlo) * 0x1p-40;
+    double accs = 0.0;
+    constexpr int PU = (LQ_PIECE_CAP + EVAL_WAVES - 1) / EVAL_WAVES;
+    for (int p0 = wv; p0 < np; p0 += EVAL_WAVES * PU) {  // (one iteration for np <= LQ_PIECE_CAP)
+      int n[PU];
+      unsigned long long f[PU];
+      double2 ab[PU];
+#pragma unroll
+      for (int k = 0; k < PU; ++k) {  // every read of the batch in flight together
+        const int p = p0 + EVAL_WAVES * k;
+        const int pc = min(p, np - 1);
+        n[k] = p < np ? s_pn[pc] : 0;
+        f[k] = s_pf[pc];
+        ab[k] = s_ab[pc * N + min(lane, N - 1)];
+      }
+#pragma unroll
+      for (int k = 0; k < PU; ++k) {
+        const double gsum = fma((double)f[k], fxi, (double)n[k] * wlo);
+        accs = fma((double)n[k], ab[k].x, accs);  // (n = 0: exact no-op, gsum = 0 below)
+        accs = fma(n[k] ? gsum : 0.0, ab[k].y, accs);
+      }
+    }
+    if (lane < N) s_accw[wv][lane] = accs;
+    wave_record();
+    __syncthreads();
+    any_inv = false;
+    for (int k = 0; k < EVAL_WAVES; ++k) any_inv |= s_red[k][PX_N_INVALID] > 0.0;
+    if (wv == 0) {  // publish the record, then arrive (nothing but the lookup's stores in flight)
+      store_record(lane, 64);
+      if (lane < EVAL_WAVES) st_wt4(a.fail_cnt + (size_t)blk * EVAL_WAVES + lane, s_fc[lane]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        const int nb = fr->blk_prefix[s + 1] - fr->blk_prefix[s];
+        const int old = __hip_atomic_fetch_add(fr->arrive + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == nb - 1;
+        if (old == nb - 1) __hip_atomic_store(fr->arrive + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  } else {
+    if (lane == 0) st_wt4(a.fail_cnt + (size_t)blk * EVAL_WAVES + wv, nlist);
+    __builtin_amdgcn_wave_barrier();  // this wave's own rows in LDS: in order
   }
-  __syncthreads();
-  double* part = a.partial + (size_t)blk * (N + NPX);
-  if (tid < N) {  // stage t: every wave's row sums, then the re-solved rows
-    double sw = 0.0;
-    for (int k = 0; k < EVAL_WAVES; ++k) sw += s_accw[k][tid];
-    st_wt8(part + tid, sw);
-  } else if (tid >= 64 && tid < 64 + NPX) {
-    const int x = tid - 64;
-    double v = 0.0;
-    for (int k = 0; k < EVAL_WAVES; ++k) v = x == PX_MAX_ERR ? fmax(v, s_red[k][x]) : v + s_red[k][x];
-    st_wt8(part + N + x, v);
+  LQ_STAMPE(2);
+  LQ_STAMPE(3);
+  // ---- rows (lane = stage pair): w_t = a_t + b_t gamma of the EV's piece -> contiguous rows
+  const int V = (N & 1) ? 1 : 2;  // stages per lane (16-B stores for even N)
+  const int Lr = N / V;           // lanes per row
+  const int R = 64 / Lr;          // rows per store instruction
+  const int rr = lane / Lr, col = lane - rr * Lr;
+  const bool rlane = rr < R;
+  const int t0 = V * col;
+  constexpr int RU = 4;  // row instructions per batch: their LDS reads in flight together
+  double acc0 = 0.0, acc1 = 0.0;
+  // a segment of the block's rows r0b .. r0b + nrows - 1 (EVs start + r, contiguous in w): every
+  // row is a plain piece lookup (re-solved and invalid EVs read a zero piece), so the loop has
+  // no per-row branch: the stores of a full batch use one address register and immediate
+  // offsets; lanes past the row width (rlane false) store out of the descriptor's range, which
+  // drops them
+  const bool fast = a.w && a.w_rsrc_ok;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(a.w, (short)0, a.w ? a.w_bytes : 0, 0x00020000);
+  auto row_segment = [&](const int r0b, const int nrows) {
+    const int* sk = s_k + r0b;
+    const double* sg = s_g + r0b;
+    const int rbase = start + r0b;
+    const int vb = rlane ? ((rbase + rr) * N + t0) * 8 : LQ_DROP_OFF;  // row rr of the segment
+    int kk[RU];
+    double gg[RU];
+#pragma unroll
+    for (int j = 0; j < RU; ++j) {
+      const int rc = min(j * R + rr, nrows - 1);
+      kk[j] = sk[rc];
+      gg[j] = sg[rc];
+    }
+    for (int r0 = 0; r0 < nrows; r0 += RU * R) {
+      double2 u0[RU], u1[RU];
+#pragma unroll
+      for (int j = 0; j < RU; ++j) {
+        u0[j] = s_ab[kk[j] * N + t0];
+        u1[j] = V == 2 ? s_ab[kk[j] * N + t0 + 1] : make_double2(0.0, 0.0);
+      }
+      int kn[RU];  // the next batch's keys and gammas (software pipeline: one LDS round per batch)
+      double gn[RU];
+#pragma unroll
+      for (int j = 0; j < RU; ++j) {
+        const int rc = min(r0 + (RU + j) * R + rr, nrows - 1);
+        kn[j] = sk[rc];
+        gn[j] = sg[rc];
+      }
+      // a batch's row math and stores; FULL (every row of the batch exists and is written: no
+      // per-row masks) and FAST (w through the descriptor: one address register, immediate
+      // offsets) are wave-uniform and specialised so the common case has no exec-mask change
+      auto rows = [&](auto full_t, auto fast_t) {
+        constexpr bool FULL = decltype(full_t)::value, FAST = decltype(fast_t)::value;
+#pragma unroll
+        for (int j = 0; j < RU; ++j) {
+          const double x0 = clampw(fma(u0[j].y, gg[j], u0[j].x), wm);
+          const double x1 = V == 2 ? clampw(fma(u1[j].y, gg[j], u1[j].x), wm) : 0.0;
+          if (FULL || (rlane && r0 + j * R + rr < nrows && (!CLOSE || kk[j] != ZD))) {
+            if (!CLOSE) {  // (FULL: lanes past the row width add 0 below)
+              acc0 += x0;
+              acc1 += x1;
+            }
+            if (FAST) {
+              const int off = vb + (r0 + j * R) * N * 8;
+              if (V == 2) st_wt16(rs, off, x0, x1);
+              else st_wt8b(rs, off, x0);
+            } else if (a.w) {
+              double* dst = a.w + (size_t)(rbase + r0 + j * R + rr) * N + t0;
+              st_wt8(dst, x0);
+              if (V == 2) st_wt8(dst + 1, x1);
+            }
+          }
+        }
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      bool full = r0 + RU * R <= nrows;  // wave-uniform
+      if constexpr (CLOSE) {  // a batch with a row left to the re-solve takes the masked path
+        bool drop = false;
+#pragma unroll
+        for (int j = 0; j < RU; ++j) drop |= kk[j] == ZD;
+        full = full && !__any(drop);
+      }
+      if (full) {
+        if (fast) rows(T_{}, T_{});
+        else rows(T_{}, F_{});
+      } else {
+        if (fast) rows(F_{}, T_{});
+        else rows(F_{}, F_{});
+      }
+#pragma unroll
+      for (int j = 0; j < RU; ++j) {
+        kk[j] = kn[j];
+        gg[j] = gn[j];
+      }
+    }
+    // rows of invalid EVs (gamma outside [0, y_max] or NaN): NaN, written after the loop's
+    // zeros of the same rows (rare; ordered by the wait)
+    if (any_inv && a.w) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int r = 0; r < nrows; ++r) {
+        const double g = sg[r];
+        if (!(g >= 0.0 && g <= ym) && lane < N) st_wt8(a.w + (size_t)(rbase + r) * N + lane, NAN);
+      }
+    }
+  };
+  if constexpr (CLOSE) {  // waves 1.. split the block's rows evenly (wave 0 published the record)
+    if (wv > 0 && a.w) {  // (no w output: nothing to write, the sums are in the record)
+      const int tot = end - start;
+      const int lo = (wv - 1) * tot / (EVAL_WAVES - 1), hi = wv * tot / (EVAL_WAVES - 1);
+      if (hi > lo) row_segment(lo, hi - lo);
+    }
+  } else {  // each wave its own lookup rows, one segment per pass
+#pragma unroll
+    for (int h = 0; h < EVAL_PASSES; ++h) {
+      const int r0b = EVAL_EVS * h + 64 * wv;
+      const int nh = max(0, min(64, end - start - r0b));  // wave-uniform
+      if (nh > 0) row_segment(r0b, nh);
+    }
+  }
+  LQ_STAMPE(4);
+  if constexpr (CLOSE) {
+    __syncthreads();  // every row written; the staged table is free (finalize_set's scratch)
+    if (s_last) {
+      double (*red)[FIN_W] = reinterpret_cast<double (*)[FIN_W]>(s_dyn);
+      finalize_set<EVAL_WAVES, true>(*fr, s, red, red + EVAL_WAVES);
+    }
+  } else {
+    if (!rlane) acc0 = acc1 = 0.0;  // (lanes past the row width read real rows in full batches)
+    // this wave's row sums per stage: lanes col, col + Lr, ... (fixed order)
+    {
+      double s0 = acc0, s1 = acc1;
+      for (int k = 1; k < R; ++k) {
+        s0 += __shfl(acc0, lane + k * Lr, 64);
+        s1 += __shfl(acc1, lane + k * Lr, 64);
+      }
+      if (lane < Lr) {
+        s_accw[wv][V * lane] = s0;
+        if (V == 2) s_accw[wv][V * lane + 1] = s1;
+      }
+    }
+    wave_record();
+    __syncthreads();
+    if (tid < 64) store_record(tid, 64);
   }
   LQ_STAMPE(5);
 }
 
 // k_eval.  CLOSE: the set's closing (finalize_set) runs inside the launch, by the workgroup of the
-// set that arrives last (an agent-scope counter per set; its records and re-solve lists are
-// write-through stores drained before the arrival, read back with sc1 loads), so no k_finalize
-// launch and no kernel boundary follow; workgroup nblk closes the sets that have no EVs.
+// set that arrives last (eval_block<..., CLOSE>), so no k_finalize launch and no kernel boundary
+// follow; workgroup nblk closes the sets that have no EVs.
 template <bool CLOSE, int NT>
 __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_eval(EvalArgs a, FinalArgs r) {  // (4 waves per SIMD: two workgroups per CU)
   extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
-  double (*red)[FIN_W] = reinterpret_cast<double (*)[FIN_W]>(s_dyn);
-  double (*rep)[FIN_W] = red + EVAL_WAVES;
   const int b = (int)blockIdx.x;
   if constexpr (CLOSE) {
     if (b == a.nblk) {
+      double (*red)[FIN_W] = reinterpret_cast<double (*)[FIN_W]>(s_dyn);
       for (int s = 0; s < a.S; ++s)
         if (r.blk_prefix[s + 1] == r.blk_prefix[s]) {
-          finalize_set<EVAL_WAVES, true>(r, s, red, rep);
+          finalize_set<EVAL_WAVES, true>(r, s, red, red + EVAL_WAVES);
           __syncthreads();  // (red / rep are rewritten for the next set)
         }
       return;
     }
   }
-  eval_block<false, NT>(a, b);
-  if constexpr (CLOSE) {
-    __shared__ int s_last;
-    const int s = __builtin_amdgcn_readfirstlane(a.blk[b].x);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record / list stores have landed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int nb = r.blk_prefix[s + 1] - r.blk_prefix[s];
-      const int old = __hip_atomic_fetch_add(r.arrive + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = old == nb - 1;
-      if (old == nb - 1) __hip_atomic_store(r.arrive + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (s_last) finalize_set<EVAL_WAVES, true>(r, s, red, rep);
-  }
+  eval_block<false, NT, CLOSE>(a, b, &r);
 }
 
 // k_eval for horizon N: exact-N instantiations for the shipped horizons, run-time N otherwise
@@ -1125,8 +1207,9 @@ int plan_events_read(std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& pool,
 // ============================================================== host
 // k_eval's dynamic LDS: up to cap pieces of one set (N double2 + 8 + 1 doubles each) + the cells
 size_t eval_lds(int N, int G, int cap) {
-  const size_t stage = (size_t)cap * (N * sizeof(double2) + 9 * sizeof(double)) + (size_t)N * sizeof(double2) +
-                       (size_t)G * (sizeof(int) + sizeof(double));
+  const size_t stage = (size_t)cap * (N * sizeof(double2) + 9 * sizeof(double)) + (size_t)2 * N * sizeof(double2) +
+                       (size_t)G * sizeof(double) + (size_t)((G + 1) & ~1) * sizeof(int) +
+                       (size_t)(cap + 2) * (sizeof(unsigned long long) + sizeof(int));
   return std::max(stage, (size_t)2 * EVAL_WAVES * FIN_W * sizeof(double));  // (close mode: red / rep)
 }
 
@@ -1585,6 +1668,22 @@ int lompc_plan_run(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   if (!p) return LOMPC_ERR_INVALID_ARG;
   HIPCHK(p, hipSetDevice(p->device));
   return lq_plan_launch(p, lmbd, lmbd_r, w, cost, w0, status, set_sum_w, set_stats, (hipStream_t)stream, nullptr);
+}
+
+int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride, const double* lmbd_r,
+                         int64_t lmbd_r_stride, int n_runs, int profile_every, double* w, double* cost, double* w0,
+                         int8_t* status, double* set_sum_w, double* set_stats, void* stream) {
+  if (!p || n_runs < 0 || profile_every < 0) return LOMPC_ERR_INVALID_ARG;
+  HIPCHK(p, hipSetDevice(p->device));
+  const int mask = p->prof;
+  int rc = LOMPC_OK;
+  for (int k = 0; k < n_runs && rc == LOMPC_OK; ++k) {
+    if (profile_every > 0) p->prof = (k % profile_every == 0) ? mask : 0;  // sampled runs carry the events
+    rc = lq_plan_launch(p, lmbd + (size_t)k * lmbd_stride, lmbd_r + (size_t)k * lmbd_r_stride, w, cost, w0, status,
+                        set_sum_w, set_stats, (hipStream_t)stream, nullptr);
+  }
+  p->prof = mask;
+  return rc;
 }
 
 int lompc_plan_status(lompc_plan* p, void* stream, int64_t* n_repaired, int64_t* n_failed, int64_t* n_invalid) {

@@ -80,6 +80,7 @@ SIGNATURES = [
     ("lompc_bimpc_solve", _I, [_I, _I, _I] + [_D] * 10 + [_P] * 6 + [_D] + [_P] * 6),
     ("lompc_plan_create", _I, [_I, _P, _P, _L, _P, _P, _P, _I, _P, ctypes.POINTER(_P)]),
     ("lompc_plan_run", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    ("lompc_plan_run_steps", _I, [_P, _P, _L, _P, _L, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_plan_status", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_get_info", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_update", _I, [_P, _L, _P, _P, _P, _P]),

@@ -497,6 +497,21 @@ class BatchPlan:
             self._check_rc(rc)
         return self.out
 
+    def run_steps(self, lmbd, lmbd_r, n_runs: int, lmbd_stride: int, lmbd_r_stride: int = 0,
+                  profile_every: int = 0) -> dict:
+        """n_runs consecutive runs in ONE C-ABI call (lompc_plan_run_steps): run k at the prices
+        lmbd + k lmbd_stride, lmbd_r + k lmbd_r_stride (device pointers or tensors, strides in
+        doubles); profile_every > 0: only every E-th run carries the enabled HIP events."""
+        if self.direct:
+            raise ValueError("run_steps: PATH-mode plans only")
+        pl = lmbd if isinstance(lmbd, int) else lmbd.data_ptr()
+        pr = lmbd_r if isinstance(lmbd_r, int) else lmbd_r.data_ptr()
+        rc = self._lib.lompc_plan_run_steps(self._plan, pl, int(lmbd_stride), pr, int(lmbd_r_stride), int(n_runs),
+                                            int(profile_every), *self._outs, self._stream)
+        if rc:
+            self._check_rc(rc)
+        return self.out
+
     def check(self) -> tuple[int, int, int]:
         """Synchronise the plan's stream; raise on uncertified QPs; returns (repaired, failed, invalid)."""
         if self.direct:

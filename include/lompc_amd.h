@@ -204,6 +204,15 @@ int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, d
                    double* cost, double* w0, int8_t* status, double* set_sum_w,
                    double* set_stats, void* stream);
 
+/* n_runs consecutive runs (as n_runs lompc_plan_run calls) at the prices lmbd + k lmbd_stride and
+ * lmbd_r + k lmbd_r_stride (k = 0 .. n_runs - 1, strides in doubles), every run writing the same
+ * outputs; with profile_every > 0 only runs k = 0, E, 2E, ... carry the enabled profiling events.
+ * One C-ABI call for a sequence of independent batches (a benchmark's timed steps). */
+int lompc_plan_run_steps(lompc_plan* plan, const double* lmbd, int64_t lmbd_stride,
+                         const double* lmbd_r, int64_t lmbd_r_stride, int n_runs,
+                         int profile_every, double* w, double* cost, double* w0, int8_t* status,
+                         double* set_sum_w, double* set_stats, void* stream);
+
 /* Synchronise ``stream``; counters of the plan's last run (as lompc_last_status). */
 int lompc_plan_status(lompc_plan* plan, void* stream, int64_t* n_repaired,
                       int64_t* n_failed, int64_t* n_invalid);

@@ -382,3 +382,33 @@ def test_reductions_only_runs_close_in_eval(gpu):
         assert torch.equal(a["cost"], b["cost"])
         for k in ("set_sum_w", "set_stats"):
             np.testing.assert_allclose(a[k].cpu().numpy(), b[k].cpu().numpy(), rtol=1e-12, atol=1e-12, err_msg=k)
+
+
+def test_run_steps_matches_single_runs(gpu):
+    """lompc_plan_run_steps (K runs in one C-ABI call, the benchmark's timed steps) writes the
+    same outputs as K lompc_plan_run calls at the same prices, and carries the HIP events on
+    every E-th run only."""
+    N, P, K, E = 24, 4, 7, 3
+    rng = np.random.default_rng(9)
+    cs = [O.small_consts(), O.large_consts()]
+    lompcs = [LoMPC(N, LoMPCConstants(c.delta, c.theta, c.y_max, c.w_max, c.ev_type), device=0) for c in cs]
+    M = [6000, 5000]
+    off1 = [np.array([(m * p) // P for p in range(P + 1)], dtype=np.int64) for m in M]
+    off = np.concatenate([off1[0], M[0] + off1[1][1:]])
+    g = torch.as_tensor(np.concatenate([c.y_max - (0.3 + 0.2 * rng.random(m)) for c, m in zip(cs, M)]), device="cuda:0")
+    lm = torch.as_tensor(np.stack([np.concatenate([c.theta * rng.random((P, 3 * N)) for c in cs]) for _ in range(K)]),
+                         device="cuda:0")
+    lr = torch.as_tensor(0.05 * rng.random((K, 2 * P)), device="cuda:0")
+    ref = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], want_status=True)
+    for k in range(K):
+        ref.run(lm[k], lr[k])
+    assert ref.check()[1:] == (0, 0)
+    plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], want_status=True)
+    plan.profile(enable=("k_eval",))
+    plan.profile(read=True, reset=True)
+    out = plan.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), profile_every=E)
+    assert plan.check()[1:] == (0, 0)
+    for key in ("w", "cost", "status", "set_sum_w", "set_stats"):
+        assert torch.equal(out[key], ref.out[key]), key
+    ms, n = plan.profile(read=True)
+    assert n == (K + E - 1) // E and ms > 0.0

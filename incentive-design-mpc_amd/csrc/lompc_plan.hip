@@ -794,6 +794,8 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
 #pragma unroll
   for (int h = 0; h < EVAL_PASSES; ++h) {
     const int i = start + tid + EVAL_EVS * h;
+    // a wave without EVs in this pass skips it (wave-uniform; its rows are never read)
+    if (h > 0 && start + EVAL_EVS * h + 64 * wv >= end) break;
     const bool act = i < end;
     const double g = gh[h];
     const bool valid = act && g >= 0.0 && g <= ym;

@@ -246,7 +246,7 @@ __device__ __forceinline__ void load_set(const QPConst& q, const double* __restr
 // to the cell's fixed slots with write-through stores (visible to any XCD once they complete).
 // NT: the horizon as a compile-time constant (0: a.N at run time) — the scans' row / bank steps
 // become straight-line code, so independent chains can be interleaved
-template <int NT = 0>
+template <int NT = 0, bool INIT_TAB = false>
 __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
   const int G = a.G;
   const int s = __builtin_amdgcn_readfirstlane(blk / G);
@@ -263,6 +263,7 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
   double l2;
   bool bad;
   load_set(q, L, lr, N, lane, ws, l2, bad);
+  if (INIT_TAB) lq_tab_init(q);  // (after the price loads are issued: the barrier overlaps them)
   if (bad || (lane == 0 && !(lr >= 0.0))) atomicOr(a.errflag, 1);
   const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);  // lompc.py:128
   const double kappa = lr / q.delta;                            // price_solver.py:191
@@ -418,10 +419,7 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
 
 template <int NT>
 __global__ __launch_bounds__(64) void k_path(PathArgs a) {
-  const int blk = (int)blockIdx.x;
-  const int s = __builtin_amdgcn_readfirstlane(blk / a.G);
-  lq_tab_init(set_consts(a.qd, a.ce, s));
-  path_cell<NT>(a, blk);
+  path_cell<NT, true>(a, (int)blockIdx.x);
 }
 
 typedef void (*PathKernel)(PathArgs);
@@ -921,6 +919,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     }
   } else {
     if (lane == 0) st_wt4(a.fail_cnt + (size_t)blk * EVAL_WAVES + wv, nlist);
+    wave_record();  // (the scalar totals are final here: their DPP scans run before the rows)
     __builtin_amdgcn_wave_barrier();  // this wave's own rows in LDS: in order
   }
   LQ_STAMPE(2);
@@ -1063,7 +1062,6 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
         if (V == 2) s_accw[wv][V * lane + 1] = s1;
       }
     }
-    wave_record();
     __syncthreads();
     if (tid < 64) store_record(tid, 64);
   }

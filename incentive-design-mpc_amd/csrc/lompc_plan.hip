@@ -61,6 +61,9 @@ __device__ long long g_stamps[65536 * 8];
 #ifndef EVAL_WAVES
 #define EVAL_WAVES 8  // k_eval: waves per workgroup (16: 16.1 us, 8: 14.8 us, 4: 16.2 us at config 3)
 #endif
+#ifndef EVAL_RU
+#define EVAL_RU 4  // k_eval: row store instructions per software-pipelined batch
+#endif
 #define EVAL_MIN_WAVES ((2 * EVAL_WAVES + 3) / 4)  // k_eval: waves per SIMD for two workgroups per CU
 #define EVAL_EVS (64 * EVAL_WAVES)         // k_eval: threads per workgroup
 #define EVAL_PASSES 2                      // k_eval: EVs per thread, at most
@@ -931,7 +934,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   const int rr = lane / Lr, col = lane - rr * Lr;
   const bool rlane = rr < R;
   const int t0 = V * col;
-  constexpr int RU = 4;  // row instructions per batch: their LDS reads in flight together
+  constexpr int RU = EVAL_RU;  // row instructions per batch: their LDS reads in flight together
   double acc0 = 0.0, acc1 = 0.0;
   // a segment of the block's rows r0b .. r0b + nrows - 1 (EVs start + r, contiguous in w): every
   // row is a plain piece lookup (re-solved and invalid EVs read a zero piece), so the loop has

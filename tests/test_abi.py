@@ -54,7 +54,8 @@ def test_header_constants_match_python():
     for name in ("LOMPC_OK", "LOMPC_ERR_INVALID_ARG", "LOMPC_ERR_NOT_CONVERGED", "LOMPC_QP_REPAIRED",
                  "LOMPC_STAT_MAX_ERR", "LOMPC_SET_STATS", "LOMPC_MAX_N", "LOMPC_MODE_DIRECT", "LOMPC_PLAN_MAX_CTX",
                  "LOMPC_PLAN_WARM_START", "LOMPC_ABI_VERSION", "LOMPC_PLAN_K_PATH", "LOMPC_PLAN_K_EVAL",
-                 "LOMPC_PLAN_K_FINAL", "LOMPC_PLAN_KERNELS"):
+                 "LOMPC_PLAN_K_FINAL", "LOMPC_PLAN_KERNELS", "LOMPC_PLAN_DIAG_REPAIR", "LOMPC_PLAN_FUSED",
+                 "LOMPC_PLAN_CLOSE_IN_EVAL"):
         m = re.search(rf"#define {name}\s+(\d+)", src)
         attr = "ABI_VERSION" if name == "LOMPC_ABI_VERSION" else name
         assert m and int(m.group(1)) == getattr(_lib, attr), name

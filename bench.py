@@ -72,13 +72,21 @@ def parse():
                     help="diagnostics: issue each timed step from Python (one lompc_plan_run per step)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-station", action="store_true", help="skip the BiMPC steps/sec leg")
-    ap.add_argument("--station-evs-per-gpu", type=int, default=262144, help="EVs per GPU, half per type")
+    ap.add_argument("--station-evs-per-gpu", type=int, default=2097152,
+                    help="EVs per GPU, half per type (default: config 5's 2 097 152 on one GPU)")
     ap.add_argument("--station-horizon", type=int, default=48)
     ap.add_argument("--station-steps", type=int, default=20)
     ap.add_argument("--station-warmup", type=int, default=3)
     ap.add_argument("--no-direct", action="store_true", help="skip the DIRECT-mode comparison leg")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (the product path); gloo only to rehearse world > 1 on one GPU")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="the sharded (N > 1) code path on one rank: a world-size-1 nccl group, every step's set "
+                         "reductions all-gathered by the extension's RCCL communicator and combined on the device")
+    ap.add_argument("--no-contracts", action="store_true",
+                    help="skip the reductions-only / w0-only contract legs (the reference's _get_w_err / get_w0_price0)")
+    ap.add_argument("--station-prof-steps", type=int, default=4,
+                    help="extra station steps with the price loops' per-part timing (after the timed steps)")
     return ap.parse_args()
 
 
@@ -90,9 +98,12 @@ def main():
     from lompc_amd import BatchPlan, LoMPC, LoMPCConstants, _lib
     from lompc_amd.dist import combine_set_results
 
+    from lompc_amd.dist import device_comm, release_comms
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    sharded = world > 1 or args.force_dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # one rank per GPU; with fewer GPUs than ranks (a gloo rehearsal on one card) ranks share
@@ -105,6 +116,18 @@ def main():
             dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
+        if args.force_dist:  # the N > 1 code path with one rank (RCCL allows one rank per device)
+            import socket
+
+            so = socket.socket()
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+            so.close()
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                        device_id=torch.device("cuda:0"))
+            else:
+                dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     dev = torch.device(f"cuda:{torch.cuda.current_device()}")
 
     N, P = args.horizon, args.partitions
@@ -163,9 +186,15 @@ def main():
     torch.cuda.synchronize()
 
     multi = len(runs) > 1
+    # sharded on RCCL: the plan carries the extension's communicator, so every run all-gathers and
+    # combines the set reductions on the device inside the same C-ABI call (no Python per step)
+    comm = device_comm(dist.group.WORLD, dev.index) if sharded and args.mode == "path" and not multi else None
+    if comm is not None:
+        runs[0]["plan"].set_comm(comm)
+    py_combine = sharded and comm is None  # gloo rehearsal / split plans: torch.distributed per step
 
     def step(k):
-        if world > 1 or multi:  # the previous step's collective reads the output buffers
+        if py_combine or multi:  # the previous step's collective reads the output buffers
             for r in runs:
                 r["stream"].wait_stream(main)
         for r in runs:
@@ -173,7 +202,7 @@ def main():
         if multi:
             for r in runs:
                 main.wait_stream(r["stream"])
-        if world > 1:
+        if py_combine:
             # every set's reductions (both EV types) in ONE collective
             combine_set_results([(r["plan"].out["set_sum_w"], r["plan"].out["set_stats"]) for r in runs])
 
@@ -181,7 +210,7 @@ def main():
     for k in range(args.warmup):
         step(k)
     for r in runs:
-        rep, fail, inv = r["plan"].check()
+        rep, fail, inv = r["plan"].check()  # (sticky tallies: every warmup step)
         assert fail == 0 and inv == 0, (fail, inv)
     for r in runs:
         r["plan"].profile(enable=("k_eval",) if not args.no_kernel_events else False)
@@ -190,10 +219,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     ev_every = max(1, args.event_every)
-    # one rank, one plan: the K timed steps are issued by ONE C-ABI call (lompc_plan_run_steps:
-    # the same three launches per step at that step's prices, the HIP events on every E-th
-    # step's k_eval), so host issue stays far below the GPU time even on a slow host CPU
-    batched = world == 1 and len(runs) == 1 and "lm_stride" in runs[0] and not args.per_step_issue
+    # one plan: the K timed steps are issued by ONE C-ABI call (lompc_plan_run_steps: the same
+    # launches per step at that step's prices — plus the RCCL all-gather and the combine kernel
+    # when sharded — the HIP events on every E-th step's k_eval), so host issue stays far below
+    # the GPU time even on a slow host CPU
+    batched = len(runs) == 1 and "lm_stride" in runs[0] and not args.per_step_issue and not py_combine
     t0 = time.perf_counter()
     if batched:
         r = runs[0]
@@ -217,8 +247,8 @@ def main():
         dt = float(t.item())
     repaired = 0
     for r in runs:
-        rep, fail, inv = r["plan"].check()
-        assert fail == 0 and inv == 0
+        rep, fail, inv = r["plan"].check()  # sticky device tallies: EVERY timed step's QPs
+        assert fail == 0 and inv == 0, (fail, inv)
         repaired += rep
     # the per-EV kernel's timing over the timed region: HIP events on its own dispatches
     k_ms, k_n, k_qps = 0.0, 0, 0
@@ -258,11 +288,16 @@ def main():
             "mode": args.mode,
             "outputs": args.outputs,
             "warm_start": bool(args.warm),
-            "parallelism": f"dp{world} (EV shards, one RCCL all-gather of both types' per-set reductions per step)",
+            "parallelism": (f"dp{world} (EV shards; per step ONE RCCL all-gather of both types' per-set "
+                            "reductions + a rank-ordered combine kernel, issued inside the C-ABI run)"
+                            if comm is not None else (f"dp{world} (EV shards, torch.distributed all-gather per step)"
+                                                      if sharded else "dp1")),
+            "sharded_code_path": bool(sharded),
+            "dist_backend": (args.dist_backend if sharded else None),
             "launches_per_step": sum(r["plan"].launches_per_run() for r in runs),
             "kernel_events": "none" if args.no_kernel_events else f"k_eval, 1 in {ev_every} timed steps",
-            "issue": "per-step lompc_plan_run" if (world > 1 or args.per_step_issue or args.mode != "path" or args.split_types)
-                     else "one lompc_plan_run_steps call for the K timed steps",
+            "issue": "one lompc_plan_run_steps call for the K timed steps" if batched else "per-step lompc_plan_run",
+            "correctness_gate": "sticky device tallies: no failed / invalid QP in any warmup or timed step",
         },
         "roofline": {
             "bound": "hbm",
@@ -285,16 +320,19 @@ def main():
         line["roofline"]["traffic_source"] = pmc["source"]
     if path and world == 1 and len(runs) == 1:
         line["kernels"] = kernel_breakdown(runs[0], step, args, nsteps, pmc, torch)
+    if path and world == 1 and not multi and not args.no_contracts:
+        line["contracts"] = contract_legs(eng, runs[0], N, P, args, nsteps, dev, torch, comm, pmc)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(eng, N, args.cpu_seconds, args.seed)
     if path and world == 1 and not args.no_direct:
         line["direct_mode"] = direct_leg(eng, N, P, args, nsteps, dev, torch)
     if not args.no_station:
         del eng, runs
-        line["bimpc"] = station_leg(args, world, dev)
+        line["bimpc"] = station_leg(args, world, dev, sharded)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if sharded:
+        release_comms()
         dist.destroy_process_group()
     if "error" in line.get("bimpc", {}):
         sys.exit(1)  # the QP/s line is printed; a failed station leg still fails the run
@@ -381,7 +419,61 @@ def direct_leg(eng, N, P, args, nsteps, dev, torch):
     return {"value": B * n / dt, "unit": "QP/s", "ms_per_step": dt / n * 1e3, "steps": n, "repaired_qps": rep}
 
 
-def station_leg(args, world, dev):
+def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
+    """The per-iteration contracts the reference actually runs on the same batch (both EV types,
+    2P sets, fresh prices every step), each K steps in one lompc_plan_run_steps call:
+
+    * ``reductions`` — PriceSolver._get_w_err (price_solver.py:196-214): only the per-set sums of
+      w, the max A_bar error and the counts leave the engine (the reference drops w0, :206);
+      algorithmic HBM bytes = gamma in = 8 B per QP; the sets close inside k_eval (2 launches);
+    * ``w0`` — get_w0_price0 (price_solver.py:272-285): w0 per EV out + price0 sums: 16 B per QP.
+
+    Each reports QP/s, ms per step and k_eval's HIP-event launch time with its HBM roofline at
+    that contract's bytes (latency-bound: 8-16 B per QP is far below what one launch can move)."""
+    from lompc_amd import BatchPlan
+
+    base = run["plan"]
+    out = {}
+    lm_ptr, lr_ptr, stride = run["lm_ptr"], run["lr_ptr"], run["lm_stride"]
+    K = args.steps
+    for name, kw, bpq in (("reductions", dict(want_w=False, want_cost=False), 8),
+                          ("w0", dict(want_w=False, want_cost=False, want_w0=True), 16)):
+        plan = BatchPlan(base.lompcs, base.gamma, base.off, sets_per_ctx=base.sets_per_ctx, w_ref=base.w_ref,
+                         want_set=True, stream=torch.cuda.current_stream(), warm_start=args.warm, **kw)
+        if comm is not None:
+            plan.set_comm(comm)
+        plan.run_steps(lm_ptr[0], lr_ptr, args.warmup, stride, 0)
+        assert plan.check()[1:] == (0, 0)
+        plan.profile(enable=("k_path", "k_eval", "k_finalize"))
+        for k in ("k_path", "k_eval", "k_finalize"):
+            plan.profile(read=True, reset=True, kernel=k)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        plan.run_steps(lm_ptr[args.warmup], lr_ptr, K, stride, 0, profile_every=args.event_every)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        rep, fail, inv = plan.check()
+        assert fail == 0 and inv == 0, (name, fail, inv)
+        ms_e, n_e = plan.profile(read=True, kernel="k_eval")
+        ms_p, n_p = plan.profile(read=True, kernel="k_path")
+        ms_f, n_f = plan.profile(read=True, kernel="k_finalize")
+        B = plan.B
+        ev_us = ms_e / max(n_e, 1) * 1e3
+        gbs = bpq * B / (ev_us * 1e-6) / 1e9 if n_e else 0.0
+        out[name] = {"value": B * K / dt, "unit": "QP/s", "ms_per_step": dt / K * 1e3, "steps": K,
+                     "launches_per_step": plan.launches_per_run(), "repaired_qps": rep,
+                     "k_path_avg_us": ms_p / max(n_p, 1) * 1e3, "k_eval_avg_us": ev_us,
+                     "k_finalize_avg_us": (ms_f / n_f * 1e3) if n_f else None,
+                     "roofline": {"bound": "hbm", "kernel": "k_eval (sets closed in the launch)", "bytes_per_qp": bpq,
+                                  "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                                  "note": "latency-bound: the staging round, the lookup and the set closing, not "
+                                          "bytes, set the launch time"}}
+        plan.profile(enable=False)
+        del plan
+    return out
+
+
+def station_leg(args, world, dev, sharded=False):
     """BiMPC steps/sec (the second half of BASELINE.json's metric; config 5 weak-scaled).
 
     One step = ``ChargingStation._step`` (charging_station.py:156-185) on the engine: partition
@@ -407,12 +499,21 @@ def station_leg(args, world, dev):
     # horizon 48 the example's 0.3 / 0.3 makes the first BiMPC infeasible (example.station_consts)
     consts = station_consts(steps + warm, M_2, n_lo=N, n_bi=N, partitions=P, price_type="linear-convex",
                             demand_scale=DEMAND_SCALE * M_2 / NUM_EVS_PER_EV_TYPE, u_b_max=0.5, x_max=0.5)
-    group = dist.group.WORLD if world > 1 else None
+    group = dist.group.WORLD if sharded else None
+    is_c5 = 2 * M_2 == 2097152 and N == 48 and P == 12
     out = {"metric": "BiMPC steps/sec", "unit": "steps/s", "steps": steps, "warmup": warm,
-           "config": {"workload": f"config5 shape: {2 * M_2} EVs ({args.station_evs_per_gpu} per GPU), horizon {N}, "
-                                  f"{P} partitions per type, linear-convex prices, regularizer on, storage "
-                                  "u_b_max = x_max = 0.5, full closed-loop step",
-                      "evs_total": 2 * M_2, "horizon": N, "partitions": P}}
+           "config": {"workload": (f"{'config5' if is_c5 else 'config5 shape'}: {2 * M_2} EVs "
+                                   f"({args.station_evs_per_gpu} per GPU), horizon {N}, {P} partitions per type, "
+                                   "linear-convex prices, regularizer on, full closed-loop step"),
+                      "evs_total": 2 * M_2, "evs_per_gpu": args.station_evs_per_gpu, "horizon_lompc": N,
+                      "horizon_bimpc": N, "partitions": P, "price_type": "linear-convex",
+                      "bimpc_cost": "EXP_UNWEIGHTED, exp_rate 5", "demand_scale": f"DEMAND_SCALE * {M_2} / 500",
+                      "storage": {"u_b_max": 0.5, "x_max": 0.5,
+                                  "why": "the example lists x_max in {0.3, 0.5} and u_b_max in {0.15, 0.3} "
+                                         "(real_time_price_control.py:45-46); at horizon 48 the first BiMPC from an "
+                                         "empty battery needs u_b_max >= 2 d_e ~ 0.37 (beta = 0.183), so 0.3 is "
+                                         "infeasible and u_b_max = 0.5 is used"},
+                      "sharded_code_path": bool(sharded)}}
     try:
         np.random.seed(args.seed)  # the reference's legacy global stream (charging_station.py:95-100)
         st = ChargingStation(consts, device=dev.index, group=group)
@@ -446,6 +547,7 @@ def station_leg(args, world, dev):
         ncalls = calls() - c0
         ms = np.asarray(per_step) * 1e3
         info = st.bimpc.last_info or {}
+        loop = price_loop_breakdown(st, args.station_prof_steps, consts, torch)
         out.update({"value": steps / dt, "ms_per_step": dt / steps * 1e3,
                     "ms_per_step_median": float(np.median(ms)), "ms_per_step_min": float(ms.min()),
                     "ms_per_step_max": float(ms.max()),
@@ -456,10 +558,49 @@ def station_leg(args, world, dev):
                                "bimpc_iterations_last": info.get("iterations"),
                                "bimpc_primal_residual_last": info.get("primal_residual"),
                                "bimpc_dual_residual_last": info.get("dual_residual"),
-                               "evs_per_type_counted": int(stats["Mp_s"][:, warm + steps - 1].sum())}})
+                               "evs_per_type_counted": int(stats["Mp_s"][:, warm + steps - 1].sum())},
+                    "price_iteration": loop})
     except Exception as e:  # reported, never hides the QP/s line
         out["error"] = f"{type(e).__name__}: {e}"
     return out
+
+
+def price_loop_breakdown(st, n, consts, torch):
+    """Where a price iteration's time goes: ``n`` more station steps (after the timed ones) with
+    the C++ price loops' per-part timing on (lompc_price_loop_args.prof): per engine call, the host
+    time issuing the copies / launches (/ the RCCL collective), the host time blocked in the
+    stream sync, the GPU span of the call (HIP events from the H2D copy to the D2H copy), the host
+    price-gradient QP and the rest of the loop's host work.  The two EV types' loops run on two
+    host threads side by side on one rank, so their parts overlap in wall time."""
+    from lompc_amd import _lib
+
+    if n <= 0:
+        return None
+    sols = (st.price_solver_s, st.price_solver_l)
+    for s in sols:
+        s.loop_prof[:] = 0.0
+        s.profile_loops = True
+    t0 = time.perf_counter()
+    try:
+        for _ in range(n):
+            st._step()
+            torch.cuda.synchronize()
+            check_station_state(st, consts)
+    finally:
+        for s in sols:
+            s.profile_loops = False
+    wall = time.perf_counter() - t0
+    tot = sols[0].loop_prof + sols[1].loop_prof
+    calls = tot[_lib.LOMPC_LOOP_PROF_ITERS]
+    if calls <= 0:
+        return {"steps": n, "note": "no native price loop ran"}
+    per = lambda k: float(tot[k] / calls)
+    return {"steps": n, "engine_calls": int(calls), "ms_per_step": wall / n * 1e3,
+            "price_loops_ms_per_step_per_type": float(tot[_lib.LOMPC_LOOP_PROF_WALL] / n / 2e3),
+            "per_engine_call_us": {"total": per(_lib.LOMPC_LOOP_PROF_WALL), "issue": per(_lib.LOMPC_LOOP_PROF_ISSUE),
+                                   "wait_sync": per(_lib.LOMPC_LOOP_PROF_WAIT), "gpu_span": per(_lib.LOMPC_LOOP_PROF_GPU),
+                                   "host_price_qp": per(_lib.LOMPC_LOOP_PROF_STEP),
+                                   "host_other": per(_lib.LOMPC_LOOP_PROF_HOST)}}
 
 
 def check_station_state(st, consts):

@@ -91,9 +91,6 @@ struct lompc_plan {
   int G = 0;                    // gamma cells per set (k_path waves per set)
   int nblk = 0;                 // k_eval workgroups (blocks of one set's EVs)
   int n_cu = 0;
-  bool fused = false;           // k_path + k_eval as one launch (k_fused)
-  int* d_fused = nullptr;       // [1 + S] k_fused's ticket + per-set published-cell counters
-  int64_t cap_fused = 0;
   bool close = false;           // the sets' closing inside k_eval (no k_finalize launch)
   bool close_no_w = true;       // ... in runs without w output
   int* d_arrive = nullptr;      // [S] k_eval's per-set arrival counters (close mode)
@@ -125,6 +122,14 @@ struct lompc_plan {
   uint8_t* t_sl = nullptr;
   uint8_t* d_ws = nullptr;        // [S*G][64] working set at each cell start (warm start)
   int* d_errflag = nullptr;
+  unsigned long long* d_tally = nullptr;  // [3] EVs repaired / failed / invalid over every run since
+                                          // the last lompc_plan_status (sticky, read and zeroed there)
+  // cross-rank combine of the per-set reductions (lompc_plan_set_comm): the sets close into the
+  // packed send record [S][N] sums | [S][8] stats, one all-gather, one rank-ordered combine kernel
+  struct lompc_comm* comm = nullptr;
+  double* d_xsend = nullptr;      // [S (N + 8)]
+  double* d_xrecv = nullptr;      // [nranks][S (N + 8)]
+  int64_t cap_xsend = 0, cap_xrecv = 0;
   // pinned staging of the host arrays
   char* h_buf = nullptr;
   int64_t cap_h = 0;
@@ -177,3 +182,11 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
 int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
                    int8_t* status, double* set_sum_w, double* set_stats, hipStream_t st, lompc_ctx* prof_ctx);
 void lq_plan_free(lompc_plan* p);
+
+// RCCL communicator of the extension (lompc_comm.cpp; RCCL resolved at run time)
+struct lompc_comm {
+  void* nccl = nullptr;  // ncclComm_t
+  int nranks = 1, rank = 0, device = 0;
+  std::string err;
+};
+int lq_comm_allgather(lompc_comm* c, const double* send, double* recv, size_t count, hipStream_t st);

@@ -32,6 +32,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <type_traits>
@@ -496,8 +497,8 @@ __device__ __forceinline__ void wave_ev_outputs(const QPConst& q, const lqw::Wav
            q.theta * q.theta * w0 * w0 * lr;
 }
 
-// loads of the path table: plain after a kernel boundary, device-coherent (sc1, past any stale
-// L2 line of this XCD) when k_path's waves published them inside the same launch (k_fused)
+// loads of k_eval's records: plain after a kernel boundary (k_finalize), device-coherent (sc1, past
+// any stale L2 line of this XCD) when other workgroups of the same launch wrote them (close mode)
 template <bool COH>
 __device__ __forceinline__ double ld_t(const double* p) {
   if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -520,8 +521,7 @@ __device__ __forceinline__ double2 ld_t(const double2* p) {
 
 struct FinalArgs {
   int N, G, want_err;
-  int* fused_tickets;      // k_fused's counters, reset here for the next run (or null)
-  int* fused_done;
+  unsigned long long* tally;  // [3] plan-wide repaired / failed / invalid since the last status read (or null)
   int* arrive;             // [S] k_eval (close mode): arrived workgroups per set, zero between runs
   const QPConst* qd;
   CtxEnds ce;
@@ -646,9 +646,11 @@ __device__ __forceinline__ void finalize_set(const FinalArgs& r, const int s, do
     }
     __syncthreads();
   }
-  if (tid == 0 && r.fused_done) {
-    r.fused_done[s] = 0;
-    if (s == 0) r.fused_tickets[0] = 0;
+  if (tid == 0 && r.tally) {  // sticky plan-wide counters (lompc_plan_status): one atomic per nonzero count
+    const double nr = red[0][N + PX_N_REPAIRED], nf = red[0][N + PX_N_FAILED], ni = red[0][N + PX_N_INVALID];
+    if (nr > 0.0) __hip_atomic_fetch_add(r.tally + 0, (unsigned long long)nr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (nf > 0.0) __hip_atomic_fetch_add(r.tally + 1, (unsigned long long)nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ni > 0.0) __hip_atomic_fetch_add(r.tally + 2, (unsigned long long)ni, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (tid < N && r.set_sum_w) r.set_sum_w[(size_t)s * N + tid] = red[0][tid];
   if (tid < LOMPC_SET_STATS) {
@@ -675,6 +677,27 @@ __global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
   finalize_set<4, false>(r, (int)blockIdx.x, red, rep);
 }
 
+// Plans with a communicator: the all-gathered records recv[rank][S (N + 8)] of every rank combined
+// in rank order — sums, max for LOMPC_STAT_MAX_ERR — into the caller's set outputs (either may be
+// null).  Every rank runs the same arithmetic on the same bytes: the results are bitwise equal.
+__global__ __launch_bounds__(256) void k_combine(const double* __restrict__ recv, int nranks, int S, int N,
+                                                 double* set_sum_w, double* set_stats) {
+  const int SN = S * N, L = S * (N + LOMPC_SET_STATS);
+  for (int c = (int)(blockIdx.x * 256 + threadIdx.x); c < L; c += (int)(gridDim.x * 256)) {
+    const bool is_max = c >= SN && (c - SN) % LOMPC_SET_STATS == LOMPC_STAT_MAX_ERR;
+    double v = recv[c];
+    for (int k = 1; k < nranks; ++k) {
+      const double x = recv[(size_t)k * L + c];
+      v = is_max ? fmax(v, x) : v + x;
+    }
+    if (c < SN) {
+      if (set_sum_w) set_sum_w[c] = v;
+    } else if (set_stats) {
+      set_stats[c - SN] = v;
+    }
+  }
+}
+
 // One k_eval block (EVs [start, end) of one set, <= EVAL_MAXB) by the whole workgroup.
 // NT: the horizon as a compile-time constant (0: a.N at run time) — the row loop's lane map
 // (stages per lane, rows per store instruction) and its address arithmetic become constants.
@@ -685,7 +708,7 @@ __global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
 // write all the rows; the set's last arriver closes it (finalize_set) after its rows.  Rows of
 // EVs left to the individual re-solve are not written here (key ZD), the closing workgroup writes
 // them, so no two writes of a row race.
-template <bool COH, int NT = 0, bool CLOSE = false>
+template <int NT = 0, bool CLOSE = false>
 __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, const FinalArgs* fr = nullptr) {
   // dynamic LDS: [cap + 2][N] piece rows (rows cap, cap + 1: zero pieces) | [cap][8] coefficients |
   // [cap] piece ends | cells: coverage start | piece count | (CLOSE) per piece: gamma sum, EV count
@@ -742,18 +765,18 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int it = tid + EVAL_EVS * u;
-      v[u] = it < nab ? ld_t<COH>(gab + it) : make_double2(0.0, 0.0);
+      v[u] = it < nab ? ld_t<false>(gab + it) : make_double2(0.0, 0.0);
     }
 #pragma unroll
     for (int u = 0; u < UC; ++u) {
       const int it = tid + EVAL_EVS * u;
-      vc[u] = it < ncf ? ld_t<COH>(gcf + it) : (it < ncf + np ? ld_t<COH>(a.t_ge + sb + it - ncf) : 0.0);
+      vc[u] = it < ncf ? ld_t<false>(gcf + it) : (it < ncf + np ? ld_t<false>(a.t_ge + sb + it - ncf) : 0.0);
     }
     int vn = 0;
     double vl = 0.0;
     if (tid < G) {
-      vn = ld_t<COH>(a.t_cnt + cb + tid);
-      vl = ld_t<COH>(a.t_lo + cb + tid);
+      vn = ld_t<false>(a.t_cnt + cb + tid);
+      vl = ld_t<false>(a.t_lo + cb + tid);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -775,10 +798,10 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       s_pf[tid] = 0ull;
       s_pn[tid] = 0;
     }
-    for (int it = tid + EVAL_EVS * U; it < nab; it += EVAL_EVS) s_ab[it] = ld_t<COH>(gab + it);
+    for (int it = tid + EVAL_EVS * U; it < nab; it += EVAL_EVS) s_ab[it] = ld_t<false>(gab + it);
     for (int c = tid + EVAL_EVS; c < G; c += EVAL_EVS) {
-      s_cnt[c] = ld_t<COH>(a.t_cnt + cb + c);
-      s_lo[c] = ld_t<COH>(a.t_lo + cb + c);
+      s_cnt[c] = ld_t<false>(a.t_cnt + cb + c);
+      s_lo[c] = ld_t<false>(a.t_lo + cb + c);
     }
   }
   lq_tab_init(q);  // (its barrier publishes the staged table)
@@ -1089,7 +1112,7 @@ __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_eval(EvalArgs a, F
       return;
     }
   }
-  eval_block<false, NT, CLOSE>(a, b, &r);
+  eval_block<NT, CLOSE>(a, b, &r);
 }
 
 // k_eval for horizon N: exact-N instantiations for the shipped horizons, run-time N otherwise
@@ -1104,66 +1127,6 @@ EvalKernel eval_kernel(int N) {
     default: return k_eval<CLOSE, 0>;
   }
 }
-
-// ---------------------------------------------------------------- k_fused
-// k_path and k_eval in ONE launch (plan option): grid = the k_eval blocks.  Phase A: every
-// workgroup takes path tickets (EVAL_WAVES consecutive cells of one set, one wave each) until
-// none are left, and publishes each cell (write-through stores, then a per-set count).  Phase B:
-// the workgroup evaluates its own block once its set's G cells are counted, reading the path
-// table with device-coherent loads.  A workgroup only ever waits for cells claimed by running
-// workgroups (it reaches phase B after the ticket counter ran out), so the launch cannot
-// deadlock whatever the dispatch order; the bounded spin is a guard, never expected to fire.
-// The early sets' evaluation overlaps the late sets' paths, and one launch boundary goes.
-struct FusedArgs {
-  int* tickets;   // [1] path tickets taken (k_finalize resets it)
-  int* set_done;  // [S] published cells per set (k_finalize resets them)
-  int* errflag;   // |= 2 if a workgroup gave up waiting
-  int n_tickets;  // S * G / EVAL_WAVES
-  int nblk;
-  int spin_max;
-};
-
-__global__ __launch_bounds__(EVAL_EVS) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_fused(PathArgs pa, EvalArgs ea, FusedArgs f) {
-  __shared__ int s_tk;
-  const int tid = (int)threadIdx.x, wv = tid >> 6;
-  for (;;) {  // phase A
-    if (tid == 0) s_tk = atomicAdd(f.tickets, 1);
-    __syncthreads();
-    const int t = s_tk;
-    __syncthreads();
-    if (t >= f.n_tickets) break;
-    const int c0 = t * EVAL_WAVES;
-    const int s = __builtin_amdgcn_readfirstlane(c0 / pa.G);
-    lq_tab_init(set_consts(pa.qd, pa.ce, s));
-    path_cell(pa, c0 + wv);
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's write-through stores have completed
-    if ((tid & 63) == 0) __hip_atomic_fetch_add(f.set_done + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();  // (the box table is rewritten by the next ticket)
-  }
-  const int b = (int)blockIdx.x;  // phase B
-  if (b >= f.nblk) return;
-  const int4 info = ea.blk[b];
-  if (tid == 0) {
-    int n = 0;
-    while (__hip_atomic_load(f.set_done + info.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pa.G &&
-           n < f.spin_max) {
-      __builtin_amdgcn_s_sleep(2);
-      ++n;
-    }
-    s_tk = n < f.spin_max;
-  }
-  __syncthreads();
-  if (s_tk) {
-    eval_block<true>(ea, b);
-  } else {  // guard: the block's EVs reported failed, the run flagged
-    const int W = ea.N + NPX;
-    double* part = ea.partial + (size_t)b * W;
-    if (tid < W) part[tid] = tid == ea.N + PX_N_FAILED ? (double)(info.z - info.y) : 0.0;
-    if (tid < EVAL_WAVES) ea.fail_cnt[(size_t)b * EVAL_WAVES + tid] = 0;
-    if (tid == 0) atomicOr(f.errflag, 2);
-  }
-}
-
 
 // ---------------------------------------------------------------- k_finalize
 
@@ -1325,23 +1288,18 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     fresh_ws = true;
   }
   if (warm && (fresh_ws || p->G != G || p->S != S)) HIPCHK(p, hipMemsetAsync(p->d_ws, 1, (size_t)ncell * 64, st));
-  // k_fused (k_path + k_eval in one launch): its ticket and per-set counters, zero between runs
-  if (S + 1 > p->cap_fused) {
-    if ((rc = grow(p, &p->d_fused, S + 1))) return rc;
-    HIPCHK(p, hipMemsetAsync(p->d_fused, 0, (S + 1) * sizeof(int), st));
-    p->cap_fused = S + 1;
+  if (!p->d_tally) {
+    if ((rc = grow(p, &p->d_tally, 3))) return rc;
+    HIPCHK(p, hipMemsetAsync(p->d_tally, 0, 3 * sizeof(unsigned long long), st));
   }
   {
-    const char* env = getenv("LOMPC_FUSED");  // diagnostics: force the split / fused launches
-    const bool want = env ? atoi(env) != 0 : (flags & LOMPC_PLAN_FUSED) != 0;
-    p->fused = want && G % EVAL_WAVES == 0;
     // the sets close inside k_eval when the plan asks for it, and by default in runs that write
     // no w rows (a price loop's reductions-only runs): nothing then makes the arriving
     // workgroups wait for row stores, and the k_finalize launch and its boundary go
     // (LOMPC_CLOSE: 1 = always, 0 = never, diagnostics)
     const char* ce = getenv("LOMPC_CLOSE");
-    p->close = !p->fused && (ce ? atoi(ce) == 1 : (flags & LOMPC_PLAN_CLOSE_IN_EVAL) != 0);
-    p->close_no_w = !p->fused && (ce ? atoi(ce) == 1 : true);
+    p->close = ce ? atoi(ce) == 1 : (flags & LOMPC_PLAN_CLOSE_IN_EVAL) != 0;
+    p->close_no_w = ce ? atoi(ce) == 1 : true;
   }
   p->B = B;
   p->S = S;
@@ -1470,16 +1428,28 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   r.cost = cost;
   r.w0 = w0;
   r.status = status;
-  r.set_sum_w = set_sum_w;
-  r.set_stats = set_stats;
+  // with a communicator the sets close into the packed send record [S][N] | [S][8]
+  const bool xr = p->comm != nullptr;
+  if (xr) {
+    const int64_t L = p->S * (N + LOMPC_SET_STATS);
+    int rc;
+    if (L > p->cap_xsend) {
+      if ((rc = grow(p, &p->d_xsend, L))) return rc;
+      p->cap_xsend = L;
+    }
+    if (L * p->comm->nranks > p->cap_xrecv) {
+      if ((rc = grow(p, &p->d_xrecv, L * p->comm->nranks))) return rc;
+      p->cap_xrecv = L * p->comm->nranks;
+    }
+  }
+  r.set_sum_w = xr ? p->d_xsend : set_sum_w;
+  r.set_stats = xr ? p->d_xsend + p->S * N : set_stats;
   r.stats = p->d_stats;
-  r.fused_tickets = p->d_fused;
-  r.fused_done = p->d_fused ? p->d_fused + 1 : nullptr;
+  r.tally = p->d_tally;
   r.arrive = p->d_arrive;
-  const bool close = (p->close || (p->close_no_w && !w)) && !p->fused && p->nblk > 0;
+  const bool close = (p->close || (p->close_no_w && !w)) && p->nblk > 0;
   const bool cprof = prof_ctx && prof_ctx->prof;  // lompc_solve_batch: the context's k_eval timing
-  const bool fused = p->fused && p->nblk > 0;
-  if (!fused) {
+  {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
     hipExtLaunchKernelGGL(path_kernel(N), dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa);
@@ -1490,10 +1460,7 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (cprof ? take_events(prof_ctx->prof_pool, &e0, &e1) : plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1))
       return fail_arg(p, "profiling events");
-    if (fused) {  // k_path + k_eval in one launch (timed as k_eval)
-      FusedArgs f{p->d_fused, p->d_fused + 1, p->d_errflag, (int)(p->S * p->G / EVAL_WAVES), p->nblk, 1 << 24};
-      hipExtLaunchKernelGGL(k_fused, dim3((unsigned)p->nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, pa, a, f);
-    } else if (close) {  // + one workgroup for the sets without EVs
+    if (close) {  // + one workgroup for the sets without EVs
       hipExtLaunchKernelGGL(eval_kernel<true>(N), dim3((unsigned)(p->nblk + (p->n_empty > 0 ? 1 : 0))), dim3(EVAL_EVS), lds, st,
                             e0, e1, 0, a, r);
     } else {
@@ -1507,12 +1474,28 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
       plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
     }
   }
-  if (close) return LOMPC_OK;  // the sets were closed inside k_eval
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (plan_prof_begin(p, LOMPC_PLAN_K_FINAL, &e0, &e1)) return fail_arg(p, "profiling events");
-  hipExtLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, e0, e1, 0, r);
-  HIPCHK(p, hipGetLastError());
-  plan_prof_end(p, LOMPC_PLAN_K_FINAL, e0, e1);
+  if (!close) {  // (else the sets were closed inside k_eval)
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (plan_prof_begin(p, LOMPC_PLAN_K_FINAL, &e0, &e1)) return fail_arg(p, "profiling events");
+    hipExtLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, e0, e1, 0, r);
+    HIPCHK(p, hipGetLastError());
+    plan_prof_end(p, LOMPC_PLAN_K_FINAL, e0, e1);
+  }
+  if (!xr) return LOMPC_OK;
+  // every rank's record, then the rank-ordered combine into the caller's set outputs (all ranks
+  // bitwise equal)
+  const int64_t L = p->S * (N + LOMPC_SET_STATS);
+  int rc = lq_comm_allgather(p->comm, p->d_xsend, p->d_xrecv, (size_t)L, st);
+  if (rc) {
+    p->err = p->comm->err;
+    return rc;
+  }
+  if (set_sum_w || set_stats) {
+    const unsigned nb = (unsigned)std::min<int64_t>((L + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_combine, dim3(nb), dim3(256), 0, st, p->d_xrecv, p->comm->nranks, (int)p->S, N, set_sum_w,
+                       set_stats);
+    HIPCHK(p, hipGetLastError());
+  }
   return LOMPC_OK;
 }
 
@@ -1522,7 +1505,7 @@ void lq_plan_free(lompc_plan* p) {
   (void)hipDeviceSynchronize();
   void* ptrs[] = {p->d_meta,  p->d_stats_own, p->d_window, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
                   p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag,
-                  p->d_fail_cnt, p->d_fail_idx, p->d_fused, p->d_wacc, p->d_arrive};
+                  p->d_fail_cnt, p->d_fail_idx, p->d_tally, p->d_wacc, p->d_arrive, p->d_xsend, p->d_xrecv};
   for (void* x : ptrs)
     if (x) (void)hipFree(x);
   if (p->h_buf) (void)hipHostFree(p->h_buf);
@@ -1584,10 +1567,28 @@ int lompc_price_loop(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd
   HIPCHK(p, hipSetDevice(p->device));
   hipStream_t st = (hipStream_t)stream;
   const size_t n_in = (size_t)6 * N + 2 + 2 * N;
+  // per-part timing (args->prof): host clock for issue / wait / price step, HIP events for the
+  // GPU span of every engine call (H2D copy .. D2H copy)
+  double* prof = a->prof;
+  hipEvent_t pe[2] = {nullptr, nullptr};
+  if (prof) {
+    for (hipEvent_t& x : pe) HIPCHK(p, hipEventCreateWithFlags(&x, hipEventDefault));
+  }
+  struct EvGuard {
+    hipEvent_t* e;
+    ~EvGuard() {
+      for (int k = 0; k < 2; ++k)
+        if (e[k]) (void)hipEventDestroy(e[k]);
+    }
+  } ev_guard{pe};
+  auto now_us = []() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t_start = prof ? now_us() : 0.0;
   // one engine call at prices x: the batch errors and the central solve (price_solver.py:106/:132)
   double e[3] = {0.0, 0.0, 0.0};
   double cost_c = 0.0;
   auto iterate = [&](const double* x) -> int {
+    const double t0 = prof ? now_us() : 0.0;
+    if (prof) HIPCHK(p, hipEventRecord(pe[0], st));
     double* h = a->host_in;
     memcpy(h, x, N3 * sizeof(double));
     memcpy(h + N3, x, N3 * sizeof(double));
@@ -1603,7 +1604,21 @@ int lompc_price_loop(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd
     if (a->dev_st != a->host_st)
       HIPCHK(p, hipMemcpyAsync(a->host_st, a->dev_st, 2 * LOMPC_SET_STATS * sizeof(double), hipMemcpyDeviceToHost,
                                st));
+    double t1 = 0.0;
+    if (prof) {
+      HIPCHK(p, hipEventRecord(pe[1], st));
+      t1 = now_us();
+    }
     HIPCHK(p, hipStreamSynchronize(st));
+    if (prof) {
+      const double t2 = now_us();
+      float ms = 0.f;
+      HIPCHK(p, hipEventElapsedTime(&ms, pe[0], pe[1]));
+      prof[LOMPC_LOOP_PROF_ITERS] += 1.0;
+      prof[LOMPC_LOOP_PROF_ISSUE] += t1 - t0;
+      prof[LOMPC_LOOP_PROF_WAIT] += t2 - t1;
+      prof[LOMPC_LOOP_PROF_GPU] += 1e3 * ms;
+    }
     const double* sw = a->host_sw;
     const double* sst = a->host_st;
     for (int s = 0; s < 2; ++s) {
@@ -1643,8 +1658,10 @@ int lompc_price_loop(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd
     if ((a->tol_avg ? e[2] : e[0]) <= a->tol) break;
     double dec = 0.0;
     int qit = 0;
+    const double ts = prof ? now_us() : 0.0;
     rc = lompc_price_step(N, r, a->theta, a->w_max, a->m, a->kappa, a->eps_reg, a->w_ref, w_k, lm.data(),
                           lm_new.data(), &dec, &qit);
+    if (prof) prof[LOMPC_LOOP_PROF_STEP] += now_us() - ts;
     if (rc) {
       p->err = "price-gradient QP: no certified optimum";
       return rc;
@@ -1660,6 +1677,13 @@ int lompc_price_loop(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd
     lm = lm_new;
   }
   *iterations = it;  // steps taken (= the reference's `iter` unless the cap was hit: then max_iter)
+  if (prof) {
+    const double wall = now_us() - t_start;
+    prof[LOMPC_LOOP_PROF_WALL] += wall;
+    // the rest of the loop's host time: convergence test, A_bar metric, copies into the staging
+    prof[LOMPC_LOOP_PROF_HOST] = prof[LOMPC_LOOP_PROF_WALL] - prof[LOMPC_LOOP_PROF_ISSUE] -
+                                 prof[LOMPC_LOOP_PROF_WAIT] - prof[LOMPC_LOOP_PROF_STEP];
+  }
   memcpy(lmbd, lm.data(), N3 * sizeof(double));
   if (dual_cost) *dual_cost = dc;
   if (errs) memcpy(errs, e, sizeof(e));
@@ -1692,21 +1716,16 @@ int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
 int lompc_plan_status(lompc_plan* p, void* stream, int64_t* n_repaired, int64_t* n_failed, int64_t* n_invalid) {
   if (!p) return LOMPC_ERR_INVALID_ARG;
   HIPCHK(p, hipSetDevice(p->device));
-  std::vector<double> h((size_t)p->S * LOMPC_SET_STATS, 0.0);
+  // the sticky tallies of every run since the last call (finalize_set adds each set's counts)
+  unsigned long long h[3] = {0, 0, 0};
   int ef = 0;
-  HIPCHK(p, hipMemcpyAsync(h.data(), p->d_stats, h.size() * sizeof(double), hipMemcpyDeviceToHost,
-                           (hipStream_t)stream));
+  HIPCHK(p, hipMemcpyAsync(h, p->d_tally, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(p, hipMemcpyAsync(&ef, p->d_errflag, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(p, hipMemsetAsync(p->d_tally, 0, sizeof(h), (hipStream_t)stream));
   HIPCHK(p, hipStreamSynchronize((hipStream_t)stream));
-  double rep = 0, fail = 0, inv = 0;
-  for (int64_t s = 0; s < p->S; ++s) {
-    rep += h[s * LOMPC_SET_STATS + LOMPC_STAT_N_REPAIRED];
-    fail += h[s * LOMPC_SET_STATS + LOMPC_STAT_N_FAILED];
-    inv += h[s * LOMPC_SET_STATS + LOMPC_STAT_N_INVALID];
-  }
-  if (n_repaired) *n_repaired = (int64_t)rep;
-  if (n_failed) *n_failed = (int64_t)fail;
-  if (n_invalid) *n_invalid = (int64_t)inv;
+  if (n_repaired) *n_repaired = (int64_t)h[0];
+  if (n_failed) *n_failed = (int64_t)h[1];
+  if (n_invalid) *n_invalid = (int64_t)h[2];
   if (ef) {
     HIPCHK(p, hipMemsetAsync(p->d_errflag, 0, sizeof(int), (hipStream_t)stream));
     return fail_arg(p, "negative or NaN price parameter (lmbd >= 0, lmbd_r >= 0 required)");
@@ -1751,6 +1770,13 @@ int lompc_plan_profile_read(lompc_plan* p, int kernel, double* total_ms, int64_t
 }
 
 const char* lompc_plan_last_error(const lompc_plan* p) { return p ? p->err.c_str() : ""; }
+
+int lompc_plan_set_comm(lompc_plan* p, lompc_comm* comm) {
+  if (!p) return LOMPC_ERR_INVALID_ARG;
+  if (comm && comm->device != p->device) return fail_arg(p, "set_comm: the communicator's device differs from the plan's");
+  p->comm = comm;
+  return LOMPC_OK;
+}
 
 int lompc_plan_destroy(lompc_plan* p) {
   lq_plan_free(p);

@@ -35,7 +35,6 @@ LOMPC_PLAN_K_FINAL = 2
 LOMPC_PLAN_KERNELS = 3
 LOMPC_PLAN_WARM_START = 1
 LOMPC_PLAN_DIAG_REPAIR = 2
-LOMPC_PLAN_FUSED = 4
 LOMPC_PLAN_CLOSE_IN_EVAL = 8
 
 LOMPC_QP_OK = 0
@@ -89,12 +88,26 @@ SIGNATURES = [
     ("lompc_plan_profile_read", _I, [_P, _I, _P, _P, _I]),
     ("lompc_plan_last_error", ctypes.c_char_p, [_P]),
     ("lompc_plan_destroy", _I, [_P]),
+    ("lompc_comm_get_unique_id", _I, [_P]),
+    ("lompc_comm_create", _I, [_P, _I, _I, _I, ctypes.POINTER(_P)]),
+    ("lompc_comm_destroy", _I, [_P]),
+    ("lompc_plan_set_comm", _I, [_P, _P]),
 ]
+LOMPC_COMM_ID_BYTES = 128
+# lompc_price_loop_args.prof entries
+LOMPC_LOOP_PROF_ITERS = 0
+LOMPC_LOOP_PROF_WALL = 1
+LOMPC_LOOP_PROF_ISSUE = 2
+LOMPC_LOOP_PROF_WAIT = 3
+LOMPC_LOOP_PROF_GPU = 4
+LOMPC_LOOP_PROF_STEP = 5
+LOMPC_LOOP_PROF_HOST = 6
+LOMPC_LOOP_PROF = 8
 LOMPC_BIMPC_WEIGHTED = 0
 LOMPC_BIMPC_UNWEIGHTED = 1
 LOMPC_BIMPC_EXP_UNWEIGHTED = 2
 LOMPC_BIMPC_INFO = 5
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class PriceLoopArgs(ctypes.Structure):
@@ -105,7 +118,7 @@ class PriceLoopArgs(ctypes.Structure):
                 ("n_evs", ctypes.c_double), ("lmbd_r", ctypes.c_double),
                 ("A_bar", ctypes.c_void_p), ("w_ref", ctypes.c_void_p), ("dev_in", ctypes.c_void_p),
                 ("host_in", ctypes.c_void_p), ("dev_sw", ctypes.c_void_p), ("dev_st", ctypes.c_void_p),
-                ("host_sw", ctypes.c_void_p), ("host_st", ctypes.c_void_p)]
+                ("host_sw", ctypes.c_void_p), ("host_st", ctypes.c_void_p), ("prof", ctypes.c_void_p)]
 
 _lock = threading.Lock()
 _lib = None

@@ -10,7 +10,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(ROOT, "csrc")
 OUT = os.path.join(PKG, "liblompc_amd.so")
-SOURCES = ["lompc_kernels.hip", "lompc_plan.hip", "lompc_price.cpp", "lompc_bimpc.cpp"]
+SOURCES = ["lompc_kernels.hip", "lompc_plan.hip", "lompc_price.cpp", "lompc_bimpc.cpp", "lompc_comm.cpp"]
 DEPS = SOURCES + ["lompc_qp.hpp", "lompc_wave.hpp", "lompc_dense.hpp", "lompc_ctx.hpp",
                   os.path.join("..", "..", "include", "lompc_amd.h")]
 ARCH = os.environ.get("LOMPC_OFFLOAD_ARCH", "gfx950")
@@ -38,7 +38,7 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines: t
     tmp = out + ".tmp"
     cmd = [_hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-result"] + [f"-D{d}" for d in defines] + \
-        [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp]
+        [os.path.join(CSRC, s) for s in SOURCES] + ["-ldl", "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

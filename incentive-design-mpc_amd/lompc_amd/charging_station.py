@@ -379,11 +379,19 @@ class ChargingStation:
             if self._pool is None:
                 self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=1)
             fut = self._pool.submit(run_chain, chains[1])
-            run_chain(chains[0])
-            fut.result()
-            for chain in chains:
-                main.wait_stream(chain[1]._stream)
+            try:
+                run_chain(chains[0])
+            finally:
+                # the large chain has finished (or failed) before anything is re-raised or the next
+                # step reuses its plans and pinned buffers; the main stream then follows both chains
+                try:
+                    fut.result()
+                finally:
+                    for chain in chains:
+                        main.wait_stream(chain[1]._stream)
         else:
+            # sharded: the two chains in the reference's interleaved order on this thread — every
+            # rank must issue the plans' device collectives in the same order
             for p in range(self.P):
                 for chain in chains:
                     one(chain, p)

@@ -10,6 +10,13 @@ with ONE all-gather and a local rank-ordered sum / max (RCCL over xGMI with
 the "nccl" backend; gloo on CPU in the tests).  Payload is S * (N + 8) doubles
 per rank — a few KB — so the collective is latency-bound and one collective
 per step beats a sum plus a max all-reduce per context.
+
+On RCCL the product path does NOT go through ``combine_set_results``: ``RcclComm`` is the
+extension's own communicator, attached to a plan, and every run of the plan all-gathers and
+combines the same records on the device inside the C-ABI call (include/lompc_amd.h,
+lompc_plan_set_comm) — the sharded price loop and ``run_steps`` issue no Python per iteration.
+``combine_set_results`` is the same rank-ordered combine for backends without a device
+communicator (gloo in the CPU tests).
 """
 from __future__ import annotations
 
@@ -80,6 +87,73 @@ def combine_set_results(pairs, group=None):
         st.copy_(sums)
         st[:, _lib.LOMPC_STAT_MAX_ERR] = maxes[:, _lib.LOMPC_STAT_MAX_ERR]
         off += S * K
+
+
+class RcclComm:
+    """The extension's own RCCL communicator over the ranks of a torch.distributed group
+    (``lompc_comm_*``, include/lompc_amd.h).  Attached to a plan (``BatchPlan.set_comm``) it makes
+    every run combine the per-set reductions across ranks ON THE DEVICE (one ncclAllGather over
+    xGMI + one rank-ordered combine kernel on the run's stream), so the C++ price loop and
+    ``run_steps`` stay in C++ on a sharded batch.  The unique id is made on the group's rank 0
+    and broadcast once over torch.distributed; creation is collective over the group."""
+
+    def __init__(self, group=None, device: int | None = None):
+        import ctypes
+
+        import torch
+        import torch.distributed as dist
+
+        self._lib = _lib.load()
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.rank = dist.get_rank(group)
+        self.nranks = dist.get_world_size(group)
+        uid = (ctypes.c_ubyte * _lib.LOMPC_COMM_ID_BYTES)()
+        if self.rank == 0:
+            rc = self._lib.lompc_comm_get_unique_id(uid)
+            if rc != _lib.LOMPC_OK:
+                raise RuntimeError("lompc_comm_get_unique_id: " + _lib.status_text(self._lib, None, rc))
+        dev = f"cuda:{self.device}" if dist.get_backend(group) == "nccl" else "cpu"
+        t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device=dev)
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        raw = bytes(t.cpu().tolist())
+        uid = (ctypes.c_ubyte * _lib.LOMPC_COMM_ID_BYTES).from_buffer_copy(raw)
+        comm = ctypes.c_void_p()
+        rc = self._lib.lompc_comm_create(uid, self.nranks, self.rank, self.device, ctypes.byref(comm))
+        if rc != _lib.LOMPC_OK:
+            raise RuntimeError("lompc_comm_create: " + _lib.status_text(self._lib, None, rc))
+        self._comm = comm
+
+    @property
+    def handle(self):
+        return self._comm
+
+    def close(self) -> None:
+        if getattr(self, "_comm", None) is not None:
+            self._lib.lompc_comm_destroy(self._comm)
+            self._comm = None
+
+
+_COMMS: dict = {}
+
+
+def device_comm(group, device: int):
+    """The process's RcclComm for (group, device), created on first use (collective), or None when
+    the group does not run on RCCL (gloo: the Python fallback combines the reductions)."""
+    import torch.distributed as dist
+
+    if group is None or dist.get_backend(group) != "nccl":
+        return None
+    key = (id(group), int(device))
+    if key not in _COMMS:
+        _COMMS[key] = RcclComm(group, device)
+    return _COMMS[key]
+
+
+def release_comms() -> None:
+    """Destroy every cached communicator (before destroy_process_group)."""
+    for c in _COMMS.values():
+        c.close()
+    _COMMS.clear()
 
 
 def global_levels(y, y_max: float, group=None) -> tuple[float, float, float, int, int]:

@@ -330,19 +330,20 @@ class BatchPlan:
     later are still solved exactly, by the individual re-solve) and the outputs are allocated.
     ``run(lmbd, lmbd_r)`` then issues one ``lompc_plan_run`` with cached pointers; lmbd:
     contiguous fp64 device tensor (S, 3N), lmbd_r (S,) on the same device (or raw device
-    pointers).  No synchronisation; ``check()`` synchronises and raises on failures.
+    pointers).  No synchronisation; ``check()`` synchronises and raises on failures of ANY run
+    since the previous check (sticky device tallies).
     w_ref (S, N) is read at every run (update it in place).  ``warm_start``: every gamma
     cell's exact solve starts from the working set the previous run ended with.  ``diag_repair``
-    (diagnostics): no solution path, every EV is re-solved individually.  ``fused``: k_path and
-    k_eval as one launch (k_fused; needs cells per set divisible by 8).  ``close_in_eval``: the per-set
-    reductions and re-solves inside k_eval (each set's last-arriving workgroup) instead of the
-    k_finalize launch (measured slower: DESIGN.md §10).
+    (diagnostics): no solution path, every EV is re-solved individually.  ``close_in_eval``: the
+    per-set reductions and re-solves inside k_eval (each set's last-arriving workgroup) instead of
+    the k_finalize launch (measured slower with w rows: DESIGN.md §10).  ``set_comm(comm)``: a
+    sharded batch — every run combines the set reductions of all ranks on the device (RCCL).
     DIRECT-mode contexts fall back to ``lompc_run`` (one context only).
     """
 
     def __init__(self, lompc, gamma, set_offsets, *, sets_per_ctx=None, w_ref=None, gamma_ref=None, want_w=True,
                  want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None, validate=True,
-                 warm_start=False, diag_repair=False, fused=False, close_in_eval=False):
+                 warm_start=False, diag_repair=False, close_in_eval=False):
         torch = _torch()
         lompcs = list(lompc) if isinstance(lompc, (list, tuple)) else [lompc]
         self.lompcs = lompcs
@@ -366,6 +367,8 @@ class BatchPlan:
         self._stream = (stream if stream is not None else torch.cuda.current_stream(lo.device)).cuda_stream
         self._lib = lo._lib
         self._plan = None
+        self._broken = None
+        self.comm = None
         self.direct = any(x.mode == "direct" for x in lompcs)
         if self.direct and len(lompcs) != 1:
             raise ValueError("DIRECT mode plans hold one context")
@@ -376,7 +379,7 @@ class BatchPlan:
         ctxs = (ctypes.c_void_p * len(lompcs))(*[x._ctx.value for x in lompcs])
         plan = ctypes.c_void_p()
         flags = ((_lib.LOMPC_PLAN_WARM_START if warm_start else 0) | (_lib.LOMPC_PLAN_DIAG_REPAIR if diag_repair else 0)
-                 | (_lib.LOMPC_PLAN_FUSED if fused else 0) | (_lib.LOMPC_PLAN_CLOSE_IN_EVAL if close_in_eval else 0))
+                 | (_lib.LOMPC_PLAN_CLOSE_IN_EVAL if close_in_eval else 0))
         self._flags = flags
         rc = self._lib.lompc_plan_create(len(lompcs), ctypes.cast(ctxs, ctypes.c_void_p), self.sets_per_ctx.ctypes.data,
                                          self.B, _ptr(self.gamma), self.off.ctypes.data, _ptr(self.w_ref), flags,
@@ -428,20 +431,28 @@ class BatchPlan:
 
     def launches_per_run(self) -> int:
         """Kernel launches of one run: k_path + k_eval + k_finalize; two when the sets close inside
-        k_eval (runs without w output, LOMPC_PLAN_CLOSE_IN_EVAL, LOMPC_CLOSE=1) or with k_fused +
-        k_finalize."""
+        k_eval (runs without w output, LOMPC_PLAN_CLOSE_IN_EVAL, LOMPC_CLOSE=1); a communicator adds
+        the all-gather and the combine kernel."""
         import os
 
         if self.direct:
-            return 2
-        if self._flags & _lib.LOMPC_PLAN_FUSED:
             return 2
         env = os.environ.get("LOMPC_CLOSE")
         if env is not None:
             close = env == "1"
         else:
             close = bool(self._flags & _lib.LOMPC_PLAN_CLOSE_IN_EVAL) or not self._want["w"]
-        return 2 if close else 3
+        return (2 if close else 3) + (2 if self.comm is not None else 0)
+
+    def set_comm(self, comm) -> "BatchPlan":
+        """Attach (None: detach) a ``dist.RcclComm``: every later run combines the set reductions of
+        all ranks on the device (lompc_plan_set_comm) — collective: every rank runs the same
+        sequence of runs."""
+        if self.direct:
+            raise ValueError("set_comm: PATH-mode plans only")
+        self._check_rc(self._lib.lompc_plan_set_comm(self._plan, None if comm is None else comm.handle))
+        self.comm = comm
+        return self
 
     def info(self) -> dict:
         """Batch size, parameter sets, gamma cells per set and k_eval workgroups of the plan."""
@@ -455,13 +466,22 @@ class BatchPlan:
     def update(self, gamma, set_offsets, w_ref=None, validate=True) -> "BatchPlan":
         """Re-target the plan at a new batch with the same contexts and set counts (e.g. the
         next partition of a price loop): device buffers, events and pinned staging are reused,
-        the outputs are reallocated only when the batch size changes."""
+        the outputs are reallocated only when the batch size changes.  If the device-side update
+        fails the plan is unusable (every later run raises): the C plan may still point at the
+        previous buffers, which stay referenced."""
+        old = (self.gamma, self.w_ref, getattr(self, "out", None))
         self._layout(gamma, set_offsets, w_ref, validate)
         if not self.direct:
             rc = self._lib.lompc_plan_update(self._plan, self.B, _ptr(self.gamma), self.off.ctypes.data,
                                              _ptr(self.w_ref), self._stream)
-            self._check_rc(rc)
+            if rc != _lib.LOMPC_OK:
+                self._broken = (old, _lib.status_text(self._lib, None, rc, plan=self._plan))
+                self._check_rc(rc)
         return self
+
+    def _usable(self) -> None:
+        if getattr(self, "_broken", None):
+            raise RuntimeError(f"BatchPlan unusable after a failed update: {self._broken[1]}")
 
     def __del__(self):
         if getattr(self, "_plan", None) is not None:
@@ -485,6 +505,7 @@ class BatchPlan:
         """lmbd / lmbd_r: device tensors, or raw device pointers (int)."""
         pl = lmbd if isinstance(lmbd, int) else lmbd.data_ptr()
         pr = lmbd_r if isinstance(lmbd_r, int) else lmbd_r.data_ptr()
+        self._usable()
         if self.direct:
             lo = self.lompc
             rc = lo._lib.lompc_run(lo._ctx, self.S, pl, pr, *self._args)
@@ -504,6 +525,7 @@ class BatchPlan:
         doubles); profile_every > 0: only every E-th run carries the enabled HIP events."""
         if self.direct:
             raise ValueError("run_steps: PATH-mode plans only")
+        self._usable()
         pl = lmbd if isinstance(lmbd, int) else lmbd.data_ptr()
         pr = lmbd_r if isinstance(lmbd_r, int) else lmbd_r.data_ptr()
         rc = self._lib.lompc_plan_run_steps(self._plan, pl, int(lmbd_stride), pr, int(lmbd_r_stride), int(n_runs),

@@ -18,9 +18,13 @@ second iteration on the price term of ``dual_cost_decrease_actual`` at :136 is
 zero) so ``solver_stats`` match the reference's entry by entry.
 
 Sharded mode (``group`` given): ``set_charge_levels`` receives this rank's EVs;
-the batch statistics (min / max / mean / count, price_solver.py:73-77) and the
-fused reductions are combined with torch.distributed (RCCL on ROCm); the price
-step runs redundantly on every rank with identical inputs.
+the batch statistics (min / max / mean / count, price_solver.py:73-77) are combined with
+torch.distributed.  On RCCL the plans carry the extension's own communicator
+(``dist.device_comm``): every engine call combines the fused reductions of all ranks on the
+device, so the whole price loop stays ONE C-ABI call (``lompc_price_loop``) exactly as on a
+single rank, and every rank takes the same price steps on bitwise identical inputs.  On gloo
+(the CPU tests) the Python loop combines them with ``dist.combine_set_results``.
+DIRECT-mode plans also take the Python loop.
 """
 from __future__ import annotations
 
@@ -100,7 +104,9 @@ class PriceSolver:
         self._A_bar = None
         self._A_bar_inv = None
         self._kappa = None
-        self.native_loop = True  # the single-rank price loop in C++ (lompc_price_loop)
+        self.native_loop = True  # the price loop in C++ (lompc_price_loop) whenever the plan allows it
+        self.profile_loops = False  # accumulate the native loop's per-part times in loop_prof
+        self.loop_prof = np.zeros(_lib.LOMPC_LOOP_PROF)
         # the solver's own stream: its loop can run beside the other EV type's (charging_station)
         self._stream = torch.cuda.Stream(device=self.lompc.device)
         self.n_batched_calls = 0
@@ -186,6 +192,20 @@ class PriceSolver:
         self.gamma_sm = self.consts.y_max - y_sum / n
         self._build_plans(self.consts.y_max - y0d)
 
+    def _device_comm(self):
+        """The extension's RCCL communicator of the group (None: single rank, gloo, DIRECT mode)."""
+        if self.group is None or self.lompc.mode == "direct":
+            return None
+        from .dist import device_comm
+
+        return device_comm(self.group, self.lompc.device)
+
+    def _native_ok(self) -> bool:
+        """The whole loop in C++: a PATH plan, single rank or combined on the device."""
+        p = self._plan
+        return (self.native_loop and p is not None and not p.direct
+                and (self.group is None or p.comm is not None))
+
     def _global_levels(self, y0d):
         """Global max / min / mean / count of a sharded y0: one all-gather, one host sync."""
         from .dist import global_levels
@@ -213,6 +233,9 @@ class PriceSolver:
         if self._plan is None:
             self._plan = BatchPlan(self.lompc, self._gam, off, w_ref=self._wr2, want_w=False, want_cost=False,
                                    want_set=True, validate=False, warm_start=True)
+            comm = self._device_comm()
+            if comm is not None:
+                self._plan.set_comm(comm)
         else:
             self._plan.update(self._gam, off, w_ref=self._wr2, validate=False)
         self._w0_live = False  # the w0 plan follows lazily (get_w0_price0_device)
@@ -239,7 +262,7 @@ class PriceSolver:
         # Initialize price iterate from previous prices.
         lmbd_k, lmbd_k_new = np.zeros((3 * self.N)), np.zeros((3 * self.N))
         lmbd_k[: self.r] = self.prev_prices
-        if self.native_loop and self.group is None and PRINT_LEVEL < 2:  # the whole loop in one C-ABI call
+        if PRINT_LEVEL < 2 and self._native_ok():  # the whole loop in one C-ABI call
             return self._finish_prices(*self._native_loop(lmbd_k, lmbd_r, w_ref, A_bar, tol), lmbd_r, w_ref, A_bar,
                                        tol, w0_err_bound)
         phi_w_ref = self.lompc.phi(w_ref)
@@ -292,7 +315,8 @@ class PriceSolver:
             self.N, self.r, MAX, 1 if _settings.PRICE_SOLVER_TOL_TYPE != "max" else 0, float(self.consts.theta),
             float(self.consts.w_max), float(self.m), float(self._kappa_of(self._A_bar_inv)), float(self.eps_reg),
             float(tol), float(self.nEVs), float(lmbd_r), A_bar.ctypes.data, w_ref.ctypes.data, self._in.data_ptr(),
-            self._h_in.data_ptr(), *self._loop_outs(), self._h_sw.data_ptr(), self._h_st.data_ptr())
+            self._h_in.data_ptr(), self._plan.out["set_sum_w"].data_ptr(), self._plan.out["set_stats"].data_ptr(),
+            self._h_sw.data_ptr(), self._h_st.data_ptr(), self.loop_prof.ctypes.data if self.profile_loops else None)
         lm = np.ascontiguousarray(lmbd_k, dtype=np.float64).copy()
         w_k = np.empty(self.N)
         dec_ac, dec_pred = np.empty(MAX), np.empty(MAX)
@@ -311,16 +335,6 @@ class PriceSolver:
         n = it.value
         self.n_batched_calls += n + 1
         return lm, w_k, min(n, MAX - 1), list(dec_ac[:n]), list(dec_pred[:n])
-
-    def _loop_outs(self):
-        """Where the native loop's plan runs write the two sets' reductions: the plan's device
-        outputs, copied to the pinned buffers (LOMPC_ZERO_COPY=1: the kernels write the pinned
-        buffers directly — measured slower, 26.6 vs 15.5 ms per station step)."""
-        import os
-
-        if os.environ.get("LOMPC_ZERO_COPY", "0") == "1":
-            return self._h_sw.data_ptr(), self._h_st.data_ptr()
-        return self._plan.out["set_sum_w"].data_ptr(), self._plan.out["set_stats"].data_ptr()
 
     def _finish_prices(self, lmbd_k, w_k, iter, dual_cost_decrease_ac, dual_cost_decrease_pred, lmbd_r, w_ref,
                        A_bar, tol, w0_err_bound):
@@ -390,7 +404,7 @@ class PriceSolver:
         out = self._plan.run(self._lm2, self._lr2)
         self.n_batched_calls += 1
         sw, st = out["set_sum_w"], out["set_stats"]
-        if self.group is not None:
+        if self.group is not None and self._plan.comm is None:  # (with a comm: combined by the run)
             from .dist import allreduce_set_results
 
             allreduce_set_results(sw, st, group=self.group)

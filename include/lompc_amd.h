@@ -148,7 +148,7 @@ const char* lompc_status_string(int status);
 const char* lompc_last_error(const lompc_ctx* ctx);
 
 /* ABI version (bumped on any signature change). */
-#define LOMPC_ABI_VERSION 2
+#define LOMPC_ABI_VERSION 3
 int lompc_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -167,7 +167,6 @@ typedef struct lompc_plan lompc_plan;
                                    that change little between price iterations) */
 #define LOMPC_PLAN_DIAG_REPAIR 2 /* diagnostics: no solution path, every EV takes the individual
                                     whole-wave re-solve (status REPAIRED) */
-#define LOMPC_PLAN_FUSED 4       /* k_path and k_eval as one launch */
 #define LOMPC_PLAN_CLOSE_IN_EVAL 8 /* the per-set reductions and re-solves inside k_eval, by each
                                       set's last-arriving workgroup, instead of the k_finalize
                                       launch, also in runs that write w rows (slower there, see
@@ -213,7 +212,10 @@ int lompc_plan_run_steps(lompc_plan* plan, const double* lmbd, int64_t lmbd_stri
                          int profile_every, double* w, double* cost, double* w0, int8_t* status,
                          double* set_sum_w, double* set_stats, void* stream);
 
-/* Synchronise ``stream``; counters of the plan's last run (as lompc_last_status). */
+/* Synchronise ``stream``; EVs repaired / failed / invalid summed over EVERY run since the previous
+ * lompc_plan_status call (sticky device tallies, zeroed here), so a failure in any of the runs of a
+ * lompc_plan_run_steps call or of a price loop is seen.  These count this rank's EVs only; with a
+ * communicator attached the set_stats outputs carry the combined counts. */
 int lompc_plan_status(lompc_plan* plan, void* stream, int64_t* n_repaired,
                       int64_t* n_failed, int64_t* n_invalid);
 
@@ -234,11 +236,36 @@ int lompc_plan_profile_read(lompc_plan* plan, int kernel, double* total_ms, int6
 const char* lompc_plan_last_error(const lompc_plan* plan);
 int lompc_plan_destroy(lompc_plan* plan);
 
+/* ---------------------------------------------------------------------------
+ * Sharded batches: one process per GPU, every set's EVs split across the ranks.
+ * The only exchange of a price iteration is the per-set reduction record the price step
+ * consumes (price_solver.py:205-214: sum of w, max A_bar error; the sums of w0 / price0 / cost
+ * and the counts, charging_station.py:356-366).  A communicator attached to a plan makes every
+ * run of it combine those records across the ranks on the device: the sets close into one
+ * packed record, ONE ncclAllGather over xGMI on the run's stream, then one kernel sums the
+ * ranks' records in rank order (max for LOMPC_STAT_MAX_ERR), so every rank holds bitwise the
+ * same set_sum_w / set_stats.  Collective calls: every rank must issue the same runs in the same
+ * order.  RCCL is loaded at run time (LOMPC_ERR_UNSUPPORTED when it is absent).
+ * ------------------------------------------------------------------------- */
+typedef struct lompc_comm lompc_comm;
+#define LOMPC_COMM_ID_BYTES 128  /* sizeof(ncclUniqueId) */
+
+/* On one rank: a fresh unique id, to be broadcast to the others (e.g. over torch.distributed). */
+int lompc_comm_get_unique_id(unsigned char* id);
+/* Collective over the nranks ranks: a communicator for this rank on ``device``. */
+int lompc_comm_create(const unsigned char* id, int nranks, int rank, int device, lompc_comm** out);
+int lompc_comm_destroy(lompc_comm* comm);
+/* Attach (NULL: detach) a communicator to a plan: from the next run on, the plan's set outputs
+ * are the combined records of all ranks (also inside lompc_plan_run_steps and lompc_price_loop). */
+int lompc_plan_set_comm(lompc_plan* plan, lompc_comm* comm);
+
 /* The price loop of one (EV type, partition) on a plan holding [this partition's EVs | the
  * central QP] (PriceSolver.compute_optimal_prices, price_solver.py:106-140): repeated
  * {lompc_plan_run at lmbd_k, one D2H copy + stream sync, convergence test, lompc_price_step}
- * without returning to the caller until convergence.  Single-rank only (the sharded loop
- * combines the reductions across ranks between iterations).  Buffers:
+ * without returning to the caller until convergence.  On a sharded plan (communicator attached:
+ * this rank's share of the partition's EVs, the central QP on one rank only, n_evs the global
+ * count) every run combines the ranks' records before the copy, and every rank takes the same
+ * price steps on bitwise identical inputs.  Buffers:
  *   dev_in / host_in  [2*3N | 2 | 2N] = both sets' prices, lmbd_r, w_ref (the plan reads
  *                     dev_in; host_in is pinned staging), dev_sw [2,N] / dev_st [2,8] the
  *                     plan's set outputs, host_sw / host_st pinned copies (dev_* == host_*:
@@ -248,7 +275,16 @@ int lompc_plan_destroy(lompc_plan* plan);
  * reference's lmbd_k / lmbd_k_new aliasing: the actual decrease drops the price term after
  * the first iteration), *iterations = price steps taken (the reference's `iter` at the break;
  * max_iter when the cap was hit, where the reference's `iter` is max_iter - 1),
- * errs [3] = (w_err_max, w0_err, w_avg_err) at the final prices. */
+ * errs [3] = (w_err_max, w0_err, w_avg_err) at the final prices.
+ * prof (may be NULL): accumulates the loop's time per part, [LOMPC_LOOP_PROF] entries: */
+#define LOMPC_LOOP_PROF_ITERS  0 /* engine calls (plan runs)                                     */
+#define LOMPC_LOOP_PROF_WALL   1 /* us, host wall time of the whole loop                          */
+#define LOMPC_LOOP_PROF_ISSUE  2 /* us, host time issuing copies / launches / the collective       */
+#define LOMPC_LOOP_PROF_WAIT   3 /* us, host time blocked in the stream synchronisation           */
+#define LOMPC_LOOP_PROF_GPU    4 /* us, GPU span of each engine call (HIP events around H2D .. D2H) */
+#define LOMPC_LOOP_PROF_STEP   5 /* us, host price-gradient QP (lompc_price_step)                 */
+#define LOMPC_LOOP_PROF_HOST   6 /* us, other host work (convergence test, metric, bookkeeping)   */
+#define LOMPC_LOOP_PROF 8
 typedef struct lompc_price_loop_args {
   int N, r, max_iter, tol_avg;          /* tol_avg: 1 = PRICE_SOLVER_TOL_TYPE "avg", 0 = "max" */
   double theta, w_max, m, kappa, eps_reg, tol, n_evs, lmbd_r;
@@ -257,6 +293,7 @@ typedef struct lompc_price_loop_args {
   double* dev_in; double* host_in;
   const double* dev_sw; const double* dev_st;
   double* host_sw; double* host_st;
+  double* prof;                         /* host [LOMPC_LOOP_PROF] or NULL */
 } lompc_price_loop_args;
 int lompc_price_loop(lompc_plan* plan, const lompc_price_loop_args* args, double* lmbd, double* w_k,
                      double* dual_cost, double* dec_actual, double* dec_pred, int* iterations,

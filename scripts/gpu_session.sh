@@ -22,6 +22,9 @@ for s in $STEPS; do
     quick) run pytest_quick 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_parity.py tests/test_gpu_baseline_configs.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     testsall) run pytest_gpu_all 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
+    bdist) run bdist 600 python bench.py --force-dist --no-cpu-baseline --no-direct ;;
+    bdistq) run bdistq 300 python bench.py --force-dist --steps 100 --warmup 10 --no-cpu-baseline --no-direct --no-station ;;
+    comm) run comm 600 python -u -m pytest tests/test_gpu_comm.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench20q) run bench20q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-station ;;
     bqtag) run "bq_${TAG}" 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct ;;
@@ -40,10 +43,6 @@ for s in $STEPS; do
     sprof) run sprof 300 python scripts/station_profile.py ;;
     bimpc) run bimpc 300 python scripts/bimpc_timing.py ;;
     stampsvar) for v in ${KS_VARIANTS}; do KS_VARIANT=$v run stamps_$v 300 python scripts/kstamps.py || exit $?; done ;;
-    qfused) LOMPC_FUSED=1 run qfused 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_parity.py tests/test_gpu_baseline_configs.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    bfused) LOMPC_FUSED=1 run bfused 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct ;;
-    bfusednoev) LOMPC_FUSED=1 run bfusednoev 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct --no-kernel-events ;;
-    sprofzc) LOMPC_ZERO_COPY=1 run sprofzc 300 python scripts/station_profile.py ;;
     sproftrace) run sproftrace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/sproft -o run --output-format csv -- python scripts/station_profile.py ;;
     bcost) run bcost 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs cost ;;
     bset) run bset 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --outputs set ;;

@@ -14,7 +14,8 @@ import torch
 import lompc_oracle as O
 import oracle_c
 from conftest import oracle_consts
-from lompc_amd import LoMPC, LoMPCConstants, PriceSolverLoops, SolverError, _lib
+from lompc_amd import LoMPC, LoMPCConstants, SolverError, _lib
+from lompc_amd.price_solver import PriceSolver
 
 pytestmark = pytest.mark.gpu
 
@@ -87,13 +88,14 @@ def test_solve_lompc_single_matches_golden(gpu, golden):
             assert abs(cost - case["cost"][i]) <= TOL_C * max(1.0, abs(case["cost"][i]))
 
 
-def test_price_solver_loops_match_reference_semantics(gpu, golden):
-    """_get_w_err / get_w0_price0 (price_solver.py:196-214, 272-285)."""
+@pytest.mark.parametrize("mode", ["path", "direct"])
+def test_price_solver_loops_match_reference_semantics(gpu, golden, mode):
+    """PriceSolver._get_w_err / get_w0_price0 (price_solver.py:196-214, 272-285), both engine modes."""
     for case in golden[::5]:
         c = case
         consts = LoMPCConstants(c["delta"], c["theta"], c["y_max"], c["w_max"], c["ev_type"])
         price_type = "linear" if c["price"] == "linear" else "linear-convex"
-        ps = PriceSolverLoops(c["N"], consts, price_type, device=0)
+        ps = PriceSolver(c["N"], consts, price_type, device=0, mode=mode)
         y0 = c["y_max"] - c["gamma"]
         ps.set_charge_levels(y0)
         A_bar, _ = ps._get_w_inner_product_metric(c["lmbd_r"])

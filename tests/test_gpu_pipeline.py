@@ -269,36 +269,72 @@ def test_warm_start_and_cell_counts(gpu, ev, N):
             os.environ["LOMPC_CELLS"] = old
 
 
-def test_fused_plan_matches_split(gpu):
-    """LOMPC_PLAN_FUSED (k_path + k_eval in one launch, k_fused) gives bitwise the split
-    launches' outputs: same path and evaluation code, the path table read coherently; repeated
-    runs check that the fused counters are reset between runs."""
-    N, P = 24, 12
-    rng = np.random.default_rng(21)
-    cs = [O.small_consts(), O.large_consts()]
-    lompcs = [LoMPC(N, LoMPCConstants(c.delta, c.theta, c.y_max, c.w_max, c.ev_type), device=0) for c in cs]
-    M = [30000, 30001]
-    off1 = [np.array([(m * p) // P for p in range(P + 1)], dtype=np.int64) for m in M]
-    off = np.concatenate([off1[0], M[0] + off1[1][1:]])
-    g = torch.as_tensor(np.concatenate([c.y_max - (0.3 + 0.2 * rng.random(m)) for c, m in zip(cs, M)]), device="cuda:0")
-    wr = torch.as_tensor(np.concatenate([c.w_max * rng.random((P, N)) for c in cs]), device="cuda:0")
-    lms = [torch.as_tensor(np.concatenate([c.theta * rng.random((P, 3 * N)) for c in cs]), device="cuda:0")
-           for _ in range(3)]
-    lr = torch.zeros(2 * P, dtype=torch.float64, device="cuda:0")
-    outs = []
-    for fused in (False, True):  # both close the sets with k_finalize
-        plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], w_ref=wr, want_status=True, fused=fused)
-        assert plan.cells % 8 == 0
-        res = []
-        for lm in lms:
-            out = plan.run(lm, lr)
-            rep, fail, inv = plan.check()
-            assert fail == 0 and inv == 0
-            res.append({k: v.clone() for k, v in out.items() if v is not None})
-        outs.append(res)
-    for a, b in zip(*outs):
-        for k in a:
-            assert torch.equal(a[k], b[k]), k
+def test_status_tallies_every_run(gpu):
+    """plan.check() sees a failure in ANY run since the previous check (sticky device tallies),
+    not only the last run's: an invalid gamma in the middle one of three runs, and a negative price in
+    the middle step of one run_steps call, both fail the check after the last run (the bench's
+    correctness gate over its timed steps)."""
+    rng = np.random.default_rng(8)
+    c = O.large_consts()
+    N, S, per = 24, 4, 3000
+    off = np.arange(S + 1, dtype=np.int64) * per
+    gn = c.y_max - (0.3 + 0.2 * rng.random(S * per))
+    g = torch.as_tensor(gn, device="cuda:0")
+    lm = torch.as_tensor(c.theta * rng.random((3, S, 3 * N)), device="cuda:0")
+    lr = torch.zeros((3, S), dtype=torch.float64, device="cuda:0")
+    lompc = mk(c, N)
+    for want_w in (True, False):
+        plan = BatchPlan(lompc, g, off, want_w=want_w, validate=False)
+        plan.run(lm[0], lr[0])
+        assert plan.check() == (0, 0, 0)
+        g[per + 7] = -1.0  # run 2 of 3 sees one invalid EV
+        plan.run(lm[0], lr[0])
+        g[per + 7] = float(gn[per + 7])
+        plan.run(lm[1], lr[1])
+        with pytest.raises(AssertionError):
+            plan.check()
+        assert plan.check() == (0, 0, 0)  # read and zeroed: the next window is clean
+        bad = lm.clone()
+        bad[1, 2, 5] = -1.0  # a negative lambda_1 in the middle step of a run_steps call (H stays SPD)
+        plan.run_steps(bad, lr, 3, bad[0].numel(), lr[0].numel())
+        with pytest.raises(ValueError):
+            plan.check()
+        plan.run_steps(lm, lr, 3, lm[0].numel(), lr[0].numel())
+        assert plan.check() == (0, 0, 0)
+
+
+@pytest.mark.parametrize("ev", ["small", "large"])
+def test_close_mode_sums_at_box_bounds(gpu, ev):
+    """Runs without w close their sets inside k_eval from per-piece aggregates (n_p a + Gamma_p b,
+    unclamped); runs with w sum the clamped rows.  With EVs at and next to the box bounds
+    (gamma = 0: nothing left to charge; gamma = y_max: empty battery) the two agree to 1e-11 and
+    match the per-EV oracle sums."""
+    rng = np.random.default_rng(70 + (ev == "large"))
+    c = O.small_consts() if ev == "small" else O.large_consts()
+    N, per = 24, 2000
+    gn = np.concatenate([np.zeros(300), np.full(300, c.y_max), 1e-9 * rng.random(300),
+                         c.y_max - 1e-9 * rng.random(300), c.y_max * rng.random(per - 1200)])
+    gn = np.concatenate([gn, c.y_max * rng.random(per)])
+    off = np.array([0, per, 2 * per], dtype=np.int64)
+    g = torch.as_tensor(gn, device="cuda:0")
+    lm = torch.as_tensor(c.theta * rng.random((2, 3 * N)), device="cuda:0")
+    lm[1, :N] = 0.0  # set 1: no charging price, the upper bound active
+    lr = torch.as_tensor([0.0, 0.2], dtype=torch.float64, device="cuda:0")
+    wr = torch.as_tensor(c.w_max * rng.random((2, N)), device="cuda:0")
+    lompc = mk(c, N)
+    full = BatchPlan(lompc, g, off, w_ref=wr, want_w=True, want_cost=True)
+    red = BatchPlan(lompc, g, off, w_ref=wr, want_w=False, want_cost=True)
+    of = full.run(lm, lr)
+    orr = red.run(lm, lr)
+    assert full.check()[1:] == (0, 0) and red.check()[1:] == (0, 0)
+    np.testing.assert_allclose(orr["set_sum_w"].cpu().numpy(), of["set_sum_w"].cpu().numpy(), rtol=1e-11, atol=1e-11)
+    np.testing.assert_allclose(orr["set_stats"].cpu().numpy(), of["set_stats"].cpu().numpy(), rtol=1e-11, atol=1e-11)
+    lmn, lrn = lm.cpu().numpy(), lr.cpu().numpy()
+    sw = orr["set_sum_w"].cpu().numpy()
+    for s in range(2):
+        wo, _, nf = oracle_c.solve_batch(N, c, lmn[s], lrn[s], gn[off[s]:off[s + 1]])
+        assert nf == 0
+        np.testing.assert_allclose(sw[s], wo.sum(0), rtol=1e-10, atol=1e-9)
 
 
 @pytest.mark.parametrize("diag_repair", [False, True])

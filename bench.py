@@ -497,7 +497,7 @@ def station_leg(args, world, dev, sharded=False):
     steps, warm = args.station_steps, args.station_warmup
     # storage rate / capacity 0.5 (x_max = 0.5 is one of the example's listed values, :47): at
     # horizon 48 the example's 0.3 / 0.3 makes the first BiMPC infeasible (example.station_consts)
-    consts = station_consts(steps + warm, M_2, n_lo=N, n_bi=N, partitions=P, price_type="linear-convex",
+    consts = station_consts(steps + warm + max(args.station_prof_steps, 0), M_2, n_lo=N, n_bi=N, partitions=P, price_type="linear-convex",
                             demand_scale=DEMAND_SCALE * M_2 / NUM_EVS_PER_EV_TYPE, u_b_max=0.5, x_max=0.5)
     group = dist.group.WORLD if sharded else None
     is_c5 = 2 * M_2 == 2097152 and N == 48 and P == 12
@@ -580,13 +580,18 @@ def price_loop_breakdown(st, n, consts, torch):
     for s in sols:
         s.loop_prof[:] = 0.0
         s.profile_loops = True
+    st.phase_ms = {}
+    st.profile_phases = True
+    bimpc_ms = 0.0
     t0 = time.perf_counter()
     try:
         for _ in range(n):
             st._step()
             torch.cuda.synchronize()
+            bimpc_ms += (st.bimpc.last_info or {}).get("solve_ms", 0.0)
             check_station_state(st, consts)
     finally:
+        st.profile_phases = False
         for s in sols:
             s.profile_loops = False
     wall = time.perf_counter() - t0
@@ -596,6 +601,7 @@ def price_loop_breakdown(st, n, consts, torch):
         return {"steps": n, "note": "no native price loop ran"}
     per = lambda k: float(tot[k] / calls)
     return {"steps": n, "engine_calls": int(calls), "ms_per_step": wall / n * 1e3,
+            "phase_ms_per_step": {**{k: v / n for k, v in st.phase_ms.items()}, "bimpc_host_ipm": bimpc_ms / n},
             "price_loops_ms_per_step_per_type": float(tot[_lib.LOMPC_LOOP_PROF_WALL] / n / 2e3),
             "per_engine_call_us": {"total": per(_lib.LOMPC_LOOP_PROF_WALL), "issue": per(_lib.LOMPC_LOOP_PROF_ISSUE),
                                    "wait_sync": per(_lib.LOMPC_LOOP_PROF_WAIT), "gpu_span": per(_lib.LOMPC_LOOP_PROF_GPU),

@@ -130,6 +130,13 @@ struct lompc_plan {
   double* d_xsend = nullptr;      // [S (N + 8)]
   double* d_xrecv = nullptr;      // [nranks][S (N + 8)]
   int64_t cap_xsend = 0, cap_xrecv = 0;
+  // device-resident price loop (lompc_loop.hip): while it runs every plan kernel first reads
+  // *skip and returns when the loop has finished (iterations enqueued ahead of the convergence)
+  const int* skip = nullptr;
+  int* d_loop = nullptr;          // [LQ_LOOP_CTL] ints | doubles: the loop's device state
+  struct lq_host_loop* h_loop = nullptr;  // pinned: progress / done / results, written by k_loop_step
+  double* h_dec = nullptr;        // pinned [2][max_iter]: dual cost decreases (actual, predicted)
+  int cap_loop_iter = 0;
   // pinned staging of the host arrays
   char* h_buf = nullptr;
   int64_t cap_h = 0;
@@ -190,3 +197,7 @@ struct lompc_comm {
   std::string err;
 };
 int lq_comm_allgather(lompc_comm* c, const double* send, double* recv, size_t count, hipStream_t st);
+
+// price loops (lompc_plan.hip: host form; lompc_loop.hip: device-resident form and the C-ABI entry)
+int lq_price_loop_host(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd, double* w_k, double* dual_cost,
+                       double* dec_actual, double* dec_pred, int* iterations, double* errs, hipStream_t st);

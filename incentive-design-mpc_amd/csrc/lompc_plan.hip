@@ -219,6 +219,7 @@ struct PathArgs {
   double* t_cf;          // [S][G*PPL][8]     K0 K1 K2 (cost) F0 F1 F2 (err^2) a_0 b_0
   double2* t_ab;         // [S][G*PPL][N]     (a_t, b_t)
   int* errflag;
+  const int* skip;       // device-resident price loop: nonzero = the loop has finished, run nothing
 };
 
 // per-stage data of set s from its prices (lompc.py:92-135 in standard form)
@@ -423,6 +424,7 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
 
 template <int NT>
 __global__ __launch_bounds__(64) void k_path(PathArgs a) {
+  if (a.skip && *a.skip) return;
   path_cell<NT, true>(a, (int)blockIdx.x);
 }
 
@@ -466,6 +468,7 @@ struct EvalArgs {
   int w_bytes;            // B*N*8 when w_rsrc_ok (the descriptor's range)
   int cap;                // pieces staged in LDS (a set with more re-solves the rest individually)
   int nblk;               // workgroups of EVs (close mode: workgroup nblk closes the empty sets)
+  const int* skip;        // device-resident price loop: nonzero = the loop has finished, run nothing
 };
 
 // cost / A_bar error / price0 of a QP solved by the whole wave (lane t = w_t), valid on every lane
@@ -522,6 +525,7 @@ __device__ __forceinline__ double2 ld_t(const double2* p) {
 struct FinalArgs {
   int N, G, want_err;
   unsigned long long* tally;  // [3] plan-wide repaired / failed / invalid since the last status read (or null)
+  const int* skip;            // device-resident price loop: nonzero = the loop has finished
   int* arrive;             // [S] k_eval (close mode): arrived workgroups per set, zero between runs
   const QPConst* qd;
   CtxEnds ce;
@@ -674,6 +678,7 @@ __device__ __forceinline__ void finalize_set(const FinalArgs& r, const int s, do
 __global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
   __shared__ double red[4][FIN_W];
   __shared__ double rep[4][FIN_W];
+  if (r.skip && *r.skip) return;
   finalize_set<4, false>(r, (int)blockIdx.x, red, rep);
 }
 
@@ -1101,6 +1106,7 @@ template <bool CLOSE, int NT>
 __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_eval(EvalArgs a, FinalArgs r) {  // (4 waves per SIMD: two workgroups per CU)
   extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
   const int b = (int)blockIdx.x;
+  if (a.skip && *a.skip) return;  // (every workgroup: the arrival counters stay at zero)
   if constexpr (CLOSE) {
     if (b == a.nblk) {
       double (*red)[FIN_W] = reinterpret_cast<double (*)[FIN_W]>(s_dyn);
@@ -1375,6 +1381,7 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   pa.t_cf = p->t_cf;
   pa.t_ab = p->t_ab;
   pa.errflag = p->d_errflag;
+  pa.skip = p->skip;
   EvalArgs a{};
   a.S = (int)p->S;
   a.G = p->G;
@@ -1406,6 +1413,7 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   a.w_bytes = a.w_rsrc_ok ? (int)(p->B * (int64_t)N * 8) : 0;
   a.cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
   a.nblk = p->nblk;
+  a.skip = p->skip;
   const size_t lds = eval_lds(N, p->G, a.cap);
   FinalArgs r{};
   r.N = N;
@@ -1446,6 +1454,7 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   r.set_stats = xr ? p->d_xsend + p->S * N : set_stats;
   r.stats = p->d_stats;
   r.tally = p->d_tally;
+  r.skip = p->skip;
   r.arrive = p->d_arrive;
   const bool close = (p->close || (p->close_no_w && !w)) && p->nblk > 0;
   const bool cprof = prof_ctx && prof_ctx->prof;  // lompc_solve_batch: the context's k_eval timing
@@ -1505,10 +1514,12 @@ void lq_plan_free(lompc_plan* p) {
   (void)hipDeviceSynchronize();
   void* ptrs[] = {p->d_meta,  p->d_stats_own, p->d_window, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
                   p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag,
-                  p->d_fail_cnt, p->d_fail_idx, p->d_tally, p->d_wacc, p->d_arrive, p->d_xsend, p->d_xrecv};
+                  p->d_fail_cnt, p->d_fail_idx, p->d_tally, p->d_wacc, p->d_arrive, p->d_xsend, p->d_xrecv, p->d_loop};
   for (void* x : ptrs)
     if (x) (void)hipFree(x);
   if (p->h_buf) (void)hipHostFree(p->h_buf);
+  if (p->h_loop) (void)hipHostFree(p->h_loop);
+  if (p->h_dec) (void)hipHostFree(p->h_dec);
   if (p->ev_stage) (void)hipEventDestroy(p->ev_stage);
   for (auto& v : p->prof_ev)
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
@@ -1557,15 +1568,13 @@ int lompc_plan_update(lompc_plan* p, int64_t B, const double* gamma, const int64
   return lq_plan_prepare(p, p->nctx, p->ctx, spc, B, gamma, set_offsets, w_ref, p->flags, (hipStream_t)stream);
 }
 
-int lompc_price_loop(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd, double* w_k, double* dual_cost,
-                     double* dec_actual, double* dec_pred, int* iterations, double* errs, void* stream) {
-  if (!p || !a || !lmbd || !w_k || !iterations || !a->A_bar || !a->w_ref || !a->dev_in || !a->host_in ||
-      !a->dev_sw || !a->dev_st || !a->host_sw || !a->host_st || a->max_iter < 1 || !(a->n_evs > 0.0))
-    return LOMPC_ERR_INVALID_ARG;
+}  // extern "C"
+
+// The host form of lompc_price_loop (device_loop = 0): per iteration one plan run, one D2H copy and a
+// stream sync, the convergence test and lompc_price_step on the host.  Arguments checked by the caller.
+int lq_price_loop_host(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd, double* w_k, double* dual_cost,
+                       double* dec_actual, double* dec_pred, int* iterations, double* errs, hipStream_t st) {
   const int N = a->N, r = a->r, N3 = 3 * N;
-  if (N != p->N || p->S != 2 || (r != 2 * N && r != 3 * N)) return fail_arg(p, "price loop: a plan of 2 sets of horizon N");
-  HIPCHK(p, hipSetDevice(p->device));
-  hipStream_t st = (hipStream_t)stream;
   const size_t n_in = (size_t)6 * N + 2 + 2 * N;
   // per-part timing (args->prof): host clock for issue / wait / price step, HIP events for the
   // GPU span of every engine call (H2D copy .. D2H copy)
@@ -1689,6 +1698,8 @@ int lompc_price_loop(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd
   if (errs) memcpy(errs, e, sizeof(e));
   return LOMPC_OK;
 }
+
+extern "C" {
 
 int lompc_plan_run(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
                    int8_t* status, double* set_sum_w, double* set_stats, void* stream) {

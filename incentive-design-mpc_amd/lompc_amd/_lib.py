@@ -103,6 +103,7 @@ LOMPC_LOOP_PROF_GPU = 4
 LOMPC_LOOP_PROF_STEP = 5
 LOMPC_LOOP_PROF_HOST = 6
 LOMPC_LOOP_PROF = 8
+LOMPC_LOOP_AHEAD = 2
 LOMPC_BIMPC_WEIGHTED = 0
 LOMPC_BIMPC_UNWEIGHTED = 1
 LOMPC_BIMPC_EXP_UNWEIGHTED = 2
@@ -118,7 +119,8 @@ class PriceLoopArgs(ctypes.Structure):
                 ("n_evs", ctypes.c_double), ("lmbd_r", ctypes.c_double),
                 ("A_bar", ctypes.c_void_p), ("w_ref", ctypes.c_void_p), ("dev_in", ctypes.c_void_p),
                 ("host_in", ctypes.c_void_p), ("dev_sw", ctypes.c_void_p), ("dev_st", ctypes.c_void_p),
-                ("host_sw", ctypes.c_void_p), ("host_st", ctypes.c_void_p), ("prof", ctypes.c_void_p)]
+                ("host_sw", ctypes.c_void_p), ("host_st", ctypes.c_void_p), ("prof", ctypes.c_void_p),
+                ("device_loop", ctypes.c_int)]
 
 _lock = threading.Lock()
 _lib = None

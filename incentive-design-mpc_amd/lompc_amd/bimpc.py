@@ -12,6 +12,8 @@ import ctypes
 from dataclasses import dataclass
 from enum import Enum
 
+import time
+
 import numpy as np
 
 from . import _lib
@@ -143,6 +145,7 @@ class BiMPC:
         arrs = [_c(params.Mp_s), _c(params.Mp_l), _c(params.beta_s), _c(params.beta_l), _c(params.gamma_sm),
                 _c(params.gamma_lm)]
         dem = _c(params.demand)
+        t0 = time.perf_counter()
         rc = self._lib.lompc_bimpc_solve(
             N, P, int(self.charging_cost_type.value), float(self.delta), float(self.c_g), float(self.u_g_max),
             float(self.u_b_max), float(self.x_max), float(self.exp_rate), float(self.theta_s), float(self.theta_l),
@@ -150,7 +153,8 @@ class BiMPC:
             dem.ctypes.data, w_s.ctypes.data, w_l.ctypes.data, u_g.ctypes.data, duals.ctypes.data,
             info.ctypes.data)
         self.last_info = dict(iterations=int(info[0]), objective=info[1], primal_residual=info[2],
-                              dual_residual=info[3], complementarity=info[4])
+                              dual_residual=info[3], complementarity=info[4],
+                              solve_ms=(time.perf_counter() - t0) * 1e3)
         self.last_duals = duals
         if rc == _lib.LOMPC_ERR_NOT_CONVERGED:
             raise SolverError("BiMPC interior point did not converge (infeasible storage bounds?)")

@@ -146,6 +146,8 @@ class ChargingStation:
         torch = _torch()
         self.group = group
         self._pool = None  # one worker thread: the large-EV price chain beside the small one
+        self.profile_phases = False  # accumulate per-phase wall times of _step in phase_ms (synchronising)
+        self.phase_ms = {}
         self.device = torch.cuda.current_device() if device is None else int(device)
         self._dev = f"cuda:{self.device}"
         # Set constants, initialize PriceSolvers and BiMPC.
@@ -262,15 +264,38 @@ class ChargingStation:
             print(f"Iteration {self.t}")
             print("-" * 50)
         lmbd_r = 0
+        tick = self._tick()
         w_hat_s, w_hat_l, u_g, stats_bi = self._get_bimpc_solution(lmbd_r)
+        tick("bimpc")
         prices_s, prices_l, stats_s, stats_l = self._get_optimal_prices(w_hat_s, w_hat_l, lmbd_r)
+        tick("prices")
         w0_s, w0_l, price0_s, price0_l, w0_stats = self._get_w0_price0(prices_s, prices_l, lmbd_r)
+        tick("w0_price0")
         nu = (w_hat_s, w_hat_l, u_g, w0_s, w0_l)
         stats = (stats_bi, stats_s, stats_l)
         price0 = (price0_s, price0_l)
         self._update_logs(lmbd_r, nu, stats, price0, w0_stats)
         self._update_state(w0_s, w0_l, u_g[0], w0_stats)
+        tick("state")
         self.t += 1
+
+    def _tick(self):
+        """Phase timer of _step (profile_phases): synchronises the device at each boundary."""
+        if not self.profile_phases:
+            return lambda name: None
+        import time
+
+        torch = _torch()
+        torch.cuda.synchronize(self.device)
+        last = [time.perf_counter()]
+
+        def tick(name):
+            torch.cuda.synchronize(self.device)
+            t = time.perf_counter()
+            self.phase_ms[name] = self.phase_ms.get(name, 0.0) + (t - last[0]) * 1e3
+            last[0] = t
+
+        return tick
 
     # ------------------------------------------------------------------ BiMPC
     def _robustness(self, solver: PriceSolver, st_row, lmbd_r):

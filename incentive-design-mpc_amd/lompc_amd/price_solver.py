@@ -28,8 +28,9 @@ DIRECT-mode plans also take the Python loop.
 """
 from __future__ import annotations
 
-import functools
 import ctypes
+import functools
+import os
 
 import numpy as np
 
@@ -106,6 +107,9 @@ class PriceSolver:
         self._kappa = None
         self.native_loop = True  # the price loop in C++ (lompc_price_loop) whenever the plan allows it
         self.profile_loops = False  # accumulate the native loop's per-part times in loop_prof
+        # the convergence test and the price QP on the GPU after every engine call, no host round trip
+        # per iteration (lompc_loop.hip); LOMPC_HOST_LOOP=1: the host form (one copy + sync per iteration)
+        self.device_loop = os.environ.get("LOMPC_HOST_LOOP", "0") != "1"
         self.loop_prof = np.zeros(_lib.LOMPC_LOOP_PROF)
         # the solver's own stream: its loop can run beside the other EV type's (charging_station)
         self._stream = torch.cuda.Stream(device=self.lompc.device)
@@ -316,7 +320,8 @@ class PriceSolver:
             float(self.consts.w_max), float(self.m), float(self._kappa_of(self._A_bar_inv)), float(self.eps_reg),
             float(tol), float(self.nEVs), float(lmbd_r), A_bar.ctypes.data, w_ref.ctypes.data, self._in.data_ptr(),
             self._h_in.data_ptr(), self._plan.out["set_sum_w"].data_ptr(), self._plan.out["set_stats"].data_ptr(),
-            self._h_sw.data_ptr(), self._h_st.data_ptr(), self.loop_prof.ctypes.data if self.profile_loops else None)
+            self._h_sw.data_ptr(), self._h_st.data_ptr(), self.loop_prof.ctypes.data if self.profile_loops else None,
+            1 if self.device_loop else 0)
         lm = np.ascontiguousarray(lmbd_k, dtype=np.float64).copy()
         w_k = np.empty(self.N)
         dec_ac, dec_pred = np.empty(MAX), np.empty(MAX)

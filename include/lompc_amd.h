@@ -106,8 +106,9 @@ int lompc_set_params(lompc_ctx* ctx, int64_t S, const double* lmbd,
  *   set_sum_w    dev  [S, N]   sum_i w_i per set (price_solver.py:205), or NULL
  *   set_stats    dev  [S, LOMPC_SET_STATS] fused per-set reductions, or NULL
  * Errors detected on device are reported through ``status``/``set_stats`` and
- * ``lompc_last_status``.  PATH mode groups the batch by gamma cell on every call (a device
- * radix sort); a batch solved at many prices should use a plan (lompc_plan_create) instead. */
+ * ``lompc_last_status``.  PATH mode prepares a transient plan on every call (gamma windows
+ * measured, block map staged); a batch solved at many prices should use a plan
+ * (lompc_plan_create) instead. */
 int lompc_solve_batch(lompc_ctx* ctx, int64_t B, const double* gamma,
                       const int64_t* set_offsets, double* w, double* cost,
                       double* w0, int8_t* status, double* set_sum_w,
@@ -276,13 +277,22 @@ int lompc_plan_set_comm(lompc_plan* plan, lompc_comm* comm);
  * the first iteration), *iterations = price steps taken (the reference's `iter` at the break;
  * max_iter when the cap was hit, where the reference's `iter` is max_iter - 1),
  * errs [3] = (w_err_max, w0_err, w_avg_err) at the final prices.
+ * device_loop = 1: the DEVICE-RESIDENT loop — the convergence test and the price-gradient QP run on
+ * the GPU (one wave, lompc_pricewave.hpp) right after each engine call, the next prices go
+ * straight into dev_in, and the host only enqueues engine calls LOMPC_LOOP_AHEAD ahead of the
+ * device's progress (read from pinned memory), with no copy and no synchronisation per iteration;
+ * engine calls enqueued past the convergence exit at once.  The number of engine calls enqueued
+ * depends only on the iteration count, so sharded ranks issue the same collectives.  Requires
+ * A_bar = A'A + kappa I (as PriceSolver passes; otherwise the host loop runs).
+ * device_loop = 0: the host loop above (one D2H copy + stream sync per iteration).
  * prof (may be NULL): accumulates the loop's time per part, [LOMPC_LOOP_PROF] entries: */
 #define LOMPC_LOOP_PROF_ITERS  0 /* engine calls (plan runs)                                     */
 #define LOMPC_LOOP_PROF_WALL   1 /* us, host wall time of the whole loop                          */
 #define LOMPC_LOOP_PROF_ISSUE  2 /* us, host time issuing copies / launches / the collective       */
 #define LOMPC_LOOP_PROF_WAIT   3 /* us, host time blocked in the stream synchronisation           */
-#define LOMPC_LOOP_PROF_GPU    4 /* us, GPU span of each engine call (HIP events around H2D .. D2H) */
-#define LOMPC_LOOP_PROF_STEP   5 /* us, host price-gradient QP (lompc_price_step)                 */
+#define LOMPC_LOOP_PROF_GPU    4 /* us, GPU span of each engine call (HIP events around H2D .. D2H;
+                                    device loop: first enqueue .. convergence, per engine call)   */
+#define LOMPC_LOOP_PROF_STEP   5 /* us, host price-gradient QP (lompc_price_step; 0 on the device) */
 #define LOMPC_LOOP_PROF_HOST   6 /* us, other host work (convergence test, metric, bookkeeping)   */
 #define LOMPC_LOOP_PROF 8
 typedef struct lompc_price_loop_args {
@@ -294,7 +304,9 @@ typedef struct lompc_price_loop_args {
   const double* dev_sw; const double* dev_st;
   double* host_sw; double* host_st;
   double* prof;                         /* host [LOMPC_LOOP_PROF] or NULL */
+  int device_loop;                      /* 1: device-resident loop (see above), 0: host loop */
 } lompc_price_loop_args;
+#define LOMPC_LOOP_AHEAD 2  /* device loop: engine calls enqueued beyond the device's progress */
 int lompc_price_loop(lompc_plan* plan, const lompc_price_loop_args* args, double* lmbd, double* w_k,
                      double* dual_cost, double* dec_actual, double* dec_pred, int* iterations,
                      double* errs, void* stream);

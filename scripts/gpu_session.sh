@@ -24,6 +24,11 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py ;;
     bdist) run bdist 600 python bench.py --force-dist --no-cpu-baseline --no-direct ;;
     bdistq) run bdistq 300 python bench.py --force-dist --steps 100 --warmup 10 --no-cpu-baseline --no-direct --no-station ;;
+    c5test) run c5test 600 python -u -m pytest tests/test_gpu_example.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k config5 ;;
+    station) run station 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-direct --no-contracts ;;
+    stationh) LOMPC_HOST_LOOP=1 run stationh 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-direct --no-contracts ;;
+    stationd) run stationd 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-direct --no-contracts --force-dist ;;
+    sprofk) run sprofk 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/sprofk -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-direct --no-contracts --station-steps 5 --station-warmup 1 --station-prof-steps 0 ;;
     comm) run comm 600 python -u -m pytest tests/test_gpu_comm.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench20q) run bench20q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-station ;;

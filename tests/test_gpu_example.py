@@ -9,6 +9,7 @@ Seeds 2 and 7 are among those whose step-3/4 BiMPC once stalled the interior poi
 csrc/lompc_bimpc.cpp, Woodbury form of the coupling rows)."""
 import numpy as np
 import pytest
+import torch
 
 from lompc_amd import settings
 from lompc_amd.charging_station import ChargingStation
@@ -59,3 +60,35 @@ def test_paper_experiment_as_shipped(gpu, monkeypatch):
     assert np.all(np.isfinite(logs["prices"]["avg_price_s"][pop]))
     assert np.all(np.isfinite(logs["inputs"]["u_g"])) and np.all(logs["inputs"]["u_g"] >= -1e-9)
     assert 0 <= st["ncharged_s"] and 0 <= st["ncharged_l"]
+
+
+def test_config5_full_size_closed_loop(gpu, monkeypatch):
+    """BASELINE config 5 at its stated size on one GPU: 2 097 152 EVs (1 048 576 per type),
+    N_lo = N_bi = 48, P = 12, linear-convex prices, regularizer on, demand scaled by M_2 / 500
+    (SURVEY.md §8(d)), storage rate / capacity 0.5 (the horizon-48 feasibility note in
+    bench.py's station leg), three closed-loop steps (charging_station.py:156-185).  Checks after
+    every step: storage within [0, x_max] up to round-off, every EV counted once per type, every
+    price loop below the iteration cap, the BiMPC converged with small residuals; any failed or
+    invalid LoMPC QP raises inside the step (the price loops' combined set tallies)."""
+    from lompc_amd.example import DEMAND_SCALE
+
+    monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
+    M_2, N, steps = 1048576, 48, 3
+    consts = station_consts(steps, M_2, n_lo=N, n_bi=N, partitions=12, price_type="linear-convex",
+                            demand_scale=DEMAND_SCALE * M_2 / NUM_EVS_PER_EV_TYPE, u_b_max=0.5, x_max=0.5)
+    np.random.seed(0)
+    cs = ChargingStation(consts, device=0)
+    x_max = consts.bimpc_consts.x_max
+    for t in range(steps):
+        cs._step()
+        assert -1e-6 <= cs.x <= x_max + 1e-6, (t, cs.x)
+        st = cs.logs["statistics"]
+        assert int(st["Mp_s"][:, t].sum()) == M_2 and int(st["Mp_l"][:, t].sum()) == M_2
+        it = np.concatenate([st["niter_s"][:, t], st["niter_l"][:, t]])
+        assert np.all(it < settings.MAX_PRICE_SOLVER_ITERATIONS), it
+        info = cs.bimpc.last_info
+        scale = 1.0 + abs(info["objective"])
+        assert info["primal_residual"] <= 1e-6 * scale and info["dual_residual"] <= 1e-6 * scale, info
+        y = torch.cat([cs.y_s, cs.y_l])
+        assert bool(((y >= 0) & (y <= 0.9)).all())
+    assert np.all(np.isfinite(cs.logs["inputs"]["u_g"]))

@@ -44,17 +44,19 @@ def compare(lm, st, lmo, sto, theta):
         np.testing.assert_allclose(st[k], sto[k], rtol=1e-6, atol=1e-6 * np.max(np.abs(sto[k]), initial=1.0))
 
 
-@pytest.mark.parametrize("native", [True, False], ids=["native_loop", "python_loop"])
+@pytest.mark.parametrize("loop", ["device", "host", "python"])
 @pytest.mark.parametrize("case", SWEEP, ids=lambda c: f"{c[0]}-{c[3]}-{c[4]}-N{c[2]}-lr{c[5]}")
-def test_compute_optimal_prices_matches_oracle(gpu, case, native, monkeypatch):
-    """Both loops: the single-rank C++ loop (lompc_price_loop) and the Python restatement (used
-    with PRINT_LEVEL >= 2 and on sharded ranks)."""
+def test_compute_optimal_prices_matches_oracle(gpu, case, loop, monkeypatch):
+    """All three loops: the device-resident loop (lompc_price_loop, device_loop = 1: convergence test
+    and price QP on the GPU, the default), the host C++ loop (device_loop = 0) and the Python
+    restatement (used with PRINT_LEVEL >= 2 and on gloo-sharded ranks)."""
     name, nev, N, ev, price_type, lmbd_r, spread = case
     monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
     c, lc = consts(ev)
     rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
     ps = PriceSolver(N, lc, price_type, device=0)
-    ps.native_loop = native
+    ps.native_loop = loop != "python"
+    ps.device_loop = loop == "device"
     po = PO.OraclePriceSolver(N, c, price_type)
     for call in range(2):  # the second call starts from prev_prices (price_solver.py:104, :166)
         y0 = spread * c.y_max * rng.random(nev)  # test_price_solver.py:32
@@ -108,3 +110,38 @@ def test_dual_cost_guarantee_large_evs(gpu, monkeypatch):
     assert len(pred) == st["iter"] and np.all(pred >= -1e-9)
     if len(act):
         assert act[0] >= pred[0] - 1e-6 * max(1.0, abs(pred[0]))
+
+
+@pytest.mark.parametrize("ev,price_type", [("small", "linear"), ("large", "linear-convex")])
+@pytest.mark.parametrize("N", [12, 24, 48])
+def test_device_loop_matches_host_loop(gpu, monkeypatch, ev, price_type, N):
+    """The device-resident loop against the host C++ loop over consecutive calls (warm prices,
+    several partitions' worth of EVs): the same iteration counts, prices within 1e-9 theta, dual
+    cost decreases within 1e-8 relative (the price QP on one wave vs the host's sequential
+    tridiagonal solves: same method, different rounding), and the loop's engine calls counted
+    once (no call of the enqueued-ahead tail reaches the results)."""
+    monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
+    c, lc = consts(ev)
+    rng = np.random.default_rng(100 + N + (ev == "large"))
+    sols = {}
+    for mode in ("device", "host"):
+        ps = PriceSolver(N, lc, price_type, device=0)
+        ps.device_loop = mode == "device"
+        sols[mode] = ps
+    for call in range(4):
+        y0 = 0.3 + (0.02 + 0.02 * call) * c.y_max * rng.random(3000 + 500 * call)
+        w_ref = c.w_max * (0.2 + 0.6 * rng.random(N))
+        lr = 0.0 if call < 2 else 3.0 * N * c.delta * rng.random()
+        res = {}
+        for mode, ps in sols.items():
+            ps.set_charge_levels(y0)
+            n0 = ps.n_batched_calls
+            lm, st = ps.compute_optimal_prices(w_ref, lr)
+            res[mode] = (lm.copy(), st, ps.n_batched_calls - n0)
+        (ld, sd, nd), (lh, sh, nh) = res["device"], res["host"]
+        assert sd["iter"] == sh["iter"] and nd == nh == sd["iter"] + 1
+        np.testing.assert_allclose(ld, lh, rtol=0, atol=1e-9 * c.theta)
+        for k in ("dual_cost_decrease_actual", "dual_cost_decrease_predicted"):
+            np.testing.assert_allclose(sd[k], sh[k], rtol=1e-8, atol=1e-8 * np.max(np.abs(sh[k]), initial=1.0), err_msg=k)
+        for k in ("price_before_reg", "price_after_reg"):
+            assert abs(sd[k] - sh[k]) <= 1e-9 * max(1.0, abs(sh[k])), k

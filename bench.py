@@ -579,6 +579,7 @@ def price_loop_breakdown(st, n, consts, torch):
     sols = (st.price_solver_s, st.price_solver_l)
     for s in sols:
         s.loop_prof[:] = 0.0
+        s.loop_host_ms = {k: 0.0 for k in s.loop_host_ms}
         s.profile_loops = True
     st.phase_ms = {}
     st.profile_phases = True
@@ -603,6 +604,8 @@ def price_loop_breakdown(st, n, consts, torch):
     return {"steps": n, "engine_calls": int(calls), "ms_per_step": wall / n * 1e3,
             "phase_ms_per_step": {**{k: v / n for k, v in st.phase_ms.items()}, "bimpc_host_ipm": bimpc_ms / n},
             "price_loops_ms_per_step_per_type": float(tot[_lib.LOMPC_LOOP_PROF_WALL] / n / 2e3),
+            "price_solver_ms_per_step": {f"{t}/{k}": v / n for t, s in zip(("small", "large"), sols)
+                                         for k, v in s.loop_host_ms.items()},
             "per_engine_call_us": {"total": per(_lib.LOMPC_LOOP_PROF_WALL), "issue": per(_lib.LOMPC_LOOP_PROF_ISSUE),
                                    "wait_sync": per(_lib.LOMPC_LOOP_PROF_WAIT), "gpu_span": per(_lib.LOMPC_LOOP_PROF_GPU),
                                    "host_price_qp": per(_lib.LOMPC_LOOP_PROF_STEP),

@@ -1,0 +1,445 @@
+// lompc_agg.hpp — reductions-only runs over gamma-sorted sets (LOMPC_PLAN_SORTED_GAMMA), included by
+// lompc_plan.hip inside its kernel namespace.
+//
+// A price iteration of PriceSolver._get_w_err (price_solver.py:196-214) needs only per-set sums
+// (sum of w, cost, price0, counts) and the max A_bar error — the reference drops the per-EV w
+// (:206).  On a certified piece every per-EV output is a polynomial in gamma (w_t = a_t + b_t gamma,
+// cost and err^2 quadratics), so the sums over the EVs of a piece need only the
+// piece's EV count n, sum of gamma and sum of gamma^2, and the max error sits at the piece's
+// smallest or largest gamma (err^2 is a convex quadratic).  When each set's gamma is ascending,
+// the EVs of a piece are one contiguous run, so:
+//   prepare (once per batch): the order is checked, gamma is quantised to x = round((gamma - lo)
+//     2^40 / (hi - lo)) in its set's window and exclusive prefix sums of x and x^2 (as the two
+//     40-bit halves) are built in exact integer arithmetic; a fine bucket index (G x KF buckets of
+//     the window) maps any gamma to a short run of sorted positions;
+//   run (k_agg, one workgroup per set, one wave per gamma cell): the piece ends of the cell become
+//     sorted positions (fine index, then one wave-wide compare over <= 64 gammas), the sums come
+//     from prefix-sum differences, the per-stage sums of w are sum_p n_p a_p + Gamma_p b_p, and EVs
+//     outside the cell's certified coverage are re-solved individually (as k_finalize does).
+// The per-iteration work is O(pieces x N), independent of the EV count; the sums are exact up to
+// the 2^-41-of-the-window quantisation of gamma (the same one k_eval's close mode uses).
+#pragma once
+
+#define LQ_AGG_KF 256  // fine buckets per gamma cell
+#define LQ_AGG_SB 1024 // sorted positions per prepare block
+
+struct SortArgs {
+  const QPConst* qd;
+  CtxEnds ce;
+  const int4* sblk;         // [nsblk] (set, first, end) blocks of <= LQ_AGG_SB EVs of one set
+  const int* sblk_prefix;   // [S+1]
+  const int64_t* set_off;   // [S+1]
+  const double* gamma;
+  const double* window;
+  unsigned long long* bsum; // [nsblk][4] block totals: sum x, sum hi(x^2), sum lo(x^2), valid | bad << 32
+  unsigned long long* P;    // [3][B + S] exclusive prefix sums (set s, position j at set_off[s] + s + j)
+  int* pos;                 // [S][F + 1] first sorted position of each fine bucket
+  int4* sinfo;              // [S] (valid EVs, order ok, -, -)
+  int S, G, F;
+  int64_t PB;               // B + S (stride of the three prefix arrays)
+};
+
+__device__ __forceinline__ bool agg_valid(double g, double ym) { return g >= 0.0 && g <= ym; }
+__device__ __forceinline__ unsigned long long agg_fix(double g, double lo, double sc) {  // round((g - lo) sc)
+  return (unsigned long long)rint(fmax(g - lo, 0.0) * sc);
+}
+__device__ __forceinline__ int agg_fine(double g, double lo, double fs, int F) {
+  const double x = (g - lo) * fs;
+  return x <= 0.0 ? 0 : (x >= (double)(F - 1) ? F - 1 : (int)x);
+}
+constexpr unsigned long long LQ_M40 = (1ull << 40) - 1ull;
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// (1) per block: the order check and the block totals of x, x^2
+__global__ __launch_bounds__(256) void k_sorted_sum(SortArgs a) {
+  __shared__ unsigned long long sh[4][4];
+  const int4 bk = a.sblk[blockIdx.x];
+  const int s = bk.x;
+  const double ym = set_consts(a.qd, a.ce, s).y_max;
+  const double lo = a.window[2 * s], sc = 0x1p40 / (a.window[2 * s + 1] - lo);
+  const int64_t s0 = a.set_off[s];
+  unsigned long long t1 = 0, th = 0, tl = 0, nv = 0, bad = 0;
+  for (int i = bk.y + (int)threadIdx.x; i < bk.z; i += 256) {
+    const double g = a.gamma[i];
+    const bool v = agg_valid(g, ym);
+    if (i > s0) {  // ascending valid values, invalid ones (NaN, outside [0, y_max]) after them
+      const double gp = a.gamma[i - 1];
+      const bool vp = agg_valid(gp, ym);
+      bad |= (v && (!vp || g < gp)) ? 1ull : 0ull;
+    }
+    if (v) {
+      const unsigned long long x = agg_fix(g, lo, sc);
+      const unsigned __int128 x2 = (unsigned __int128)x * x;
+      t1 += x;
+      th += (unsigned long long)(x2 >> 40);
+      tl += (unsigned long long)x2 & LQ_M40;
+      ++nv;
+    }
+  }
+  t1 = wave_sum_u64(t1);
+  th = wave_sum_u64(th);
+  tl = wave_sum_u64(tl);
+  nv = wave_sum_u64(nv | (bad << 32));
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[wv][0] = t1;
+    sh[wv][1] = th;
+    sh[wv][2] = tl;
+    sh[wv][3] = nv;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    unsigned long long v = 0;
+    for (int w = 0; w < 4; ++w) v += sh[w][threadIdx.x];
+    if (threadIdx.x == 3 && (v >> 32)) v = (v & 0xffffffffull) | (1ull << 32);  // any bad element
+    a.bsum[(size_t)blockIdx.x * 4 + threadIdx.x] = v;
+  }
+}
+
+// (2) per set (one workgroup): exclusive scan of the block totals (written back in place as
+// offsets), the set's valid count and order flag; an empty index for a set without valid EVs
+__global__ __launch_bounds__(256) void k_sorted_scan(SortArgs a) {
+  __shared__ int s_nv;
+  const int s = blockIdx.x;
+  const int b0 = a.sblk_prefix[s], b1 = a.sblk_prefix[s + 1];
+  if (threadIdx.x == 0) {  // (a few thousand blocks at most: one thread, in order)
+    unsigned long long c[3] = {0, 0, 0}, nv = 0, bad = 0;
+    for (int b = b0; b < b1; ++b) {
+      unsigned long long* r = a.bsum + (size_t)b * 4;
+      const unsigned long long v[4] = {r[0], r[1], r[2], r[3]};
+      r[0] = c[0];
+      r[1] = c[1];
+      r[2] = c[2];
+      r[3] = nv;
+      c[0] += v[0];
+      c[1] += v[1];
+      c[2] += v[2];
+      nv += v[3] & 0xffffffffull;
+      bad |= v[3] >> 32;
+    }
+    // the set's totals at position n (valid EVs are the first nv positions)
+    const size_t e = (size_t)(a.set_off[s + 1] + s);
+    a.P[e] = c[0];
+    a.P[a.PB + e] = c[1];
+    a.P[2 * a.PB + e] = c[2];
+    a.sinfo[s] = make_int4((int)nv, bad ? 0 : 1, 0, 0);
+    s_nv = (int)nv;
+  }
+  __syncthreads();
+  if (s_nv == 0) {
+    for (int b = threadIdx.x; b <= a.F; b += 256) a.pos[(size_t)s * (a.F + 1) + b] = 0;
+  }
+}
+
+// (3) per block: exclusive prefix sums at every position and the fine bucket index
+__global__ __launch_bounds__(256) void k_sorted_fill(SortArgs a) {
+  __shared__ unsigned long long sh[3][256];
+  const int4 bk = a.sblk[blockIdx.x];
+  const int s = bk.x;
+  const double ym = set_consts(a.qd, a.ce, s).y_max;
+  const double lo = a.window[2 * s], W = a.window[2 * s + 1] - lo;
+  const double sc = 0x1p40 / W, fs = (double)a.F / W;
+  const int64_t s0 = a.set_off[s];
+  const int4 si = a.sinfo[s];
+  const int nv = si.x;
+  const unsigned long long* off = a.bsum + (size_t)blockIdx.x * 4;
+  // 4 consecutive positions per thread
+  const int t = threadIdx.x;
+  const int i0 = bk.y + 4 * t;
+  unsigned long long x1[4], xh[4], xl[4], c1 = 0, ch = 0, cl = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = i0 + u;
+    const double g = i < bk.z ? a.gamma[i] : -1.0;
+    unsigned long long x = 0, h = 0, l = 0;
+    if (i < bk.z && agg_valid(g, ym)) {
+      x = agg_fix(g, lo, sc);
+      const unsigned __int128 x2 = (unsigned __int128)x * x;
+      h = (unsigned long long)(x2 >> 40);
+      l = (unsigned long long)x2 & LQ_M40;
+    }
+    x1[u] = c1;
+    xh[u] = ch;
+    xl[u] = cl;
+    c1 += x;
+    ch += h;
+    cl += l;
+  }
+  sh[0][t] = c1;
+  sh[1][t] = ch;
+  sh[2][t] = cl;
+  __syncthreads();
+  if (t < 3) {  // exclusive scan of the 256 thread totals (one thread per quantity)
+    unsigned long long acc = off[t];
+    for (int k = 0; k < 256; ++k) {
+      const unsigned long long v = sh[t][k];
+      sh[t][k] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = i0 + u;
+    if (i < bk.z) {
+      const size_t e = (size_t)(i + s);
+      a.P[e] = sh[0][t] + x1[u];
+      a.P[a.PB + e] = sh[1][t] + xh[u];
+      a.P[2 * a.PB + e] = sh[2][t] + xl[u];
+      // fine bucket boundaries: bucket b starts at the first valid position whose bucket is >= b
+      const int j = (int)(i - s0);
+      if (j < nv) {
+        const int fb = agg_fine(a.gamma[i], lo, fs, a.F);
+        const int fp = j == 0 ? -1 : agg_fine(a.gamma[i - 1], lo, fs, a.F);
+        int* ps = a.pos + (size_t)s * (a.F + 1);
+        for (int b = fp + 1; b <= fb; ++b) ps[b] = j;
+        if (j == nv - 1)
+          for (int b = fb + 1; b <= a.F; ++b) ps[b] = nv;
+      }
+    }
+  }
+}
+
+struct AggArgs {
+  int S, G, N, F;
+  const QPConst* qd;
+  CtxEnds ce;
+  const int64_t* set_off;
+  const double* window;
+  const double* gamma;
+  const double* lmbd;
+  const double* lmbd_r;
+  const double* w_ref;
+  const int* t_cnt;
+  const double* t_lo;
+  const uint8_t* t_sl;
+  const double* t_ge;
+  const double* t_cf;
+  const double2* t_ab;
+  const unsigned long long* P;
+  int64_t PB;
+  const int* pos;
+  const int4* sinfo;
+  double* set_sum_w;
+  double* set_stats;
+  double* stats;
+  unsigned long long* tally;
+  const int* skip;
+};
+
+// sorted position of the first gamma >= v (lower) or > v (!lower) within [a, b) of set s,
+// b - a <= 64: one load per lane, one ballot; more: binary search (wave-uniform)
+__device__ __forceinline__ int agg_search(const double* __restrict__ g, int a, int b, double v, bool lower, int lane) {
+  if (b - a <= 64) {
+    const double x = a + lane < b ? g[a + lane] : INFINITY;
+    const bool before = lower ? (x < v) : (x <= v);
+    return a + (int)__popcll(__ballot(before && a + lane < b));
+  }
+  while (a < b) {
+    const int mid = (a + b) >> 1;
+    const double x = g[mid];
+    if (lower ? (x < v) : (x <= v)) a = mid + 1;
+    else b = mid;
+  }
+  return a;
+}
+
+constexpr int LQ_AGG_W = 16;  // k_agg: waves per workgroup (cells per pass)
+
+template <int NT>
+__global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
+  __shared__ double s_w[LQ_AGG_W][LOMPC_MAX_N];
+  __shared__ double s_x[LQ_AGG_W][8];  // cost, price0, max err^2, repaired, failed
+  __shared__ double s_fin[8];          // the set's scalars
+  if (r.skip && *r.skip) return;
+  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+  const int N = NT ? NT : r.N, G = r.G, KF = r.F / G;
+  const QPConst& q = set_consts(r.qd, r.ce, s);
+  lq_tab_init(q);  // (the individual re-solves' box table)
+  const int64_t so = r.set_off[s];
+  const int n_s = (int)(r.set_off[s + 1] - so);
+  const int4 si = r.sinfo[s];
+  const double* __restrict__ g = r.gamma + so;
+  const unsigned long long* P1 = r.P + so + s;
+  const unsigned long long* PH = P1 + r.PB;
+  const unsigned long long* PL = P1 + 2 * r.PB;
+  const int* ps = r.pos + (size_t)s * (r.F + 1);
+  const double wlo = r.window[2 * s], W = r.window[2 * s + 1] - wlo;
+  const double h1 = W * 0x1p-40, fs = (double)r.F / W;
+  const double* __restrict__ L = r.lmbd + (size_t)s * 3 * N;
+  const double lr = r.lmbd_r[s];
+  const double l1 = L[0], l2 = L[N], l3 = L[2 * N];
+  const double tt = q.theta * q.theta, wm = q.w_max;
+  double accw = 0.0, acost = 0.0, ap0 = 0.0, aerr = 0.0;
+  int nrep = 0, nfail = 0;
+  const bool order_ok = si.y != 0;
+  for (int c = wv; order_ok && c < G; c += nw) {
+    const int cell = s * G + c;
+    const int cs = ps[c * KF], ce = ps[(c + 1) * KF];  // the cell's sorted positions
+    if (ce <= cs) continue;
+    const int cnt = r.t_cnt[cell];
+    const double lo = r.t_lo[cell];
+    const size_t sb = (size_t)cell * LQ_PPL;
+    // the cell's pieces: piece ends (lane k), coefficients (lane k), rows (lane t, all slots)
+    const double ge = lane < cnt ? r.t_ge[sb + lane] : INFINITY;
+    double cf[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cf[k] = lane < cnt ? r.t_cf[(sb + lane) * 8 + k] : 0.0;
+    double2 ab[LQ_PPL];
+#pragma unroll
+    for (int k = 0; k < LQ_PPL; ++k) ab[k] = (lane < N && k < cnt) ? r.t_ab[(sb + k) * N + lane] : make_double2(0.0, 0.0);
+    // boundary j (lane j <= cnt): j = 0 the coverage start (first gamma >= lo), j >= 1 the end of
+    // piece j - 1 (first gamma > ge_{j-1}); its fine bucket clamped to the cell's
+    const double gprev = __shfl(ge, max(lane - 1, 0), 64);  // (every lane: no read of an inactive lane)
+    const double vb = lane == 0 ? lo : gprev;
+    const int fb = min(max(agg_fine(vb, wlo, fs, r.F), c * KF), (c + 1) * KF - 1);
+    int qa = lane <= cnt ? ps[fb] : 0, qb = lane <= cnt ? ps[fb + 1] : 0;
+    qa = min(max(qa, cs), ce);
+    qb = min(max(qb, cs), ce);
+    int qpos = cs;
+    for (int j = 0; j <= cnt; ++j) {  // (wave-uniform loop over the boundaries)
+      const int a = __shfl(qa, j, 64), b = __shfl(qb, j, 64);
+      const double v = __shfl(vb, j, 64);
+      const int pj = agg_search(g, a, b, v, j == 0, lane);
+      if (lane == j) qpos = pj;
+    }
+    if (cnt == 0) qpos = ce;
+    // per piece k = lane: [qpos_k, qpos_{k+1})
+    const int qn = __shfl(qpos, min(lane + 1, 63), 64);
+    const bool pk = lane < cnt;
+    const int na = pk ? qpos : 0, nb = pk ? max(qn, qpos) : 0;
+    const double n = (double)(nb - na);
+    unsigned long long d1 = 0, dh = 0, dl = 0;
+    double gf = 0.0, gl = 0.0;
+    if (pk && nb > na) {
+      d1 = P1[nb] - P1[na];
+      dh = PH[nb] - PH[na];
+      dl = PL[nb] - PL[na];
+      gf = g[na];
+      gl = g[nb - 1];
+    }
+    const double X1 = (double)d1;
+    const double X2 = fma((double)dh, 0x1p40, (double)dl);
+    const double Gm = fma(h1, X1, n * wlo);                                 // sum gamma
+    const double G2 = fma(h1 * h1, X2, fma(2.0 * wlo * h1, X1, n * wlo * wlo));  // sum gamma^2
+    if (pk && nb > na) {
+      acost += fma(cf[2], G2, fma(cf[1], Gm, cf[0] * n));
+      const double e_f = fma(fma(cf[5], gf, cf[4]), gf, cf[3]), e_l = fma(fma(cf[5], gl, cf[4]), gl, cf[3]);
+      aerr = fmax(aerr, fmax(fmax(e_f, e_l), 0.0));
+      const double a0 = cf[6], b0 = cf[7];
+      const double sw0 = fma(b0, Gm, a0 * n), sw02 = fma(b0 * b0, G2, fma(2.0 * a0 * b0, Gm, a0 * a0 * n));
+      ap0 += q.theta * fma(l1, sw0, l2 * fma(wm, n, -sw0)) + fma(q.q_scale, l3, tt * lr) * sw02;  // lompc.py:164-170
+    }
+    // per-stage sums of w: sum over pieces of n_k a_kt + Gamma_k b_kt (lane t)
+#pragma unroll
+    for (int k = 0; k < LQ_PPL; ++k) {
+      const double nk = __shfl(n, k, 64), gk = __shfl(Gm, k, 64);
+      accw = fma(gk, ab[k].y, fma(nk, ab[k].x, accw));  // (slots past cnt: n = 0, Gamma = 0)
+    }
+    // EVs of the cell outside its certified coverage: re-solved one by one (k_finalize's method)
+    const int u0 = cs, u1 = __shfl(qpos, 0, 64), v0 = __shfl(qpos, cnt, 64), v1 = ce;
+    if (u1 > u0 || v1 > v0) {
+      lqw::WaveSet ws;
+      double l2w;
+      bool bad;
+      load_set(q, L, lr, N, lane, ws, l2w, bad);
+      const double c0 = q.theta * q.w_max * lqw::wave_sum(l2w, N);
+      const double kappa = lr / q.delta;
+      const double l0[3] = {l1, l2, l3};
+      const double wr = (r.w_ref && lane < N) ? r.w_ref[(size_t)s * N + lane] : 0.0;
+      for (int part = 0; part < 2; ++part) {
+        const int e0 = part ? v0 : u0, e1 = part ? v1 : u1;
+        for (int j = e0; j < e1; ++j) {
+          const double gj = g[j];
+          int sl = lane < N ? (int)r.t_sl[(size_t)cell * 64 + lane] : 0;
+          double wl = 0.0, rl = 0.0;
+          const bool okk = lqw::wave_solve(q, ws, gj, sl, wl, rl);
+          double co, eo, po;
+          wave_ev_outputs(q, ws, c0, kappa, l0, lr, wr, gj, wl, co, eo, po);
+          accw += lane < N ? wl : 0.0;
+          if (lane == 0) {
+            acost += co;
+            ap0 += po;
+            aerr = fmax(aerr, eo * eo);
+            nrep += okk ? 1 : 0;
+            nfail += okk ? 0 : 1;
+          }
+        }
+      }
+    }
+  }
+  // the waves' partials, combined in wave order
+  double xs[4] = {acost, ap0, 0.0, 0.0};
+  lqw::wave_totals(xs, 64);
+  const double emx = lqw::wave_max(aerr, 64);
+  const int rp = __shfl(nrep, 0, 64), fl = __shfl(nfail, 0, 64);
+  if (lane < N) s_w[wv][lane] = accw;
+  if (lane == 0) {
+    s_x[wv][0] = xs[0];
+    s_x[wv][1] = xs[1];
+    s_x[wv][2] = emx;
+    s_x[wv][3] = (double)rp;
+    s_x[wv][4] = (double)fl;
+  }
+  __syncthreads();
+  if (tid < N) {
+    double v = 0.0;
+    for (int k = 0; k < nw; ++k) v += s_w[k][tid];
+    if (r.set_sum_w) r.set_sum_w[(size_t)s * N + tid] = v;
+    if (tid == 0) s_fin[5] = v;  // (sum of w0)
+  }
+  if (tid == 0) {  // (after its own sum above)
+    double c = 0.0, p0 = 0.0, e = 0.0, rr = 0.0, ff = 0.0;
+    for (int k = 0; k < nw; ++k) {
+      c += s_x[k][0];
+      p0 += s_x[k][1];
+      e = fmax(e, s_x[k][2]);
+      rr += s_x[k][3];
+      ff += s_x[k][4];
+    }
+    if (!order_ok) ff = (double)n_s;  // gamma not ascending: every EV reported failed, nothing summed
+    s_fin[0] = c;
+    s_fin[1] = p0;
+    s_fin[2] = sqrt(e);
+    s_fin[3] = rr;
+    s_fin[4] = ff;
+  }
+  __syncthreads();
+  if (tid < LOMPC_SET_STATS) {
+    double v = 0.0;
+    switch (tid) {
+      case LOMPC_STAT_COUNT: v = (double)n_s; break;
+      case LOMPC_STAT_SUM_W0: v = s_fin[5]; break;
+      case LOMPC_STAT_SUM_PRICE0: v = s_fin[1]; break;
+      case LOMPC_STAT_MAX_ERR: v = s_fin[2]; break;
+      case LOMPC_STAT_SUM_COST: v = s_fin[0]; break;
+      case LOMPC_STAT_N_REPAIRED: v = s_fin[3]; break;
+      case LOMPC_STAT_N_FAILED: v = s_fin[4]; break;
+      default: v = (double)(n_s - (order_ok ? si.x : n_s)); break;  // invalid gamma: after the valid ones
+    }
+    if (r.set_stats) r.set_stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
+    r.stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
+  }
+  if (tid == 0 && r.tally) {
+    const double nr = s_fin[3], nf = s_fin[4], ni = (double)(n_s - (order_ok ? si.x : n_s));
+    if (nr > 0.0) __hip_atomic_fetch_add(r.tally + 0, (unsigned long long)nr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (nf > 0.0) __hip_atomic_fetch_add(r.tally + 1, (unsigned long long)nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ni > 0.0) __hip_atomic_fetch_add(r.tally + 2, (unsigned long long)ni, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+typedef void (*AggKernel)(AggArgs);
+AggKernel agg_kernel(int N) {
+  switch (N) {
+    case 12: return k_agg<12>;
+    case 16: return k_agg<16>;
+    case 24: return k_agg<24>;
+    case 48: return k_agg<48>;
+    default: return k_agg<0>;
+  }
+}

@@ -137,6 +137,17 @@ struct lompc_plan {
   struct lq_host_loop* h_loop = nullptr;  // pinned: progress / done / results, written by k_loop_step
   double* h_dec = nullptr;        // pinned [2][max_iter]: dual cost decreases (actual, predicted)
   int cap_loop_iter = 0;
+  // gamma-sorted sets (LOMPC_PLAN_SORTED_GAMMA, lompc_agg.hpp): runs without per-EV outputs
+  // aggregate per piece from prefix sums built at prepare (k_agg) instead of k_eval
+  bool sorted = false;
+  int nsblk = 0, aggF = 0;
+  int4* d_sblk = nullptr;          // [nsblk] (view of d_meta)
+  int* d_sblk_prefix = nullptr;    // [S+1]   (view of d_meta)
+  unsigned long long* d_bsum = nullptr;  // [nsblk][4]
+  unsigned long long* d_P = nullptr;     // [3][B + S]
+  int* d_pos = nullptr;                  // [S][F + 1]
+  int4* d_sinfo = nullptr;               // [S]
+  int64_t cap_sblk = 0, cap_P = 0, cap_pos = 0, cap_sinfo = 0;
   // pinned staging of the host arrays
   char* h_buf = nullptr;
   int64_t cap_h = 0;

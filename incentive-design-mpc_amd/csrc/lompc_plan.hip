@@ -1134,7 +1134,9 @@ EvalKernel eval_kernel(int N) {
   }
 }
 
-// ---------------------------------------------------------------- k_finalize
+#include "lompc_agg.hpp"
+
+// ---------------------------------------------------------------- host helpers
 
 int pick_cells(int64_t max_set) {
   const char* env = getenv("LOMPC_CELLS");  // diagnostics (cell-count sweeps)
@@ -1320,7 +1322,14 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   const size_t o_blk = up16(LQ_PLAN_MAX_CTX * sizeof(QPConst));
   const size_t o_off = o_blk + up16((size_t)nblk * sizeof(int4));
   const size_t o_pre = o_off + up16((size_t)(S + 1) * sizeof(int64_t));
-  const size_t need_h = o_pre + up16((size_t)(S + 1) * sizeof(int));
+  // gamma-sorted sets: blocks of <= LQ_AGG_SB positions of one set for the prepare kernels
+  const bool sorted = (flags & LOMPC_PLAN_SORTED_GAMMA) != 0;
+  int64_t nsblk = 0;
+  if (sorted)
+    for (int64_t s = 0; s < S; ++s) nsblk += (set_offsets[s + 1] - set_offsets[s] + LQ_AGG_SB - 1) / LQ_AGG_SB;
+  const size_t o_sblk = o_pre + up16((size_t)(S + 1) * sizeof(int));
+  const size_t o_spre = o_sblk + up16((size_t)nsblk * sizeof(int4));
+  const size_t need_h = sorted ? o_spre + up16((size_t)(S + 1) * sizeof(int)) : o_sblk;
   HIPCHK(p, hipEventSynchronize(p->ev_stage));  // (the staging may still feed the previous copy)
   if ((int64_t)need_h > p->cap_h) {
     if (p->h_buf) HIPCHK(p, hipHostFree(p->h_buf));
@@ -1350,11 +1359,52 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   p->d_blk = reinterpret_cast<int4*>(p->d_meta + o_blk);
   p->d_set_off = reinterpret_cast<int64_t*>(p->d_meta + o_off);
   p->d_blk_prefix = reinterpret_cast<int*>(p->d_meta + o_pre);
+  p->sorted = sorted;
+  p->nsblk = (int)nsblk;
+  if (sorted) {
+    int4* hs = reinterpret_cast<int4*>(p->h_buf + o_sblk);
+    int* hsp = reinterpret_cast<int*>(p->h_buf + o_spre);
+    int64_t k = 0;
+    hsp[0] = 0;
+    for (int64_t s = 0; s < S; ++s) {
+      for (int64_t i = set_offsets[s]; i < set_offsets[s + 1]; i += LQ_AGG_SB)
+        hs[k++] = make_int4((int)s, (int)i, (int)std::min<int64_t>(i + LQ_AGG_SB, set_offsets[s + 1]), 0);
+      hsp[s + 1] = (int)k;
+    }
+    p->d_sblk = reinterpret_cast<int4*>(p->d_meta + o_sblk);
+    p->d_sblk_prefix = reinterpret_cast<int*>(p->d_meta + o_spre);
+    p->aggF = G * LQ_AGG_KF;
+    const int64_t nP = 3 * (B + S), npos = S * (int64_t)(p->aggF + 1);
+    if (nsblk > p->cap_sblk) {
+      if ((rc = grow(p, &p->d_bsum, (size_t)nsblk * 4))) return rc;
+      p->cap_sblk = nsblk;
+    }
+    if (nP > p->cap_P) {
+      if ((rc = grow(p, &p->d_P, nP))) return rc;
+      p->cap_P = nP;
+    }
+    if (npos > p->cap_pos) {
+      if ((rc = grow(p, &p->d_pos, npos))) return rc;
+      p->cap_pos = npos;
+    }
+    if (S > p->cap_sinfo) {
+      if ((rc = grow(p, &p->d_sinfo, S))) return rc;
+      p->cap_sinfo = S;
+    }
+  }
   HIPCHK(p, hipMemcpyAsync(p->d_meta, p->h_buf, need_h, hipMemcpyHostToDevice, st));
   HIPCHK(p, hipEventRecord(p->ev_stage, st));
   WindowArgs wa{p->d_q, p->ce, p->d_blk, p->d_blk_prefix, gamma, p->d_wacc, p->d_window, (int)S, (int)nblk};
   hipLaunchKernelGGL(k_plan_window, dim3((unsigned)nblk + 1), dim3(256), 0, st, wa);
   HIPCHK(p, hipGetLastError());
+  if (sorted) {  // order check, prefix sums and fine index of the sorted sets (lompc_agg.hpp)
+    SortArgs sa{p->d_q, p->ce, p->d_sblk, p->d_sblk_prefix, p->d_set_off, gamma, p->d_window, p->d_bsum, p->d_P,
+                p->d_pos, p->d_sinfo, (int)S, G, p->aggF, B + S};
+    if (nsblk > 0) hipLaunchKernelGGL(k_sorted_sum, dim3((unsigned)nsblk), dim3(256), 0, st, sa);
+    hipLaunchKernelGGL(k_sorted_scan, dim3((unsigned)S), dim3(256), 0, st, sa);
+    if (nsblk > 0) hipLaunchKernelGGL(k_sorted_fill, dim3((unsigned)nsblk), dim3(256), 0, st, sa);
+    HIPCHK(p, hipGetLastError());
+  }
   return LOMPC_OK;
 }
 
@@ -1456,7 +1506,9 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   r.tally = p->d_tally;
   r.skip = p->skip;
   r.arrive = p->d_arrive;
-  const bool close = (p->close || (p->close_no_w && !w)) && p->nblk > 0;
+  // gamma-sorted sets and no per-EV output: per-piece aggregation (k_agg) instead of k_eval
+  const bool agg = p->sorted && !w && !cost && !w0 && !status && p->nblk > 0;
+  const bool close = !agg && (p->close || (p->close_no_w && !w)) && p->nblk > 0;
   const bool cprof = prof_ctx && prof_ctx->prof;  // lompc_solve_batch: the context's k_eval timing
   {
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1465,7 +1517,17 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
     HIPCHK(p, hipGetLastError());
     plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
   }
-  if (p->nblk > 0) {
+  if (agg) {  // timed as k_eval
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1)) return fail_arg(p, "profiling events");
+    AggArgs ga{(int)p->S, p->G, N, p->aggF, p->d_q, p->ce, p->d_set_off, p->d_window, p->gamma, lmbd, lmbd_r,
+               p->w_ref, p->t_cnt, p->t_lo, p->t_sl, p->t_ge, p->t_cf, p->t_ab, p->d_P, p->B + p->S, p->d_pos,
+               p->d_sinfo, r.set_sum_w, r.set_stats, p->d_stats, p->d_tally, p->skip};
+    const int nw = std::min(p->G, (int)LQ_AGG_W);
+    hipExtLaunchKernelGGL(agg_kernel(N), dim3((unsigned)p->S), dim3(64 * nw), 0, st, e0, e1, 0, ga);
+    HIPCHK(p, hipGetLastError());
+    plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
+  } else if (p->nblk > 0) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (cprof ? take_events(prof_ctx->prof_pool, &e0, &e1) : plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1))
       return fail_arg(p, "profiling events");
@@ -1483,7 +1545,7 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
       plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
     }
   }
-  if (!close) {  // (else the sets were closed inside k_eval)
+  if (!close && !agg) {  // (else the sets were closed inside k_eval / k_agg)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (plan_prof_begin(p, LOMPC_PLAN_K_FINAL, &e0, &e1)) return fail_arg(p, "profiling events");
     hipExtLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, e0, e1, 0, r);
@@ -1514,7 +1576,8 @@ void lq_plan_free(lompc_plan* p) {
   (void)hipDeviceSynchronize();
   void* ptrs[] = {p->d_meta,  p->d_stats_own, p->d_window, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
                   p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag,
-                  p->d_fail_cnt, p->d_fail_idx, p->d_tally, p->d_wacc, p->d_arrive, p->d_xsend, p->d_xrecv, p->d_loop};
+                  p->d_fail_cnt, p->d_fail_idx, p->d_tally, p->d_wacc, p->d_arrive, p->d_xsend, p->d_xrecv, p->d_loop,
+                  p->d_bsum, p->d_P, p->d_pos, p->d_sinfo};
   for (void* x : ptrs)
     if (x) (void)hipFree(x);
   if (p->h_buf) (void)hipHostFree(p->h_buf);
@@ -1795,3 +1858,18 @@ int lompc_plan_destroy(lompc_plan* p) {
 }
 
 }  // extern "C"
+
+// diagnostics (scripts/, not in the header): synchronous copies of a plan's path table and sorted index
+extern "C" int lompc_debug_plan_tables(lompc_plan* p, int* cnt, double* lo, double* ge, int* pos, int* sinfo,
+                                       unsigned long long* P) {
+  if (!p) return LOMPC_ERR_INVALID_ARG;
+  HIPCHK(p, hipDeviceSynchronize());
+  const size_t nc = (size_t)p->S * p->G;
+  if (cnt) HIPCHK(p, hipMemcpy(cnt, p->t_cnt, nc * sizeof(int), hipMemcpyDeviceToHost));
+  if (lo) HIPCHK(p, hipMemcpy(lo, p->t_lo, nc * sizeof(double), hipMemcpyDeviceToHost));
+  if (ge) HIPCHK(p, hipMemcpy(ge, p->t_ge, nc * LQ_PPL * sizeof(double), hipMemcpyDeviceToHost));
+  if (pos && p->d_pos) HIPCHK(p, hipMemcpy(pos, p->d_pos, (size_t)p->S * (p->aggF + 1) * sizeof(int), hipMemcpyDeviceToHost));
+  if (sinfo && p->d_sinfo) HIPCHK(p, hipMemcpy(sinfo, p->d_sinfo, (size_t)p->S * sizeof(int4), hipMemcpyDeviceToHost));
+  if (P && p->d_P) HIPCHK(p, hipMemcpy(P, p->d_P, (size_t)3 * (p->B + p->S) * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return LOMPC_OK;
+}

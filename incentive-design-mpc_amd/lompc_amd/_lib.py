@@ -36,6 +36,7 @@ LOMPC_PLAN_KERNELS = 3
 LOMPC_PLAN_WARM_START = 1
 LOMPC_PLAN_DIAG_REPAIR = 2
 LOMPC_PLAN_CLOSE_IN_EVAL = 8
+LOMPC_PLAN_SORTED_GAMMA = 16
 
 LOMPC_QP_OK = 0
 LOMPC_QP_REPAIRED = 1

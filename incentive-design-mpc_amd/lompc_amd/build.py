@@ -12,7 +12,7 @@ CSRC = os.path.join(ROOT, "csrc")
 OUT = os.path.join(PKG, "liblompc_amd.so")
 SOURCES = ["lompc_kernels.hip", "lompc_plan.hip", "lompc_price.cpp", "lompc_bimpc.cpp", "lompc_comm.cpp",
            "lompc_loop.hip"]
-DEPS = SOURCES + ["lompc_qp.hpp", "lompc_wave.hpp", "lompc_pricewave.hpp", "lompc_dense.hpp", "lompc_ctx.hpp",
+DEPS = SOURCES + ["lompc_qp.hpp", "lompc_wave.hpp", "lompc_pricewave.hpp", "lompc_agg.hpp", "lompc_dense.hpp", "lompc_ctx.hpp",
                   os.path.join("..", "..", "include", "lompc_amd.h")]
 ARCH = os.environ.get("LOMPC_OFFLOAD_ARCH", "gfx950")
 

@@ -25,6 +25,7 @@ redundantly on identical inputs; the re-draw replays the global random stream.
 from __future__ import annotations
 
 import concurrent.futures
+import time
 
 from dataclasses import dataclass
 
@@ -371,16 +372,26 @@ class ChargingStation:
         for kind, _, y, idx, *_ in chains:  # (on this thread: the layouts' host sync)
             self._partition_layout(kind, y, idx)
 
+        prof = self.profile_phases
+
         def one(chain, p):
             kind, solver, y, idx, st, w_hat, prices, stats = chain
             if st[p, 0] > 0:
+                t0 = time.perf_counter() if prof else 0.0
                 ys, off = self._partition_layout(kind, y, idx)
-                solver.set_charge_levels_stats(ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3])
+                solver.set_charge_levels_stats(ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3],
+                                               descending=True)
                 if PRINT_LEVEL >= 1 and self._rank0():
                     print(f"{kind} EVs, partition {p:2d}: ", end="")
                     if PRINT_LEVEL >= 2:
                         print("\n" + "-" * 27)
+                t1 = time.perf_counter() if prof else 0.0
                 lmbd_, stats_ = solver.compute_optimal_prices(w_hat[p, :], lmbd_r)
+                if prof:
+                    t2 = time.perf_counter()
+                    acc = self.phase_ms
+                    acc[f"prices/{kind}/levels"] = acc.get(f"prices/{kind}/levels", 0.0) + (t1 - t0) * 1e3
+                    acc[f"prices/{kind}/optimal_prices"] = acc.get(f"prices/{kind}/optimal_prices", 0.0) + (t2 - t1) * 1e3
                 prices[p, :] = lmbd_[: self.r]
                 stats.append(stats_)
                 if PRINT_LEVEL >= 2:
@@ -423,12 +434,17 @@ class ChargingStation:
         return prices_s, prices_l, stats_s, stats_l
 
     def _partition_layout(self, kind, y, idx):
-        """This rank's EVs of one type grouped by partition (stable), once per step: (charge
-        levels in that order, host offsets [P+1]) — per-partition slices without boolean
-        indexing (one host sync per type and step instead of one per partition)."""
+        """This rank's EVs of one type grouped by partition, each partition in descending charge
+        level (ascending gamma = y_max - y: the price loops' plans aggregate per certified piece,
+        LOMPC_PLAN_SORTED_GAMMA), once per step: (charge levels in that order, host offsets
+        [P+1]) — per-partition slices without boolean indexing (one host sync per type and step
+        instead of one per partition)."""
         torch = _torch()
         if kind not in self._layout:
-            perm = torch.argsort(idx, stable=True)
+            # (partition, -y) order exactly: a stable sort by descending y, then a stable sort by
+            # partition (a composite float key would round near-equal charge levels out of order)
+            by_y = torch.argsort(y, descending=True, stable=True)
+            perm = by_y[torch.argsort(idx[by_y], stable=True)]
             counts = torch.bincount(idx, minlength=self.P)[: self.P].cpu().numpy()
             off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
             self._layout[kind] = (perm, off, y[perm])

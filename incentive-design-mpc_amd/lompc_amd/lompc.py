@@ -336,14 +336,17 @@ class BatchPlan:
     cell's exact solve starts from the working set the previous run ended with.  ``diag_repair``
     (diagnostics): no solution path, every EV is re-solved individually.  ``close_in_eval``: the
     per-set reductions and re-solves inside k_eval (each set's last-arriving workgroup) instead of
-    the k_finalize launch (measured slower with w rows: DESIGN.md §10).  ``set_comm(comm)``: a
+    the k_finalize launch (measured slower with w rows: DESIGN.md §10).  ``sorted_gamma``: every
+    set's gamma is ascending and stays unmodified until the next ``update`` — runs without per-EV
+    outputs then aggregate per certified piece from prefix sums (k_agg, O(pieces) per run; a set
+    found unsorted reports all its EVs failed).  ``set_comm(comm)``: a
     sharded batch — every run combines the set reductions of all ranks on the device (RCCL).
     DIRECT-mode contexts fall back to ``lompc_run`` (one context only).
     """
 
     def __init__(self, lompc, gamma, set_offsets, *, sets_per_ctx=None, w_ref=None, gamma_ref=None, want_w=True,
                  want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None, validate=True,
-                 warm_start=False, diag_repair=False, close_in_eval=False):
+                 warm_start=False, diag_repair=False, close_in_eval=False, sorted_gamma=False):
         torch = _torch()
         lompcs = list(lompc) if isinstance(lompc, (list, tuple)) else [lompc]
         self.lompcs = lompcs
@@ -379,7 +382,8 @@ class BatchPlan:
         ctxs = (ctypes.c_void_p * len(lompcs))(*[x._ctx.value for x in lompcs])
         plan = ctypes.c_void_p()
         flags = ((_lib.LOMPC_PLAN_WARM_START if warm_start else 0) | (_lib.LOMPC_PLAN_DIAG_REPAIR if diag_repair else 0)
-                 | (_lib.LOMPC_PLAN_CLOSE_IN_EVAL if close_in_eval else 0))
+                 | (_lib.LOMPC_PLAN_CLOSE_IN_EVAL if close_in_eval else 0)
+                 | (_lib.LOMPC_PLAN_SORTED_GAMMA if sorted_gamma else 0))
         self._flags = flags
         rc = self._lib.lompc_plan_create(len(lompcs), ctypes.cast(ctxs, ctypes.c_void_p), self.sets_per_ctx.ctypes.data,
                                          self.B, _ptr(self.gamma), self.off.ctypes.data, _ptr(self.w_ref), flags,
@@ -437,6 +441,8 @@ class BatchPlan:
 
         if self.direct:
             return 2
+        if self._flags & _lib.LOMPC_PLAN_SORTED_GAMMA and not any(self._want[k] for k in ("w", "cost", "w0", "status")):
+            return 2 + (2 if self.comm is not None else 0)  # k_path + k_agg
         env = os.environ.get("LOMPC_CLOSE")
         if env is not None:
             close = env == "1"

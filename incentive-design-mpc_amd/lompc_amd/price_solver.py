@@ -31,6 +31,7 @@ from __future__ import annotations
 import ctypes
 import functools
 import os
+import time
 
 import numpy as np
 
@@ -111,6 +112,7 @@ class PriceSolver:
         # per iteration (lompc_loop.hip); LOMPC_HOST_LOOP=1: the host form (one copy + sync per iteration)
         self.device_loop = os.environ.get("LOMPC_HOST_LOOP", "0") != "1"
         self.loop_prof = np.zeros(_lib.LOMPC_LOOP_PROF)
+        self.loop_host_ms = {"native_loop": 0.0, "finish_prices": 0.0}
         # the solver's own stream: its loop can run beside the other EV type's (charging_station)
         self._stream = torch.cuda.Stream(device=self.lompc.device)
         self.n_batched_calls = 0
@@ -182,10 +184,12 @@ class PriceSolver:
 
 
     @_solver_stream
-    def set_charge_levels_stats(self, y0d, n: int, y_hi: float, y_lo: float, y_sum: float) -> None:
+    def set_charge_levels_stats(self, y0d, n: int, y_hi: float, y_lo: float, y_sum: float,
+                                descending: bool = False) -> None:
         """set_charge_levels for a device slice of charge levels whose (global) count / max /
         min / sum the caller already has (ChargingStation computes every partition's in one pass
-        per step, charging_station.py:187-266): no host sync, no collective."""
+        per step, charging_station.py:187-266): no host sync, no collective.  ``descending``: y0d
+        is already in descending order (gamma ascending), so the loop plan needs no sort."""
         if not (n > 0 and 0.0 <= y_lo <= y_hi <= self.consts.y_max):
             raise AssertionError("0 <= y0 <= y_max required (price_solver.py:71)")
         self.y0 = y0d
@@ -194,7 +198,7 @@ class PriceSolver:
         self.y0_rng = (y_hi - y_lo) / 2  # = \bar{\Gamma}
         self.gamma_sc = self.consts.y_max - (y_hi + y_lo) / 2
         self.gamma_sm = self.consts.y_max - y_sum / n
-        self._build_plans(self.consts.y_max - y0d)
+        self._build_plans(self.consts.y_max - y0d, presorted=descending)
 
     def _device_comm(self):
         """The extension's RCCL communicator of the group (None: single rank, gloo, DIRECT mode)."""
@@ -219,13 +223,19 @@ class PriceSolver:
         self.nEVs = n
         return y_hi, y_lo, y_mean
 
-    def _build_plans(self, gamma) -> None:
-        """Batch layout of one price iteration: set 0 = this rank's EVs, set 1 = the central QP."""
+    def _build_plans(self, gamma, presorted: bool = False) -> None:
+        """Batch layout of one price iteration: set 0 = this rank's EVs, set 1 = the central QP.
+        The loop plan holds set 0's gamma in ascending order (LOMPC_PLAN_SORTED_GAMMA: its runs
+        aggregate per certified piece, O(pieces) per iteration; only the per-set sums leave the
+        loop, price_solver.py:196-214, so the EV order does not matter there); the w0 plan keeps
+        the caller's order (get_w0_price0 returns w0 per EV)."""
         torch = _torch()
         B = int(gamma.numel())
         central = 1 if self._rank() == 0 else 0
+        gamma = gamma.reshape(-1).to(dtype=torch.float64).contiguous()
         self._gam = torch.empty(B + central, dtype=torch.float64, device=self._dev)
-        self._gam[:B] = gamma
+        self._gam[:B] = gamma if presorted else torch.sort(gamma).values
+        self._gam_w0 = gamma
         self._gcentral = None if not central else self._gam[B:]
         if central:
             self._gam[B] = float(self.gamma_sc)
@@ -236,7 +246,8 @@ class PriceSolver:
         # and re-targeted at every partition (lompc_plan_update: no allocation, no device sync).
         if self._plan is None:
             self._plan = BatchPlan(self.lompc, self._gam, off, w_ref=self._wr2, want_w=False, want_cost=False,
-                                   want_set=True, validate=False, warm_start=True)
+                                   want_set=True, validate=False, warm_start=True,
+                                   sorted_gamma=self.lompc.mode != "direct")
             comm = self._device_comm()
             if comm is not None:
                 self._plan.set_comm(comm)
@@ -267,8 +278,16 @@ class PriceSolver:
         lmbd_k, lmbd_k_new = np.zeros((3 * self.N)), np.zeros((3 * self.N))
         lmbd_k[: self.r] = self.prev_prices
         if PRINT_LEVEL < 2 and self._native_ok():  # the whole loop in one C-ABI call
-            return self._finish_prices(*self._native_loop(lmbd_k, lmbd_r, w_ref, A_bar, tol), lmbd_r, w_ref, A_bar,
-                                       tol, w0_err_bound)
+            if not self.profile_loops:
+                return self._finish_prices(*self._native_loop(lmbd_k, lmbd_r, w_ref, A_bar, tol), lmbd_r, w_ref,
+                                           A_bar, tol, w0_err_bound)
+            t0 = time.perf_counter()
+            res = self._native_loop(lmbd_k, lmbd_r, w_ref, A_bar, tol)
+            t1 = time.perf_counter()
+            out = self._finish_prices(*res, lmbd_r, w_ref, A_bar, tol, w0_err_bound)
+            self.loop_host_ms["native_loop"] += (t1 - t0) * 1e3
+            self.loop_host_ms["finish_prices"] += (time.perf_counter() - t1) * 1e3
+            return out
         phi_w_ref = self.lompc.phi(w_ref)
         # one engine call: the batch error at lmbd_k and the central solve (price_solver.py:106)
         errs, (w_k, dual_cost) = self._iterate(lmbd_k, lmbd_r, w_ref, A_bar)
@@ -502,10 +521,10 @@ class PriceSolver:
         B = self._B
         if B and not self._w0_live:
             if self._plan_w0 is None:
-                self._plan_w0 = BatchPlan(self.lompc, self._gam[:B], np.array([0, B], dtype=np.int64), want_w=False,
+                self._plan_w0 = BatchPlan(self.lompc, self._gam_w0, np.array([0, B], dtype=np.int64), want_w=False,
                                           want_cost=False, want_w0=True, want_set=True, validate=False)
             else:
-                self._plan_w0.update(self._gam[:B], np.array([0, B], dtype=np.int64), validate=False)
+                self._plan_w0.update(self._gam_w0, np.array([0, B], dtype=np.int64), validate=False)
             self._w0_live = True
         if B:
             out = self._plan_w0.run(self._lm2[:1], self._lr2[:1])

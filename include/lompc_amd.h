@@ -172,6 +172,12 @@ typedef struct lompc_plan lompc_plan;
                                       set's last-arriving workgroup, instead of the k_finalize
                                       launch, also in runs that write w rows (slower there, see
                                       DESIGN.md); runs without w output always close this way */
+#define LOMPC_PLAN_SORTED_GAMMA 16 /* every set's valid gamma is ascending (invalid values after them)
+                                      and gamma is not modified until the next lompc_plan_update:
+                                      runs with no per-EV output (w, cost, w0, status all NULL — a
+                                      price loop's) aggregate each certified piece's EVs from prefix
+                                      sums built at create / update (k_agg: work per run O(pieces),
+                                      not O(EVs)); a set found unsorted reports every EV failed */
 
 /* Build a plan over B EVs grouped by set (S = sum of sets_per_ctx sets):
  *   ctxs         host [n_ctx]   contexts (same N and device), n_ctx <= LOMPC_PLAN_MAX_CTX

@@ -55,7 +55,7 @@ def test_header_constants_match_python():
                  "LOMPC_STAT_MAX_ERR", "LOMPC_SET_STATS", "LOMPC_MAX_N", "LOMPC_MODE_DIRECT", "LOMPC_PLAN_MAX_CTX",
                  "LOMPC_PLAN_WARM_START", "LOMPC_ABI_VERSION", "LOMPC_PLAN_K_PATH", "LOMPC_PLAN_K_EVAL",
                  "LOMPC_PLAN_K_FINAL", "LOMPC_PLAN_KERNELS", "LOMPC_PLAN_DIAG_REPAIR",
-                 "LOMPC_PLAN_CLOSE_IN_EVAL", "LOMPC_COMM_ID_BYTES", "LOMPC_LOOP_PROF_ITERS", "LOMPC_LOOP_PROF_WALL",
+                 "LOMPC_PLAN_CLOSE_IN_EVAL", "LOMPC_PLAN_SORTED_GAMMA", "LOMPC_COMM_ID_BYTES", "LOMPC_LOOP_PROF_ITERS", "LOMPC_LOOP_PROF_WALL",
                  "LOMPC_LOOP_PROF_ISSUE", "LOMPC_LOOP_PROF_WAIT", "LOMPC_LOOP_PROF_GPU", "LOMPC_LOOP_PROF_STEP",
                  "LOMPC_LOOP_PROF_HOST", "LOMPC_LOOP_PROF", "LOMPC_LOOP_AHEAD"):
         m = re.search(rf"#define {name}\s+(\d+)", src)

@@ -450,3 +450,88 @@ def test_run_steps_matches_single_runs(gpu, want_w):
             assert torch.equal(out[key], ref.out[key]), key
     ms, n = plan.profile(read=True)
     assert n == (K + E - 1) // E and ms > 0.0
+
+
+@pytest.mark.parametrize("N", [24, 48])
+@pytest.mark.parametrize("diag_repair", [False, True])
+def test_sorted_gamma_aggregation(gpu, N, diag_repair):
+    """LOMPC_PLAN_SORTED_GAMMA: reductions-only runs aggregate each certified piece's EVs from
+    prefix sums over the gamma-sorted set (k_agg) instead of evaluating every EV.  The set sums,
+    costs, price0 sums, max A_bar errors and counts equal the full per-EV evaluation's (k_finalize
+    over the w rows) to 1e-11 and the oracle's per-EV sums to 1e-9; sets: empty, one EV, one
+    wave, clustered (duplicate gammas), 300 000 EVs, gammas at the box bounds, and invalid
+    gammas after the valid ones (counted, AssertionError).  diag_repair: no certified pieces, every
+    EV takes the individual re-solve path of k_agg.  An unsorted set reports all its EVs failed."""
+    rng = np.random.default_rng(500 + N + diag_repair)
+    cs = [O.small_consts(), O.large_consts()]
+    lompcs = [mk(c, N) for c in cs]
+    small = diag_repair  # the re-solve path: keep it short
+    sizes = [[0, 1, 64, 3000], [2000, 0, 1500, 7]] if small else [[0, 1, 64, 300000], [20000, 0, 1500, 7]]
+    parts = []
+    for k, c in enumerate(cs):
+        for j, m in enumerate(sizes[k]):
+            g = c.y_max * rng.random(m)
+            if m == 1500:
+                g = np.repeat(c.y_max * rng.random(50), 30)  # clustered, duplicates
+            if m >= 2000:
+                g[:5] = 0.0
+                g[5:10] = c.y_max
+            parts.append(np.sort(g))
+    off = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.int64)
+    P = len(sizes[0])
+    gn = np.concatenate(parts)
+    g = torch.as_tensor(gn, device="cuda:0")
+    lm = torch.as_tensor(np.concatenate([c.theta * rng.random((P, 3 * N)) for c in cs]), device="cuda:0")
+    lr = torch.as_tensor(np.concatenate([[0.0, 0.3, 0.0, 0.1]] * 2), device="cuda:0")
+    wr = torch.as_tensor(np.concatenate([c.w_max * rng.random((P, N)) for c in cs]), device="cuda:0")
+    kw = dict(sets_per_ctx=[P, P], w_ref=wr, diag_repair=diag_repair)
+    agg = BatchPlan(lompcs, g, off, want_w=False, want_cost=False, sorted_gamma=True, **kw)
+    full = BatchPlan(lompcs, g, off, want_w=True, want_cost=True, **kw)
+    assert agg.launches_per_run() == 2
+    oa = {k: v.clone() for k, v in agg.run(lm, lr).items() if v is not None}
+    of = full.run(lm, lr)
+    ra, fa, ia = agg.check()
+    rf, ff, i_f = full.check()
+    assert (fa, ia) == (0, 0) and (ff, i_f) == (0, 0) and ra == rf
+    if diag_repair:
+        assert ra == len(gn)
+    np.testing.assert_allclose(oa["set_sum_w"].cpu().numpy(), of["set_sum_w"].cpu().numpy(), rtol=1e-11, atol=1e-9)
+    sa, sf = oa["set_stats"].cpu().numpy(), of["set_stats"].cpu().numpy()
+    np.testing.assert_array_equal(sa[:, _lib.LOMPC_STAT_COUNT], np.diff(off))
+    np.testing.assert_allclose(sa, sf, rtol=1e-11, atol=1e-9)
+    w, cost = of["w"].cpu().numpy(), of["cost"].cpu().numpy()
+    for s in range(2 * P):
+        a, b = off[s], off[s + 1]
+        if b == a:
+            continue
+        c = cs[s // P]
+        wo, co, nf = oracle_c.solve_batch(N, c, lm[s].cpu().numpy(), float(lr[s]), gn[a:b])
+        assert nf == 0
+        np.testing.assert_allclose(oa["set_sum_w"][s].cpu().numpy(), wo.sum(0), rtol=1e-10, atol=1e-9)
+        assert abs(sa[s, _lib.LOMPC_STAT_SUM_COST] - co.sum()) <= 1e-10 * max(1.0, abs(co.sum()))
+    # repeated runs at other prices through the same prefix sums
+    lm2 = lm.flip(1).contiguous()
+    oa2 = agg.run(lm2, lr)
+    of2 = full.run(lm2, lr)
+    assert agg.check()[1:] == (0, 0) and full.check()[1:] == (0, 0)
+    np.testing.assert_allclose(oa2["set_stats"].cpu().numpy(), of2["set_stats"].cpu().numpy(), rtol=1e-11, atol=1e-9)
+    if small:
+        return
+    # invalid gammas after the valid ones: counted; an unsorted set: every EV failed
+    g2 = gn.copy()
+    e = off[P + 1]  # end of the second type's first set
+    g2[e - 3:e] = [np.nan, -1.0, 7.0]
+    bad = BatchPlan(lompcs, torch.as_tensor(g2, device="cuda:0"), off, want_w=False, want_cost=False,
+                    sorted_gamma=True, validate=False, **kw)
+    ob = bad.run(lm, lr)
+    with pytest.raises(AssertionError):
+        bad.check()
+    assert ob["set_stats"].cpu().numpy()[P, _lib.LOMPC_STAT_N_INVALID] == 3
+    g3 = gn.copy()
+    g3[off[3] + 10], g3[off[3] + 11] = g3[off[3] + 11], g3[off[3] + 10] + 1e-3
+    uns = BatchPlan(lompcs, torch.as_tensor(g3, device="cuda:0"), off, want_w=False, want_cost=False,
+                    sorted_gamma=True, **kw)
+    ou = uns.run(lm, lr)
+    with pytest.raises(Exception):
+        uns.check()
+    assert ou["set_stats"].cpu().numpy()[3, _lib.LOMPC_STAT_N_FAILED] == off[4] - off[3]

@@ -901,7 +901,7 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
   // reference accepts Clarabel's "optimal_inaccurate" silently, lompc.py / bimpc.py never check status)
   std::vector<double> zb(n), llob(n), lhib(n), lgb(mg), sgb(mg);
   double best_merit = INFINITY, bpres = 0, bdres = 0, bgap = 0, bf = 0;
-  int since_best = 0;
+  int since_best = 0, spikes = 0;
   for (it = 0; it < max_iter; ++it) {
     const double mu = residuals();
     double merit = std::max({pres / (1.0 + hmax), dres / (1.0 + gmax), gap / (1.0 + std::fabs(fval))});
@@ -920,13 +920,17 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
       bgap = gap;
       bf = fval;
       since_best = 0;
+      spikes = 0;
     } else if (++since_best >= 15) {
       break;
     } else if (best_merit < 1e-6 && merit > 1e3 * best_merit) {
       // breakdown next to the optimum (the exp weights' flat directions: the Newton steps lose
-      // accuracy, the step length collapses and the residuals blow up): the iterates do not
-      // come back, the best one is returned as below
-      break;
+      // accuracy, the step length collapses and the residuals blow up): once it persists for 3
+      // iterations the iterates do not come back, the best one is returned as below (a single
+      // transient spike keeps iterating)
+      if (++spikes >= 3) break;
+    } else {
+      spikes = 0;
     }
     if (pres <= 1e-10 * (1.0 + hmax) && dres <= 1e-9 * (1.0 + gmax) && gap <= 1e-10 * (1.0 + std::fabs(fval))) {
       status = LOMPC_OK;

@@ -31,15 +31,41 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(os.path.join(CSRC, d)) <= t for d in DEPS)
 
 
+def _compile(src: str, obj: str, flags: list, verbose: bool) -> None:
+    cmd = [_hipcc()] + flags + ["-c", os.path.join(CSRC, src), "-o", obj + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(obj + ".tmp", obj)
+
+
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines: tuple = ()) -> str:
-    """Compile the extension; ``defines`` (e.g. ("LOMPC_K1_STATS",)) builds a diagnostic
-    variant into ``out`` (never the product library)."""
+    """Compile the extension (one object per source, in parallel, then one link); ``defines``
+    (e.g. ("LOMPC_K1_STATS",)) builds a diagnostic variant into ``out`` (never the product
+    library)."""
     if not force and out == OUT and up_to_date():
         return OUT
+    flags = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wno-unused-result"] + \
+        [f"-D{d}" for d in defines]
+    tag = "_".join(d.replace("=", "-") for d in defines) or "product"
+    odir = os.path.join(ROOT, "build", tag)
+    os.makedirs(odir, exist_ok=True)
+    deps_t = max(os.path.getmtime(os.path.join(CSRC, d)) for d in DEPS)
+    objs, todo = [], []
+    for s in SOURCES:
+        o = os.path.join(odir, os.path.splitext(s)[0] + ".o")
+        objs.append(o)
+        if force or not os.path.exists(o) or os.path.getmtime(o) < deps_t:
+            todo.append((s, o))
+    if todo:
+        from concurrent.futures import ThreadPoolExecutor
+
+        jobs = max(1, min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+        with ThreadPoolExecutor(jobs) as ex:
+            for f in [ex.submit(_compile, s, o, flags, verbose) for s, o in todo]:
+                f.result()
     tmp = out + ".tmp"
-    cmd = [_hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result"] + [f"-D{d}" for d in defines] + \
-        [os.path.join(CSRC, s) for s in SOURCES] + ["-ldl", "-o", tmp]
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared"] + objs + ["-ldl", "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -223,7 +223,6 @@ __global__ __launch_bounds__(64) void k_central(QPConst q, CentralArgs pa) {
   lqw::WaveSet ws;
   ws.N = N;
   ws.lane = lane;
-  ws.rsrc = lane < N ? N - 1 - lane : lane;
   double l2 = 0.0;
   if (lane < N) {
     const double l1 = L[lane], l3 = L[2 * N + lane];
@@ -231,11 +230,8 @@ __global__ __launch_bounds__(64) void k_central(QPConst q, CentralArgs pa) {
     if (!(l1 >= 0.0 && l2 >= 0.0 && l3 >= 0.0)) atomicOr(pa.errflag, 1);
     ws.d_nat = 2.0 * lr * tt + 2.0 * q.q_scale * l3 + q.dsmall;
     ws.e_nat = q.theta * (l1 - l2);
-    const int tr = ws.rsrc;
-    ws.d_rev = 2.0 * lr * tt + 2.0 * q.q_scale * L[2 * N + tr] + q.dsmall;
-    ws.e_rev = q.theta * (L[tr] - L[N + tr]);
   } else {
-    ws.d_nat = ws.e_nat = ws.d_rev = ws.e_rev = 0.0;
+    ws.d_nat = ws.e_nat = 0.0;
   }
   const double wr_nat = (pa.w_ref && lane < N) ? pa.w_ref[(size_t)s * N + lane] : 0.0;
   const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);  // lompc.py:128

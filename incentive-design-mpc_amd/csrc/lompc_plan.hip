@@ -229,7 +229,6 @@ __device__ __forceinline__ void load_set(const QPConst& q, const double* __restr
   const double tt = q.theta * q.theta;
   ws.N = N;
   ws.lane = lane;
-  ws.rsrc = lane < N ? N - 1 - lane : lane;
   l2 = 0.0;
   bad = false;
   if (lane < N) {
@@ -238,11 +237,8 @@ __device__ __forceinline__ void load_set(const QPConst& q, const double* __restr
     bad = !(l1 >= 0.0 && l2 >= 0.0 && l3 >= 0.0);
     ws.d_nat = 2.0 * lr * tt + 2.0 * q.q_scale * l3 + q.dsmall;
     ws.e_nat = q.theta * (l1 - l2);
-    const int tr = ws.rsrc;
-    ws.d_rev = 2.0 * lr * tt + 2.0 * q.q_scale * L[2 * N + tr] + q.dsmall;
-    ws.e_rev = q.theta * (L[tr] - L[N + tr]);
   } else {
-    ws.d_nat = ws.e_nat = ws.d_rev = ws.e_rev = 0.0;
+    ws.d_nat = ws.e_nat = 0.0;
   }
 }
 

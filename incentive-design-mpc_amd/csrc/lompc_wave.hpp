@@ -9,10 +9,10 @@
 //   (2) p_t  = al_t p_{t+1} + be_t   affine map    (given P_{t+1})
 //   (3) y_t  = (1+K_t) y_{t-1} + k_t affine map    forward, w_t = K_t y_{t-1} + k_t
 //
-// (1) and (2) run as prefix scans in the REVERSED layout (lane l = stage N-1-l),
-// (3) in the natural layout; one ds_bpermute round moves the per-stage gains
-// between layouts.  Scans use DPP row_shr 1/2/4/8 + row_bcast 15/31 (gfx9-family
-// cross-lane moves at ALU latency).  The multiplier of coordinate t comes from
+// All three run in the natural layout: (1) and (2) as SUFFIX scans (DPP row_shl 1/2/4/8 inside
+// each 16-lane row, then the rows' totals carried down by v_readlane: scalar broadcasts, no LDS
+// round trip), (3) as a prefix scan (DPP row_shr 1/2/4/8 + row_bcast 15/31).  The per-stage gains
+// of (1)-(2) are then already on the lanes (3) needs.  The multiplier of coordinate t comes from
 // the cost-to-go derivative (envelope theorem), so no fourth scan is needed:
 //   r_t = c (y_t - gamma) + P_{t+1} y_t + p_{t+1} + d_t w_t + e_t .
 #pragma once
@@ -45,6 +45,15 @@ __device__ __forceinline__ double dpp(double old, double x) {
 }
 // value of lane l-1 (lane 0 gets `old`): DPP wave_shr:1
 __device__ __forceinline__ double shr1(double old, double x) { return dpp<0x138, 0xf>(old, x); }
+// value of lane l+1 (lane 63 gets `old`): DPP wave_shl:1
+__device__ __forceinline__ double shl1(double old, double x) { return dpp<0x130, 0xf>(old, x); }
+
+__device__ __forceinline__ double readlane_d(double x, int lane) {
+  const long long xi = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_readlane((int)xi, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(xi >> 32), lane);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
 
 struct Mob {  // Moebius map P -> (a P + b) / (c P + d), entries >= 0
   double a, b, c, d;
@@ -60,6 +69,9 @@ struct Mob {  // Moebius map P -> (a P + b) / (c P + d), entries >= 0
   __device__ __forceinline__ Mob from() const {  // DPP source, identity where no source lane
     return {dpp<CTRL, ROW_MASK>(1.0, a), dpp<CTRL, ROW_MASK>(0.0, b), dpp<CTRL, ROW_MASK>(0.0, c),
             dpp<CTRL, ROW_MASK>(1.0, d)};
+  }
+  __device__ __forceinline__ Mob rl(int l) const {  // lane l's value, wave-uniform
+    return {readlane_d(a, l), readlane_d(b, l), readlane_d(c, l), readlane_d(d, l)};
   }
 };
 
@@ -89,6 +101,13 @@ struct Aff {  // y -> A y + B[k]
     for (int k = 0; k < NB; ++k) r.B[k] = dpp<CTRL, ROW_MASK>(0.0, B[k]);
     return r;
   }
+  __device__ __forceinline__ Aff rl(int l) const {
+    Aff r;
+    r.A = readlane_d(A, l);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) r.B[k] = readlane_d(B[k], l);
+    return r;
+  }
 };
 
 // Inclusive prefix scan across the lanes [0, n) (lane order = application order);
@@ -106,9 +125,49 @@ __device__ __forceinline__ T wave_scan(T x, int n = 64) {
   return x;
 }
 
+// Inclusive SUFFIX scan across the lanes [0, n): lane l holds x_l o x_{l+1} o ... (the highest
+// lane applied first); lanes >= n hold identities.  DPP row_shl 1/2/4/8 scans each 16-lane row
+// backwards, then every row below the last one combines with the totals of the rows above it,
+// read from their first lanes with v_readlane (wave-uniform, no LDS).
+template <typename T>
+__device__ __forceinline__ T wave_scan_rev(T x, int n = 64) {
+  x = T::combine(x.template from<0x101, 0xf>(), x);  // row_shl:1
+  x = T::combine(x.template from<0x102, 0xf>(), x);  // row_shl:2
+  x = T::combine(x.template from<0x104, 0xf>(), x);  // row_shl:4
+  x = T::combine(x.template from<0x108, 0xf>(), x);  // row_shl:8
+  if (n > 16) {
+    const int row = (int)(threadIdx.x & 63) >> 4;
+    const T t1 = x.rl(16);
+    T c0 = t1, c1 = T::identity(), c2 = T::identity();
+    if (n > 32) {
+      const T t2 = x.rl(32);
+      c1 = t2;
+      if (n > 48) {
+        c2 = x.rl(48);
+        c1 = T::combine(c2, t2);
+      }
+      c0 = T::combine(c1, t1);
+    }
+    x = T::combine(row == 0 ? c0 : (row == 1 ? c1 : (row == 2 ? c2 : T::identity())), x);
+  }
+  return x;
+}
+
 template <int K>
 struct Sums {  // K independent running sums
   double v[K];
+  __device__ __forceinline__ static Sums identity() {
+    Sums r;
+#pragma unroll
+    for (int k = 0; k < K; ++k) r.v[k] = 0.0;
+    return r;
+  }
+  __device__ __forceinline__ Sums rl(int l) const {
+    Sums r;
+#pragma unroll
+    for (int k = 0; k < K; ++k) r.v[k] = readlane_d(v[k], l);
+    return r;
+  }
   __device__ __forceinline__ static Sums combine(const Sums& L, const Sums& R) {
     Sums r;
 #pragma unroll
@@ -123,13 +182,6 @@ struct Sums {  // K independent running sums
     return r;
   }
 };
-
-__device__ __forceinline__ double readlane_d(double x, int lane) {
-  const long long xi = __builtin_bit_cast(long long, x);
-  const int lo = __builtin_amdgcn_readlane((int)xi, lane);
-  const int hi = __builtin_amdgcn_readlane((int)(xi >> 32), lane);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
-}
 
 // totals over lanes [0, n) of K values (lanes >= n must hold 0), broadcast
 template <int K>
@@ -180,18 +232,15 @@ __device__ __forceinline__ double wave_sum(double v, int n) {
   return readlane_d(wave_scan(x, n).v[0], n - 1);
 }
 
-// Per-set stage data of one wave: lane t holds stage t (natural) and stage N-1-t (reversed).
+// Per-set stage data of one wave: lane t holds stage t.
 struct WaveSet {
-  int N, lane, rsrc;
-  double d_nat, e_nat, d_rev, e_rev;
+  int N, lane;
+  double d_nat, e_nat;
   __device__ __forceinline__ void load(const double* __restrict__ sd, int N_) {
     N = N_;
     lane = threadIdx.x & 63;
-    rsrc = lane < N ? N - 1 - lane : lane;
     d_nat = lane < N ? sd[lane] : 0.0;
     e_nat = lane < N ? sd[N + lane] : 0.0;
-    d_rev = lane < N ? sd[rsrc] : 0.0;
-    e_rev = lane < N ? sd[N + rsrc] : 0.0;
   }
 };
 
@@ -204,65 +253,55 @@ struct StageSol {
 };
 
 template <int NB>
-__device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const WaveSet& ws, double gamma, int s_nat) {
+__device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const WaveSet& ws, double gamma, int s) {
   const double c = q.c;
   const int N = ws.N;
   const int lane = ws.lane;
   const bool act = lane < N;
-  const int s_rev = bperm_i(ws.rsrc, s_nat);
-  const Box br = lq_box(act ? s_rev : 0);
-  const double d_rev = ws.d_rev;
-  // ---- (1) Moebius scan, reversed layout (lane l = stage N-1-l)
-  const bool fr = act && (s_rev & 1);
+  const Box bx = lq_box(act ? s : 0);
+  const double d = ws.d_nat;
+  // ---- (1) Moebius suffix scan: lane t = F_t o ... o F_{N-1}
+  const bool fr = act && (s & 1);
   Mob f = Mob::identity();
   if (fr) {  // P -> d (c+P) / (c+P+d), scaled to d-entry 1
-    const double u = lq_rcp(c + d_rev);
-    f = {d_rev * u, d_rev * c * u, u, 1.0};
+    const double u = lq_rcp(c + d);
+    f = {d * u, d * c * u, u, 1.0};
   } else if (act) {
     f = {1.0, c, 0.0, 1.0};  // P -> c + P
   }
-  const Mob T = wave_scan(f, N);
+  const Mob T = wave_scan_rev(f, N);
   const double P_here = T.b * lq_rcp(T.d);          // P_t = T_t(0)
-  const double P_next = shr1(0.0, P_here);          // P_{t+1}
-  // ---- (2) affine scan for p
+  const double P_next = shl1(0.0, P_here);          // P_{t+1}
+  // ---- (2) affine suffix scan for p
   const double Q = c + P_next;
-  const double iv = lq_rcp(Q + d_rev);
-  const double et = ws.e_rev + br.slo;
+  const double iv = lq_rcp(Q + d);
+  const double et = ws.e_nat + bx.slo;
   Aff<NB> g = Aff<NB>::identity();
   if (fr) {
-    g.A = d_rev * iv;
-    if (NB == 1) g.B[0] = -(c * gamma * d_rev + et * Q) * iv;
+    g.A = d * iv;
+    if (NB == 1) g.B[0] = -(c * gamma * d + et * Q) * iv;
     else {
       g.B[0] = -et * Q * iv;
-      g.B[NB - 1] = -c * d_rev * iv;
+      g.B[NB - 1] = -c * d * iv;
     }
   } else if (act) {
-    if (NB == 1) g.B[0] = fma(Q, br.lo, -c * gamma);
+    if (NB == 1) g.B[0] = fma(Q, bx.lo, -c * gamma);
     else {
-      g.B[0] = Q * br.lo;
+      g.B[0] = Q * bx.lo;
       g.B[NB - 1] = -c;
     }
   }
-  const Aff<NB> Gp = wave_scan(g, N);
-  double p_next[NB];
+  const Aff<NB> Gp = wave_scan_rev(g, N);
+  double pn[NB];
 #pragma unroll
-  for (int k = 0; k < NB; ++k) p_next[k] = shr1(0.0, Gp.B[k]);
-  const double Kr = fr ? -Q * iv : 0.0;
-  double kr[NB];
+  for (int k = 0; k < NB; ++k) pn[k] = shl1(0.0, Gp.B[k]);  // p_{t+1}
+  const double K = fr ? -Q * iv : 0.0;
+  double kk[NB];
   if (NB == 1) {
-    kr[0] = fr ? -(p_next[0] - c * gamma + et) * iv : br.lo;
+    kk[0] = fr ? -(pn[0] - c * gamma + et) * iv : bx.lo;
   } else {
-    kr[0] = fr ? -(p_next[0] + et) * iv : br.lo;
-    kr[NB - 1] = fr ? -(p_next[NB - 1] - c) * iv : 0.0;
-  }
-  // ---- reversed -> natural layout (lane t reads lane N-1-t)
-  const double K = bperm(ws.rsrc, Kr);
-  const double Pn = bperm(ws.rsrc, P_next);
-  double kk[NB], pn[NB];
-#pragma unroll
-  for (int k = 0; k < NB; ++k) {
-    kk[k] = bperm(ws.rsrc, kr[k]);
-    pn[k] = bperm(ws.rsrc, p_next[k]);
+    kk[0] = fr ? -(pn[0] + et) * iv : bx.lo;
+    kk[NB - 1] = fr ? -(pn[NB - 1] - c) * iv : 0.0;
   }
   // ---- (3) forward scan y_t = (1+K_t) y_{t-1} + k_t
   Aff<NB> h = Aff<NB>::identity();
@@ -279,7 +318,7 @@ __device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const Wave
     const double yp = shr1(0.0, y);
     out.w[k] = fma(K, yp, kk[k]);
     const double base = (NB == 1) ? ws.e_nat - c * gamma : (k == 0 ? ws.e_nat : -c);
-    out.r[k] = fma(c + Pn, y, pn[k]) + fma(ws.d_nat, out.w[k], base);
+    out.r[k] = fma(c + P_next, y, pn[k]) + fma(d, out.w[k], base);
   }
   return out;
 }
@@ -417,6 +456,7 @@ struct MobF {
     return {dppf<CTRL, ROW_MASK>(1.f, a), dppf<CTRL, ROW_MASK>(0.f, b), dppf<CTRL, ROW_MASK>(0.f, c),
             dppf<CTRL, ROW_MASK>(1.f, d)};
   }
+  __device__ __forceinline__ MobF rl(int l) const;
 };
 struct AffF {
   float A, B;
@@ -426,51 +466,53 @@ struct AffF {
   __device__ __forceinline__ AffF from() const {
     return {dppf<CTRL, ROW_MASK>(1.f, A), dppf<CTRL, ROW_MASK>(0.f, B)};
   }
+  __device__ __forceinline__ AffF rl(int l) const;
 };
 __device__ __forceinline__ float shr1f(float old, float x) { return dppf<0x138, 0xf>(old, x); }
-__device__ __forceinline__ float bpermf(int src_lane, float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_lane << 2, __builtin_bit_cast(int, x)));
+__device__ __forceinline__ float readlane_f(float x, int l);
+__device__ __forceinline__ MobF MobF::rl(int l) const {
+  return {readlane_f(a, l), readlane_f(b, l), readlane_f(c, l), readlane_f(d, l)};
+}
+__device__ __forceinline__ AffF AffF::rl(int l) const { return {readlane_f(A, l), readlane_f(B, l)}; }
+__device__ __forceinline__ float shl1f(float old, float x) { return dppf<0x130, 0xf>(old, x); }
+__device__ __forceinline__ float readlane_f(float x, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
 
 // solve_stage<1> in fp32 (same recursions, see the file header)
-__device__ __forceinline__ void solve_stage_f32(const QPConst& q, const WaveSet& ws, float gamma, int s_nat,
+__device__ __forceinline__ void solve_stage_f32(const QPConst& q, const WaveSet& ws, float gamma, int s,
                                                 float& w_out, float& r_out) {
   const float c = (float)q.c;
   const int N = ws.N;
   const int lane = ws.lane;
   const bool act = lane < N;
-  const int s_rev = bperm_i(ws.rsrc, s_nat);
-  const BoxF br = lq_boxf(act ? s_rev : 0);
-  const float d_rev = (float)ws.d_rev;
-  const bool fr = act && (s_rev & 1);
+  const BoxF bx = lq_boxf(act ? s : 0);
+  const float d = (float)ws.d_nat;
+  const bool fr = act && (s & 1);
   MobF f = MobF::identity();
   if (fr) {
-    const float u = __builtin_amdgcn_rcpf(c + d_rev);
-    f = {d_rev * u, d_rev * c * u, u, 1.f};
+    const float u = __builtin_amdgcn_rcpf(c + d);
+    f = {d * u, d * c * u, u, 1.f};
   } else if (act) {
     f = {1.f, c, 0.f, 1.f};
   }
-  const MobF T = wave_scan(f, N);
+  const MobF T = wave_scan_rev(f, N);
   const float P_here = T.b * __builtin_amdgcn_rcpf(T.d);
-  const float P_next = shr1f(0.f, P_here);
+  const float P_next = shl1f(0.f, P_here);
   const float Q = c + P_next;
-  const float iv = __builtin_amdgcn_rcpf(Q + d_rev);
-  const float et = (float)ws.e_rev + br.slo;
+  const float iv = __builtin_amdgcn_rcpf(Q + d);
+  const float et = (float)ws.e_nat + bx.slo;
   AffF g = AffF::identity();
   if (fr) {
-    g.A = d_rev * iv;
-    g.B = -(c * gamma * d_rev + et * Q) * iv;
+    g.A = d * iv;
+    g.B = -(c * gamma * d + et * Q) * iv;
   } else if (act) {
-    g.B = fmaf(Q, br.lo, -c * gamma);
+    g.B = fmaf(Q, bx.lo, -c * gamma);
   }
-  const AffF Gp = wave_scan(g, N);
-  const float p_next = shr1f(0.f, Gp.B);
-  const float Kr = fr ? -Q * iv : 0.f;
-  const float kr = fr ? -(p_next - c * gamma + et) * iv : br.lo;
-  const float K = bpermf(ws.rsrc, Kr);
-  const float Pn = bpermf(ws.rsrc, P_next);
-  const float kk = bpermf(ws.rsrc, kr);
-  const float pn = bpermf(ws.rsrc, p_next);
+  const AffF Gp = wave_scan_rev(g, N);
+  const float pn = shl1f(0.f, Gp.B);
+  const float K = fr ? -Q * iv : 0.f;
+  const float kk = fr ? -(pn - c * gamma + et) * iv : bx.lo;
   AffF h = AffF::identity();
   if (act) {
     h.A = 1.f + K;
@@ -479,7 +521,7 @@ __device__ __forceinline__ void solve_stage_f32(const QPConst& q, const WaveSet&
   const AffF Y = wave_scan(h, N);
   const float yp = shr1f(0.f, Y.B);
   w_out = fmaf(K, yp, kk);
-  r_out = fmaf(c + Pn, Y.B, pn) + fmaf((float)ws.d_nat, w_out, (float)ws.e_nat - c * gamma);
+  r_out = fmaf(c + P_next, Y.B, pn) + fmaf(d, w_out, (float)ws.e_nat - c * gamma);
 }
 
 // fp32 PDAS on the working set s (jump moves first, as wave_pdas), relative tolerances at fp32

@@ -79,6 +79,16 @@ struct CtxEnds {  // cumulative set counts of a plan's contexts (a kernel argume
   int end[LQ_PLAN_MAX_CTX];
 };
 
+// one copy of the path table (k_path writes it, k_eval / k_agg / k_finalize read it)
+struct PathTab {
+  int* cnt = nullptr;
+  double* lo = nullptr;
+  double* ge = nullptr;
+  double* cf = nullptr;
+  double2* ab = nullptr;
+  uint8_t* sl = nullptr;
+};
+
 struct lompc_plan {
   int device = 0;
   int N = 0;
@@ -121,6 +131,12 @@ struct lompc_plan {
   double2* t_ab = nullptr;
   uint8_t* t_sl = nullptr;
   uint8_t* d_ws = nullptr;        // [S*G][64] working set at each cell start (warm start)
+  // pipelined lompc_plan_run_steps: a second path table, the path kernels on their own stream,
+  // run k + 1's path overlapping run k's evaluation (events order the two tables' reuse)
+  PathTab alt{};
+  int64_t cap_alt = 0;
+  hipStream_t st_path = nullptr;
+  hipEvent_t ev_go = nullptr, ev_path[2] = {nullptr, nullptr}, ev_eval[2] = {nullptr, nullptr};
   int* d_errflag = nullptr;
   unsigned long long* d_tally = nullptr;  // [3] EVs repaired / failed / invalid over every run since
                                           // the last lompc_plan_status (sticky, read and zeroed there)

@@ -31,8 +31,14 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(os.path.join(CSRC, d)) <= t for d in DEPS)
 
 
+# host-only sources (the BiMPC interior point, the price QP, RCCL glue): AVX2 + FMA, which every
+# x86-64 host of an MI355X node has
+HOST_FLAGS = ["-mavx2", "-mfma"]
+
+
 def _compile(src: str, obj: str, flags: list, verbose: bool) -> None:
-    cmd = [_hipcc()] + flags + ["-c", os.path.join(CSRC, src), "-o", obj + ".tmp"]
+    extra = HOST_FLAGS if src.endswith(".cpp") else []
+    cmd = [_hipcc()] + flags + extra + ["-c", os.path.join(CSRC, src), "-o", obj + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

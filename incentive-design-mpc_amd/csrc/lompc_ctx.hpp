@@ -131,12 +131,6 @@ struct lompc_plan {
   double2* t_ab = nullptr;
   uint8_t* t_sl = nullptr;
   uint8_t* d_ws = nullptr;        // [S*G][64] working set at each cell start (warm start)
-  // pipelined lompc_plan_run_steps: a second path table, the path kernels on their own stream,
-  // run k + 1's path overlapping run k's evaluation (events order the two tables' reuse)
-  PathTab alt{};
-  int64_t cap_alt = 0;
-  hipStream_t st_path = nullptr;
-  hipEvent_t ev_go = nullptr, ev_path[2] = {nullptr, nullptr}, ev_eval[2] = {nullptr, nullptr};
   int* d_errflag = nullptr;
   unsigned long long* d_tally = nullptr;  // [3] EVs repaired / failed / invalid over every run since
                                           // the last lompc_plan_status (sticky, read and zeroed there)

@@ -1592,52 +1592,6 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   return lq_launch_eval(p, lmbd, lmbd_r, w, cost, w0, status, set_sum_w, set_stats, tb, st, prof_ctx);
 }
 
-// K independent runs (lompc_plan_run_steps), pipelined: run k's path on the plan's path stream into
-// table k % 2 while run k - 1's evaluation reads the other table on the caller's stream.  Run k's
-// evaluation waits for its path; run k's path waits for run k - 2's evaluation (the table it
-// overwrites).  Same kernels, same inputs: the results equal the sequential runs' bit for bit.
-int lq_run_steps_pipelined(lompc_plan* p, const double* lmbd, int64_t lmbd_stride, const double* lmbd_r,
-                           int64_t lmbd_r_stride, int n_runs, int profile_every, double* w, double* cost, double* w0,
-                           int8_t* status, double* set_sum_w, double* set_stats, hipStream_t st) {
-  const int64_t ncell = p->S * p->G;
-  int rc;
-  if (ncell > p->cap_alt) {
-    if ((rc = grow(p, &p->alt.cnt, ncell)) || (rc = grow(p, &p->alt.lo, ncell)) ||
-        (rc = grow(p, &p->alt.ge, ncell * LQ_PPL)) || (rc = grow(p, &p->alt.cf, ncell * LQ_PPL * 8)) ||
-        (rc = grow(p, &p->alt.ab, ncell * LQ_PPL * p->N)) || (rc = grow(p, &p->alt.sl, ncell * 64)))
-      return rc;
-    p->cap_alt = ncell;
-  }
-  if (!p->st_path) {
-    int lo = 0, hi = 0;
-    HIPCHK(p, hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIPCHK(p, hipStreamCreateWithPriority(&p->st_path, hipStreamNonBlocking, hi));  // the latency-bound chain first
-    HIPCHK(p, hipEventCreateWithFlags(&p->ev_go, hipEventDisableTiming));
-    for (int b = 0; b < 2; ++b) {
-      HIPCHK(p, hipEventCreateWithFlags(&p->ev_path[b], hipEventDisableTiming));
-      HIPCHK(p, hipEventCreateWithFlags(&p->ev_eval[b], hipEventDisableTiming));
-    }
-  }
-  const PathTab tabs[2] = {own_tab(p), p->alt};
-  HIPCHK(p, hipEventRecord(p->ev_go, st));  // the path stream after the caller's earlier work
-  HIPCHK(p, hipStreamWaitEvent(p->st_path, p->ev_go, 0));
-  const int mask = p->prof;
-  for (int k = 0; k < n_runs; ++k) {
-    const int b = k & 1;
-    if (profile_every > 0) p->prof = (k % profile_every == 0) ? mask : 0;
-    const double* lm = lmbd + (size_t)k * lmbd_stride;
-    const double* lr = lmbd_r + (size_t)k * lmbd_r_stride;
-    if (k >= 2) HIPCHK(p, hipStreamWaitEvent(p->st_path, p->ev_eval[b], 0));
-    if ((rc = lq_launch_path(p, lm, lr, tabs[b], p->st_path))) break;
-    HIPCHK(p, hipEventRecord(p->ev_path[b], p->st_path));
-    HIPCHK(p, hipStreamWaitEvent(st, p->ev_path[b], 0));
-    if ((rc = lq_launch_eval(p, lm, lr, w, cost, w0, status, set_sum_w, set_stats, tabs[b], st, nullptr))) break;
-    HIPCHK(p, hipEventRecord(p->ev_eval[b], st));
-  }
-  p->prof = mask;
-  return rc;
-}
-
 void lq_plan_free(lompc_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
@@ -1645,13 +1599,9 @@ void lq_plan_free(lompc_plan* p) {
   void* ptrs[] = {p->d_meta,  p->d_stats_own, p->d_window, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
                   p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag,
                   p->d_fail_cnt, p->d_fail_idx, p->d_tally, p->d_wacc, p->d_arrive, p->d_xsend, p->d_xrecv, p->d_loop,
-                  p->d_bsum, p->d_P, p->d_pos, p->d_sinfo,
-                  p->alt.cnt, p->alt.lo, p->alt.ge, p->alt.cf, p->alt.ab, p->alt.sl};
+                  p->d_bsum, p->d_P, p->d_pos, p->d_sinfo};
   for (void* x : ptrs)
     if (x) (void)hipFree(x);
-  if (p->st_path) (void)hipStreamDestroy(p->st_path);
-  for (hipEvent_t e : {p->ev_go, p->ev_path[0], p->ev_path[1], p->ev_eval[0], p->ev_eval[1]})
-    if (e) (void)hipEventDestroy(e);
   if (p->h_buf) (void)hipHostFree(p->h_buf);
   if (p->h_loop) (void)hipHostFree(p->h_loop);
   if (p->h_dec) (void)hipHostFree(p->h_dec);
@@ -1848,12 +1798,6 @@ int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
                          int8_t* status, double* set_sum_w, double* set_stats, void* stream) {
   if (!p || n_runs < 0 || profile_every < 0) return LOMPC_ERR_INVALID_ARG;
   HIPCHK(p, hipSetDevice(p->device));
-  // independent runs overlap pairwise (the path chain is latency-bound, the evaluation HBM-bound);
-  // LOMPC_PIPELINE=0: one run after the other (diagnostics / A-B)
-  const char* pe = getenv("LOMPC_PIPELINE");
-  if (n_runs >= 2 && !p->skip && !(pe && atoi(pe) == 0))
-    return lq_run_steps_pipelined(p, lmbd, lmbd_stride, lmbd_r, lmbd_r_stride, n_runs, profile_every, w, cost, w0,
-                                  status, set_sum_w, set_stats, (hipStream_t)stream);
   const int mask = p->prof;
   int rc = LOMPC_OK;
   for (int k = 0; k < n_runs && rc == LOMPC_OK; ++k) {

@@ -327,6 +327,7 @@ class ChargingStation:
                 assert st_l[p, 2] >= 0 and st_l[p, 1] <= self.consts_l.y_max
                 beta_l[p], gamma_lm[p] = self._robustness(self.price_solver_l, st_l[p], lmbd_r)
         self._pstats = (st_s, st_l)
+        self._stage_partitions()
         Mp_s_ = Mp_s / self.B
         Mp_l_ = Mp_l / self.B
         demand = self.demand[self.t: self.t + self.N_bi] / self.B
@@ -378,9 +379,7 @@ class ChargingStation:
             kind, solver, y, idx, st, w_hat, prices, stats = chain
             if st[p, 0] > 0:
                 t0 = time.perf_counter() if prof else 0.0
-                ys, off = self._partition_layout(kind, y, idx)
-                solver.set_charge_levels_stats(ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3],
-                                               descending=True)
+                solver.use_partition(p)  # (staged before the BiMPC solve, _stage_partitions)
                 if PRINT_LEVEL >= 1 and self._rank0():
                     print(f"{kind} EVs, partition {p:2d}: ", end="")
                     if PRINT_LEVEL >= 2:
@@ -432,6 +431,21 @@ class ChargingStation:
                 for chain in chains:
                     one(chain, p)
         return prices_s, prices_l, stats_s, stats_l
+
+    def _stage_partitions(self):
+        """Every partition's loop plan of this step, prepared on the price solvers' streams before
+        the BiMPC solve (PriceSolver.stage_partition): the GPU builds them while the host runs the
+        interior point; the partitions' price loops then start at once.  (The partitions' levels
+        depend only on the state, not on the BiMPC.)"""
+        st_s, st_l = self._pstats
+        for kind, solver, y, idx, st in (("Small", self.price_solver_s, self.y_s, self.idx_s, st_s),
+                                         ("Large", self.price_solver_l, self.y_l, self.idx_l, st_l)):
+            ys, off = self._partition_layout(kind, y, idx)
+            solver._stream.wait_stream(_torch().cuda.current_stream(self.device))
+            for p in range(self.P):
+                if st[p, 0] > 0:
+                    solver.stage_partition(p, ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3],
+                                           descending=True)
 
     def _partition_layout(self, kind, y, idx):
         """This rank's EVs of one type grouped by partition, each partition in descending charge

@@ -103,6 +103,7 @@ class PriceSolver:
         self._plan = None
         self._plan_w0 = None
         self._w0_live = False
+        self._staged = {}  # partition -> its loop plan and levels (stage_partition / use_partition)
         self._A_bar = None
         self._A_bar_inv = None
         self._kappa = None
@@ -222,6 +223,37 @@ class PriceSolver:
         assert bad == 0  # price_solver.py:71 (0 <= y0 <= y_max on every rank)
         self.nEVs = n
         return y_hi, y_lo, y_mean
+
+    _PART_STATE = ("y0", "nEVs", "_y_hi", "_y_lo", "y0_rng", "gamma_sc", "gamma_sm", "_gam", "_gam_w0", "_gcentral",
+                   "_plan", "_B")
+
+    @_solver_stream
+    def stage_partition(self, p: int, y0d, n: int, y_hi: float, y_lo: float, y_sum: float,
+                        descending: bool = False) -> None:
+        """set_charge_levels_stats for partition p ahead of its price loop: the partition's own
+        loop plan is (re)prepared now, on the solver's stream, and kept with its levels until
+        use_partition(p).  ChargingStation stages every partition of a step before the BiMPC
+        solve, so the plans' device preparation overlaps the host interior point instead of
+        sitting in front of each partition's loop (every partition keeps its own warm start)."""
+        cur = {k: getattr(self, k, None) for k in self._PART_STATE}
+        st = self._staged.get(p)
+        if st is not None:  # the partition's plan from the previous step: re-targeted
+            for k in self._PART_STATE:
+                setattr(self, k, st[k])
+        else:
+            self._plan = None
+        try:
+            self.set_charge_levels_stats(y0d, n, y_hi, y_lo, y_sum, descending=descending)
+            self._staged[p] = {k: getattr(self, k) for k in self._PART_STATE}
+        finally:
+            for k in self._PART_STATE:
+                setattr(self, k, cur[k])
+
+    def use_partition(self, p: int) -> None:
+        """Make the plan and levels staged for partition p current (set_charge_levels done)."""
+        for k, v in self._staged[p].items():
+            setattr(self, k, v)
+        self._w0_live = False
 
     def _build_plans(self, gamma, presorted: bool = False) -> None:
         """Batch layout of one price iteration: set 0 = this rank's EVs, set 1 = the central QP.

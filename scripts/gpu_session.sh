@@ -36,7 +36,6 @@ for s in $STEPS; do
     bclose) LOMPC_CLOSE=1 run bclose 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct ;;
     qclose) LOMPC_CLOSE=1 run qclose 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_parity.py tests/test_gpu_baseline_configs.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sclose) LOMPC_CLOSE=1 run stamps_close 300 python scripts/kstamps.py ;;
-    bnopipe) LOMPC_PIPELINE=0 run bnopipe 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --no-direct ;;
     pipetest) run pipetest 600 python -u -m pytest tests/test_gpu_pipeline.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k run_steps ;;
     bench100q) run bench100q 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station ;;
     bsplit) run bsplit 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-station --split-types ;;

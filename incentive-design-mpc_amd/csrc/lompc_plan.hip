@@ -424,7 +424,13 @@ __global__ __launch_bounds__(64) void k_path(PathArgs a) {
   path_cell<NT, true>(a, (int)blockIdx.x);
 }
 
+// forward (defined with k_finalize below)
+struct FinalArgs;
+template <int NT>
+__global__ __launch_bounds__(64) void k_path_fin(PathArgs a, FinalArgs r);
+
 typedef void (*PathKernel)(PathArgs);
+typedef void (*PathKernel2)(PathArgs, FinalArgs);
 PathKernel path_kernel(int N) {
   switch (N) {
     case 12: return k_path<12>;
@@ -676,6 +682,33 @@ __global__ __launch_bounds__(256) void k_finalize(FinalArgs r) {
   __shared__ double rep[4][FIN_W];
   if (r.skip && *r.skip) return;
   finalize_set<4, false>(r, (int)blockIdx.x, red, rep);
+}
+
+// lompc_plan_run_steps: run k's path (workgroups [0, S G)) and run k - 1's closing (one one-wave
+// workgroup per set after them) in ONE launch — the two are independent (run k - 1's records
+// are complete at the kernel boundary behind its k_eval; run k's path writes the other half of
+// the cell-start working sets the closing's individual re-solves read), so every run after the
+// first costs two launches instead of three.
+template <int NT>
+__global__ __launch_bounds__(64) void k_path_fin(PathArgs a, FinalArgs r) {
+  const int b = (int)blockIdx.x, nc = a.S * a.G;
+  if (b < nc) {
+    path_cell<NT, true>(a, b);
+  } else {
+    __shared__ double red[1][FIN_W];
+    __shared__ double rep[1][FIN_W];
+    finalize_set<1, false>(r, b - nc, red, rep);
+  }
+}
+
+PathKernel2 path_fin_kernel(int N) {
+  switch (N) {
+    case 12: return k_path_fin<12>;
+    case 16: return k_path_fin<16>;
+    case 24: return k_path_fin<24>;
+    case 48: return k_path_fin<48>;
+    default: return k_path_fin<0>;
+  }
 }
 
 // Plans with a communicator: the all-gathered records recv[rank][S (N + 8)] of every rank combined
@@ -1285,7 +1318,7 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   if (ncell > p->cap_cells || (warm && !p->d_ws)) {
     if ((rc = grow(p, &p->t_cnt, ncell)) || (rc = grow(p, &p->t_lo, ncell)) ||
         (rc = grow(p, &p->t_ge, ncell * LQ_PPL)) || (rc = grow(p, &p->t_cf, ncell * LQ_PPL * 8)) ||
-        (rc = grow(p, &p->t_ab, ncell * LQ_PPL * N)) || (rc = grow(p, &p->t_sl, ncell * 64)))
+        (rc = grow(p, &p->t_ab, ncell * LQ_PPL * N)) || (rc = grow(p, &p->t_sl, 2 * ncell * 64)))
       return rc;
     if (warm && (rc = grow(p, &p->d_ws, (size_t)ncell * 64))) return rc;
     p->cap_cells = ncell;
@@ -1404,22 +1437,23 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   return LOMPC_OK;
 }
 
-PathTab own_tab(const lompc_plan* p) {
+// the plan's path table; `half` selects one of the two halves of the cell-start working sets
+// (run_steps alternates them: a run's closing may re-solve from its own while the next run's path
+// writes the other)
+PathTab own_tab(const lompc_plan* p, int half = 0) {
   PathTab t;
   t.cnt = p->t_cnt;
   t.lo = p->t_lo;
   t.ge = p->t_ge;
   t.cf = p->t_cf;
   t.ab = p->t_ab;
-  t.sl = p->t_sl;
+  t.sl = p->t_sl + (size_t)half * p->S * p->G * 64;
   return t;
 }
 
-// k_path of one run into the path table `tb`
-int lq_launch_path(lompc_plan* p, const double* lmbd, const double* lmbd_r, const PathTab& tb, hipStream_t st) {
-  if (!lmbd || !lmbd_r) return fail_arg(p, "run: lmbd and lmbd_r required");
-  const int N = p->N;
+PathArgs path_args(lompc_plan* p, const double* lmbd, const double* lmbd_r, const PathTab& tb) {
   PathArgs pa{};
+  const int N = p->N;
   pa.S = (int)p->S;
   pa.G = p->G;
   pa.N = N;
@@ -1439,9 +1473,22 @@ int lq_launch_path(lompc_plan* p, const double* lmbd, const double* lmbd_r, cons
   pa.t_ab = tb.ab;
   pa.errflag = p->d_errflag;
   pa.skip = p->skip;
+  return pa;
+}
+
+// k_path of one run into the path table `tb`; with `fin` (run_steps) the previous run's closing
+// rides in the same launch (k_path_fin)
+int lq_launch_path(lompc_plan* p, const double* lmbd, const double* lmbd_r, const PathTab& tb, hipStream_t st,
+                   const FinalArgs* fin = nullptr) {
+  if (!lmbd || !lmbd_r) return fail_arg(p, "run: lmbd and lmbd_r required");
+  const PathArgs pa = path_args(p, lmbd, lmbd_r, tb);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
-  hipExtLaunchKernelGGL(path_kernel(N), dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa);
+  const unsigned ncell = (unsigned)(p->S * p->G);
+  if (fin)
+    hipExtLaunchKernelGGL(path_fin_kernel(p->N), dim3(ncell + (unsigned)p->S), dim3(64), 0, st, e0, e1, 0, pa, *fin);
+  else
+    hipExtLaunchKernelGGL(path_kernel(p->N), dim3(ncell), dim3(64), 0, st, e0, e1, 0, pa);
   HIPCHK(p, hipGetLastError());
   plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
   return LOMPC_OK;
@@ -1449,9 +1496,12 @@ int lq_launch_path(lompc_plan* p, const double* lmbd, const double* lmbd_r, cons
 
 // the rest of one run from the path table `tb`: k_eval (or k_agg) and k_finalize, then with a
 // communicator the all-gather and the combine
+// defer (run_steps, no communicator): a k_finalize launch is not issued but its arguments are
+// returned in *defer (defer->N = 0 when this run needs none) for the next run's k_path_fin
 int lq_launch_eval(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
                    int8_t* status, double* set_sum_w, double* set_stats, const PathTab& tb, hipStream_t st,
-                   lompc_ctx* prof_ctx) {
+                   lompc_ctx* prof_ctx, FinalArgs* defer = nullptr) {
+  if (defer) defer->N = 0;
   const int N = p->N;
   EvalArgs a{};
   a.S = (int)p->S;
@@ -1558,6 +1608,10 @@ int lq_launch_eval(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
     } else {
       plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
     }
+  }
+  if (!close && !agg && defer && !xr && N + NPX <= 64) {  // (one-wave closing: a record fits the wave)
+    *defer = r;
+    return LOMPC_OK;
   }
   if (!close && !agg) {  // (else the sets were closed inside k_eval / k_agg)
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1800,12 +1854,24 @@ int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   HIPCHK(p, hipSetDevice(p->device));
   const int mask = p->prof;
   int rc = LOMPC_OK;
+  hipStream_t st = (hipStream_t)stream;
+  // run k's closing (k_finalize) rides in run k + 1's path launch (k_path_fin); the last run's
+  // closes on its own.  The cell-start working sets alternate halves between runs.
+  FinalArgs fin{};
+  fin.N = 0;
   for (int k = 0; k < n_runs && rc == LOMPC_OK; ++k) {
     if (profile_every > 0) p->prof = (k % profile_every == 0) ? mask : 0;  // sampled runs carry the events
-    rc = lq_plan_launch(p, lmbd + (size_t)k * lmbd_stride, lmbd_r + (size_t)k * lmbd_r_stride, w, cost, w0, status,
-                        set_sum_w, set_stats, (hipStream_t)stream, nullptr);
+    const double* lm = lmbd + (size_t)k * lmbd_stride;
+    const double* lr = lmbd_r + (size_t)k * lmbd_r_stride;
+    const PathTab tb = own_tab(p, k & 1);
+    if ((rc = lq_launch_path(p, lm, lr, tb, st, fin.N ? &fin : nullptr))) break;
+    rc = lq_launch_eval(p, lm, lr, w, cost, w0, status, set_sum_w, set_stats, tb, st, nullptr, &fin);
   }
   p->prof = mask;
+  if (rc == LOMPC_OK && fin.N) {  // the last run's closing
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, fin);
+    HIPCHK(p, hipGetLastError());
+  }
   return rc;
 }
 

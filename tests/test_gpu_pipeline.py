@@ -454,6 +454,44 @@ def test_run_steps_matches_single_runs(gpu, want_w, K):
 
 
 @pytest.mark.parametrize("N", [24, 48])
+def test_run_steps_repairs_match_single_runs(gpu, N):
+    """run_steps closes run k inside run k + 1's path launch (k_path_fin, one wave per set); its
+    individual re-solves start from run k's cell-start working sets, which run k + 1's path must
+    not overwrite (the two halves alternate).  With EVs moved outside the plan's gamma windows
+    after its creation (re-solved individually from the edge cells' working sets) and
+    warm-started paths, K runs through run_steps equal K single runs bit for bit, and the oracle."""
+    rng = np.random.default_rng(60 + N)
+    c = O.large_consts()
+    sizes = [3000, 0, 1, 2570]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    S, K, B = len(sizes), 3, int(off[-1])
+    gn = c.y_max - (0.3 + 0.2 * rng.random(B))
+    g = torch.as_tensor(gn, device="cuda:0")
+    lm = torch.as_tensor(c.theta * rng.random((K, S, 3 * N)), device="cuda:0")
+    lr = torch.as_tensor(0.05 * rng.random((K, S)), device="cuda:0")
+    wr = torch.as_tensor(c.w_max * rng.random((S, N)), device="cuda:0")
+    lompc = mk(c, N)
+    kw = dict(w_ref=wr, want_w=True, want_cost=True, want_status=True, warm_start=True)
+    ref = BatchPlan(lompc, g, off, **kw)
+    plan = BatchPlan(lompc, g, off, **kw)
+    moved = rng.choice(B, B // 10, replace=False)  # outside every window: below / above it
+    gm = gn.copy()
+    gm[moved] = np.where(rng.random(moved.size) < 0.5, 0.02 * rng.random(moved.size) * c.y_max,
+                         c.y_max * (1.0 - 0.02 * rng.random(moved.size)))
+    g.copy_(torch.as_tensor(gm))
+    outs = []
+    for k in range(K):
+        outs.append({n: v.clone() for n, v in ref.run(lm[k], lr[k]).items() if v is not None})
+    rep, fail, inv = ref.check()
+    assert rep >= K * (moved.size - 2) and fail == 0 and inv == 0
+    out = plan.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel())
+    assert plan.check() == (rep, 0, 0)
+    for key in ("w", "cost", "status", "set_sum_w", "set_stats"):
+        assert torch.equal(out[key], outs[-1][key]), key
+    oracle_check(outs[-1], g, lm[-1], lr[-1], off, c, N, rng)
+
+
+@pytest.mark.parametrize("N", [24, 48])
 @pytest.mark.parametrize("diag_repair", [False, True])
 def test_sorted_gamma_aggregation(gpu, N, diag_repair):
     """LOMPC_PLAN_SORTED_GAMMA: reductions-only runs aggregate each certified piece's EVs from

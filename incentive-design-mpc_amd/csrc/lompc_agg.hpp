@@ -303,8 +303,8 @@ __global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
     qb = min(max(qb, cs), ce);
     int qpos = cs;
     for (int j = 0; j <= cnt; ++j) {  // (wave-uniform loop over the boundaries)
-      const int a = __shfl(qa, j, 64), b = __shfl(qb, j, 64);
-      const double v = __shfl(vb, j, 64);
+      const int a = lqw::readlane_i(qa, j), b = lqw::readlane_i(qb, j);  // (j wave-uniform)
+      const double v = lqw::readlane_d(vb, j);
       const int pj = agg_search(g, a, b, v, j == 0, lane);
       if (lane == j) qpos = pj;
     }
@@ -338,11 +338,11 @@ __global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
     // per-stage sums of w: sum over pieces of n_k a_kt + Gamma_k b_kt (lane t)
 #pragma unroll
     for (int k = 0; k < LQ_PPL; ++k) {
-      const double nk = __shfl(n, k, 64), gk = __shfl(Gm, k, 64);
+      const double nk = lqw::readlane_d(n, k), gk = lqw::readlane_d(Gm, k);
       accw = fma(gk, ab[k].y, fma(nk, ab[k].x, accw));  // (slots past cnt: n = 0, Gamma = 0)
     }
     // EVs of the cell outside its certified coverage: re-solved one by one (k_finalize's method)
-    const int u0 = cs, u1 = __shfl(qpos, 0, 64), v0 = __shfl(qpos, cnt, 64), v1 = ce;
+    const int u0 = cs, u1 = lqw::readlane_i(qpos, 0), v0 = lqw::readlane_i(qpos, cnt), v1 = ce;
     if (u1 > u0 || v1 > v0) {
       lqw::WaveSet ws;
       double l2w;
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
   double xs[4] = {acost, ap0, 0.0, 0.0};
   lqw::wave_totals(xs, 64);
   const double emx = lqw::wave_max(aerr, 64);
-  const int rp = __shfl(nrep, 0, 64), fl = __shfl(nfail, 0, 64);
+  const int rp = lqw::readlane_i(nrep, 0), fl = lqw::readlane_i(nfail, 0);
   if (lane < N) s_w[wv][lane] = accw;
   if (lane == 0) {
     s_x[wv][0] = xs[0];

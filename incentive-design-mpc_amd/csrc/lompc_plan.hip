@@ -340,7 +340,7 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
         // depend on this piece's certificate and quadratics: all of them in one basic block, so
         // the scheduler interleaves the independent DPP-scan chains (the next solve is wasted
         // work, not latency, when this piece is the last).
-        const int bns = __shfl(ns, bj < 0 ? 0 : bj, 64);
+        const int bns = lqw::readlane_i(ns, bj < 0 ? 0 : bj);  // (bj wave-uniform: from a ballot)
         const int sln = lane == bj ? bns : sl;
         lqw::StageSol<2> nsol;
         double res;
@@ -388,7 +388,7 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
             st_wt8(dst, av);
             st_wt8(dst + 1, bv);
           }
-          const double a0 = __shfl(av, 0, 64), b0v = __shfl(bv, 0, 64);
+          const double a0 = lqw::readlane_d(av, 0), b0v = lqw::readlane_d(bv, 0);
           if (lane < 8) {
             double v = t[0] + c0;
 #pragma unroll
@@ -497,7 +497,7 @@ __device__ __forceinline__ void wave_ev_outputs(const QPConst& q, const lqw::Wav
   const double tw = q.theta * q.w_max;
   cost = v[0] + c0 + tw * tw * v[3];
   err = sqrt(fmax(v[1] + kappa * v[2], 0.0));
-  const double w0 = __shfl(w, 0, 64);
+  const double w0 = lqw::readlane_d(w, 0);
   price0 = q.theta * (w0 * l0[0] + (q.w_max - w0) * l0[1]) + q.q_scale * w0 * w0 * l0[2] +
            q.theta * q.theta * w0 * w0 * lr;
 }
@@ -849,29 +849,64 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   double acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
   int n_ok = 0, n_fail = 0, n_inv = 0, nlist = 0;
   bool inv_rows = false;  // (wave-uniform) some row of this wave has an invalid gamma
+  // both passes' lookups side by side: each step's LDS reads (cell counts, then the cell's piece
+  // ends and coverage start, then the piece's coefficients) of the two EVs are in flight together,
+  // so the dependent LDS rounds are paid once, not once per pass
+  static_assert(EVAL_PASSES == 2, "the lookup is written for two EVs per thread");
+  const bool has1 = start + EVAL_EVS + 64 * wv < end;  // (wave-uniform) this wave has pass-1 EVs
+  int iv[2], cc[2], nc[2], key[2];
+  bool act[2], valid[2], cov[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    iv[h] = start + tid + EVAL_EVS * h;
+    act[h] = iv[h] < end;
+    valid[h] = act[h] && gh[h] >= 0.0 && gh[h] <= ym;
+    cc[h] = valid[h] ? cell_of(gh[h], wlo, cscale, G) : 0;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) nc[h] = s_cnt[cc[h]];
+  double ge[2][LQ_PPL], glo_c[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int kb = cc[h] * LQ_PPL;
+#pragma unroll
+    for (int k = 0; k < LQ_PPL; ++k) ge[h][k] = s_ge[min(kb + k, cap - 1)];
+    glo_c[h] = s_lo[cc[h]];
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    // piece = number of piece ends below g (every end read at once, no loop)
+    const int kb = cc[h] * LQ_PPL, ke = kb + nc[h];
+    const double g = gh[h];
+    int kk = kb;
+    double gend = ge[h][0];
+#pragma unroll
+    for (int k = 0; k + 1 < LQ_PPL; ++k) kk += (k + 1 < nc[h] && g > ge[h][k]) ? 1 : 0;
+#pragma unroll
+    for (int k = 1; k < LQ_PPL; ++k) gend = nc[h] == k + 1 ? ge[h][k] : gend;  // the last piece's end
+    key[h] = kk;
+    cov[h] = valid[h] && ke > kb && ke <= np && g >= glo_c[h] && g <= gend;
+  }
+  double4 cf0[2], cf1[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int kc = cov[h] ? key[h] : 0;
+    cf0[h] = *reinterpret_cast<const double4*>(s_cf + kc * 8);
+    cf1[h] = *reinterpret_cast<const double4*>(s_cf + kc * 8 + 4);
+  }
 #pragma unroll
   for (int h = 0; h < EVAL_PASSES; ++h) {
-    const int i = start + tid + EVAL_EVS * h;
     // a wave without EVs in this pass skips it (wave-uniform; its rows are never read)
-    if (h > 0 && start + EVAL_EVS * h + 64 * wv >= end) break;
-    const bool act = i < end;
+    if (h > 0 && !has1) break;
+    const int i = iv[h];
     const double g = gh[h];
-    const bool valid = act && g >= 0.0 && g <= ym;
-    const int c = valid ? cell_of(g, wlo, cscale, G) : 0;
-    const int nc = s_cnt[c];
-    const int kb = c * LQ_PPL, ke = kb + nc;  // the cell's pieces [kb, ke), ascending gamma
-    int key = kb;  // piece = number of piece ends below g: every end read at once (no loop)
-#pragma unroll
-    for (int k = 0; k + 1 < LQ_PPL; ++k) key += (k + 1 < nc && g > s_ge[min(kb + k, cap - 1)]) ? 1 : 0;
-    const bool cov = valid && ke > kb && ke <= np && g >= s_lo[c] && g <= s_ge[max(ke - 1, 0)];
-    if (act && !valid) {
+    if (act[h] && !valid[h]) {
       ++n_inv;
       if (a.cost) st_wt8(a.cost + i, NAN);
       if (a.w0) st_wt8(a.w0 + i, NAN);
       if (a.status) a.status[i] = LOMPC_QP_INVALID;
-    } else if (cov) {
-      const double4 c0 = *reinterpret_cast<const double4*>(s_cf + key * 8);
-      const double4 c1 = *reinterpret_cast<const double4*>(s_cf + key * 8 + 4);
+    } else if (cov[h]) {
+      const double4 c0 = cf0[h], c1 = cf1[h];
       const double cst = fma(fma(c0.z, g, c0.y), g, c0.x);
       const double e2 = fma(fma(c1.y, g, c1.x), g, c0.w);
       const double er = a.want_err ? fmax(e2, 0.0) : 0.0;  // squared: sqrt of the max at the record
@@ -886,15 +921,15 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       if (a.w0) st_wt8(a.w0 + i, w0v);
       if (a.status) a.status[i] = LOMPC_QP_OK;
       if (CLOSE) {
-        atomicAdd(s_pn + key, 1);
-        atomicAdd(s_pf + key, (unsigned long long)rint(fmax(g - wlo, 0.0) * fxs));
+        atomicAdd(s_pn + key[h], 1);
+        atomicAdd(s_pf + key[h], (unsigned long long)rint(fmax(g - wlo, 0.0) * fxs));
       }
     }
     s_g[tid + EVAL_EVS * h] = g;
-    s_k[tid + EVAL_EVS * h] = cov ? key : ((CLOSE && valid) ? ZD : ZK);
-    inv_rows |= __ballot(act && !valid) != 0ull;
-    const unsigned long long need = __ballot(valid && !cov);
-    if (valid && !cov) {
+    s_k[tid + EVAL_EVS * h] = cov[h] ? key[h] : ((CLOSE && valid[h]) ? ZD : ZK);
+    inv_rows |= __ballot(act[h] && !valid[h]) != 0ull;
+    const unsigned long long need = __ballot(valid[h] && !cov[h]);
+    if (valid[h] && !cov[h]) {
       st_wt4(a.fail_idx + (size_t)blk * EVAL_MAXB + 64 * EVAL_PASSES * wv + nlist +
                  __popcll(need & ((1ull << lane) - 1ull)), i);
       ++n_fail;
@@ -956,9 +991,10 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       }
 #pragma unroll
       for (int k = 0; k < PU; ++k) {
+        // (n = 0: an unused slot, whose row is not read into the sum)
         const double gsum = fma((double)f[k], fxi, (double)n[k] * wlo);
-        accs = fma((double)n[k], ab[k].x, accs);  // (n = 0: exact no-op, gsum = 0 below)
-        accs = fma(n[k] ? gsum : 0.0, ab[k].y, accs);
+        accs = fma((double)n[k], n[k] ? ab[k].x : 0.0, accs);
+        accs = fma(n[k] ? gsum : 0.0, n[k] ? ab[k].y : 0.0, accs);
       }
     }
     if (lane < N) s_accw[wv][lane] = accs;

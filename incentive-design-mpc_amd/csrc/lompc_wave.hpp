@@ -48,12 +48,15 @@ __device__ __forceinline__ double shr1(double old, double x) { return dpp<0x138,
 // value of lane l+1 (lane 63 gets `old`): DPP wave_shl:1
 __device__ __forceinline__ double shl1(double old, double x) { return dpp<0x130, 0xf>(old, x); }
 
+// lane `lane`'s value on every lane (lane wave-uniform): v_readlane into scalar registers, no LDS
+// round trip (a __shfl is a ds_bpermute)
 __device__ __forceinline__ double readlane_d(double x, int lane) {
   const long long xi = __builtin_bit_cast(long long, x);
   const int lo = __builtin_amdgcn_readlane((int)xi, lane);
   const int hi = __builtin_amdgcn_readlane((int)(xi >> 32), lane);
   return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
 }
+__device__ __forceinline__ int readlane_i(int x, int lane) { return __builtin_amdgcn_readlane(x, lane); }
 
 struct Mob {  // Moebius map P -> (a P + b) / (c P + d), entries >= 0
   double a, b, c, d;
@@ -427,7 +430,7 @@ __device__ __forceinline__ double wave_kkt_point(const QPConst& q, const WaveSet
   Aff<1> z = Aff<1>::identity();
   if (act) z.B[0] = y;
   const double Z = wave_scan(z, N).B[0];   // Z_t = sum_{i<=t} y_i
-  const double Zt = __shfl(Z, N - 1, 64);
+  const double Zt = readlane_d(Z, N - 1);
   const double r = q.c * (Zt - Z + y - (double)(N - ws.lane) * gamma) + ws.d_nat * w + ws.e_nat;
   const double res = act ? lq_resid(q, lq_box(s), w, r) : 0.0;
   return wave_max(res, N);

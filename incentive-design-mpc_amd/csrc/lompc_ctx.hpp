@@ -131,6 +131,24 @@ struct lompc_plan {
   double2* t_ab = nullptr;
   uint8_t* t_sl = nullptr;
   uint8_t* d_ws = nullptr;        // [S*G][64] working set at each cell start (warm start)
+  // lompc_plan_run_steps, stepped form (k_step: run k + 1's path, run k's evaluation and run k - 1's
+  // closing in one launch): a second path table, triple cell-start working sets, two sets of
+  // evaluation records and the evaluation block map sized for the slots the path leaves
+  struct Stepped {
+    bool ok = false;              // built for the current prepare
+    int nblk = 0, np_wg = 0;      // evaluation workgroups, path workgroups of a launch
+    char* d_map = nullptr;        // int4 blocks [nblk] | int prefix [S+1]
+    char* h_map = nullptr;        // pinned staging of the map
+    int64_t cap_map = 0;
+    PathTab alt{};
+    uint8_t* sl3 = nullptr;       // [3][S*G][64]
+    int64_t cap_cells = 0;
+    double* part[2] = {nullptr, nullptr};
+    int* fcnt[2] = {nullptr, nullptr};
+    int* fidx[2] = {nullptr, nullptr};
+    int64_t cap_blk = 0;
+    int occ = 0, occ_N = -1;      // k_step workgroups per CU (occupancy query) and its horizon
+  } stp;
   int* d_errflag = nullptr;
   unsigned long long* d_tally = nullptr;  // [3] EVs repaired / failed / invalid over every run since
                                           // the last lompc_plan_status (sticky, read and zeroed there)
@@ -161,6 +179,7 @@ struct lompc_plan {
   // pinned staging of the host arrays
   char* h_buf = nullptr;
   int64_t cap_h = 0;
+  int64_t h_off_at = 0;           // byte offset of the set offsets in h_buf
   hipEvent_t ev_stage = nullptr;
   // HIP-event profiling, per kernel (LOMPC_PLAN_K_*): enabled mask, pairs since the last read
   int prof = 0;

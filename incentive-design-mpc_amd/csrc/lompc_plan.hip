@@ -44,6 +44,12 @@
 // diagnostic build only (scripts/kstamps.py): per-wave s_memtime at k_path's and k_eval's phase
 // boundaries (k_eval: workgroup b at g_stamps[(32768 + b) * 8 + k])
 __device__ long long g_stamps[65536 * 8];
+__device__ long long g_wstart[32768 * 8];  // k_eval: start of wave w of workgroup b at [b * 8 + w]
+#define LQ_WSTART()                                                                              \
+  do {                                                                                           \
+    const long long t__ = __builtin_amdgcn_s_memtime();                                          \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 32768) g_wstart[blockIdx.x * 8 + (threadIdx.x >> 6)] = t__; \
+  } while (0)
 #define LQ_STAMPE(k)                                                                        \
   do {                                                                                      \
     const long long t__ = __builtin_amdgcn_s_memtime();                                     \
@@ -57,6 +63,7 @@ __device__ long long g_stamps[65536 * 8];
 #else
 #define LQ_STAMP(k)
 #define LQ_STAMPE(k)
+#define LQ_WSTART()
 #endif
 
 #ifndef EVAL_WAVES
@@ -71,6 +78,13 @@ __device__ long long g_stamps[65536 * 8];
 #define EVAL_MAXB (EVAL_EVS * EVAL_PASSES)  // k_eval: EVs per workgroup, at most
 #define LQ_PIECE_CAP 128                   // k_eval: piece slots of one set staged in LDS (more: re-solved)
 #define LQ_GMAX 1024                       // max cells per set
+#ifndef LQ_STEP_CELLS
+#define LQ_STEP_CELLS 4                    // k_step: path cells per workgroup, one per wave (<= EVAL_WAVES; 4: one per
+                                           // SIMD — 19.2 us per step vs 22.4 with 8, 19.9 with 2, profiles/r03_v5)
+#endif
+#ifndef LQ_STEP_PRIO
+#define LQ_STEP_PRIO 1                     // k_step: path waves at raised issue priority
+#endif
 #define LQ_DROP_OFF 0x7fff0000             // k_eval: a store offset past any w descriptor's range (dropped)
 
 namespace {
@@ -350,14 +364,25 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
         auto piece = [&]() {
           // KKT certificate at the piece's end; its start is the previous certified end (same w
           // and r, only the switched coordinate's box changed and it contains the value)
+          // (the gradient from the prefix sums of a and b, which the cost quadratics need anyway:
+          // y = Ya + gamma Yb, Z = sum_{i<=t} y_i = Za + gamma Zb — two 2-value scans instead of
+          // wave_kkt_point's two affine scans over w; the same point up to rounding)
           const double wz = fmin(fmax(fma(bv, best, av), bx.lo), bx.hi);
-          res = lqw::wave_kkt_point(q, ws, best, sl, wz);
-          // cost and err^2 are quadratics in gamma on the piece
           lqw::Sums<2> pf;
           pf.v[0] = act ? av : 0.0;
           pf.v[1] = act ? bv : 0.0;
           pf = lqw::wave_scan(pf, N);
           const double Ya = pf.v[0], Yb = pf.v[1];
+          {
+            lqw::Sums<2> zf;
+            zf.v[0] = act ? Ya : 0.0;
+            zf.v[1] = act ? Yb : 0.0;
+            zf = lqw::wave_scan(zf, N);
+            const double y = fma(best, Yb, Ya), Z = fma(best, zf.v[1], zf.v[0]);
+            const double Zt = lqw::readlane_d(Z, N - 1);
+            const double rr = q.c * (Zt - Z + y - (double)(N - lane) * best) + ws.d_nat * wz + ws.e_nat;
+            res = lqw::wave_max(act ? lq_resid(q, bx, wz, rr) : 0.0, N);
+          }
           const double Ea = Ya - Ywr, da = av - wr_nat;
           const double dd = ws.d_nat, cc = q.c;
           const double sg = (sl & 1) ? bx.slo : 0.0;  // PWL slope of a free coordinate
@@ -753,6 +778,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   __shared__ double s_red[EVAL_WAVES][8];
   __shared__ int s_fc[EVAL_WAVES];  // (CLOSE) re-solve list lengths
   __shared__ int s_last;            // (CLOSE) this workgroup closes the set
+  __shared__ int s_mx;              // the set's largest piece count of a cell
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int4 info = a.blk[blk];
   const int s = info.x, start = info.y, end = info.z;  // thread: EVs start + tid + EVAL_EVS h
@@ -763,6 +789,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
                            // branch in the row loop
   const int ZD = cap + 1;  // (CLOSE) zero piece whose row is not written: re-solved EVs
   LQ_STAMPE(0);
+  LQ_WSTART();
   double2* s_ab = s_dyn;
   double* s_cf = reinterpret_cast<double*>(s_ab + (size_t)(cap + 2) * N);
   double* s_ge = s_cf + (size_t)cap * 8;
@@ -827,6 +854,10 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       s_cnt[tid] = vn;
       s_lo[tid] = vl;
     }
+    if (wv == 0) {  // the set's largest cell piece count: the lookup reads no piece end past it
+      const double m = lqw::wave_max(tid < G ? (double)vn : 0.0, 64);
+      if (lane == 0) s_mx = G <= 64 ? (int)m : LQ_PPL;
+    }
     if (tid < 2 * N) s_ab[ZK * N + tid] = make_double2(0.0, 0.0);  // both zero pieces
     if (CLOSE && tid < cap + 2) {
       s_pf[tid] = 0ull;
@@ -849,64 +880,35 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   double acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
   int n_ok = 0, n_fail = 0, n_inv = 0, nlist = 0;
   bool inv_rows = false;  // (wave-uniform) some row of this wave has an invalid gamma
-  // both passes' lookups side by side: each step's LDS reads (cell counts, then the cell's piece
-  // ends and coverage start, then the piece's coefficients) of the two EVs are in flight together,
-  // so the dependent LDS rounds are paid once, not once per pass
-  static_assert(EVAL_PASSES == 2, "the lookup is written for two EVs per thread");
-  const bool has1 = start + EVAL_EVS + 64 * wv < end;  // (wave-uniform) this wave has pass-1 EVs
-  int iv[2], cc[2], nc[2], key[2];
-  bool act[2], valid[2], cov[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    iv[h] = start + tid + EVAL_EVS * h;
-    act[h] = iv[h] < end;
-    valid[h] = act[h] && gh[h] >= 0.0 && gh[h] <= ym;
-    cc[h] = valid[h] ? cell_of(gh[h], wlo, cscale, G) : 0;
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) nc[h] = s_cnt[cc[h]];
-  double ge[2][LQ_PPL], glo_c[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int kb = cc[h] * LQ_PPL;
-#pragma unroll
-    for (int k = 0; k < LQ_PPL; ++k) ge[h][k] = s_ge[min(kb + k, cap - 1)];
-    glo_c[h] = s_lo[cc[h]];
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    // piece = number of piece ends below g (every end read at once, no loop)
-    const int kb = cc[h] * LQ_PPL, ke = kb + nc[h];
+  const int mxc = s_mx;  // (block-uniform) the set's largest cell piece count: no piece end past it is read
+  // one pass of the lookup: this thread's EV h
+  auto lookup = [&](const int h) {
+    const int i = start + tid + EVAL_EVS * h;
+    const bool act = i < end;
     const double g = gh[h];
-    int kk = kb;
-    double gend = ge[h][0];
+    const bool valid = act && g >= 0.0 && g <= ym;
+    const int c = valid ? cell_of(g, wlo, cscale, G) : 0;
+    const int nc = s_cnt[c];
+    const int kb = c * LQ_PPL, ke = kb + nc;  // the cell's pieces [kb, ke), ascending gamma
+    double ge[LQ_PPL];
 #pragma unroll
-    for (int k = 0; k + 1 < LQ_PPL; ++k) kk += (k + 1 < nc[h] && g > ge[h][k]) ? 1 : 0;
+    for (int k = 0; k < LQ_PPL; ++k) ge[k] = k < mxc ? s_ge[min(kb + k, cap - 1)] : 0.0;
+    const double glo_c = s_lo[c];
+    int key = kb;  // piece = number of piece ends below g (every end read at once, no loop)
+    double gend = ge[0];
 #pragma unroll
-    for (int k = 1; k < LQ_PPL; ++k) gend = nc[h] == k + 1 ? ge[h][k] : gend;  // the last piece's end
-    key[h] = kk;
-    cov[h] = valid[h] && ke > kb && ke <= np && g >= glo_c[h] && g <= gend;
-  }
-  double4 cf0[2], cf1[2];
+    for (int k = 0; k + 1 < LQ_PPL; ++k) key += (k + 1 < nc && g > ge[k]) ? 1 : 0;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int kc = cov[h] ? key[h] : 0;
-    cf0[h] = *reinterpret_cast<const double4*>(s_cf + kc * 8);
-    cf1[h] = *reinterpret_cast<const double4*>(s_cf + kc * 8 + 4);
-  }
-#pragma unroll
-  for (int h = 0; h < EVAL_PASSES; ++h) {
-    // a wave without EVs in this pass skips it (wave-uniform; its rows are never read)
-    if (h > 0 && !has1) break;
-    const int i = iv[h];
-    const double g = gh[h];
-    if (act[h] && !valid[h]) {
+    for (int k = 1; k < LQ_PPL; ++k) gend = nc == k + 1 ? ge[k] : gend;  // the last piece's end
+    const bool cov = valid && ke > kb && ke <= np && g >= glo_c && g <= gend;
+    if (act && !valid) {
       ++n_inv;
       if (a.cost) st_wt8(a.cost + i, NAN);
       if (a.w0) st_wt8(a.w0 + i, NAN);
       if (a.status) a.status[i] = LOMPC_QP_INVALID;
-    } else if (cov[h]) {
-      const double4 c0 = cf0[h], c1 = cf1[h];
+    } else if (cov) {
+      const double4 c0 = *reinterpret_cast<const double4*>(s_cf + key * 8);
+      const double4 c1 = *reinterpret_cast<const double4*>(s_cf + key * 8 + 4);
       const double cst = fma(fma(c0.z, g, c0.y), g, c0.x);
       const double e2 = fma(fma(c1.y, g, c1.x), g, c0.w);
       const double er = a.want_err ? fmax(e2, 0.0) : 0.0;  // squared: sqrt of the max at the record
@@ -921,21 +923,29 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       if (a.w0) st_wt8(a.w0 + i, w0v);
       if (a.status) a.status[i] = LOMPC_QP_OK;
       if (CLOSE) {
-        atomicAdd(s_pn + key[h], 1);
-        atomicAdd(s_pf + key[h], (unsigned long long)rint(fmax(g - wlo, 0.0) * fxs));
+        atomicAdd(s_pn + key, 1);
+        atomicAdd(s_pf + key, (unsigned long long)rint(fmax(g - wlo, 0.0) * fxs));
       }
     }
     s_g[tid + EVAL_EVS * h] = g;
-    s_k[tid + EVAL_EVS * h] = cov[h] ? key[h] : ((CLOSE && valid[h]) ? ZD : ZK);
-    inv_rows |= __ballot(act[h] && !valid[h]) != 0ull;
-    const unsigned long long need = __ballot(valid[h] && !cov[h]);
-    if (valid[h] && !cov[h]) {
+    s_k[tid + EVAL_EVS * h] = cov ? key : ((CLOSE && valid) ? ZD : ZK);
+    inv_rows |= __ballot(act && !valid) != 0ull;
+    const unsigned long long need = __ballot(valid && !cov);
+    if (valid && !cov) {
       st_wt4(a.fail_idx + (size_t)blk * EVAL_MAXB + 64 * EVAL_PASSES * wv + nlist +
                  __popcll(need & ((1ull << lane) - 1ull)), i);
       ++n_fail;
     }
     nlist += __popcll(need);
+  };
+  // a wave without EVs in a pass skips it (wave-uniform; its rows are never read)
+  auto pass_live = [&](const int h) { return h == 0 || start + EVAL_EVS * h + 64 * wv < end; };
+  if constexpr (CLOSE) {  // (the record is built before the rows: every lookup first)
+#pragma unroll
+    for (int h = 0; h < EVAL_PASSES; ++h)
+      if (pass_live(h)) lookup(h);
   }
+  LQ_STAMPE(7);
   // per-wave totals of the scalar outputs
   auto wave_record = [&]() {
     double tot[4] = {acc_cost, acc_p0, (double)n_ok, 0.0};
@@ -1013,10 +1023,6 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
         if (old == nb - 1) __hip_atomic_store(fr->arrive + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-  } else {
-    if (lane == 0) st_wt4(a.fail_cnt + (size_t)blk * EVAL_WAVES + wv, nlist);
-    wave_record();  // (the scalar totals are final here: their DPP scans run before the rows)
-    __builtin_amdgcn_wave_barrier();  // this wave's own rows in LDS: in order
   }
   LQ_STAMPE(2);
   LQ_STAMPE(3);
@@ -1129,13 +1135,20 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       const int lo = (wv - 1) * tot / (EVAL_WAVES - 1), hi = wv * tot / (EVAL_WAVES - 1);
       if (hi > lo) row_segment(lo, hi - lo);
     }
-  } else {  // each wave its own lookup rows, one segment per pass
+  } else {  // each wave: the lookup of a pass, then that pass's rows (the first row stores leave
+            // half a lookup earlier and the second lookup overlaps their drain)
 #pragma unroll
     for (int h = 0; h < EVAL_PASSES; ++h) {
+      if (!pass_live(h)) break;
+      lookup(h);
+      __builtin_amdgcn_wave_barrier();  // this wave's own rows in LDS: in order
+      any_inv = inv_rows;
       const int r0b = EVAL_EVS * h + 64 * wv;
       const int nh = max(0, min(64, end - start - r0b));  // wave-uniform
       if (nh > 0) row_segment(r0b, nh);
     }
+    if (lane == 0) st_wt4(a.fail_cnt + (size_t)blk * EVAL_WAVES + wv, nlist);
+    wave_record();
   }
   LQ_STAMPE(4);
   if constexpr (CLOSE) {
@@ -1196,6 +1209,49 @@ EvalKernel eval_kernel(int N) {
     case 24: return k_eval<CLOSE, 24>;
     case 48: return k_eval<CLOSE, 48>;
     default: return k_eval<CLOSE, 0>;
+  }
+}
+
+// lompc_plan_run_steps, stepped form: ONE launch carries run k + 1's path (workgroups
+// [0, np_wg): EVAL_WAVES cells of one set each, one per wave), run k's evaluation (the next nblk
+// workgroups, k_eval's block) and run k - 1's closing (one workgroup per set after them).  The
+// three are independent (separate path tables, records and cell-start working sets per run), so
+// the latency-bound path chain runs beside the bandwidth-bound evaluation instead of before it.
+template <int NT>
+__global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_step(PathArgs pa, EvalArgs ea, FinalArgs fe, FinalArgs ff,
+                                                                    int np_wg, int nf) {
+  extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
+  int b = (int)blockIdx.x;
+  if (b < np_wg) {
+    const int c0 = b * LQ_STEP_CELLS;  // (G % LQ_STEP_CELLS == 0: every cell of the workgroup in one set)
+    lq_tab_init(set_consts(pa.qd, pa.ce, c0 / pa.G));
+    const int wv = (int)(threadIdx.x >> 6), cell = c0 + wv;
+    // the path chain is the launch's critical path: its waves issue first on a SIMD they share
+    // with evaluation waves (which mostly wait on memory)
+    if (LQ_STEP_PRIO) __builtin_amdgcn_s_setprio(3);
+    if (wv < LQ_STEP_CELLS && cell < pa.S * pa.G) path_cell<NT, false>(pa, cell);
+    return;
+  }
+  b -= np_wg;
+  if (b < ea.nblk) {
+    eval_block<NT, false>(ea, b, &fe);
+    return;
+  }
+  b -= ea.nblk;
+  if (b < nf) {
+    double (*red)[FIN_W] = reinterpret_cast<double (*)[FIN_W]>(s_dyn);
+    finalize_set<EVAL_WAVES, false>(ff, b, red, red + EVAL_WAVES);
+  }
+}
+
+typedef void (*StepKernel)(PathArgs, EvalArgs, FinalArgs, FinalArgs, int, int);
+StepKernel step_kernel(int N) {
+  switch (N) {
+    case 12: return k_step<12>;
+    case 16: return k_step<16>;
+    case 24: return k_step<24>;
+    case 48: return k_step<48>;
+    default: return k_step<0>;
   }
 }
 
@@ -1380,6 +1436,7 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   p->nblk = (int)nblk;
   p->n_empty = (int)n_empty;
   p->d_stats = p->d_stats_own;
+  p->stp.ok = false;
   // host arrays -> pinned staging -> device (the staging may still feed the previous prepare)
   // the plan's host-built metadata, one block in pinned memory and one copy to its device
   // mirror: [QPConst x LQ_PLAN_MAX_CTX | int4 blocks | int64 set offsets | int block prefix]
@@ -1407,6 +1464,7 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   for (int k = 0; k < nctx; ++k) hq[k] = ctxs[k]->q;
   int4* hblk = reinterpret_cast<int4*>(p->h_buf + o_blk);
   int64_t* hoff = reinterpret_cast<int64_t*>(p->h_buf + o_off);
+  p->h_off_at = (int64_t)o_off;
   int* hpre = reinterpret_cast<int*>(p->h_buf + o_pre);
   memcpy(hoff, set_offsets, (S + 1) * sizeof(int64_t));
   int64_t b = 0;
@@ -1534,12 +1592,11 @@ int lq_launch_path(lompc_plan* p, const double* lmbd, const double* lmbd_r, cons
 // communicator the all-gather and the combine
 // defer (run_steps, no communicator): a k_finalize launch is not issued but its arguments are
 // returned in *defer (defer->N = 0 when this run needs none) for the next run's k_path_fin
-int lq_launch_eval(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
-                   int8_t* status, double* set_sum_w, double* set_stats, const PathTab& tb, hipStream_t st,
-                   lompc_ctx* prof_ctx, FinalArgs* defer = nullptr) {
-  if (defer) defer->N = 0;
+// the arguments of k_eval and of the set closing for one run from path table `tb`
+void eval_args(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
+               int8_t* status, const PathTab& tb, EvalArgs& a, FinalArgs& r) {
   const int N = p->N;
-  EvalArgs a{};
+  a = EvalArgs{};
   a.S = (int)p->S;
   a.G = p->G;
   a.N = N;
@@ -1571,8 +1628,7 @@ int lq_launch_eval(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   a.cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
   a.nblk = p->nblk;
   a.skip = p->skip;
-  const size_t lds = eval_lds(N, p->G, a.cap);
-  FinalArgs r{};
+  r = FinalArgs{};
   r.N = N;
   r.G = p->G;
   r.want_err = 1;
@@ -1593,6 +1649,21 @@ int lq_launch_eval(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   r.cost = cost;
   r.w0 = w0;
   r.status = status;
+  r.stats = p->d_stats;
+  r.tally = p->d_tally;
+  r.skip = p->skip;
+  r.arrive = p->d_arrive;
+}
+
+int lq_launch_eval(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
+                   int8_t* status, double* set_sum_w, double* set_stats, const PathTab& tb, hipStream_t st,
+                   lompc_ctx* prof_ctx, FinalArgs* defer = nullptr) {
+  if (defer) defer->N = 0;
+  const int N = p->N;
+  EvalArgs a;
+  FinalArgs r;
+  eval_args(p, lmbd, lmbd_r, w, cost, w0, status, tb, a, r);
+  const size_t lds = eval_lds(N, p->G, a.cap);
   // with a communicator the sets close into the packed send record [S][N] | [S][8]
   const bool xr = p->comm != nullptr;
   if (xr) {
@@ -1609,10 +1680,6 @@ int lq_launch_eval(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   }
   r.set_sum_w = xr ? p->d_xsend : set_sum_w;
   r.set_stats = xr ? p->d_xsend + p->S * N : set_stats;
-  r.stats = p->d_stats;
-  r.tally = p->d_tally;
-  r.skip = p->skip;
-  r.arrive = p->d_arrive;
   // gamma-sorted sets and no per-EV output: per-piece aggregation (k_agg) instead of k_eval
   const bool agg = p->sorted && !w && !cost && !w0 && !status && p->nblk > 0;
   const bool close = !agg && (p->close || (p->close_no_w && !w)) && p->nblk > 0;
@@ -1692,6 +1759,14 @@ void lq_plan_free(lompc_plan* p) {
                   p->d_bsum, p->d_P, p->d_pos, p->d_sinfo};
   for (void* x : ptrs)
     if (x) (void)hipFree(x);
+  {
+    auto& z = p->stp;
+    void* zs[] = {z.d_map, z.alt.cnt, z.alt.lo, z.alt.ge, z.alt.cf, z.alt.ab, z.sl3, z.part[0], z.part[1],
+                  z.fcnt[0], z.fcnt[1], z.fidx[0], z.fidx[1]};
+    for (void* x : zs)
+      if (x) (void)hipFree(x);
+    if (z.h_map) (void)hipHostFree(z.h_map);
+  }
   if (p->h_buf) (void)hipHostFree(p->h_buf);
   if (p->h_loop) (void)hipHostFree(p->h_loop);
   if (p->h_dec) (void)hipHostFree(p->h_dec);
@@ -1705,6 +1780,12 @@ void lq_plan_free(lompc_plan* p) {
 extern "C" {
 
 #ifdef LOMPC_STAMPS
+int lompc_debug_wstart(long long* host, int n) {
+  if (n > 32768 * 8) n = 32768 * 8;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wstart), sizeof(long long) * n, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? LOMPC_OK
+             : LOMPC_ERR_HIP;
+}
 int lompc_debug_stamps(long long* host, int n) {
   if (n > 65536 * 8) n = 65536 * 8;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(long long) * n, 0, hipMemcpyDeviceToHost) == hipSuccess
@@ -1874,6 +1955,154 @@ int lq_price_loop_host(lompc_plan* p, const lompc_price_loop_args* a, double* lm
   return LOMPC_OK;
 }
 
+// The stepped form's block map, tables and records (once per prepare).  The path takes np_wg of
+// the k_step workgroup slots for the whole launch, so the evaluation blocks are sized to fill the
+// rest once (or a whole number of times for big batches).
+int stepped_setup(lompc_plan* p, hipStream_t st) {
+  auto& z = p->stp;
+  const int N = p->N;
+  const int64_t S = p->S, G = p->G, ncell = S * G, B = p->B;
+  const int cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
+  if (z.occ_N != N) {
+    HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&z.occ, step_kernel(N), EVAL_EVS, eval_lds(N, p->G, cap)));
+    z.occ = std::max(z.occ, 1);
+    z.occ_N = N;
+  }
+  z.np_wg = (int)((ncell + LQ_STEP_CELLS - 1) / LQ_STEP_CELLS);
+  const int64_t slots = (int64_t)p->n_cu * z.occ;
+  const int64_t free1 = std::max<int64_t>(slots - z.np_wg, slots / 2);  // the first round, beside the path
+  const int64_t rounds = std::max<int64_t>(1, (10 * B + 9ll * slots * EVAL_MAXB - 1) / (9ll * slots * EVAL_MAXB));
+  const int64_t target = free1 + (rounds - 1) * slots;
+  std::vector<int64_t> off(S + 1);
+  {  // the set offsets from the prepared map (host copy kept in the pinned metadata)
+    const int64_t* hoff = reinterpret_cast<const int64_t*>(p->h_buf + p->h_off_at);
+    for (int64_t s = 0; s <= S; ++s) off[s] = hoff[s];
+  }
+  auto blocks_of = [&](int64_t m) -> int64_t {
+    if (m <= 0) return 0;
+    const int64_t lo = (m + EVAL_MAXB - 1) / EVAL_MAXB, hi = (m + 255) / 256;
+    return std::max<int64_t>(lo, std::min<int64_t>(hi, m * target / std::max<int64_t>(B, 1)));
+  };
+  int64_t nblk = 0;
+  for (int64_t s = 0; s < S; ++s) nblk += blocks_of(off[s + 1] - off[s]);
+  const size_t o_pre = ((size_t)nblk * sizeof(int4) + 15) & ~(size_t)15;
+  const size_t bytes = o_pre + (size_t)(S + 1) * sizeof(int);
+  int rc;
+  if ((int64_t)bytes > z.cap_map) {
+    if (z.h_map) HIPCHK(p, hipHostFree(z.h_map));
+    z.h_map = nullptr;
+    HIPCHK(p, hipHostMalloc((void**)&z.h_map, bytes, hipHostMallocDefault));
+    if ((rc = grow(p, &z.d_map, bytes))) return rc;
+    z.cap_map = (int64_t)bytes;
+  }
+  HIPCHK(p, hipStreamSynchronize(st));  // (the pinned map may still feed an earlier copy)
+  int4* hb = reinterpret_cast<int4*>(z.h_map);
+  int* hp = reinterpret_cast<int*>(z.h_map + o_pre);
+  int64_t b = 0;
+  hp[0] = 0;
+  for (int64_t s = 0; s < S; ++s) {
+    const int64_t o = off[s], m = off[s + 1] - o, nb = blocks_of(m);
+    for (int64_t k = 0; k < nb; ++k) hb[b++] = make_int4((int)s, (int)(o + m * k / nb), (int)(o + m * (k + 1) / nb), 0);
+    hp[s + 1] = (int)b;
+  }
+  HIPCHK(p, hipMemcpyAsync(z.d_map, z.h_map, bytes, hipMemcpyHostToDevice, st));
+  z.nblk = (int)nblk;
+  if (ncell > z.cap_cells) {
+    auto& t = z.alt;
+    if ((rc = grow(p, &t.cnt, ncell)) || (rc = grow(p, &t.lo, ncell)) || (rc = grow(p, &t.ge, ncell * LQ_PPL)) ||
+        (rc = grow(p, &t.cf, ncell * LQ_PPL * 8)) || (rc = grow(p, &t.ab, ncell * LQ_PPL * N)) ||
+        (rc = grow(p, &z.sl3, 3 * ncell * 64)))
+      return rc;
+    z.cap_cells = ncell;
+  }
+  if (nblk > z.cap_blk) {
+    for (int k = 0; k < 2; ++k)
+      if ((rc = grow(p, &z.part[k], (size_t)nblk * (N + NPX))) || (rc = grow(p, &z.fcnt[k], (size_t)nblk * EVAL_WAVES)) ||
+          (rc = grow(p, &z.fidx[k], (size_t)nblk * EVAL_MAXB)))
+        return rc;
+    z.cap_blk = nblk;
+  }
+  z.ok = true;
+  return LOMPC_OK;
+}
+
+// K >= 2 independent runs, stepped: launch 0 = run 0's path; launch k (1 <= k < K) = k_step(run k's
+// path, run k - 1's evaluation, run k - 2's closing); then run K - 2's closing, run K - 1's
+// evaluation and its closing as their own launches (a closing's individual re-solves write their
+// rows; the last evaluation must not share a launch with the previous closing, so the buffers end
+// holding exactly the last run's outputs).  Run j uses path table j % 2, records j % 2 and
+// cell-start working sets j % 3.
+int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride, const double* lmbd_r,
+                         int64_t lmbd_r_stride, int n_runs, int profile_every, double* w, double* cost, double* w0,
+                         int8_t* status, double* set_sum_w, double* set_stats, hipStream_t st) {
+  auto& z = p->stp;
+  int rc;
+  if (!z.ok && (rc = stepped_setup(p, st))) return rc;
+  const int N = p->N;
+  const int64_t ncell = p->S * p->G;
+  auto tab = [&](int j) {
+    PathTab t = (j & 1) ? z.alt : own_tab(p);
+    t.sl = z.sl3 + (size_t)(j % 3) * ncell * 64;
+    return t;
+  };
+  auto lm = [&](int j) { return lmbd + (size_t)j * lmbd_stride; };
+  auto lr = [&](int j) { return lmbd_r + (size_t)j * lmbd_r_stride; };
+  auto args = [&](int j, EvalArgs& a, FinalArgs& r) {
+    eval_args(p, lm(j), lr(j), w, cost, w0, status, tab(j), a, r);
+    a.blk = reinterpret_cast<const int4*>(z.d_map);
+    a.nblk = z.nblk;
+    a.partial = z.part[j & 1];
+    r.partial = z.part[j & 1];
+    a.fail_cnt = z.fcnt[j & 1];
+    r.fail_cnt = z.fcnt[j & 1];
+    a.fail_idx = z.fidx[j & 1];
+    r.fail_idx = z.fidx[j & 1];
+    r.blk_prefix = reinterpret_cast<const int*>(z.d_map + (((size_t)z.nblk * sizeof(int4) + 15) & ~(size_t)15));
+    r.set_sum_w = set_sum_w;
+    r.set_stats = set_stats;
+  };
+  const int cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
+  const size_t lds = eval_lds(N, p->G, cap);
+  const int mask = p->prof;
+  if ((rc = lq_launch_path(p, lm(0), lr(0), tab(0), st))) return rc;
+  for (int k = 1; k < n_runs; ++k) {
+    if (profile_every > 0) p->prof = ((k - 1) % profile_every == 0) ? mask : 0;  // sampled runs carry the events
+    const PathArgs pa = path_args(p, lm(k), lr(k), tab(k));
+    EvalArgs ea;
+    FinalArgs fe, ff;
+    args(k - 1, ea, fe);
+    int nf = 0;
+    if (k >= 2) {
+      EvalArgs dummy;
+      args(k - 2, dummy, ff);
+      nf = (int)p->S;
+    } else {
+      ff = fe;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1)) return fail_arg(p, "profiling events");
+    hipExtLaunchKernelGGL(step_kernel(N), dim3((unsigned)(z.np_wg + z.nblk + nf)), dim3(EVAL_EVS), lds, st, e0, e1, 0, pa,
+                          ea, fe, ff, z.np_wg, nf);
+    HIPCHK(p, hipGetLastError());
+    plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
+  }
+  p->prof = mask;
+  const int K = n_runs;
+  EvalArgs ea;
+  FinalArgs fr;
+  if (K >= 2) {
+    args(K - 2, ea, fr);
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, fr);
+    HIPCHK(p, hipGetLastError());
+  }
+  args(K - 1, ea, fr);
+  hipLaunchKernelGGL(eval_kernel<false>(N), dim3((unsigned)z.nblk), dim3(EVAL_EVS), lds, st, ea, fr);
+  HIPCHK(p, hipGetLastError());
+  hipLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, fr);
+  HIPCHK(p, hipGetLastError());
+  return LOMPC_OK;
+}
+
 extern "C" {
 
 int lompc_plan_run(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
@@ -1888,9 +2117,20 @@ int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
                          int8_t* status, double* set_sum_w, double* set_stats, void* stream) {
   if (!p || n_runs < 0 || profile_every < 0) return LOMPC_ERR_INVALID_ARG;
   HIPCHK(p, hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  {
+    // stepped form: full per-EV outputs (no communicator, the sets closed by k_finalize), cells in
+    // whole workgroups of one set; LOMPC_STEPPED=0 keeps the form below (diagnostics / A-B)
+    const char* se = getenv("LOMPC_STEPPED");
+    const bool agg = p->sorted && !w && !cost && !w0 && !status;
+    const bool close = p->close || (p->close_no_w && !w);
+    if (n_runs >= 2 && !(se && atoi(se) == 0) && !p->comm && !p->skip && !agg && !close && p->nblk > 0 &&
+        p->G % LQ_STEP_CELLS == 0 && p->N + NPX <= FIN_W)
+      return lq_run_steps_stepped(p, lmbd, lmbd_stride, lmbd_r, lmbd_r_stride, n_runs, profile_every, w, cost, w0,
+                                  status, set_sum_w, set_stats, st);
+  }
   const int mask = p->prof;
   int rc = LOMPC_OK;
-  hipStream_t st = (hipStream_t)stream;
   // run k's closing (k_finalize) rides in run k + 1's path launch (k_path_fin); the last run's
   // closes on its own.  The cell-start working sets alternate halves between runs.
   FinalArgs fin{};

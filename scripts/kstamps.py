@@ -82,5 +82,16 @@ print(f"k_eval workgroups {len(e)} (shader cycles)")
 for j, nm in enumerate(names):
     x = e[:, j + 1] - e[:, j]
     print(f"   {nm:15s} mean {x.mean():8.0f}  p90 {np.percentile(x, 90):8.0f}  max {x.max():8.0f}")
+# wave launch: each wave's start vs its workgroup's wave 0, and the workgroups' starts over the grid
+lib.lompc_debug_wstart.restype = ctypes.c_int
+lib.lompc_debug_wstart.argtypes = [ctypes.c_void_p, ctypes.c_int]
+ws = np.zeros(32768 * 8, dtype=np.int64)
+assert lib.lompc_debug_wstart(ws.ctypes.data, ws.size) == 0
+nwg = min(32768, len(e))
+wsr = ws.reshape(32768, 8)[:plan.info()["workgroups"]].astype(np.float64)
+t0 = wsr[:, 0].min()
+print(f"   wave launch: wave k - wave 0 of its workgroup: mean {np.mean(wsr.max(1) - wsr[:, 0]):.0f} max "
+      f"{np.max(wsr.max(1) - wsr[:, 0]):.0f};  workgroup starts over the grid: p50 {np.percentile(wsr[:, 0] - t0, 50):.0f}"
+      f" p90 {np.percentile(wsr[:, 0] - t0, 90):.0f} max {np.max(wsr[:, 0] - t0):.0f}")
 x = e[:, 5] - e[:, 0]
 print(f"   {'total':15s} mean {x.mean():8.0f}  p90 {np.percentile(x, 90):8.0f}  max {x.max():8.0f}")

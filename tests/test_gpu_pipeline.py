@@ -424,8 +424,9 @@ def test_reductions_only_runs_close_in_eval(gpu):
 @pytest.mark.parametrize("want_w", [True, False])
 def test_run_steps_matches_single_runs(gpu, want_w, K):
     """lompc_plan_run_steps (K runs in one C-ABI call, the benchmark's timed steps) writes the
-    same outputs as K lompc_plan_run calls at the same prices, bit for bit, and carries the HIP
-    events on every E-th run only; also for runs without w (the sets closed inside k_eval)."""
+    same outputs as K lompc_plan_run calls at the same prices, bit for bit, in both its forms
+    (stepped and launch per kernel), and carries the HIP events on sampled runs only; also for runs
+    without w (the sets closed inside k_eval)."""
     N, P, E = 24, 4, 3
     rng = np.random.default_rng(9)
     cs = [O.small_consts(), O.large_consts()]
@@ -450,7 +451,19 @@ def test_run_steps_matches_single_runs(gpu, want_w, K):
         if out.get(key) is not None:
             assert torch.equal(out[key], ref.out[key]), key
     ms, n = plan.profile(read=True)
-    assert n == (K + E - 1) // E and ms > 0.0
+    assert n >= (K - 1 + E - 1) // E and ms > 0.0
+    # the stepped form (k_step: run k + 1's path, run k's evaluation and run k - 1's closing in one
+    # launch, the default for full outputs) equals the launch-per-kernel form bit for bit
+    os.environ["LOMPC_STEPPED"] = "0"
+    try:
+        seq = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], want_status=True, want_w=want_w)
+        out_s = seq.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel())
+        assert seq.check()[1:] == (0, 0)
+    finally:
+        del os.environ["LOMPC_STEPPED"]
+    for key in ("w", "cost", "status", "set_sum_w", "set_stats"):
+        if out.get(key) is not None:
+            assert torch.equal(out[key], out_s[key]), key
 
 
 @pytest.mark.parametrize("N", [24, 48])

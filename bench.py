@@ -13,19 +13,23 @@ reductions of both types are combined by ONE RCCL all-gather (lompc_amd.dist.
 combine_set_results, rank-ordered local sum / max).  Weak scaling:
 262 144 EVs per GPU (config 3; at 8 GPUs this is config 4's 2 097 152).
 
-Every step is one plan run = three launches on one stream: k_path (per (set, gamma cell)
-solution paths), k_eval (per-EV evaluation + rows) and k_finalize (per-set reductions and any
-individual re-solve).
+A plan run is three kernels: k_path (per (set, gamma cell) solution paths), k_eval (per-EV
+evaluation + rows) and k_finalize (per-set reductions and any individual re-solve).  The K timed
+steps are independent runs (fresh prices each), issued by ONE lompc_plan_run_steps call in its
+stepped form: one k_step launch per step carries step k+1's path, step k's evaluation and step
+k-1's closing (the latency-bound path chain runs beside the bandwidth-bound evaluation), plus
+three launches after the last step; every step's work is done in full, the results equal the
+launch-per-kernel form bit for bit.
 
-Rank 0 prints ONE JSON line.  ``roofline`` prices the per-EV kernel (k_eval, the only
-kernel whose work scales with the EV count) by its algorithmic bytes per QP (gamma in 8 B,
-w out 8N B, cost out 8 B) over its launch duration from HIP events attached to its dispatch
-in the timed region; ``kernels`` gives every kernel's average duration from a separate
-20-step pass with events on all three (after the timed region, so the timed steps carry
-one event pair only) and k_path's latency roof (PMC figures from profiles/, when they match
-this configuration); ``cpu_baseline`` times the C oracle (oracle/, dense active set) on a
-bounded sample of the same workload: all host threads, one thread, and the lmbd_r > 0
-variant; ``direct_mode`` times the per-EV DIRECT mode on the same batch.
+Rank 0 prints ONE JSON line.  ``roofline`` prices the launch that carries the per-EV work
+(k_step; k_eval when the stepped form does not apply) by the evaluation's algorithmic bytes
+per QP (gamma in 8 B, w out 8N B, cost out 8 B) over its duration from HIP events attached to
+its dispatch in the timed region; ``kernels`` gives each plan kernel's average duration as its
+own launch from a separate 20-step pass with events on all three (after the timed region) and
+k_path's latency roof (PMC figures from profiles/, when they match this configuration);
+``cpu_baseline`` times the C oracle (oracle/, dense active set) on a bounded sample of the same
+workload: all host threads, one thread, and the lmbd_r > 0 variant; ``direct_mode`` times the
+per-EV DIRECT mode on the same batch.
 """
 from __future__ import annotations
 
@@ -261,6 +265,12 @@ def main():
     qp_per_launch = k_qps / max(k_n, 1)
     bytes_per_qp = 8 * (N + 2)
     achieved_gbs = bytes_per_qp * qp_per_launch / avg_launch_s / 1e9 if k_n else 0.0
+    # the stepped form (lompc_plan_run_steps, full outputs, no communicator): the timed region's
+    # events sit on its k_step launches
+    stepped = (batched and args.mode == "path" and args.outputs == "full" and comm is None
+               and os.environ.get("LOMPC_STEPPED", "1") != "0" and runs[0]["plan"].info()["cells"] % 4 == 0)
+    rkernel = ("k_step (step k+1's path + step k's evaluation + step k-1's closing)" if stepped
+               else ("k_eval" if args.mode == "path" else "k_direct"))
 
     total_qp = world * B * args.steps
     value = total_qp / dt
@@ -294,9 +304,11 @@ def main():
                                                       if sharded else "dp1")),
             "sharded_code_path": bool(sharded),
             "dist_backend": (args.dist_backend if sharded else None),
-            "launches_per_step": sum(r["plan"].launches_per_run() for r in runs),
-            "kernel_events": "none" if args.no_kernel_events else f"k_eval, 1 in {ev_every} timed steps",
-            "issue": "one lompc_plan_run_steps call for the K timed steps" if batched else "per-step lompc_plan_run",
+            "launches_per_step": (f"1 (k_step) + 3 after the last of the K steps" if stepped
+                                  else sum(r["plan"].launches_per_run() for r in runs)),
+            "kernel_events": "none" if args.no_kernel_events else f"{rkernel.split()[0]}, 1 in {ev_every} timed steps",
+            "issue": ("one lompc_plan_run_steps call for the K timed steps" + (" (stepped form)" if stepped else ""))
+                     if batched else "per-step lompc_plan_run",
             "correctness_gate": "sticky device tallies: no failed / invalid QP in any warmup or timed step",
         },
         "roofline": {
@@ -306,8 +318,10 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": None,
-            "kernel": "k_eval" if path else "k_direct",
+            "kernel": rkernel,
             "bytes_per_qp": bytes_per_qp,
+            "bytes_note": ("the evaluation's algorithmic bytes (gamma in, w and cost out); the path's table "
+                           "writes (~1 MB per launch) are not counted") if stepped else "gamma in, w and cost out",
             "qp_per_launch": qp_per_launch,
             "avg_launch_us": avg_launch_s * 1e6,
         },
@@ -315,11 +329,19 @@ def main():
         "host_issue_us_per_step": t_issue / args.steps * 1e6,
     }
     pmc = load_pmc(args, N, qp_per_launch)
-    if pmc and "k_eval" in pmc:
-        line["roofline"]["traffic"] = pmc["k_eval"]["hbm_bytes_per_launch"]
+    pk = "k_step" if stepped else "k_eval"
+    if pmc and pk in pmc and "hbm_bytes_per_launch" in pmc[pk]:
+        line["roofline"]["traffic"] = pmc[pk]["hbm_bytes_per_launch"]
         line["roofline"]["traffic_source"] = pmc["source"]
     if path and world == 1 and len(runs) == 1:
         line["kernels"] = kernel_breakdown(runs[0], step, args, nsteps, pmc, torch)
+        if stepped:
+            line["kernels"]["k_step"] = {"avg_us": avg_launch_s * 1e6, "launches_timed": k_n,
+                                         "note": "the timed region's launches (each as k_path + k_eval + k_finalize of "
+                                                 "three different steps); the entries above: each kernel as its own "
+                                                 "launch"}
+            if pmc and "k_step" in pmc:
+                line["kernels"]["k_step"]["pmc"] = {x: pmc["k_step"][x] for x in pmc["k_step"] if x != "hbm_bytes_per_launch"}
     if path and world == 1 and not multi and not args.no_contracts:
         line["contracts"] = contract_legs(eng, runs[0], N, P, args, nsteps, dev, torch, comm, pmc)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

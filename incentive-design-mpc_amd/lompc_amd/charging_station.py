@@ -25,6 +25,7 @@ redundantly on identical inputs; the re-draw replays the global random stream.
 from __future__ import annotations
 
 import concurrent.futures
+import os
 import time
 
 from dataclasses import dataclass
@@ -327,7 +328,9 @@ class ChargingStation:
                 assert st_l[p, 2] >= 0 and st_l[p, 1] <= self.consts_l.y_max
                 beta_l[p], gamma_lm[p] = self._robustness(self.price_solver_l, st_l[p], lmbd_r)
         self._pstats = (st_s, st_l)
-        self._stage_partitions()
+        self._staged = os.environ.get("LOMPC_STAGE_PARTITIONS", "1") != "0"  # (0: diagnostics / A-B)
+        if self._staged:
+            self._stage_partitions()
         Mp_s_ = Mp_s / self.B
         Mp_l_ = Mp_l / self.B
         demand = self.demand[self.t: self.t + self.N_bi] / self.B
@@ -379,7 +382,12 @@ class ChargingStation:
             kind, solver, y, idx, st, w_hat, prices, stats = chain
             if st[p, 0] > 0:
                 t0 = time.perf_counter() if prof else 0.0
-                solver.use_partition(p)  # (staged before the BiMPC solve, _stage_partitions)
+                if self._staged:
+                    solver.use_partition(p)  # (staged before the BiMPC solve, _stage_partitions)
+                else:
+                    ys, off = self._partition_layout(kind, y, idx)
+                    solver.set_charge_levels_stats(ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3],
+                                                   descending=True)
                 if PRINT_LEVEL >= 1 and self._rank0():
                     print(f"{kind} EVs, partition {p:2d}: ", end="")
                     if PRINT_LEVEL >= 2:

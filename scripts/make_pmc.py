@@ -19,7 +19,7 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc.json"
 qp = float(sys.argv[3]) if len(sys.argv) > 3 else 262144.0
 N = int(sys.argv[4]) if len(sys.argv) > 4 else 24
-KERNELS = ("k_path", "k_eval", "k_finalize")
+KERNELS = ("k_step", "k_path", "k_eval", "k_finalize")
 vals = {k: collections.defaultdict(list) for k in KERNELS}
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
@@ -56,7 +56,7 @@ for k in KERNELS:
         d["fetch_bytes_per_launch"] = 2.0 * fs * 1024.0
         d["write_bytes_per_launch"] = ws * 1024.0
         d["hbm_bytes_per_launch"] = d["fetch_bytes_per_launch"] + d["write_bytes_per_launch"]
-        if k == "k_eval":
+        if k in ("k_eval", "k_step"):
             d["algorithmic_bytes_per_launch"] = 8.0 * (N + 2) * qp
     d["dispatches"] = max((len(v) for v in vals[k].values()), default=0)
     if d["dispatches"]:

@@ -1259,6 +1259,11 @@ StepKernel step_kernel(int N) {
 
 // ---------------------------------------------------------------- host helpers
 
+// capacities of the buffers a re-targeted plan (lompc_plan_update) may outgrow: 1/4 headroom, so a
+// batch that varies a little from call to call (a station's partitions, step to step) stops
+// reallocating (hipMalloc / hipHostMalloc synchronise the device and cost far more than a run)
+int64_t with_slack(int64_t n) { return n + n / 4 + 16; }
+
 int pick_cells(int64_t max_set) {
   const char* env = getenv("LOMPC_CELLS");  // diagnostics (cell-count sweeps)
   if (env) {
@@ -1400,10 +1405,11 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     p->cap_S = S;
   }
   if (nblk > p->cap_blk) {
-    if ((rc = grow(p, &p->d_partial, (size_t)nblk * (N + NPX))) ||
-        (rc = grow(p, &p->d_fail_cnt, (size_t)nblk * EVAL_WAVES)) || (rc = grow(p, &p->d_fail_idx, (size_t)nblk * EVAL_MAXB)))
+    const int64_t c = with_slack(nblk);
+    if ((rc = grow(p, &p->d_partial, (size_t)c * (N + NPX))) ||
+        (rc = grow(p, &p->d_fail_cnt, (size_t)c * EVAL_WAVES)) || (rc = grow(p, &p->d_fail_idx, (size_t)c * EVAL_MAXB)))
       return rc;
-    p->cap_blk = nblk;
+    p->cap_blk = c;
   }
   const bool warm = (flags & LOMPC_PLAN_WARM_START) != 0;
   bool fresh_ws = false;
@@ -1454,11 +1460,12 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   const size_t need_h = sorted ? o_spre + up16((size_t)(S + 1) * sizeof(int)) : o_sblk;
   HIPCHK(p, hipEventSynchronize(p->ev_stage));  // (the staging may still feed the previous copy)
   if ((int64_t)need_h > p->cap_h) {
+    const int64_t c = with_slack((int64_t)need_h);
     if (p->h_buf) HIPCHK(p, hipHostFree(p->h_buf));
     p->h_buf = nullptr;
-    HIPCHK(p, hipHostMalloc((void**)&p->h_buf, need_h, hipHostMallocDefault));
-    if ((rc = grow(p, &p->d_meta, need_h))) return rc;
-    p->cap_h = (int64_t)need_h;
+    HIPCHK(p, hipHostMalloc((void**)&p->h_buf, (size_t)c, hipHostMallocDefault));
+    if ((rc = grow(p, &p->d_meta, (size_t)c))) return rc;
+    p->cap_h = c;
   }
   QPConst* hq = reinterpret_cast<QPConst*>(p->h_buf);
   for (int k = 0; k < nctx; ++k) hq[k] = ctxs[k]->q;
@@ -1499,12 +1506,14 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     p->aggF = G * LQ_AGG_KF;
     const int64_t nP = 3 * (B + S), npos = S * (int64_t)(p->aggF + 1);
     if (nsblk > p->cap_sblk) {
-      if ((rc = grow(p, &p->d_bsum, (size_t)nsblk * 4))) return rc;
-      p->cap_sblk = nsblk;
+      const int64_t c = with_slack(nsblk);
+      if ((rc = grow(p, &p->d_bsum, (size_t)c * 4))) return rc;
+      p->cap_sblk = c;
     }
     if (nP > p->cap_P) {
-      if ((rc = grow(p, &p->d_P, nP))) return rc;
-      p->cap_P = nP;
+      const int64_t c = with_slack(nP);
+      if ((rc = grow(p, &p->d_P, c))) return rc;
+      p->cap_P = c;
     }
     if (npos > p->cap_pos) {
       if ((rc = grow(p, &p->d_pos, npos))) return rc;

@@ -148,6 +148,7 @@ class ChargingStation:
         torch = _torch()
         self.group = group
         self._pool = None  # one worker thread: the large-EV price chain beside the small one
+        self._stage_pool = None  # two worker threads: the partition plans staged beside the BiMPC solve
         self.profile_phases = False  # accumulate per-phase wall times of _step in phase_ms (synchronising)
         self.phase_ms = {}
         self.device = torch.cuda.current_device() if device is None else int(device)
@@ -329,13 +330,16 @@ class ChargingStation:
                 beta_l[p], gamma_lm[p] = self._robustness(self.price_solver_l, st_l[p], lmbd_r)
         self._pstats = (st_s, st_l)
         self._staged = os.environ.get("LOMPC_STAGE_PARTITIONS", "1") != "0"  # (0: diagnostics / A-B)
-        if self._staged:
-            self._stage_partitions()
+        staging = self._stage_partitions() if self._staged else []
         Mp_s_ = Mp_s / self.B
         Mp_l_ = Mp_l / self.B
         demand = self.demand[self.t: self.t + self.N_bi] / self.B
         bimpc_params = BiMPCParameters(Mp_s_, Mp_l_, beta_s, beta_l, gamma_sm, gamma_lm, self.x, demand)
-        w_hat_s, w_hat_l, u_g = self.bimpc.solve_bimpc(bimpc_params)
+        try:
+            w_hat_s, w_hat_l, u_g = self.bimpc.solve_bimpc(bimpc_params)
+        finally:
+            for f in staging:  # (the partition plans were staged beside the host interior point)
+                f.result()
         stats_bi = {"Mp_s": Mp_s, "Mp_l": Mp_l, "beta_s": beta_s, "beta_l": beta_l, "gamma_sm": gamma_sm,
                     "gamma_lm": gamma_lm}
         if _settings.PRINT_LEVEL >= 1 and self._rank0():
@@ -441,19 +445,36 @@ class ChargingStation:
         return prices_s, prices_l, stats_s, stats_l
 
     def _stage_partitions(self):
-        """Every partition's loop plan of this step, prepared on the price solvers' streams before
-        the BiMPC solve (PriceSolver.stage_partition): the GPU builds them while the host runs the
-        interior point; the partitions' price loops then start at once.  (The partitions' levels
-        depend only on the state, not on the BiMPC.)"""
+        """Every partition's loop plan of this step, prepared (PriceSolver.stage_partition) on one
+        host thread per EV type and on the price solvers' streams WHILE the main thread runs the
+        BiMPC interior point (a C call without the GIL): the partitions' price loops then start at
+        once.  The partitions' levels depend only on the state, not on the BiMPC.  Returns the
+        futures (waited for after the solve).  Sharded: on this thread, in order (every rank
+        creates its plans' device communicators in the same order)."""
+        torch = _torch()
         st_s, st_l = self._pstats
+        jobs = []
         for kind, solver, y, idx, st in (("Small", self.price_solver_s, self.y_s, self.idx_s, st_s),
                                          ("Large", self.price_solver_l, self.y_l, self.idx_l, st_l)):
-            ys, off = self._partition_layout(kind, y, idx)
-            solver._stream.wait_stream(_torch().cuda.current_stream(self.device))
-            for p in range(self.P):
-                if st[p, 0] > 0:
-                    solver.stage_partition(p, ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3],
-                                           descending=True)
+            ys, off = self._partition_layout(kind, y, idx)  # (host sync: on this thread)
+            solver._stream.wait_stream(torch.cuda.current_stream(self.device))
+            jobs.append((solver, ys, off, st))
+
+        def stage(job):
+            solver, ys, off, st = job
+            with torch.cuda.device(self.device), torch.cuda.stream(solver._stream):
+                for p in range(self.P):
+                    if st[p, 0] > 0:
+                        solver.stage_partition(p, ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3],
+                                               descending=True)
+
+        if self.group is not None:
+            for job in jobs:
+                stage(job)
+            return []
+        if self._stage_pool is None:
+            self._stage_pool = concurrent.futures.ThreadPoolExecutor(max_workers=2)
+        return [self._stage_pool.submit(stage, job) for job in jobs]
 
     def _partition_layout(self, kind, y, idx):
         """This rank's EVs of one type grouped by partition, each partition in descending charge

@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
-ARGS=${BENCH_ARGS:-"--steps 3 --warmup 2 --no-cpu-baseline --no-station --no-direct"}
+ARGS=${BENCH_ARGS:-"--steps 3 --warmup 2 --no-cpu-baseline --no-station --no-direct --no-contracts"}
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
@@ -17,4 +17,5 @@ SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM
 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
 FETCH_SIZE
 WRITE_SIZE
+SQ_WAVES SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS
 GROUPS

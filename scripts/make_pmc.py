@@ -51,6 +51,9 @@ for k in KERNELS:
             d["wait_any_frac"] = wa / cyc
         if wi is not None:
             d["wait_inst_frac"] = wi / cyc
+    bc, ia = mean(k, "SQ_LDS_BANK_CONFLICT"), mean(k, "SQ_LDS_IDX_ACTIVE")
+    if bc is not None and ia:
+        d["lds_bank_conflict_frac"] = bc / ia  # conflict cycles / all LDS-array cycles
     fs, ws = mean(k, "FETCH_SIZE"), mean(k, "WRITE_SIZE")
     if fs is not None and ws is not None:
         d["fetch_bytes_per_launch"] = 2.0 * fs * 1024.0

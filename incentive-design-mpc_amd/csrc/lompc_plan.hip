@@ -109,6 +109,16 @@ __device__ __forceinline__ void st_wt4(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// k_eval: double2 per LDS piece row (padding shifts consecutive rows across the banks)
+__host__ __device__ constexpr int eval_row_stride(int N) { return N + 1; }
+// k_eval: LDS double of coefficient j of piece k; the record's four 16-B quarters are permuted
+// by bits 2..3 of k, so lanes reading quarter q of different pieces spread over all 64 banks
+// (records are 64 B: unswizzled, quarter q of every piece falls on one of 4 bank slots)
+__device__ __forceinline__ int cfx(const int k, const int j) {
+  return k * 8 + ((((j >> 1) ^ (k >> 2)) & 3) << 1) + (j & 1);
+}
+static_assert((LQ_PPL & (LQ_PPL - 1)) == 0, "k_eval's piece-end transpose needs a power-of-two LQ_PPL");
+
 __device__ __forceinline__ double clampw(double x, double wmax) { return fmin(fmax(x, 0.0), wmax); }
 
 // ---------------------------------------------------------------- plan kernel
@@ -321,6 +331,7 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
       const int max_iter = 4 * LQ_PPL + 16;
       const double ee = ws.e_nat;
       if (!has_sol) sol = lqw::solve_stage<2>(q, ws, 0.0, sl);  // (else the start's solve is reused)
+      Box bxn = lq_box(lane < N ? sl : 0);  // the working set's boxes (carried: read with its solve)
       for (int it = 0; it < max_iter && npc < LQ_PPL; ++it) {
 #ifdef LOMPC_STAMPS
         if (lane == 0 && blk < 32768) g_stamps[blk * 8 + 5] = it + 1;
@@ -328,8 +339,9 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
         const double av = sol.w[0], bv = sol.w[1], r0 = sol.r[0], r1 = sol.r[1];
         double gc = INFINITY;
         int ns = sl;
-        if (lane < N) {
-          const Box bx = lq_box(sl);
+        const bool act = lane < N;
+        const Box bx = bxn;
+        if (act) {
           if (sl & 1) {  // free: w(gamma) = a + b gamma leaves [lo, hi]
             if (bv > 0.0) { gc = (bx.hi - av) / bv; ns = sl + 1; }
             else if (bv < 0.0) { gc = (bx.lo - av) / bv; ns = sl - 1; }
@@ -359,8 +371,6 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
         lqw::StageSol<2> nsol;
         double res;
         double t[6];
-        const bool act = lane < N;
-        const Box bx = lq_box(act ? sl : 0);
         auto piece = [&]() {
           // KKT certificate at the piece's end; its start is the previous certified end (same w
           // and r, only the switched coordinate's box changed and it contains the value)
@@ -401,7 +411,8 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
           lqw::wave_totals(t, N);
         };
         if (bj >= 0) {  // (wave-uniform) the next solve beside this piece's certificate
-          nsol = lqw::solve_stage<2>(q, ws, 0.0, sln);
+          bxn = lq_box(act ? sln : 0);
+          nsol = lqw::solve_stage<2>(q, ws, bxn, 0.0, sln);
           piece();
         } else {
           piece();
@@ -769,8 +780,13 @@ __global__ __launch_bounds__(256) void k_combine(const double* __restrict__ recv
 // them, so no two writes of a row race.
 template <int NT = 0, bool CLOSE = false>
 __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, const FinalArgs* fr = nullptr) {
-  // dynamic LDS: [cap + 2][N] piece rows (rows cap, cap + 1: zero pieces) | [cap][8] coefficients |
-  // [cap] piece ends | cells: coverage start | piece count | (CLOSE) per piece: gamma sum, EV count
+  // dynamic LDS: [cap + 2][NS] piece rows (rows cap, cap + 1: zero pieces) | [cap][8]
+  // coefficients (cfx) | [LQ_PPL][Gs] piece ends | cells: coverage start | piece count | (CLOSE) per
+  // piece: gamma sum, EV count.  Laid out for the banks (64 dwords for ds_read_b64 / b128): a
+  // piece row holds its even stages, then its odd ones (even N: the row phase's two 16-B reads
+  // per lane are contiguous across a row's lanes, not 32 B apart), and rows, coefficient records
+  // and piece ends are padded / swizzled / transposed so that lanes reading different pieces or cells
+  // spread over the banks instead of landing on the same few
   extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
   __shared__ double s_g[EVAL_MAXB];  // block row r = EV start + r: gamma
   __shared__ int s_k[EVAL_MAXB];     //   its piece (ZK / ZD: zero pieces)
@@ -790,14 +806,24 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   const int ZD = cap + 1;  // (CLOSE) zero piece whose row is not written: re-solved EVs
   LQ_STAMPE(0);
   LQ_WSTART();
+  const int NS = eval_row_stride(N);
+  // LDS index of stage t of piece row k
+  auto abx = [&](const int k, const int t) { return k * NS + ((N & 1) ? t : (t & 1) * (N >> 1) + (t >> 1)); };
   double2* s_ab = s_dyn;
-  double* s_cf = reinterpret_cast<double*>(s_ab + (size_t)(cap + 2) * N);
+  double* s_cf = reinterpret_cast<double*>(s_ab + (size_t)(cap + 2) * NS);
   double* s_ge = s_cf + (size_t)cap * 8;
   double* s_lo = s_ge + cap;
   int* s_cnt = reinterpret_cast<int*>(s_lo + G);
   unsigned long long* s_pf = reinterpret_cast<unsigned long long*>(s_cnt + ((G + 1) & ~1));
   int* s_pn = reinterpret_cast<int*>(s_pf + cap + 2);
-  // this thread's EVs (caller order), the cells and the set's piece count: one memory round
+  const int np = min(G * LQ_PPL, cap);
+  const int Gs = np / LQ_PPL;  // cells with staged pieces (the rest are re-solved)
+  // staged cells per wave (wv, wv + W, ...) and piece-row loads per lane and cell
+  constexpr int CPW = (LQ_PIECE_CAP / LQ_PPL + EVAL_WAVES - 1) / EVAL_WAVES;
+  constexpr int UA = ((NT ? NT : LOMPC_MAX_N) * LQ_PPL + 63) / 64;
+  int wc = 0;  // lane j < CPW: piece count of cell wv + W j
+  if (lane < CPW && wv + EVAL_WAVES * lane < Gs) wc = ld_t<false>(a.t_cnt + (size_t)s * G + wv + EVAL_WAVES * lane);
+  // this thread's EVs (caller order)
   double gh[EVAL_PASSES];
 #pragma unroll
   for (int h = 0; h < EVAL_PASSES; ++h) {
@@ -810,45 +836,48 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   const double l0[3] = {L[0], L[N], L[2 * N]};  // price0 (lompc.py:164-170)
   const double lr = a.lmbd_r[s];
   const int cb = s * G;
-  // the set's piece slots (the first `cap`: cells past them are re-solved individually), all
-  // of them whatever the cells' counts, and the cells' counts / coverage starts: ONE memory
-  // round — every thread issues all its staging loads (behind its gamma loads) before its first
-  // LDS store; only N > 32 or more than EVAL_EVS cells leave a remainder for a second round
+  // the set's USED piece slots (a cell's first t_cnt of its LQ_PPL; cells past the first `cap`
+  // slots are re-solved individually) and the cells' counts / coverage starts.  Two memory rounds,
+  // both wave-local (no barrier): each wave reads the counts of the cells whose pieces it stages
+  // (issued before the gamma loads, above), then only those cells' used rows, coefficient records
+  // and piece ends — cells hold 1-2 pieces on average, so this moves a fraction of the 8 slots
   const size_t sb = (size_t)s * G * LQ_PPL;
-  const int np = min(G * LQ_PPL, cap);
   {
-    const int nab = np * N, ncf = np * 8;
-    const double2* gab = a.t_ab + sb * N;
-    const double* gcf = a.t_cf + sb * 8;
-    constexpr int U = 8, UC = (LQ_PIECE_CAP * 9 + EVAL_EVS - 1) / EVAL_EVS;
-    double2 v[U];
-    double vc[UC];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int it = tid + EVAL_EVS * u;
-      v[u] = it < nab ? ld_t<false>(gab + it) : make_double2(0.0, 0.0);
-    }
-#pragma unroll
-    for (int u = 0; u < UC; ++u) {
-      const int it = tid + EVAL_EVS * u;
-      vc[u] = it < ncf ? ld_t<false>(gcf + it) : (it < ncf + np ? ld_t<false>(a.t_ge + sb + it - ncf) : 0.0);
-    }
     int vn = 0;
     double vl = 0.0;
     if (tid < G) {
       vn = ld_t<false>(a.t_cnt + cb + tid);
       vl = ld_t<false>(a.t_lo + cb + tid);
     }
+    double2 v[CPW][UA];
+    double vc[CPW], vg[CPW];
+    int nc[CPW];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int it = tid + EVAL_EVS * u;
-      if (it < nab) s_ab[it] = v[u];
+    for (int j = 0; j < CPW; ++j) {
+      const int c = wv + EVAL_WAVES * j;
+      nc[j] = c < Gs ? min(max(lqw::readlane_i(wc, j), 0), LQ_PPL) : 0;  // (wave-uniform)
+      const size_t so = sb + (size_t)c * LQ_PPL;  // the cell's first slot
+#pragma unroll
+      for (int u = 0; u < UA; ++u) {
+        const int it = lane + 64 * u;
+        v[j][u] = it < nc[j] * N ? ld_t<false>(a.t_ab + so * N + it) : make_double2(0.0, 0.0);
+      }
+      vc[j] = lane < nc[j] * 8 ? ld_t<false>(a.t_cf + so * 8 + lane) : 0.0;
+      vg[j] = lane < nc[j] ? ld_t<false>(a.t_ge + so + lane) : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < UC; ++u) {
-      const int it = tid + EVAL_EVS * u;
-      if (it < ncf) s_cf[it] = vc[u];
-      else if (it < ncf + np) s_ge[it - ncf] = vc[u];
+    for (int j = 0; j < CPW; ++j) {
+      const int c = wv + EVAL_WAVES * j;
+#pragma unroll
+      for (int u = 0; u < UA; ++u) {
+        const int it = lane + 64 * u;
+        if (it < nc[j] * N) {
+          const int k = it / N;
+          s_ab[abx(c * LQ_PPL + k, it - k * N)] = v[j][u];
+        }
+      }
+      if (lane < nc[j] * 8) s_cf[cfx(c * LQ_PPL + (lane >> 3), lane & 7)] = vc[j];
+      if (lane < nc[j]) s_ge[lane * Gs + c] = vg[j];
     }
     if (tid < G) {
       s_cnt[tid] = vn;
@@ -858,12 +887,11 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       const double m = lqw::wave_max(tid < G ? (double)vn : 0.0, 64);
       if (lane == 0) s_mx = G <= 64 ? (int)m : LQ_PPL;
     }
-    if (tid < 2 * N) s_ab[ZK * N + tid] = make_double2(0.0, 0.0);  // both zero pieces
+    if (tid < 2 * NS) s_ab[ZK * NS + tid] = make_double2(0.0, 0.0);  // both zero pieces
     if (CLOSE && tid < cap + 2) {
       s_pf[tid] = 0ull;
       s_pn[tid] = 0;
     }
-    for (int it = tid + EVAL_EVS * U; it < nab; it += EVAL_EVS) s_ab[it] = ld_t<false>(gab + it);
     for (int c = tid + EVAL_EVS; c < G; c += EVAL_EVS) {
       s_cnt[c] = ld_t<false>(a.t_cnt + cb + c);
       s_lo[c] = ld_t<false>(a.t_lo + cb + c);
@@ -892,7 +920,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     const int kb = c * LQ_PPL, ke = kb + nc;  // the cell's pieces [kb, ke), ascending gamma
     double ge[LQ_PPL];
 #pragma unroll
-    for (int k = 0; k < LQ_PPL; ++k) ge[k] = k < mxc ? s_ge[min(kb + k, cap - 1)] : 0.0;
+    for (int k = 0; k < LQ_PPL; ++k) ge[k] = k < mxc ? s_ge[k * Gs + min(c, Gs - 1)] : 0.0;
     const double glo_c = s_lo[c];
     int key = kb;  // piece = number of piece ends below g (every end read at once, no loop)
     double gend = ge[0];
@@ -907,8 +935,11 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       if (a.w0) st_wt8(a.w0 + i, NAN);
       if (a.status) a.status[i] = LOMPC_QP_INVALID;
     } else if (cov) {
-      const double4 c0 = *reinterpret_cast<const double4*>(s_cf + key * 8);
-      const double4 c1 = *reinterpret_cast<const double4*>(s_cf + key * 8 + 4);
+      const double2 q0 = *reinterpret_cast<const double2*>(s_cf + cfx(key, 0));
+      const double2 q1 = *reinterpret_cast<const double2*>(s_cf + cfx(key, 2));
+      const double2 q2 = *reinterpret_cast<const double2*>(s_cf + cfx(key, 4));
+      const double2 q3 = *reinterpret_cast<const double2*>(s_cf + cfx(key, 6));
+      const double4 c0 = make_double4(q0.x, q0.y, q1.x, q1.y), c1 = make_double4(q2.x, q2.y, q3.x, q3.y);
       const double cst = fma(fma(c0.z, g, c0.y), g, c0.x);
       const double e2 = fma(fma(c1.y, g, c1.x), g, c0.w);
       const double er = a.want_err ? fmax(e2, 0.0) : 0.0;  // squared: sqrt of the max at the record
@@ -997,7 +1028,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
         const int pc = min(p, np - 1);
         n[k] = p < np ? s_pn[pc] : 0;
         f[k] = s_pf[pc];
-        ab[k] = s_ab[pc * N + min(lane, N - 1)];
+        ab[k] = s_ab[abx(pc, min(lane, N - 1))];
       }
 #pragma unroll
       for (int k = 0; k < PU; ++k) {
@@ -1060,8 +1091,8 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       double2 u0[RU], u1[RU];
 #pragma unroll
       for (int j = 0; j < RU; ++j) {
-        u0[j] = s_ab[kk[j] * N + t0];
-        u1[j] = V == 2 ? s_ab[kk[j] * N + t0 + 1] : make_double2(0.0, 0.0);
+        u0[j] = s_ab[kk[j] * NS + col];  // stages t0, t0 + 1 (abx)
+        u1[j] = V == 2 ? s_ab[kk[j] * NS + (N >> 1) + col] : make_double2(0.0, 0.0);
       }
       int kn[RU];  // the next batch's keys and gammas (software pipeline: one LDS round per batch)
       double gn[RU];
@@ -1305,9 +1336,10 @@ int plan_events_read(std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& pool,
 }  // namespace
 
 // ============================================================== host
-// k_eval's dynamic LDS: up to cap pieces of one set (N double2 + 8 + 1 doubles each) + the cells
+// k_eval's dynamic LDS: up to cap pieces of one set (NS double2 + 8 + 1 doubles each) + the cells
 size_t eval_lds(int N, int G, int cap) {
-  const size_t stage = (size_t)cap * (N * sizeof(double2) + 9 * sizeof(double)) + (size_t)2 * N * sizeof(double2) +
+  const size_t stage = (size_t)cap * (eval_row_stride(N) * sizeof(double2) + 9 * sizeof(double)) +
+                       (size_t)2 * eval_row_stride(N) * sizeof(double2) +
                        (size_t)G * sizeof(double) + (size_t)((G + 1) & ~1) * sizeof(int) +
                        (size_t)(cap + 2) * (sizeof(unsigned long long) + sizeof(int));
   return std::max(stage, (size_t)2 * EVAL_WAVES * FIN_W * sizeof(double));  // (close mode: red / rep)
@@ -2073,6 +2105,11 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   const int cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
   const size_t lds = eval_lds(N, p->G, cap);
   const int mask = p->prof;
+  // diagnostics (timing of the launch's parts): from launch 3 on, LOMPC_STEP_DIAG=1 drops the path
+  // workgroups (the evaluations then read the tables of runs 1 / 2: same coverage, same work),
+  // =2 drops the evaluation and closing workgroups.  Outputs are not the runs' in either case.
+  const char* dg = getenv("LOMPC_STEP_DIAG");
+  const int diag = dg ? atoi(dg) : 0;
   if ((rc = lq_launch_path(p, lm(0), lr(0), tab(0), st))) return rc;
   for (int k = 1; k < n_runs; ++k) {
     if (profile_every > 0) p->prof = ((k - 1) % profile_every == 0) ? mask : 0;  // sampled runs carry the events
@@ -2088,10 +2125,13 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     } else {
       ff = fe;
     }
+    int npw = z.np_wg;
+    if (diag == 1 && k >= 3) npw = 0;
+    if (diag == 2 && k >= 3) ea.nblk = nf = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1)) return fail_arg(p, "profiling events");
-    hipExtLaunchKernelGGL(step_kernel(N), dim3((unsigned)(z.np_wg + z.nblk + nf)), dim3(EVAL_EVS), lds, st, e0, e1, 0, pa,
-                          ea, fe, ff, z.np_wg, nf);
+    hipExtLaunchKernelGGL(step_kernel(N), dim3((unsigned)(npw + ea.nblk + nf)), dim3(EVAL_EVS), lds, st, e0, e1, 0, pa,
+                          ea, fe, ff, npw, nf);
     HIPCHK(p, hipGetLastError());
     plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
   }

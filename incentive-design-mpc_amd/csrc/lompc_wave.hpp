@@ -255,13 +255,15 @@ struct StageSol {
   double r[NB];  // multiplier r_t = gradient of the smooth part
 };
 
+// (bx: lq_box(s) on the active lanes, read by the caller — one LDS round per iteration feeds both
+// the solve and the caller's move test, and it can be issued an iteration ahead)
 template <int NB>
-__device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const WaveSet& ws, double gamma, int s) {
+__device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const WaveSet& ws, const Box& bx, double gamma,
+                                                    int s) {
   const double c = q.c;
   const int N = ws.N;
   const int lane = ws.lane;
   const bool act = lane < N;
-  const Box bx = lq_box(act ? s : 0);
   const double d = ws.d_nat;
   // ---- (1) Moebius suffix scan: lane t = F_t o ... o F_{N-1}
   const bool fr = act && (s & 1);
@@ -325,6 +327,10 @@ __device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const Wave
   }
   return out;
 }
+template <int NB>
+__device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const WaveSet& ws, double gamma, int s) {
+  return solve_stage<NB>(q, ws, lq_box(ws.lane < ws.N ? s : 0), gamma, s);
+}
 
 // Wave-parallel PDAS at gamma from working set s (lane t = stage t).
 // Returns true on convergence; s, w, r then hold the final working set,
@@ -332,10 +338,10 @@ __device__ __forceinline__ StageSol<NB> solve_stage(const QPConst& q, const Wave
 __device__ __forceinline__ bool wave_pdas(const QPConst& q, const WaveSet& ws, double gamma, int& s, double& w,
                                           double& r, int max_it, int* nit = nullptr) {
   for (int it = 0; it < max_it; ++it) {
-    const StageSol<1> sol = solve_stage<1>(q, ws, gamma, s);
+    const Box bx = lq_box(ws.lane < ws.N ? s : 0);
+    const StageSol<1> sol = solve_stage<1>(q, ws, bx, gamma, s);
     w = sol.w[0];
     r = sol.r[0];
-    const Box bx = lq_box(s);
     const int ns = ws.lane < ws.N ? (it < LQ_JUMP_IT ? lq_move_jump(q, s, bx, w, r) : lq_move(q, s, bx, w, r)) : s;
     const bool changed = __any(ns != s);
     s = ns;
@@ -483,13 +489,13 @@ __device__ __forceinline__ float readlane_f(float x, int l) {
 }
 
 // solve_stage<1> in fp32 (same recursions, see the file header)
-__device__ __forceinline__ void solve_stage_f32(const QPConst& q, const WaveSet& ws, float gamma, int s,
-                                                float& w_out, float& r_out) {
+// (bx: lq_boxf(s) on the active lanes, from the caller, as solve_stage)
+__device__ __forceinline__ void solve_stage_f32(const QPConst& q, const WaveSet& ws, const BoxF& bx, float gamma,
+                                                int s, float& w_out, float& r_out) {
   const float c = (float)q.c;
   const int N = ws.N;
   const int lane = ws.lane;
   const bool act = lane < N;
-  const BoxF bx = lq_boxf(act ? s : 0);
   const float d = (float)ws.d_nat;
   const bool fr = act && (s & 1);
   MobF f = MobF::identity();
@@ -533,12 +539,14 @@ __device__ __forceinline__ int wave_pdas_f32(const QPConst& q, const WaveSet& ws
                                              int max_it) {
   const float gf = (float)gamma;
   const float ktol = (float)(1e-6 * q.w_max), stol = (float)(1e-6 * q.scale);
+  int m = q.m;
+  asm volatile("" : "+s"(m));  // (read once, before the loop: not re-loaded inside the jump branch)
   for (int it = 0; it < max_it; ++it) {
     float w, r;
-    solve_stage_f32(q, ws, gf, s, w, r);
+    const BoxF bx = lq_boxf(ws.lane < ws.N ? s : 0);
+    solve_stage_f32(q, ws, bx, gf, s, w, r);
     int ns = s;
     if (ws.lane < ws.N) {
-      const BoxF bx = lq_boxf(s);
       const float v = -r;
       const bool freec = (s & 1) != 0;
       const bool up = freec ? (w > bx.hi + ktol) : (v > bx.shi + stol);
@@ -547,11 +555,11 @@ __device__ __forceinline__ int wave_pdas_f32(const QPConst& q, const WaveSet& ws
         if (!(w > (float)q.knots[0])) {
           ns = 0;
         } else if (!(w < (float)q.w_max)) {
-          ns = 2 * q.m;
+          ns = 2 * m;
         } else {
           int seg = 0;
 #pragma unroll
-          for (int k = 1; k < LQ_MAXSEG; ++k) seg += (k < q.m && w > (float)q.knots[k]) ? 1 : 0;
+          for (int k = 1; k < LQ_MAXSEG; ++k) seg += (k < m && w > (float)q.knots[k]) ? 1 : 0;
 #if LQ_JUMP_FREE
           ns = 2 * seg + 1;  // free in the segment that contains w
 #else
@@ -606,10 +614,10 @@ __device__ __forceinline__ bool wave_solve_path(const QPConst& q, const WaveSet&
   bool ok = false;
   double w = 0.0, r = 0.0;
   for (int it = 0; it < max_it; ++it) {
-    sol = solve_stage<2>(q, ws, 0.0, s);
+    const Box bx = lq_box(ws.lane < ws.N ? s : 0);
+    sol = solve_stage<2>(q, ws, bx, 0.0, s);
     w = fma(sol.w[1], gamma, sol.w[0]);
     r = fma(sol.r[1], gamma, sol.r[0]);
-    const Box bx = lq_box(s);
     const int ns = ws.lane < ws.N ? (it < LQ_JUMP_IT ? lq_move_jump(q, s, bx, w, r) : lq_move(q, s, bx, w, r)) : s;
     const bool changed = __any(ns != s);
     s = ns;

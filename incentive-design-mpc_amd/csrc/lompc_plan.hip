@@ -42,7 +42,11 @@
 
 #ifdef LOMPC_STAMPS
 // diagnostic build only (scripts/kstamps.py): per-wave s_memtime at k_path's and k_eval's phase
-// boundaries (k_eval: workgroup b at g_stamps[(32768 + b) * 8 + k])
+// boundaries (k_eval: workgroup b at g_stamps[(32768 + b) * 8 + k]); LOMPC_STAMPS_RT: the
+// device-wide 100 MHz s_memrealtime instead (comparable across XCDs: launch timelines)
+#ifdef LOMPC_STAMPS_RT
+#define __builtin_amdgcn_s_memtime __builtin_amdgcn_s_memrealtime
+#endif
 __device__ long long g_stamps[65536 * 8];
 __device__ long long g_wstart[32768 * 8];  // k_eval: start of wave w of workgroup b at [b * 8 + w]
 #define LQ_WSTART()                                                                              \
@@ -55,6 +59,11 @@ __device__ long long g_wstart[32768 * 8];  // k_eval: start of wave w of workgro
     const long long t__ = __builtin_amdgcn_s_memtime();                                     \
     if (threadIdx.x == 0 && blockIdx.x < 32768) g_stamps[(32768 + blockIdx.x) * 8 + (k)] = t__; \
   } while (0)
+#define LQ_STAMPW(k)                                                                        \
+  do {                                                                                      \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                        \
+    LQ_STAMPE(k);                                                                           \
+  } while (0)
 #define LQ_STAMP(k)                                                                         \
   do {                                                                                      \
     const long long t__ = __builtin_amdgcn_s_memtime();                                     \
@@ -63,6 +72,7 @@ __device__ long long g_wstart[32768 * 8];  // k_eval: start of wave w of workgro
 #else
 #define LQ_STAMP(k)
 #define LQ_STAMPE(k)
+#define LQ_STAMPW(k)
 #define LQ_WSTART()
 #endif
 
@@ -798,6 +808,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int4 info = a.blk[blk];
   const int s = info.x, start = info.y, end = info.z;  // thread: EVs start + tid + EVAL_EVS h
+  LQ_STAMPW(6);  // (diagnostic build: the block map's load round)
   const int N = NT ? NT : a.N, G = a.G;
   const int cap = a.cap;
   const int ZK = cap;      // the zero piece (a = b = 0): rows of invalid (and, without CLOSE,
@@ -831,10 +842,10 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     gh[h] = i < end ? a.gamma[i] : 0.0;
   }
   const QPConst& q = set_consts(a.qd, a.ce, s);
-  const double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
+  double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
   const double* __restrict__ L = a.lmbd + (size_t)s * 3 * N;
-  const double l0[3] = {L[0], L[N], L[2 * N]};  // price0 (lompc.py:164-170)
-  const double lr = a.lmbd_r[s];
+  double l0[3] = {L[0], L[N], L[2 * N]};  // price0 (lompc.py:164-170)
+  double lr = a.lmbd_r[s];
   const int cb = s * G;
   // the set's USED piece slots (a cell's first t_cnt of its LQ_PPL; cells past the first `cap`
   // slots are re-solved individually) and the cells' counts / coverage starts.  Two memory rounds,
@@ -849,13 +860,25 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       vn = ld_t<false>(a.t_cnt + cb + tid);
       vl = ld_t<false>(a.t_lo + cb + tid);
     }
+    // the set's constants and this workgroup's scalars land with this round, not after the
+    // staging (scalar loads are otherwise issued at first use, each a memory round of its own)
+    lq_tab_fill(q);  // (published by the barrier below)
+    lq_pin(wlo);
+    lq_pin(whi);
+    lq_pin(l0[0]);
+    lq_pin(l0[1]);
+    lq_pin(l0[2]);
+    lq_pin(lr);
+    LQ_STAMPW(2);  // (diagnostic build: counts, gamma and the cells' loads)
     double2 v[CPW][UA];
     double vc[CPW], vg[CPW];
     int nc[CPW];
 #pragma unroll
+    for (int j = 0; j < CPW; ++j)  // (every count read before any piece load is issued; a lane of
+      nc[j] = min(max(lqw::readlane_i(wc, j), 0), LQ_PPL);  //  a cell past Gs loaded 0)
+#pragma unroll
     for (int j = 0; j < CPW; ++j) {
       const int c = wv + EVAL_WAVES * j;
-      nc[j] = c < Gs ? min(max(lqw::readlane_i(wc, j), 0), LQ_PPL) : 0;  // (wave-uniform)
       const size_t so = sb + (size_t)c * LQ_PPL;  // the cell's first slot
 #pragma unroll
       for (int u = 0; u < UA; ++u) {
@@ -865,6 +888,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       vc[j] = lane < nc[j] * 8 ? ld_t<false>(a.t_cf + so * 8 + lane) : 0.0;
       vg[j] = lane < nc[j] ? ld_t<false>(a.t_ge + so + lane) : 0.0;
     }
+    LQ_STAMPW(3);  // (diagnostic build: the pieces' load round)
 #pragma unroll
     for (int j = 0; j < CPW; ++j) {
       const int c = wv + EVAL_WAVES * j;
@@ -897,7 +921,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       s_lo[c] = ld_t<false>(a.t_lo + cb + c);
     }
   }
-  lq_tab_init(q);  // (its barrier publishes the staged table)
+  __syncthreads();  // the staged table and the box table (lq_tab_fill) published
   LQ_STAMPE(1);
   // ---- lane = EV: piece, scalar outputs; EVs no certified piece covers listed for the
   //      individual re-solve (counted as pending failures until then)
@@ -1055,8 +1079,6 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       }
     }
   }
-  LQ_STAMPE(2);
-  LQ_STAMPE(3);
   // ---- rows (lane = stage pair): w_t = a_t + b_t gamma of the EV's piece -> contiguous rows
   const int V = (N & 1) ? 1 : 2;  // stages per lane (16-B stores for even N)
   const int Lr = N / V;           // lanes per row

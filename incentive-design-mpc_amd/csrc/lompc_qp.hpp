@@ -88,8 +88,8 @@ __device__ __forceinline__ float* lq_tabf() {
   __shared__ __attribute__((aligned(16))) float tabf[LQ_NSTATE * 4];
   return tabf;
 }
-// Every kernel calls this (all threads, before anything else).
-__device__ __forceinline__ void lq_tab_init(const QPConst& q) {
+// The box table's rows (threads < LQ_NSTATE), without the barrier that publishes them.
+__device__ __forceinline__ void lq_tab_fill(const QPConst& q) {
   double* tb = lq_tab();
   const int s = threadIdx.x;
   if (s < LQ_NSTATE) {
@@ -128,7 +128,19 @@ __device__ __forceinline__ void lq_tab_init(const QPConst& q) {
     tf[4 * s + 2] = (float)slo;
     tf[4 * s + 3] = (float)shi;
   }
+}
+// Every kernel calls this (all threads, before anything else).
+__device__ __forceinline__ void lq_tab_init(const QPConst& q) {
+  lq_tab_fill(q);
   __syncthreads();
+}
+// a wave-uniform value materialised here (its scalar load completes by this point instead of
+// being issued at its first use)
+__device__ __forceinline__ void lq_pin(double& x) {
+  const long long b = __builtin_bit_cast(long long, x);
+  int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  asm volatile("" : "+s"(lo), "+s"(hi));
+  x = __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
 }
 __device__ __forceinline__ Box lq_box(int s) {
   const double2* tb = reinterpret_cast<const double2*>(lq_tab());

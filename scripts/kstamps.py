@@ -77,21 +77,27 @@ buf2 = np.zeros(65536 * 8, dtype=np.int64)
 assert lib.lompc_debug_stamps(buf2.ctypes.data, buf2.size) == 0
 e = buf2[32768 * 8:].reshape(32768, 8)[: min(32768, (B + 255) // 256)]
 e = e[e[:, 0] != 0].astype(np.float64)
-names = ["loads+stage", "lookup+outputs", "(lists)", "rows", "record"]
 print(f"k_eval workgroups {len(e)} (shader cycles)")
-for j, nm in enumerate(names):
-    x = e[:, j + 1] - e[:, j]
+for (a, b), nm in (((0, 1), "loads+stage"), ((1, 4), "lookup+rows"), ((4, 5), "record")):
+    x = e[:, b] - e[:, a]
     print(f"   {nm:15s} mean {x.mean():8.0f}  p90 {np.percentile(x, 90):8.0f}  max {x.max():8.0f}")
 # wave launch: each wave's start vs its workgroup's wave 0, and the workgroups' starts over the grid
 lib.lompc_debug_wstart.restype = ctypes.c_int
 lib.lompc_debug_wstart.argtypes = [ctypes.c_void_p, ctypes.c_int]
 ws = np.zeros(32768 * 8, dtype=np.int64)
 assert lib.lompc_debug_wstart(ws.ctypes.data, ws.size) == 0
-nwg = min(32768, len(e))
 wsr = ws.reshape(32768, 8)[:plan.info()["workgroups"]].astype(np.float64)
+wsr = wsr[wsr[:, 0] != 0]
 t0 = wsr[:, 0].min()
 print(f"   wave launch: wave k - wave 0 of its workgroup: mean {np.mean(wsr.max(1) - wsr[:, 0]):.0f} max "
       f"{np.max(wsr.max(1) - wsr[:, 0]):.0f};  workgroup starts over the grid: p50 {np.percentile(wsr[:, 0] - t0, 50):.0f}"
       f" p90 {np.percentile(wsr[:, 0] - t0, 90):.0f} max {np.max(wsr[:, 0] - t0):.0f}")
 x = e[:, 5] - e[:, 0]
 print(f"   {'total':15s} mean {x.mean():8.0f}  p90 {np.percentile(x, 90):8.0f}  max {x.max():8.0f}")
+if os.environ.get("KS_RT") == "1":  # s_memrealtime build (10 ns ticks, one clock for every XCD)
+    z = e[:, 0].min()
+    for j, nm in ((0, "start"), (6, "block map"), (2, "round 1"), (3, "pieces"), (1, "staged"), (4, "rows done"),
+                  (5, "end")):
+        x = (e[:, j] - z) / 100.0
+        print(f"   timeline {nm:10s} us: p10 {np.percentile(x, 10):6.2f} p50 {np.percentile(x, 50):6.2f}"
+              f" p90 {np.percentile(x, 90):6.2f} max {x.max():6.2f}")

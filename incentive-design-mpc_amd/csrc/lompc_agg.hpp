@@ -280,19 +280,25 @@ __global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
   const bool order_ok = si.y != 0;
   for (int c = wv; order_ok && c < G; c += nw) {
     const int cell = s * G + c;
-    const int cs = ps[c * KF], ce = ps[(c + 1) * KF];  // the cell's sorted positions
-    if (ce <= cs) continue;
-    const int cnt = r.t_cnt[cell];
-    const double lo = r.t_lo[cell];
     const size_t sb = (size_t)cell * LQ_PPL;
-    // the cell's pieces: piece ends (lane k), coefficients (lane k), rows (lane t, all slots)
-    const double ge = lane < cnt ? r.t_ge[sb + lane] : INFINITY;
+    // one memory round: the cell's sorted positions, its piece count and coverage start, and
+    // every piece slot (whatever the count: no round waits on it) — piece ends and coefficients
+    // on lane k, rows on lane t
+    const int cs = ps[c * KF], ce = ps[(c + 1) * KF];
+    const int cnt_l = r.t_cnt[cell];
+    const double lo = r.t_lo[cell];
+    const double ge_l = lane < LQ_PPL ? r.t_ge[sb + lane] : INFINITY;
     double cf[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) cf[k] = lane < cnt ? r.t_cf[(sb + lane) * 8 + k] : 0.0;
+    for (int k = 0; k < 8; ++k) cf[k] = lane < LQ_PPL ? r.t_cf[(sb + lane) * 8 + k] : 0.0;
     double2 ab[LQ_PPL];
 #pragma unroll
-    for (int k = 0; k < LQ_PPL; ++k) ab[k] = (lane < N && k < cnt) ? r.t_ab[(sb + k) * N + lane] : make_double2(0.0, 0.0);
+    for (int k = 0; k < LQ_PPL; ++k) ab[k] = lane < N ? r.t_ab[(sb + k) * N + lane] : make_double2(0.0, 0.0);
+    if (ce <= cs) continue;
+    const int cnt = min(max(cnt_l, 0), LQ_PPL);
+    const double ge = lane < cnt ? ge_l : INFINITY;
+#pragma unroll
+    for (int k = 0; k < LQ_PPL; ++k) ab[k] = k < cnt ? ab[k] : make_double2(0.0, 0.0);
     // boundary j (lane j <= cnt): j = 0 the coverage start (first gamma >= lo), j >= 1 the end of
     // piece j - 1 (first gamma > ge_{j-1}); its fine bucket clamped to the cell's
     const double gprev = __shfl(ge, max(lane - 1, 0), 64);  // (every lane: no read of an inactive lane)
@@ -302,11 +308,29 @@ __global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
     qa = min(max(qa, cs), ce);
     qb = min(max(qb, cs), ce);
     int qpos = cs;
-    for (int j = 0; j <= cnt; ++j) {  // (wave-uniform loop over the boundaries)
-      const int a = lqw::readlane_i(qa, j), b = lqw::readlane_i(qb, j);  // (j wave-uniform)
-      const double v = lqw::readlane_d(vb, j);
-      const int pj = agg_search(g, a, b, v, j == 0, lane);
-      if (lane == j) qpos = pj;
+    {
+      // every boundary's candidates in flight together (one memory round, not one per boundary);
+      // a bucket wider than 64 EVs falls back to agg_search's binary search
+      double xg[LQ_PPL + 1];
+#pragma unroll
+      for (int j = 0; j <= LQ_PPL; ++j) {
+        const int a = lqw::readlane_i(qa, j), b = lqw::readlane_i(qb, j);  // (j wave-uniform)
+        xg[j] = (j <= cnt && b - a <= 64 && a + lane < b) ? g[a + lane] : INFINITY;
+      }
+#pragma unroll
+      for (int j = 0; j <= LQ_PPL; ++j) {
+        if (j > cnt) break;  // (wave-uniform)
+        const int a = lqw::readlane_i(qa, j), b = lqw::readlane_i(qb, j);
+        const double v = lqw::readlane_d(vb, j);
+        int pj;
+        if (b - a <= 64) {
+          const bool before = j == 0 ? (xg[j] < v) : (xg[j] <= v);
+          pj = a + (int)__popcll(__ballot(before && a + lane < b));
+        } else {
+          pj = agg_search(g, a, b, v, j == 0, lane);
+        }
+        if (lane == j) qpos = pj;
+      }
     }
     if (cnt == 0) qpos = ce;
     // per piece k = lane: [qpos_k, qpos_{k+1})

@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
       }
 #pragma unroll
       for (int j = 0; j <= LQ_PPL; ++j) {
-        if (j > cnt) break;  // (wave-uniform)
+        if (j > cnt) continue;  // (wave-uniform)
         const int a = lqw::readlane_i(qa, j), b = lqw::readlane_i(qb, j);
         const double v = lqw::readlane_d(vb, j);
         int pj;

@@ -404,7 +404,14 @@ def kernel_breakdown(run, step, args, nsteps, pmc, torch):
             if k in pmc and k in out:
                 out[k]["pmc"] = {x: pmc[k][x] for x in pmc[k] if x != "hbm_bytes_per_launch"}
         if "k_path" in pmc and "valu_issue_frac" in pmc["k_path"]:
-            out["k_path"]["valu_issue_frac"] = pmc["k_path"]["valu_issue_frac"]
+            kp = pmc["k_path"]
+            out["k_path"]["valu_issue_frac"] = kp["valu_issue_frac"]  # of a wave's own lifetime
+            # chip level: the waves' VALU-busy cycles over every SIMD (256 CUs x 4) for the
+            # launch's duration at the 2.4 GHz max clock (MI355X_MICROARCH.md) — a lower bound
+            # on the true fraction if the clock ran lower
+            if "waves" in kp and "wave_cycles_avg" in kp and out["k_path"].get("avg_us"):
+                busy = kp["valu_issue_frac"] * kp["wave_cycles_avg"] * kp["waves"]
+                out["k_path"]["valu_chip_frac"] = busy / (1024 * out["k_path"]["avg_us"] * 1e-6 * 2.4e9)
     return out
 
 

@@ -94,8 +94,34 @@ def parse():
     return ap.parse_args()
 
 
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: start the N rank processes (torch.distributed.run, one rank
+    per GPU) from this process, which never touches HIP, and return their exit code; rank 0 prints
+    the line."""
+    import socket
+    import subprocess
+
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def check_env():
+    """No diagnostic knob may be set for a measured run (they select other libraries / forms)."""
+    bad = sorted(k for k in os.environ if k.startswith("LOMPC_"))
+    if bad:
+        raise SystemExit(f"bench.py: diagnostic variables set ({', '.join(bad)}); unset them for a measured run")
+
+
 def main():
     args = parse()
+    check_env()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     import torch
     import torch.distributed as dist
 
@@ -107,6 +133,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:  # (a line must describe the ranks that ran)
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}")
     sharded = world > 1 or args.force_dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -210,29 +238,40 @@ def main():
             # every set's reductions (both EV types) in ONE collective
             combine_set_results([(r["plan"].out["set_sum_w"], r["plan"].out["set_stats"]) for r in runs])
 
-    # warmup (and correctness gate: every QP certified)
-    for k in range(args.warmup):
-        step(k)
+    # one plan: the K timed steps are issued by ONE C-ABI call (lompc_plan_run_steps: the same
+    # launches per step at that step's prices — plus the RCCL all-gather and the combine kernel
+    # when sharded — the HIP events on every E-th step's k_step), so host issue stays far below
+    # the GPU time even on a slow host CPU; every step's set reductions are kept ([K][S][...])
+    batched = len(runs) == 1 and "lm_stride" in runs[0] and not args.per_step_issue and not py_combine
+    # warmup (and correctness gate: every QP certified) — in the timed region's own form, so its
+    # one-time setup (the stepped form's tables and block map) is not timed
+    if batched:
+        r = runs[0]
+        r["plan"].run_steps(r["lm_ptr"][0], r["lr_ptr"], max(args.warmup, 1), r["lm_stride"], 0)
+    else:
+        for k in range(args.warmup):
+            step(k)
     for r in runs:
         rep, fail, inv = r["plan"].check()  # (sticky tallies: every warmup step)
         assert fail == 0 and inv == 0, (fail, inv)
     for r in runs:
         r["plan"].profile(enable=("k_eval",) if not args.no_kernel_events else False)
         r["plan"].profile(read=True, reset=True)
+    sets_t = sets_v = None
+    if batched:
+        S_all = runs[0]["plan"].S
+        sets_t = (torch.empty((args.steps, S_all, N), dtype=torch.float64, device=dev),
+                  torch.empty((args.steps, S_all, 8), dtype=torch.float64, device=dev))
+        sets_v = tuple(torch.empty_like(x) for x in sets_t)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ev_every = max(1, args.event_every)
-    # one plan: the K timed steps are issued by ONE C-ABI call (lompc_plan_run_steps: the same
-    # launches per step at that step's prices — plus the RCCL all-gather and the combine kernel
-    # when sharded — the HIP events on every E-th step's k_eval), so host issue stays far below
-    # the GPU time even on a slow host CPU
-    batched = len(runs) == 1 and "lm_stride" in runs[0] and not args.per_step_issue and not py_combine
     t0 = time.perf_counter()
     if batched:
         r = runs[0]
         r["plan"].run_steps(r["lm_ptr"][args.warmup], r["lr_ptr"], args.steps, r["lm_stride"], 0,
-                            profile_every=0 if args.no_kernel_events else ev_every)
+                            profile_every=0 if args.no_kernel_events else ev_every, set_out=sets_t)
     else:
         for k in range(args.warmup, nsteps):
             sample = not args.no_kernel_events and (k - args.warmup) % ev_every == 0
@@ -261,14 +300,14 @@ def main():
         k_ms += ms
         k_n += n
         k_qps += r["qps"] * n
+    verified = verify_steps(runs[0], args, sets_t, sets_v, torch) if batched else None
     avg_launch_s = (k_ms / 1e3) / max(k_n, 1)
     qp_per_launch = k_qps / max(k_n, 1)
     bytes_per_qp = 8 * (N + 2)
     achieved_gbs = bytes_per_qp * qp_per_launch / avg_launch_s / 1e9 if k_n else 0.0
     # the stepped form (lompc_plan_run_steps, full outputs, no communicator): the timed region's
     # events sit on its k_step launches
-    stepped = (batched and args.mode == "path" and args.outputs == "full" and comm is None
-               and os.environ.get("LOMPC_STEPPED", "1") != "0" and runs[0]["plan"].info()["cells"] % 4 == 0)
+    stepped = batched and args.mode == "path" and runs[0]["plan"].info()["cells"] % 4 == 0
     rkernel = ("k_step (step k+1's path + step k's evaluation + step k-1's closing)" if stepped
                else ("k_eval" if args.mode == "path" else "k_direct"))
 
@@ -304,8 +343,9 @@ def main():
                                                       if sharded else "dp1")),
             "sharded_code_path": bool(sharded),
             "dist_backend": (args.dist_backend if sharded else None),
-            "launches_per_step": (f"1 (k_step) + 3 after the last of the K steps" if stepped
-                                  else sum(r["plan"].launches_per_run() for r in runs)),
+            "launches_per_step": (("1 (k_step) + 2 for the K steps' pipeline fill and drain"
+                                   + ("; + the all-gather and the combine kernel" if comm is not None else ""))
+                                  if stepped else sum(r["plan"].launches_per_run() for r in runs)),
             "kernel_events": "none" if args.no_kernel_events else f"{rkernel.split()[0]}, 1 in {ev_every} timed steps",
             "issue": ("one lompc_plan_run_steps call for the K timed steps" + (" (stepped form)" if stepped else ""))
                      if batched else "per-step lompc_plan_run",
@@ -327,6 +367,8 @@ def main():
         },
         "repaired_qps": repaired,
         "host_issue_us_per_step": t_issue / args.steps * 1e6,
+        "verified_steps": verified["steps"] if verified else 0,
+        "verification": verified or "per-step issue: no per-step records kept",
     }
     pmc = load_pmc(args, N, qp_per_launch)
     pk = "k_step" if stepped else "k_eval"
@@ -358,6 +400,30 @@ def main():
         dist.destroy_process_group()
     if "error" in line.get("bimpc", {}):
         sys.exit(1)  # the QP/s line is printed; a failed station leg still fails the run
+
+
+def verify_steps(run, args, sets_t, sets_v, torch):
+    """Every timed step checked after the timed region: the same K prices re-run through
+    lompc_plan_run_steps in its LOMPC_STEPS_PER_KERNEL form (the same kernels on the same arguments,
+    one part per launch: no overlap inside a launch) must give every step's set reductions (sums of
+    w, counts, sums of cost / w0 / price0, max A_bar error, tallies) and the last step's per-EV w and
+    cost bit for bit.  A mismatch fails the run."""
+    plan = run["plan"]
+    plan.profile(enable=False)
+    last = {k: plan.out[k].clone() for k in ("w", "cost") if plan.out.get(k) is not None}
+    plan.run_steps(run["lm_ptr"][args.warmup], run["lr_ptr"], args.steps, run["lm_stride"], 0, per_kernel=True,
+                   set_out=sets_v)
+    rep, fail, inv = plan.check()
+    assert fail == 0 and inv == 0, (fail, inv)
+    ok = [bool(torch.equal(sets_t[0][k], sets_v[0][k]) and torch.equal(sets_t[1][k], sets_v[1][k]))
+          for k in range(args.steps)]
+    rows = all(torch.equal(v, plan.out[k]) for k, v in last.items())
+    if not (all(ok) and rows):
+        raise SystemExit(f"bench.py: timed steps differ from their re-run: per-step {ok}, last rows {rows}")
+    return {"steps": sum(ok), "how": "every timed step's set reductions and the last step's w / cost re-run "
+                                     "through lompc_plan_run_steps(LOMPC_STEPS_PER_KERNEL) after the timed "
+                                     "region: bitwise equal",
+            "counts_ok": bool((sets_t[1][:, :, 0].sum(dim=1) == plan.B).all())}
 
 
 def load_pmc(args, N, qp_per_launch):
@@ -450,15 +516,18 @@ def direct_leg(eng, N, P, args, nsteps, dev, torch):
 
 def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
     """The per-iteration contracts the reference actually runs on the same batch (both EV types,
-    2P sets, fresh prices every step), each K steps in one lompc_plan_run_steps call:
+    2P sets, fresh prices every step), each K steps in one lompc_plan_run_steps call (the stepped
+    form: one k_step launch per step carries step k+1's path, step k's evaluation — lookups and the
+    per-stage row sums, no rows stored — and step k-1's closing):
 
     * ``reductions`` — PriceSolver._get_w_err (price_solver.py:196-214): only the per-set sums of
       w, the max A_bar error and the counts leave the engine (the reference drops w0, :206);
-      algorithmic HBM bytes = gamma in = 8 B per QP; the sets close inside k_eval (2 launches);
+      algorithmic HBM bytes = gamma in = 8 B per QP;
     * ``w0`` — get_w0_price0 (price_solver.py:272-285): w0 per EV out + price0 sums: 16 B per QP.
 
-    Each reports QP/s, ms per step and k_eval's HIP-event launch time with its HBM roofline at
-    that contract's bytes (latency-bound: 8-16 B per QP is far below what one launch can move)."""
+    Each reports QP/s, ms per step and the k_step launch time (HIP events on its own dispatches)
+    with its HBM roofline at that contract's bytes (latency-bound: 8-16 B per QP is far below what
+    one launch can move; the path chain sets the launch time)."""
     from lompc_amd import BatchPlan
 
     base = run["plan"]
@@ -471,11 +540,10 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
                          want_set=True, stream=torch.cuda.current_stream(), warm_start=args.warm, **kw)
         if comm is not None:
             plan.set_comm(comm)
-        plan.run_steps(lm_ptr[0], lr_ptr, args.warmup, stride, 0)
+        plan.run_steps(lm_ptr[0], lr_ptr, max(args.warmup, 1), stride, 0)
         assert plan.check()[1:] == (0, 0)
-        plan.profile(enable=("k_path", "k_eval", "k_finalize"))
-        for k in ("k_path", "k_eval", "k_finalize"):
-            plan.profile(read=True, reset=True, kernel=k)
+        plan.profile(enable=("k_eval",))
+        plan.profile(read=True, reset=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         plan.run_steps(lm_ptr[args.warmup], lr_ptr, K, stride, 0, profile_every=args.event_every)
@@ -483,20 +551,16 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
         dt = time.perf_counter() - t0
         rep, fail, inv = plan.check()
         assert fail == 0 and inv == 0, (name, fail, inv)
-        ms_e, n_e = plan.profile(read=True, kernel="k_eval")
-        ms_p, n_p = plan.profile(read=True, kernel="k_path")
-        ms_f, n_f = plan.profile(read=True, kernel="k_finalize")
+        ms_e, n_e = plan.profile(read=True)
         B = plan.B
         ev_us = ms_e / max(n_e, 1) * 1e3
         gbs = bpq * B / (ev_us * 1e-6) / 1e9 if n_e else 0.0
         out[name] = {"value": B * K / dt, "unit": "QP/s", "ms_per_step": dt / K * 1e3, "steps": K,
-                     "launches_per_step": plan.launches_per_run(), "repaired_qps": rep,
-                     "k_path_avg_us": ms_p / max(n_p, 1) * 1e3, "k_eval_avg_us": ev_us,
-                     "k_finalize_avg_us": (ms_f / n_f * 1e3) if n_f else None,
-                     "roofline": {"bound": "hbm", "kernel": "k_eval (sets closed in the launch)", "bytes_per_qp": bpq,
+                     "launches_per_step": "1 (k_step) + 2 for the K steps' pipeline fill and drain",
+                     "repaired_qps": rep, "k_step_avg_us": ev_us, "k_step_launches_timed": n_e,
+                     "roofline": {"bound": "hbm", "kernel": "k_step", "bytes_per_qp": bpq,
                                   "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-                                  "note": "latency-bound: the staging round, the lookup and the set closing, not "
-                                          "bytes, set the launch time"}}
+                                  "note": "latency-bound: the path chain of the launch, not bytes, sets its time"}}
         plan.profile(enable=False)
         del plan
     return out

@@ -239,5 +239,6 @@ struct lompc_comm {
 int lq_comm_allgather(lompc_comm* c, const double* send, double* recv, size_t count, hipStream_t st);
 
 // price loops (lompc_plan.hip: host form; lompc_loop.hip: device-resident form and the C-ABI entry)
+const char* lq_failed_text(lompc_plan* p, hipStream_t st);
 int lq_price_loop_host(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd, double* w_k, double* dual_cost,
                        double* dec_actual, double* dec_pred, int* iterations, double* errs, hipStream_t st);

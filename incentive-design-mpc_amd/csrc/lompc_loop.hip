@@ -211,8 +211,7 @@ int lq_price_loop_device(lompc_plan* p, const lompc_price_loop_args* a, double* 
   StepArgs sa{N,        a->r,        MI,       a->tol_avg, a->theta, a->w_max, a->m,
               a->kappa, a->eps_reg,  a->tol,   a->n_evs,   a->dev_sw, a->dev_st, a->dev_in,
               p->d_loop, reinterpret_cast<double*>(reinterpret_cast<char*>(p->d_loop) + 16), d_h, d_dec};
-  int ahead = LOMPC_LOOP_AHEAD;
-  if (const char* e = getenv("LOMPC_LOOP_AHEAD")) ahead = std::max(0, atoi(e));
+  const int ahead = LOMPC_LOOP_AHEAD;
   auto done = [&]() { return __atomic_load_n(const_cast<long long*>(&h->done), __ATOMIC_ACQUIRE) != 0; };
   auto progress = [&]() { return __atomic_load_n(const_cast<long long*>(&h->progress), __ATOMIC_ACQUIRE); };
   // spin until cond() (the device's progress lives in pinned memory); a generous guard against a hang
@@ -264,7 +263,7 @@ int lq_price_loop_device(lompc_plan* p, const lompc_price_loop_args* a, double* 
   }
   if (err == 1) return fail_arg(p, "gamma outside [0, y_max]");
   if (err == 2) {
-    p->err = "LoMPC QPs without a certified optimum";
+    p->err = lq_failed_text(p, st);
     return LOMPC_ERR_NOT_CONVERGED;
   }
   if (err == 3) {

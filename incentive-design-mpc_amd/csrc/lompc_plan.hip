@@ -1317,12 +1317,9 @@ StepKernel step_kernel(int N) {
 // reallocating (hipMalloc / hipHostMalloc synchronise the device and cost far more than a run)
 int64_t with_slack(int64_t n) { return n + n / 4 + 16; }
 
-int pick_cells(int64_t max_set) {
-  const char* env = getenv("LOMPC_CELLS");  // diagnostics (cell-count sweeps)
-  if (env) {
-    const int g = atoi(env);
-    if (g >= 1 && g <= LQ_GMAX) return g;
-  }
+int pick_cells(int64_t max_set, int flags) {
+  const int g = (flags >> LOMPC_PLAN_CELLS_SHIFT) & 2047;  // the caller's choice (LOMPC_PLAN_CELLS)
+  if (g >= 1 && g <= LQ_GMAX) return g;
   // the path of a set has a handful of breakpoints over its gamma window: the cell count trades
   // per-wave tracking latency against more cold starts; one cell for tiny sets
   if (max_set <= 64) return 1;
@@ -1404,7 +1401,8 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   if (B > 0 && !gamma) return fail_arg(p, "plan: gamma required");
   const int N = ctxs[0]->N;
   HIPCHK(p, hipSetDevice(ctxs[0]->device));
-  const int G = pick_cells(max_set);
+  if (((flags >> LOMPC_PLAN_CELLS_SHIFT) & 2047) > LQ_GMAX) return fail_arg(p, "plan: at most 1024 cells per set");
+  const int G = pick_cells(max_set, flags);
   const int64_t ncell = S * G;
   // k_eval work split: every set in nb near-equal blocks of <= EVAL_MAXB EVs, the block count
   // chosen so the workgroups fill the CUs a whole number of times (r rounds of n_cu, at most 90%
@@ -1481,15 +1479,11 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     if ((rc = grow(p, &p->d_tally, 3))) return rc;
     HIPCHK(p, hipMemsetAsync(p->d_tally, 0, 3 * sizeof(unsigned long long), st));
   }
-  {
-    // the sets close inside k_eval when the plan asks for it, and by default in runs that write
-    // no w rows (a price loop's reductions-only runs): nothing then makes the arriving
-    // workgroups wait for row stores, and the k_finalize launch and its boundary go
-    // (LOMPC_CLOSE: 1 = always, 0 = never, diagnostics)
-    const char* ce = getenv("LOMPC_CLOSE");
-    p->close = ce ? atoi(ce) == 1 : (flags & LOMPC_PLAN_CLOSE_IN_EVAL) != 0;
-    p->close_no_w = ce ? atoi(ce) == 1 : true;
-  }
+  // the sets close inside k_eval when the plan asks for it, and by default in single runs that
+  // write no w rows (a price loop's reductions-only runs): nothing then makes the arriving
+  // workgroups wait for row stores, and the k_finalize launch and its boundary go
+  p->close = (flags & LOMPC_PLAN_CLOSE_IN_EVAL) != 0;
+  p->close_no_w = (flags & LOMPC_PLAN_CLOSE_IN_FINALIZE) == 0;
   p->B = B;
   p->S = S;
   p->G = G;
@@ -1505,7 +1499,9 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   const size_t o_off = o_blk + up16((size_t)nblk * sizeof(int4));
   const size_t o_pre = o_off + up16((size_t)(S + 1) * sizeof(int64_t));
   // gamma-sorted sets: blocks of <= LQ_AGG_SB positions of one set for the prepare kernels
-  const bool sorted = (flags & LOMPC_PLAN_SORTED_GAMMA) != 0;
+  // (the exact prefix sums hold 2^40-scaled gamma in 64 bits: a set of 2^24 EVs or more would wrap,
+  // so such a plan evaluates every EV instead)
+  const bool sorted = (flags & LOMPC_PLAN_SORTED_GAMMA) != 0 && max_set < (1ll << 24);
   int64_t nsblk = 0;
   if (sorted)
     for (int64_t s = 0; s < S; ++s) nsblk += (set_offsets[s + 1] - set_offsets[s] + LQ_AGG_SB - 1) / LQ_AGG_SB;
@@ -1718,6 +1714,44 @@ void eval_args(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* 
   r.arrive = p->d_arrive;
 }
 
+// with a communicator: `slots` packed send records [S][N] sums | [S][8] stats and the all-gather's
+// receive buffer [nranks][S (N + 8)] (grown when the plan or the communicator outgrows them)
+int lq_xbufs(lompc_plan* p, int slots) {
+  const int64_t L = p->S * (p->N + LOMPC_SET_STATS);
+  int rc;
+  if (L * slots > p->cap_xsend) {
+    if ((rc = grow(p, &p->d_xsend, L * slots))) return rc;
+    p->cap_xsend = L * slots;
+  }
+  if (L * p->comm->nranks > p->cap_xrecv) {
+    if ((rc = grow(p, &p->d_xrecv, L * p->comm->nranks))) return rc;
+    p->cap_xrecv = L * p->comm->nranks;
+  }
+  return LOMPC_OK;
+}
+
+void lq_combine(const double* recv, int nranks, int64_t S, int N, double* set_sum_w, double* set_stats, hipStream_t st) {
+  const int64_t L = S * (N + LOMPC_SET_STATS);
+  const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>((L + 255) / 256, 1024));
+  hipLaunchKernelGGL(k_combine, dim3(nb), dim3(256), 0, st, recv, nranks, (int)S, N, set_sum_w, set_stats);
+}
+
+// a run's send record (closed on this rank) -> every rank's record -> the rank-ordered combine into
+// the caller's set outputs (all ranks bitwise equal)
+int lq_exchange(lompc_plan* p, const double* send, double* set_sum_w, double* set_stats, hipStream_t st) {
+  const int64_t L = p->S * (p->N + LOMPC_SET_STATS);
+  int rc = lq_comm_allgather(p->comm, send, p->d_xrecv, (size_t)L, st);
+  if (rc) {
+    p->err = p->comm->err;
+    return rc;
+  }
+  if (set_sum_w || set_stats) {
+    lq_combine(p->d_xrecv, p->comm->nranks, p->S, p->N, set_sum_w, set_stats, st);
+    HIPCHK(p, hipGetLastError());
+  }
+  return LOMPC_OK;
+}
+
 int lq_launch_eval(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
                    int8_t* status, double* set_sum_w, double* set_stats, const PathTab& tb, hipStream_t st,
                    lompc_ctx* prof_ctx, FinalArgs* defer = nullptr) {
@@ -1730,16 +1764,8 @@ int lq_launch_eval(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   // with a communicator the sets close into the packed send record [S][N] | [S][8]
   const bool xr = p->comm != nullptr;
   if (xr) {
-    const int64_t L = p->S * (N + LOMPC_SET_STATS);
-    int rc;
-    if (L > p->cap_xsend) {
-      if ((rc = grow(p, &p->d_xsend, L))) return rc;
-      p->cap_xsend = L;
-    }
-    if (L * p->comm->nranks > p->cap_xrecv) {
-      if ((rc = grow(p, &p->d_xrecv, L * p->comm->nranks))) return rc;
-      p->cap_xrecv = L * p->comm->nranks;
-    }
+    const int rc = lq_xbufs(p, 1);
+    if (rc) return rc;
   }
   r.set_sum_w = xr ? p->d_xsend : set_sum_w;
   r.set_stats = xr ? p->d_xsend + p->S * N : set_stats;
@@ -1787,21 +1813,7 @@ int lq_launch_eval(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
     plan_prof_end(p, LOMPC_PLAN_K_FINAL, e0, e1);
   }
   if (!xr) return LOMPC_OK;
-  // every rank's record, then the rank-ordered combine into the caller's set outputs (all ranks
-  // bitwise equal)
-  const int64_t L = p->S * (N + LOMPC_SET_STATS);
-  int rc = lq_comm_allgather(p->comm, p->d_xsend, p->d_xrecv, (size_t)L, st);
-  if (rc) {
-    p->err = p->comm->err;
-    return rc;
-  }
-  if (set_sum_w || set_stats) {
-    const unsigned nb = (unsigned)std::min<int64_t>((L + 255) / 256, 1024);
-    hipLaunchKernelGGL(k_combine, dim3(nb), dim3(256), 0, st, p->d_xrecv, p->comm->nranks, (int)p->S, N, set_sum_w,
-                       set_stats);
-    HIPCHK(p, hipGetLastError());
-  }
-  return LOMPC_OK;
+  return lq_exchange(p, p->d_xsend, set_sum_w, set_stats, st);
 }
 
 int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
@@ -1889,6 +1901,20 @@ int lompc_plan_update(lompc_plan* p, int64_t B, const double* gamma, const int64
 
 }  // extern "C"
 
+// the message for QPs reported failed by a gamma-sorted plan: a set whose gamma is not ascending
+// (k_agg reports all its EVs failed) says so instead of "no certified optimum" (synchronises `st`)
+const char* lq_failed_text(lompc_plan* p, hipStream_t st) {
+  const char* none = "LoMPC QPs without a certified optimum";
+  if (!p->sorted || !p->d_sinfo || p->S < 1) return none;
+  std::vector<int4> si((size_t)p->S);
+  if (hipMemcpyAsync(si.data(), p->d_sinfo, si.size() * sizeof(int4), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return none;
+  for (const int4& x : si)
+    if (x.y == 0) return "LOMPC_PLAN_SORTED_GAMMA: a set's valid gamma is not ascending (all its EVs reported failed)";
+  return none;
+}
+
 // The host form of lompc_price_loop (device_loop = 0): per iteration one plan run, one D2H copy and a
 // stream sync, the convergence test and lompc_price_step on the host.  Arguments checked by the caller.
 int lq_price_loop_host(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd, double* w_k, double* dual_cost,
@@ -1952,7 +1978,7 @@ int lq_price_loop_host(lompc_plan* p, const lompc_price_loop_args* a, double* lm
     for (int s = 0; s < 2; ++s) {
       if (sst[s * LOMPC_SET_STATS + LOMPC_STAT_N_INVALID] > 0) return fail_arg(p, "gamma outside [0, y_max]");
       if (sst[s * LOMPC_SET_STATS + LOMPC_STAT_N_FAILED] > 0) {
-        p->err = "LoMPC QPs without a certified optimum";
+        p->err = lq_failed_text(p, st);
         return LOMPC_ERR_NOT_CONVERGED;
       }
     }
@@ -2089,20 +2115,28 @@ int stepped_setup(lompc_plan* p, hipStream_t st) {
   return LOMPC_OK;
 }
 
-// K >= 2 independent runs, stepped: launch 0 = run 0's path; launch k (1 <= k < K) = k_step(run k's
-// path, run k - 1's evaluation, run k - 2's closing); then run K - 2's closing, run K - 1's
-// evaluation and its closing as their own launches (a closing's individual re-solves write their
-// rows; the last evaluation must not share a launch with the previous closing, so the buffers end
-// holding exactly the last run's outputs).  Run j uses path table j % 2, records j % 2 and
-// cell-start working sets j % 3.
+// K >= 1 independent runs, stepped: launch 0 = run 0's path; launch k (1 <= k <= K) = k_step(run k's
+// path (k < K), run k - 1's evaluation, run k - 2's closing (k >= 2)); launch K + 1 = run K - 1's
+// closing.  Run j uses path table j % 2, records j % 2 and cell-start working sets j % 3.  Only the
+// LAST run's closing writes per-EV outputs (the rows of EVs it re-solved): every earlier closing
+// shares its launch with a later run's evaluation, whose rows must win, and the per-EV outputs end
+// holding the last run's (the set outputs of every run are its own, at the per-run strides).
+// With a communicator, run j's closing fills send slot j % 2 and its all-gather + combine follow the
+// launch that carried it, on the same stream (one collective per run).
+// split (LOMPC_STEPS_PER_KERNEL): every launch above issued as one launch per part (path /
+// evaluation / closing), in that order — the same kernels on the same arguments without the overlap,
+// so the same bits (what the bench's verification compares).
 int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride, const double* lmbd_r,
                          int64_t lmbd_r_stride, int n_runs, int profile_every, double* w, double* cost, double* w0,
-                         int8_t* status, double* set_sum_w, double* set_stats, hipStream_t st) {
+                         int8_t* status, double* set_sum_w, int64_t sw_stride, double* set_stats, int64_t st_stride,
+                         bool split, hipStream_t st) {
   auto& z = p->stp;
   int rc;
   if (!z.ok && (rc = stepped_setup(p, st))) return rc;
   const int N = p->N;
-  const int64_t ncell = p->S * p->G;
+  const int64_t ncell = p->S * p->G, L = p->S * (N + LOMPC_SET_STATS);
+  const bool xr = p->comm != nullptr;
+  if (xr && (rc = lq_xbufs(p, 2))) return rc;
   auto tab = [&](int j) {
     PathTab t = (j & 1) ? z.alt : own_tab(p);
     t.sl = z.sl3 + (size_t)(j % 3) * ncell * 64;
@@ -2110,6 +2144,10 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   };
   auto lm = [&](int j) { return lmbd + (size_t)j * lmbd_stride; };
   auto lr = [&](int j) { return lmbd_r + (size_t)j * lmbd_r_stride; };
+  auto sw_of = [&](int j) { return set_sum_w ? set_sum_w + (size_t)j * sw_stride : nullptr; };
+  auto st_of = [&](int j) { return set_stats ? set_stats + (size_t)j * st_stride : nullptr; };
+  auto xsend = [&](int j) { return p->d_xsend + (size_t)(j & 1) * L; };
+  const int K = n_runs;
   auto args = [&](int j, EvalArgs& a, FinalArgs& r) {
     eval_args(p, lm(j), lr(j), w, cost, w0, status, tab(j), a, r);
     a.blk = reinterpret_cast<const int4*>(z.d_map);
@@ -2121,24 +2159,37 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     a.fail_idx = z.fidx[j & 1];
     r.fail_idx = z.fidx[j & 1];
     r.blk_prefix = reinterpret_cast<const int*>(z.d_map + (((size_t)z.nblk * sizeof(int4) + 15) & ~(size_t)15));
-    r.set_sum_w = set_sum_w;
-    r.set_stats = set_stats;
+    r.set_sum_w = xr ? xsend(j) : sw_of(j);
+    r.set_stats = xr ? xsend(j) + p->S * N : st_of(j);
+    if (j != K - 1) {  // (its re-solved rows would race the next evaluation's and are overwritten anyway)
+      r.w = r.cost = r.w0 = nullptr;
+      r.status = nullptr;
+    }
   };
   const int cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
   const size_t lds = eval_lds(N, p->G, cap);
-  const int mask = p->prof;
-  // diagnostics (timing of the launch's parts): from launch 3 on, LOMPC_STEP_DIAG=1 drops the path
-  // workgroups (the evaluations then read the tables of runs 1 / 2: same coverage, same work),
-  // =2 drops the evaluation and closing workgroups.  Outputs are not the runs' in either case.
-  const char* dg = getenv("LOMPC_STEP_DIAG");
-  const int diag = dg ? atoi(dg) : 0;
+  const StepKernel kern = step_kernel(N);
+  // one k_step launch of (npw path workgroups, ea.nblk evaluation workgroups, nf closing workgroups)
+  auto launch = [&](const PathArgs& pa, const EvalArgs& ea, const FinalArgs& fe, const FinalArgs& ff, int npw, int nf,
+                    bool prof) -> int {
+    if (npw + ea.nblk + nf == 0) return LOMPC_OK;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (prof && plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1)) return fail_arg(p, "profiling events");
+    hipExtLaunchKernelGGL(kern, dim3((unsigned)(npw + ea.nblk + nf)), dim3(EVAL_EVS), lds, st, e0, e1, 0, pa, ea, fe,
+                          ff, npw, nf);
+    HIPCHK(p, hipGetLastError());
+    if (prof) plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
+    return LOMPC_OK;
+  };
   if ((rc = lq_launch_path(p, lm(0), lr(0), tab(0), st))) return rc;
-  for (int k = 1; k < n_runs; ++k) {
-    if (profile_every > 0) p->prof = ((k - 1) % profile_every == 0) ? mask : 0;  // sampled runs carry the events
-    const PathArgs pa = path_args(p, lm(k), lr(k), tab(k));
-    EvalArgs ea;
-    FinalArgs fe, ff;
-    args(k - 1, ea, fe);
+  for (int k = 1; k <= K + 1; ++k) {
+    // sampled runs carry the events (launches 1 .. K - 1: the full k_step form)
+    const bool prof = k < K && (profile_every <= 0 || (k - 1) % profile_every == 0);
+    PathArgs pa = k < K ? path_args(p, lm(k), lr(k), tab(k)) : PathArgs{};
+    EvalArgs ea{};
+    FinalArgs fe{}, ff{};
+    if (k - 1 < K) args(k - 1, ea, fe);
+    else ea.nblk = 0;
     int nf = 0;
     if (k >= 2) {
       EvalArgs dummy;
@@ -2147,30 +2198,27 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     } else {
       ff = fe;
     }
-    int npw = z.np_wg;
-    if (diag == 1 && k >= 3) npw = 0;
-    if (diag == 2 && k >= 3) ea.nblk = nf = 0;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1)) return fail_arg(p, "profiling events");
-    hipExtLaunchKernelGGL(step_kernel(N), dim3((unsigned)(npw + ea.nblk + nf)), dim3(EVAL_EVS), lds, st, e0, e1, 0, pa,
-                          ea, fe, ff, npw, nf);
-    HIPCHK(p, hipGetLastError());
-    plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
+    const int npw = k < K ? z.np_wg : 0;
+#ifdef LQ_STEP_DIAG
+    // diagnostic builds only (-DLQ_STEP_DIAG=1 / 2, timing of the launch's parts): from launch 3 on,
+    // 1 drops the path workgroups, 2 the evaluation and closing workgroups; outputs are not the runs'
+    if (k >= 3 && k < K && LQ_STEP_DIAG == 2) ea.nblk = nf = 0;
+    const int npw_l = (LQ_STEP_DIAG == 1 && k >= 3 && k < K) ? 0 : npw;
+#else
+    const int npw_l = npw;
+#endif
+    if (split) {  // the same parts, one launch each (no overlap)
+      EvalArgs e0 = ea, e1 = ea;
+      e0.nblk = 0;
+      e1.nblk = 0;
+      if ((rc = launch(pa, e0, fe, ff, npw_l, 0, false)) || (rc = launch(pa, ea, fe, ff, 0, 0, prof)) ||
+          (rc = launch(pa, e1, fe, ff, 0, nf, false)))
+        return rc;
+    } else if ((rc = launch(pa, ea, fe, ff, npw_l, nf, prof))) {
+      return rc;
+    }
+    if (xr && k >= 2 && (rc = lq_exchange(p, xsend(k - 2), sw_of(k - 2), st_of(k - 2), st))) return rc;
   }
-  p->prof = mask;
-  const int K = n_runs;
-  EvalArgs ea;
-  FinalArgs fr;
-  if (K >= 2) {
-    args(K - 2, ea, fr);
-    hipLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, fr);
-    HIPCHK(p, hipGetLastError());
-  }
-  args(K - 1, ea, fr);
-  hipLaunchKernelGGL(eval_kernel<false>(N), dim3((unsigned)z.nblk), dim3(EVAL_EVS), lds, st, ea, fr);
-  HIPCHK(p, hipGetLastError());
-  hipLaunchKernelGGL(k_finalize, dim3((unsigned)p->S), dim3(256), 0, st, fr);
-  HIPCHK(p, hipGetLastError());
   return LOMPC_OK;
 }
 
@@ -2185,21 +2233,21 @@ int lompc_plan_run(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
 
 int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride, const double* lmbd_r,
                          int64_t lmbd_r_stride, int n_runs, int profile_every, double* w, double* cost, double* w0,
-                         int8_t* status, double* set_sum_w, double* set_stats, void* stream) {
-  if (!p || n_runs < 0 || profile_every < 0) return LOMPC_ERR_INVALID_ARG;
+                         int8_t* status, double* set_sum_w, double* set_stats, int64_t set_sum_w_stride,
+                         int64_t set_stats_stride, int steps_flags, void* stream) {
+  if (!p || n_runs < 0 || profile_every < 0 || set_sum_w_stride < 0 || set_stats_stride < 0 ||
+      (steps_flags & ~LOMPC_STEPS_PER_KERNEL))
+    return LOMPC_ERR_INVALID_ARG;
   HIPCHK(p, hipSetDevice(p->device));
   hipStream_t st = (hipStream_t)stream;
-  {
-    // stepped form: full per-EV outputs (no communicator, the sets closed by k_finalize), cells in
-    // whole workgroups of one set; LOMPC_STEPPED=0 keeps the form below (diagnostics / A-B)
-    const char* se = getenv("LOMPC_STEPPED");
-    const bool agg = p->sorted && !w && !cost && !w0 && !status;
-    const bool close = p->close || (p->close_no_w && !w);
-    if (n_runs >= 2 && !(se && atoi(se) == 0) && !p->comm && !p->skip && !agg && !close && p->nblk > 0 &&
-        p->G % LQ_STEP_CELLS == 0 && p->N + NPX <= FIN_W)
-      return lq_run_steps_stepped(p, lmbd, lmbd_stride, lmbd_r, lmbd_r_stride, n_runs, profile_every, w, cost, w0,
-                                  status, set_sum_w, set_stats, st);
-  }
+  // stepped form: the k_eval / k_finalize plans (not k_agg, not closed inside k_eval on request),
+  // cells in whole workgroups of one set; runs without w output take it too (their evaluation then
+  // sums the rows it does not store)
+  const bool agg = p->sorted && !w && !cost && !w0 && !status;
+  if (n_runs >= 1 && !p->skip && !agg && !p->close && p->nblk > 0 && p->G % LQ_STEP_CELLS == 0)
+    return lq_run_steps_stepped(p, lmbd, lmbd_stride, lmbd_r, lmbd_r_stride, n_runs, profile_every, w, cost, w0,
+                                status, set_sum_w, set_sum_w_stride, set_stats, set_stats_stride,
+                                (steps_flags & LOMPC_STEPS_PER_KERNEL) != 0, st);
   const int mask = p->prof;
   int rc = LOMPC_OK;
   // run k's closing (k_finalize) rides in run k + 1's path launch (k_path_fin); the last run's
@@ -2212,7 +2260,8 @@ int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     const double* lr = lmbd_r + (size_t)k * lmbd_r_stride;
     const PathTab tb = own_tab(p, k & 1);
     if ((rc = lq_launch_path(p, lm, lr, tb, st, fin.N ? &fin : nullptr))) break;
-    rc = lq_launch_eval(p, lm, lr, w, cost, w0, status, set_sum_w, set_stats, tb, st, nullptr, &fin);
+    rc = lq_launch_eval(p, lm, lr, w, cost, w0, status, set_sum_w ? set_sum_w + (size_t)k * set_sum_w_stride : nullptr,
+                        set_stats ? set_stats + (size_t)k * set_stats_stride : nullptr, tb, st, nullptr, &fin);
   }
   p->prof = mask;
   if (rc == LOMPC_OK && fin.N) {  // the last run's closing
@@ -2235,6 +2284,7 @@ int lompc_plan_status(lompc_plan* p, void* stream, int64_t* n_repaired, int64_t*
   if (n_repaired) *n_repaired = (int64_t)h[0];
   if (n_failed) *n_failed = (int64_t)h[1];
   if (n_invalid) *n_invalid = (int64_t)h[2];
+  if (h[1]) p->err = lq_failed_text(p, (hipStream_t)stream);  // (the caller's exception text)
   if (ef) {
     HIPCHK(p, hipMemsetAsync(p->d_errflag, 0, sizeof(int), (hipStream_t)stream));
     return fail_arg(p, "negative or NaN price parameter (lmbd >= 0, lmbd_r >= 0 required)");
@@ -2285,6 +2335,15 @@ int lompc_plan_set_comm(lompc_plan* p, lompc_comm* comm) {
   if (comm && comm->device != p->device) return fail_arg(p, "set_comm: the communicator's device differs from the plan's");
   p->comm = comm;
   return LOMPC_OK;
+}
+
+int lompc_combine_records(const double* recv, int nranks, int64_t S, int N, double* set_sum_w, double* set_stats,
+                          int device, void* stream) {
+  if (!recv || nranks < 1 || S < 1 || N < 1 || N > LOMPC_MAX_N || S * (N + LOMPC_SET_STATS) >= (1ll << 31))
+    return LOMPC_ERR_INVALID_ARG;
+  if (hipSetDevice(device) != hipSuccess) return LOMPC_ERR_HIP;
+  lq_combine(recv, nranks, S, N, set_sum_w, set_stats, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? LOMPC_OK : LOMPC_ERR_HIP;
 }
 
 int lompc_plan_destroy(lompc_plan* p) {

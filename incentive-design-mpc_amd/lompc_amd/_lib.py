@@ -37,6 +37,15 @@ LOMPC_PLAN_WARM_START = 1
 LOMPC_PLAN_DIAG_REPAIR = 2
 LOMPC_PLAN_CLOSE_IN_EVAL = 8
 LOMPC_PLAN_SORTED_GAMMA = 16
+LOMPC_PLAN_CLOSE_IN_FINALIZE = 32
+LOMPC_PLAN_CELLS_SHIFT = 20
+LOMPC_STEPS_PER_KERNEL = 1
+
+
+def LOMPC_PLAN_CELLS(g: int) -> int:
+    """flags | LOMPC_PLAN_CELLS(g): g gamma cells per set (include/lompc_amd.h)."""
+    return int(g) << LOMPC_PLAN_CELLS_SHIFT
+
 
 LOMPC_QP_OK = 0
 LOMPC_QP_REPAIRED = 1
@@ -80,7 +89,7 @@ SIGNATURES = [
     ("lompc_bimpc_solve", _I, [_I, _I, _I] + [_D] * 10 + [_P] * 6 + [_D] + [_P] * 6),
     ("lompc_plan_create", _I, [_I, _P, _P, _L, _P, _P, _P, _I, _P, ctypes.POINTER(_P)]),
     ("lompc_plan_run", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
-    ("lompc_plan_run_steps", _I, [_P, _P, _L, _P, _L, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    ("lompc_plan_run_steps", _I, [_P, _P, _L, _P, _L, _I, _I, _P, _P, _P, _P, _P, _P, _L, _L, _I, _P]),
     ("lompc_plan_status", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_get_info", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_update", _I, [_P, _L, _P, _P, _P, _P]),
@@ -93,6 +102,7 @@ SIGNATURES = [
     ("lompc_comm_create", _I, [_P, _I, _I, _I, ctypes.POINTER(_P)]),
     ("lompc_comm_destroy", _I, [_P]),
     ("lompc_plan_set_comm", _I, [_P, _P]),
+    ("lompc_combine_records", _I, [_P, _I, _L, _I, _P, _P, _I, _P]),
 ]
 LOMPC_COMM_ID_BYTES = 128
 # lompc_price_loop_args.prof entries
@@ -109,7 +119,7 @@ LOMPC_BIMPC_WEIGHTED = 0
 LOMPC_BIMPC_UNWEIGHTED = 1
 LOMPC_BIMPC_EXP_UNWEIGHTED = 2
 LOMPC_BIMPC_INFO = 5
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class PriceLoopArgs(ctypes.Structure):

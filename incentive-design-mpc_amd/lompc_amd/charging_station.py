@@ -438,10 +438,20 @@ class ChargingStation:
                         main.wait_stream(chain[1]._stream)
         else:
             # sharded: the two chains in the reference's interleaved order on this thread — every
-            # rank must issue the plans' device collectives in the same order
+            # rank must issue the plans' device collectives in the same order.  Each loop's stream
+            # first waits for the previous loop's (its last engine calls and their collectives may
+            # still be queued), so no two collectives on the shared communicator run concurrently,
+            # and the main stream waits for both before any torch.distributed collective follows
+            torch = _torch()
+            main = torch.cuda.current_stream(self.device)
+            prev = main
             for p in range(self.P):
                 for chain in chains:
+                    chain[1]._stream.wait_stream(prev)
                     one(chain, p)
+                    prev = chain[1]._stream
+            for chain in chains:
+                main.wait_stream(chain[1]._stream)
         return prices_s, prices_l, stats_s, stats_l
 
     def _stage_partitions(self):

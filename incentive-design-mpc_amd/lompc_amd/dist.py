@@ -71,7 +71,15 @@ def combine_set_results(pairs, group=None):
     # the same collective on every backend (RCCL on the GPUs; gloo in the CPU tests)
     out = torch.empty(world * L, dtype=packed.dtype, device=packed.device)
     dist.all_gather_into_tensor(out, packed, group=group)
-    rows = out.view(world, L)
+    combine_rows(out.view(world, L), pairs)
+
+
+def combine_rows(rows, pairs) -> None:
+    """The rank-ordered combine of all-gathered records ``rows`` [world, L] (L = the packed
+    (set_sum_w, set_stats) pairs) into ``pairs`` in place: column sums in rank order, the max for
+    LOMPC_STAT_MAX_ERR — what the device combine (lompc_combine_records, k_combine) computes on the
+    same bytes, bit for bit."""
+    world = rows.shape[0]
     tot = rows[0].clone()
     for r in range(1, world):  # fixed rank order
         tot += rows[r]

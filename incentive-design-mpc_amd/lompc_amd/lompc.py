@@ -301,8 +301,10 @@ class LoMPC:
         self._check_rc(rc)
         if inv.value:
             raise AssertionError(f"{inv.value} EVs with gamma outside [0, y_max]")
-        if fail.value:
-            raise SolverError(f"{fail.value} LoMPC QPs without a certified optimum")
+        if fail.value:  # (the plan's text names an unsorted set of a sorted_gamma plan)
+            why = self._lib.lompc_plan_last_error(self._plan).decode(errors="replace") or \
+                "LoMPC QPs without a certified optimum"
+            raise SolverError(f"{fail.value} EVs failed: {why}")
         return rep.value, fail.value, inv.value
 
     def profile(self, enable: bool | None = None, read: bool = False, reset: bool = False):
@@ -339,14 +341,17 @@ class BatchPlan:
     the k_finalize launch (measured slower with w rows: DESIGN.md §10).  ``sorted_gamma``: every
     set's gamma is ascending and stays unmodified until the next ``update`` — runs without per-EV
     outputs then aggregate per certified piece from prefix sums (k_agg, O(pieces) per run; a set
-    found unsorted reports all its EVs failed).  ``set_comm(comm)``: a
+    found unsorted reports all its EVs failed).  ``close_in_finalize``: runs without w output close
+    their sets in the k_finalize launch as well (A/B of the close mode).  ``cells``: gamma cells per
+    set instead of the plan's choice (the answer does not depend on it).  ``set_comm(comm)``: a
     sharded batch — every run combines the set reductions of all ranks on the device (RCCL).
     DIRECT-mode contexts fall back to ``lompc_run`` (one context only).
     """
 
     def __init__(self, lompc, gamma, set_offsets, *, sets_per_ctx=None, w_ref=None, gamma_ref=None, want_w=True,
                  want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None, validate=True,
-                 warm_start=False, diag_repair=False, close_in_eval=False, sorted_gamma=False):
+                 warm_start=False, diag_repair=False, close_in_eval=False, sorted_gamma=False,
+                 close_in_finalize=False, cells=None):
         torch = _torch()
         lompcs = list(lompc) if isinstance(lompc, (list, tuple)) else [lompc]
         self.lompcs = lompcs
@@ -383,7 +388,9 @@ class BatchPlan:
         plan = ctypes.c_void_p()
         flags = ((_lib.LOMPC_PLAN_WARM_START if warm_start else 0) | (_lib.LOMPC_PLAN_DIAG_REPAIR if diag_repair else 0)
                  | (_lib.LOMPC_PLAN_CLOSE_IN_EVAL if close_in_eval else 0)
-                 | (_lib.LOMPC_PLAN_SORTED_GAMMA if sorted_gamma else 0))
+                 | (_lib.LOMPC_PLAN_SORTED_GAMMA if sorted_gamma else 0)
+                 | (_lib.LOMPC_PLAN_CLOSE_IN_FINALIZE if close_in_finalize else 0)
+                 | (_lib.LOMPC_PLAN_CELLS(cells) if cells else 0))
         self._flags = flags
         rc = self._lib.lompc_plan_create(len(lompcs), ctypes.cast(ctxs, ctypes.c_void_p), self.sets_per_ctx.ctypes.data,
                                          self.B, _ptr(self.gamma), self.off.ctypes.data, _ptr(self.w_ref), flags,
@@ -435,19 +442,14 @@ class BatchPlan:
 
     def launches_per_run(self) -> int:
         """Kernel launches of one run: k_path + k_eval + k_finalize; two when the sets close inside
-        k_eval (runs without w output, LOMPC_PLAN_CLOSE_IN_EVAL, LOMPC_CLOSE=1); a communicator adds
-        the all-gather and the combine kernel."""
-        import os
-
+        k_eval (runs without w output unless close_in_finalize, LOMPC_PLAN_CLOSE_IN_EVAL); a
+        communicator adds the all-gather and the combine kernel."""
         if self.direct:
             return 2
         if self._flags & _lib.LOMPC_PLAN_SORTED_GAMMA and not any(self._want[k] for k in ("w", "cost", "w0", "status")):
             return 2 + (2 if self.comm is not None else 0)  # k_path + k_agg
-        env = os.environ.get("LOMPC_CLOSE")
-        if env is not None:
-            close = env == "1"
-        else:
-            close = bool(self._flags & _lib.LOMPC_PLAN_CLOSE_IN_EVAL) or not self._want["w"]
+        close = bool(self._flags & _lib.LOMPC_PLAN_CLOSE_IN_EVAL) or (
+            not self._want["w"] and not self._flags & _lib.LOMPC_PLAN_CLOSE_IN_FINALIZE)
         return (2 if close else 3) + (2 if self.comm is not None else 0)
 
     def set_comm(self, comm) -> "BatchPlan":
@@ -488,6 +490,8 @@ class BatchPlan:
     def _usable(self) -> None:
         if getattr(self, "_broken", None):
             raise RuntimeError(f"BatchPlan unusable after a failed update: {self._broken[1]}")
+        if self.comm is not None and self.comm.handle is None:  # (dist.release_comms destroyed it)
+            raise RuntimeError("BatchPlan: its communicator was closed; attach another (set_comm) or None")
 
     def __del__(self):
         if getattr(self, "_plan", None) is not None:
@@ -525,20 +529,44 @@ class BatchPlan:
         return self.out
 
     def run_steps(self, lmbd, lmbd_r, n_runs: int, lmbd_stride: int, lmbd_r_stride: int = 0,
-                  profile_every: int = 0) -> dict:
+                  profile_every: int = 0, per_run_sets: bool = False, per_kernel: bool = False,
+                  set_out=None) -> dict:
         """n_runs consecutive runs in ONE C-ABI call (lompc_plan_run_steps): run k at the prices
         lmbd + k lmbd_stride, lmbd_r + k lmbd_r_stride (device pointers or tensors, strides in
-        doubles); profile_every > 0: only every E-th run carries the enabled HIP events."""
+        doubles); profile_every > 0: only every E-th run carries the enabled HIP events.
+        per_run_sets: every run's set reductions are kept — the returned dict's ``set_sum_w`` /
+        ``set_stats`` are then (n_runs, S, N) / (n_runs, S, 8) tensors (fresh each call); else they
+        hold the last run's.  per_kernel: LOMPC_STEPS_PER_KERNEL (the same runs, one kernel per
+        launch, bit for bit the same outputs).  set_out: (set_sum_w, set_stats) tensors of shapes
+        (n_runs, S, N) / (n_runs, S, 8) to write every run's reductions into (implies per_run_sets)."""
         if self.direct:
             raise ValueError("run_steps: PATH-mode plans only")
         self._usable()
         pl = lmbd if isinstance(lmbd, int) else lmbd.data_ptr()
         pr = lmbd_r if isinstance(lmbd_r, int) else lmbd_r.data_ptr()
+        outs, out = list(self._outs), self.out
+        sw_stride = st_stride = 0
+        if (per_run_sets or set_out is not None) and self._want["set"]:
+            torch = _torch()
+            dev = f"cuda:{self.lompc.device}"
+            shp = ((int(n_runs), self.S, self.N), (int(n_runs), self.S, _lib.LOMPC_SET_STATS))
+            if set_out is not None:
+                sw, st = set_out
+                if (tuple(sw.shape), tuple(st.shape)) != shp or sw.dtype != torch.float64 or st.dtype != torch.float64 \
+                        or not (sw.is_contiguous() and st.is_contiguous()) or sw.device != self.out["set_sum_w"].device:
+                    raise ValueError(f"run_steps: set_out must be contiguous fp64 tensors of shapes {shp}")
+            else:
+                sw = torch.empty(shp[0], dtype=torch.float64, device=dev)
+                st = torch.empty(shp[1], dtype=torch.float64, device=dev)
+            outs[4], outs[5] = sw.data_ptr(), st.data_ptr()
+            sw_stride, st_stride = self.S * self.N, self.S * _lib.LOMPC_SET_STATS
+            out = dict(self.out, set_sum_w=sw, set_stats=st)
         rc = self._lib.lompc_plan_run_steps(self._plan, pl, int(lmbd_stride), pr, int(lmbd_r_stride), int(n_runs),
-                                            int(profile_every), *self._outs, self._stream)
+                                            int(profile_every), *outs, sw_stride, st_stride,
+                                            _lib.LOMPC_STEPS_PER_KERNEL if per_kernel else 0, self._stream)
         if rc:
             self._check_rc(rc)
-        return self.out
+        return out
 
     def check(self) -> tuple[int, int, int]:
         """Synchronise the plan's stream; raise on uncertified QPs; returns (repaired, failed, invalid)."""
@@ -552,8 +580,10 @@ class BatchPlan:
         self._check_rc(rc)
         if inv.value:
             raise AssertionError(f"{inv.value} EVs with gamma outside [0, y_max]")
-        if fail.value:
-            raise SolverError(f"{fail.value} LoMPC QPs without a certified optimum")
+        if fail.value:  # (the plan's text names an unsorted set of a sorted_gamma plan)
+            why = self._lib.lompc_plan_last_error(self._plan).decode(errors="replace") or \
+                "LoMPC QPs without a certified optimum"
+            raise SolverError(f"{fail.value} EVs failed: {why}")
         return rep.value, fail.value, inv.value
 
     KERNELS = ("k_path", "k_eval", "k_finalize")

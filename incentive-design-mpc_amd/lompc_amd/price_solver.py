@@ -112,6 +112,14 @@ class PriceSolver:
         # the convergence test and the price QP on the GPU after every engine call, no host round trip
         # per iteration (lompc_loop.hip); LOMPC_HOST_LOOP=1: the host form (one copy + sync per iteration)
         self.device_loop = os.environ.get("LOMPC_HOST_LOOP", "0") != "1"
+        if self.group is not None:
+            import torch.distributed as dist
+
+            # several ranks: the host-synchronous C++ loop (one engine call, its collective and a sync
+            # per iteration, nothing enqueued ahead) until the device loop's ahead-enqueued collectives
+            # have run on RCCL at world >= 2 (only world-1 RCCL runs on the one-GPU test box)
+            if dist.get_world_size(self.group) > 1:
+                self.device_loop = False
         self.loop_prof = np.zeros(_lib.LOMPC_LOOP_PROF)
         self.loop_host_ms = {"native_loop": 0.0, "finish_prices": 0.0}
         # the solver's own stream: its loop can run beside the other EV type's (charging_station)
@@ -363,6 +371,7 @@ class PriceSolver:
         price steps stay in C++ until convergence."""
         if self._plan is None:
             raise RuntimeError("set_charge_levels first")
+        self._plan._usable()  # (a closed communicator: raise instead of a collective on freed memory)
         MAX = _settings.MAX_PRICE_SOLVER_ITERATIONS
         A_bar = np.ascontiguousarray(A_bar, dtype=np.float64)
         w_ref = np.ascontiguousarray(w_ref, dtype=np.float64)

@@ -149,7 +149,7 @@ const char* lompc_status_string(int status);
 const char* lompc_last_error(const lompc_ctx* ctx);
 
 /* ABI version (bumped on any signature change). */
-#define LOMPC_ABI_VERSION 3
+#define LOMPC_ABI_VERSION 4
 int lompc_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -177,7 +177,16 @@ typedef struct lompc_plan lompc_plan;
                                       runs with no per-EV output (w, cost, w0, status all NULL — a
                                       price loop's) aggregate each certified piece's EVs from prefix
                                       sums built at create / update (k_agg: work per run O(pieces),
-                                      not O(EVs)); a set found unsorted reports every EV failed */
+                                      not O(EVs)); a set found unsorted reports every EV failed
+                                      (lompc_plan_last_error then says so) */
+#define LOMPC_PLAN_CLOSE_IN_FINALIZE 32 /* runs without w output close their sets in the k_finalize
+                                           launch like runs with w (default: inside k_eval); the
+                                           A/B form of the close-mode parity tests */
+/* gamma cells per set (1 .. 1024) instead of the plan's own choice: flags | LOMPC_PLAN_CELLS(g).
+ * The answer does not depend on it (every piece is certified); it trades per-cell tracking
+ * latency against cold starts. */
+#define LOMPC_PLAN_CELLS_SHIFT 20
+#define LOMPC_PLAN_CELLS(g) ((int)(g) << LOMPC_PLAN_CELLS_SHIFT)
 
 /* Build a plan over B EVs grouped by set (S = sum of sets_per_ctx sets):
  *   ctxs         host [n_ctx]   contexts (same N and device), n_ctx <= LOMPC_PLAN_MAX_CTX
@@ -210,14 +219,23 @@ int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, d
                    double* cost, double* w0, int8_t* status, double* set_sum_w,
                    double* set_stats, void* stream);
 
-/* n_runs consecutive runs (as n_runs lompc_plan_run calls) at the prices lmbd + k lmbd_stride and
- * lmbd_r + k lmbd_r_stride (k = 0 .. n_runs - 1, strides in doubles), every run writing the same
- * outputs; with profile_every > 0 only runs k = 0, E, 2E, ... carry the enabled profiling events.
- * One C-ABI call for a sequence of independent batches (a benchmark's timed steps). */
+/* n_runs consecutive independent runs (as n_runs lompc_plan_run calls) at the prices
+ * lmbd + k lmbd_stride and lmbd_r + k lmbd_r_stride (k = 0 .. n_runs - 1, strides in doubles).
+ * Run k's set reductions go to set_sum_w + k set_sum_w_stride and set_stats + k set_stats_stride
+ * (strides in doubles; 0 = every run writes the same rows, the last run's remain), so every run
+ * of the call is observable; the per-EV outputs (w, cost, w0, status) end holding the last run's.
+ * With profile_every > 0 only runs k = 0, E, 2E, ... carry the enabled profiling events.
+ * One C-ABI call for a sequence of independent batches (a benchmark's timed steps).  Plans whose
+ * cells fill whole path workgroups take the STEPPED form (one launch per run carries run k + 1's
+ * path, run k's evaluation and run k - 1's closing); steps_flags:
+ *   LOMPC_STEPS_PER_KERNEL  the same runs issued one kernel per launch, with the same evaluation
+ *                           block map, so bit for bit the same outputs (verification / A-B) */
+#define LOMPC_STEPS_PER_KERNEL 1
 int lompc_plan_run_steps(lompc_plan* plan, const double* lmbd, int64_t lmbd_stride,
                          const double* lmbd_r, int64_t lmbd_r_stride, int n_runs,
                          int profile_every, double* w, double* cost, double* w0, int8_t* status,
-                         double* set_sum_w, double* set_stats, void* stream);
+                         double* set_sum_w, double* set_stats, int64_t set_sum_w_stride,
+                         int64_t set_stats_stride, int steps_flags, void* stream);
 
 /* Synchronise ``stream``; EVs repaired / failed / invalid summed over EVERY run since the previous
  * lompc_plan_status call (sticky device tallies, zeroed here), so a failure in any of the runs of a
@@ -265,6 +283,15 @@ int lompc_comm_destroy(lompc_comm* comm);
 /* Attach (NULL: detach) a communicator to a plan: from the next run on, the plan's set outputs
  * are the combined records of all ranks (also inside lompc_plan_run_steps and lompc_price_loop). */
 int lompc_plan_set_comm(lompc_plan* plan, lompc_comm* comm);
+/* The device combine every run of a plan with a communicator issues after its ncclAllGather,
+ * on its own (tests / verification): recv dev [nranks][S (N + 8)] = each rank's packed record
+ * (set_sum_w [S][N] | set_stats [S][8]) -> set_sum_w dev [S][N], set_stats dev [S][8] (either may
+ * be NULL), summed in rank order with LOMPC_STAT_MAX_ERR taken as the max: bitwise what
+ * lompc_amd.dist.combine_set_results computes on the same bytes.  Replaces the aggregate of
+ * price_solver.py:205-214 / charging_station.py:356-366 over a sharded batch.  Asynchronous on
+ * ``stream`` of ``device``. */
+int lompc_combine_records(const double* recv, int nranks, int64_t S, int N, double* set_sum_w,
+                          double* set_stats, int device, void* stream);
 
 /* The price loop of one (EV type, partition) on a plan holding [this partition's EVs | the
  * central QP] (PriceSolver.compute_optimal_prices, price_solver.py:106-140): repeated

@@ -87,6 +87,52 @@ def test_plan_with_comm_equals_plain(nccl1, want_w):
     for key, v in plain.out.items():
         if v is not None:
             assert torch.equal(v, shard.out[key]), key
+    # the stepped run_steps with the communicator (one all-gather + combine per run, after the launch
+    # that closed it), every run's records kept: the plain plan's, both issue forms
+    for per_kernel in (False, True):
+        o_s = shard.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, per_kernel=per_kernel)
+        o_p = plain.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True)
+        assert shard.check()[1:] == (0, 0) and plain.check()[1:] == (0, 0)
+        for key, v in o_p.items():
+            if v is not None:
+                assert torch.equal(v, o_s[key]), (per_kernel, key)
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+@pytest.mark.parametrize("S,N", [(24, 24), (24, 48), (5000, 64)])
+def test_combine_records_matches_python_combine(gpu, nranks, S, N):
+    """The device combine that every sharded run issues after its all-gather (k_combine, exposed as
+    lompc_combine_records) on nranks synthetic rank records equals dist.combine_rows (the combine of
+    the gloo path, dist.combine_set_results) on the same bytes bit for bit: rank-ordered sums of every
+    column, the max of LOMPC_STAT_MAX_ERR.  S (N + 8) = 5000 x 72 doubles exceeds the kernel's
+    1024 x 256-thread grid (its grid-stride loop) and any record a plan has all-gathered before."""
+    from lompc_amd import _lib
+    from lompc_amd.dist import combine_rows
+
+    lib = _lib.load()
+    rng = np.random.default_rng(nranks * 1000 + S + N)
+    K = _lib.LOMPC_SET_STATS
+    L = S * (N + K)
+    rows = rng.standard_normal((nranks, L)) * 10.0 ** rng.integers(-6, 6, size=(nranks, L))
+    st = rows[:, S * N:].reshape(nranks, S, K)
+    st[:, :, _lib.LOMPC_STAT_MAX_ERR] = np.abs(st[:, :, _lib.LOMPC_STAT_MAX_ERR]) + 1e-300  # errors >= 0
+    recv = torch.as_tensor(rows, device="cuda:0").contiguous()
+    sw_d = torch.full((S, N), np.nan, dtype=torch.float64, device="cuda:0")
+    st_d = torch.full((S, K), np.nan, dtype=torch.float64, device="cuda:0")
+    stream = torch.cuda.current_stream().cuda_stream
+    assert lib.lompc_combine_records(recv.data_ptr(), nranks, S, N, sw_d.data_ptr(), st_d.data_ptr(), 0, stream) == 0
+    sw_h = torch.empty((S, N), dtype=torch.float64)
+    st_h = torch.empty((S, K), dtype=torch.float64)
+    combine_rows(torch.as_tensor(rows), [(sw_h, st_h)])
+    torch.cuda.synchronize()
+    assert torch.equal(sw_d.cpu(), sw_h) and torch.equal(st_d.cpu(), st_h)
+    # one output only (the other may be NULL), and bad arguments refused
+    st_d.fill_(np.nan)
+    assert lib.lompc_combine_records(recv.data_ptr(), nranks, S, N, None, st_d.data_ptr(), 0, stream) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(st_d.cpu(), st_h)
+    assert lib.lompc_combine_records(recv.data_ptr(), 0, S, N, None, None, 0, stream) == _lib.LOMPC_ERR_INVALID_ARG
+    assert lib.lompc_combine_records(None, nranks, S, N, None, None, 0, stream) == _lib.LOMPC_ERR_INVALID_ARG
 
 
 def test_sharded_price_loop_runs_native(nccl1, monkeypatch):

@@ -251,22 +251,14 @@ def test_warm_start_and_cell_counts(gpu, ev, N):
         np.testing.assert_allclose(ow["cost"].cpu().numpy(), oc["cost"].cpu().numpy(), rtol=1e-12, atol=1e-12)
         check_reductions(ow, off, N)
     oracle_check(oc, g, lms[2], lr, off, c, N, rng)
-    old = os.environ.get("LOMPC_CELLS")
-    try:
-        for G in (1, 16, 512):
-            os.environ["LOMPC_CELLS"] = str(G)
-            p = BatchPlan(lompc, g, off, **kw)
-            assert p.cells == G
-            o = p.run(lms[2], lr)
-            assert p.check()[1:] == (0, 0)
-            np.testing.assert_allclose(o["w"].cpu().numpy(), oc["w"].cpu().numpy(), rtol=0, atol=1e-12)
-            np.testing.assert_allclose(o["set_sum_w"].cpu().numpy(), oc["set_sum_w"].cpu().numpy(), rtol=1e-11,
-                                       atol=1e-10)
-    finally:
-        if old is None:
-            os.environ.pop("LOMPC_CELLS", None)
-        else:
-            os.environ["LOMPC_CELLS"] = old
+    for G in (1, 16, 512):
+        p = BatchPlan(lompc, g, off, cells=G, **kw)
+        assert p.cells == G
+        o = p.run(lms[2], lr)
+        assert p.check()[1:] == (0, 0)
+        np.testing.assert_allclose(o["w"].cpu().numpy(), oc["w"].cpu().numpy(), rtol=0, atol=1e-12)
+        np.testing.assert_allclose(o["set_sum_w"].cpu().numpy(), oc["set_sum_w"].cpu().numpy(), rtol=1e-11,
+                                   atol=1e-10)
 
 
 def test_status_tallies_every_run(gpu):
@@ -382,7 +374,7 @@ def test_close_in_eval_matches_k_finalize(gpu, diag_repair):
 
 def test_reductions_only_runs_close_in_eval(gpu):
     """Runs without w output (a price loop's) close their sets inside k_eval by default; the
-    same plan with LOMPC_CLOSE=0 (k_finalize launch) gives the same costs bitwise and the same
+    same plan with close_in_finalize (k_finalize launch) gives the same costs bitwise and the same
     set reductions up to the summation order (an empty set and a set of one EV included)."""
     N, P = 48, 3
     rng = np.random.default_rng(5)
@@ -394,26 +386,15 @@ def test_reductions_only_runs_close_in_eval(gpu):
     lm = torch.as_tensor(c.theta * rng.random((P, 3 * N)), device="cuda:0")
     lr = torch.as_tensor([0.0, 0.3, 0.1], dtype=torch.float64, device="cuda:0")
     outs = []
-    old = os.environ.get("LOMPC_CLOSE")
-    try:
-        for env in (None, "0"):
-            if env is None:
-                os.environ.pop("LOMPC_CLOSE", None)
-            else:
-                os.environ["LOMPC_CLOSE"] = env
-            plan = BatchPlan(lo, g, off, w_ref=wr, want_w=False, want_cost=True, warm_start=True)
-            assert plan.launches_per_run() == (2 if env is None else 3)
-            res = []
-            for _ in range(3):
-                out = plan.run(lm, lr)
-                assert plan.check()[1:] == (0, 0)
-                res.append({k: v.clone() for k, v in out.items() if v is not None})
-            outs.append(res)
-    finally:
-        if old is None:
-            os.environ.pop("LOMPC_CLOSE", None)
-        else:
-            os.environ["LOMPC_CLOSE"] = old
+    for fin in (False, True):
+        plan = BatchPlan(lo, g, off, w_ref=wr, want_w=False, want_cost=True, warm_start=True, close_in_finalize=fin)
+        assert plan.launches_per_run() == (3 if fin else 2)
+        res = []
+        for _ in range(3):
+            out = plan.run(lm, lr)
+            assert plan.check()[1:] == (0, 0)
+            res.append({k: v.clone() for k, v in out.items() if v is not None})
+        outs.append(res)
     for a, b in zip(*outs):
         assert torch.equal(a["cost"], b["cost"])
         for k in ("set_sum_w", "set_stats"):
@@ -423,10 +404,13 @@ def test_reductions_only_runs_close_in_eval(gpu):
 @pytest.mark.parametrize("K", [2, 3, 7])
 @pytest.mark.parametrize("want_w", [True, False])
 def test_run_steps_matches_single_runs(gpu, want_w, K):
-    """lompc_plan_run_steps (K runs in one C-ABI call, the benchmark's timed steps) writes the
-    same outputs as K lompc_plan_run calls at the same prices, bit for bit, in both its forms
-    (stepped and launch per kernel), and carries the HIP events on sampled runs only; also for runs
-    without w (the sets closed inside k_eval)."""
+    """lompc_plan_run_steps (K runs in one C-ABI call, the benchmark's timed steps) with per-run set
+    outputs: EVERY run's set reductions equal those of an independent lompc_plan_run at the same
+    prices bit for bit, and the oracle's per-EV sums to 1e-9; the per-EV outputs equal the last
+    run's.  Both issue forms (stepped k_step and LOMPC_STEPS_PER_KERNEL, the same parts one launch
+    each) give the same bits; HIP events sit on the sampled runs only; runs without w (their
+    evaluation sums rows it does not store) take the stepped form too.  A plan whose cells do not
+    fill whole path workgroups (6 cells) takes the launch-per-kernel form: the same equalities."""
     N, P, E = 24, 4, 3
     rng = np.random.default_rng(9)
     cs = [O.small_consts(), O.large_consts()]
@@ -434,36 +418,53 @@ def test_run_steps_matches_single_runs(gpu, want_w, K):
     M = [6000, 5000]
     off1 = [np.array([(m * p) // P for p in range(P + 1)], dtype=np.int64) for m in M]
     off = np.concatenate([off1[0], M[0] + off1[1][1:]])
-    g = torch.as_tensor(np.concatenate([c.y_max - (0.3 + 0.2 * rng.random(m)) for c, m in zip(cs, M)]), device="cuda:0")
+    gn = np.concatenate([c.y_max - (0.3 + 0.2 * rng.random(m)) for c, m in zip(cs, M)])
+    g = torch.as_tensor(gn, device="cuda:0")
     lm = torch.as_tensor(np.stack([np.concatenate([c.theta * rng.random((P, 3 * N)) for c in cs]) for _ in range(K)]),
                          device="cuda:0")
     lr = torch.as_tensor(0.05 * rng.random((K, 2 * P)), device="cuda:0")
-    ref = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], want_status=True, want_w=want_w)
-    for k in range(K):
-        ref.run(lm[k], lr[k])
-    assert ref.check()[1:] == (0, 0)
-    plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], want_status=True, want_w=want_w)
-    plan.profile(enable=("k_eval",))
-    plan.profile(read=True, reset=True)
-    out = plan.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), profile_every=E)
-    assert plan.check()[1:] == (0, 0)
-    for key in ("w", "cost", "status", "set_sum_w", "set_stats"):
-        if out.get(key) is not None:
-            assert torch.equal(out[key], ref.out[key]), key
-    ms, n = plan.profile(read=True)
-    assert n >= (K - 1 + E - 1) // E and ms > 0.0
-    # the stepped form (k_step: run k + 1's path, run k's evaluation and run k - 1's closing in one
-    # launch, the default for full outputs) equals the launch-per-kernel form bit for bit
-    os.environ["LOMPC_STEPPED"] = "0"
-    try:
-        seq = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], want_status=True, want_w=want_w)
-        out_s = seq.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel())
+    for cells in (None, 6):
+        # (single runs without w close in k_finalize here, summing rows as run_steps' evaluation does;
+        # by default they close inside k_eval from piece aggregates, equal only to ~1e-12)
+        kw = dict(sets_per_ctx=[P, P], want_status=True, want_w=want_w, cells=cells, close_in_finalize=True)
+        ref = BatchPlan(lompcs, g, off, **kw)
+        runs = []
+        for k in range(K):
+            runs.append({n: v.clone() for n, v in ref.run(lm[k], lr[k]).items() if v is not None})
+        assert ref.check()[1:] == (0, 0)
+        plan = BatchPlan(lompcs, g, off, **kw)
+        plan.profile(enable=("k_eval",))
+        plan.profile(read=True, reset=True)
+        out = plan.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), profile_every=E, per_run_sets=True)
+        assert plan.check()[1:] == (0, 0)
+        for key in ("w", "cost", "status"):
+            if out.get(key) is not None:
+                assert torch.equal(out[key], runs[-1][key]), key
+        for k in range(K):
+            for key in ("set_sum_w", "set_stats"):
+                assert torch.equal(out[key][k], runs[k][key]), (cells, k, key)
+        ms, n = plan.profile(read=True)
+        if cells is None:
+            assert n >= (K - 1 + E - 1) // E and ms > 0.0
+        # the same runs, one kernel per launch: the same bits
+        seq = BatchPlan(lompcs, g, off, **kw)
+        out_s = seq.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, per_kernel=True)
         assert seq.check()[1:] == (0, 0)
-    finally:
-        del os.environ["LOMPC_STEPPED"]
-    for key in ("w", "cost", "status", "set_sum_w", "set_stats"):
-        if out.get(key) is not None:
-            assert torch.equal(out[key], out_s[key]), key
+        for key in ("w", "cost", "status", "set_sum_w", "set_stats"):
+            if out.get(key) is not None:
+                assert torch.equal(out[key], out_s[key]), key
+    if K != 7 or not want_w:
+        return
+    # every run vs the oracle: per-set sums of the per-EV optima
+    sw, st = out["set_sum_w"].cpu().numpy(), out["set_stats"].cpu().numpy()
+    for k in range(K):
+        for s in range(2 * P):
+            a, b = off[s], off[s + 1]
+            wo, co, nf = oracle_c.solve_batch(N, cs[s // P], lm[k, s].cpu().numpy(), float(lr[k, s]), gn[a:b])
+            assert nf == 0
+            np.testing.assert_allclose(sw[k, s], wo.sum(0), rtol=1e-10, atol=1e-9)
+            assert abs(st[k, s, _lib.LOMPC_STAT_SUM_COST] - co.sum()) <= 1e-9 * max(1.0, abs(co.sum()))
+            assert st[k, s, _lib.LOMPC_STAT_COUNT] == b - a
 
 
 @pytest.mark.parametrize("N", [24, 48])

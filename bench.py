@@ -67,11 +67,13 @@ def parse():
                          "set = reductions only")
     ap.add_argument("--split-types", action="store_true",
                     help="path mode: one plan per EV type, each on its own stream (overlapping)")
-    ap.add_argument("--no-kernel-events", action="store_true",
-                    help="diagnostics: no HIP events on the per-EV kernel's dispatches in the timed region")
-    ap.add_argument("--event-every", type=int, default=4,
-                    help="HIP events on the per-EV kernel's dispatch of every E-th timed step (the "
-                         "events' own cost, ~2 us per pair, stays out of the other steps)")
+    ap.add_argument("--no-kernel-events", action="store_true", help="= --kernel-events none")
+    ap.add_argument("--kernel-events", choices=["span", "sampled", "none"], default="span",
+                    help="HIP events of the timed region's stepped launches: span = ONE pair from the start of "
+                         "the first full k_step dispatch to the end of the last (hipExtLaunchKernel events), "
+                         "read as that many launches (each event boundary costs ~4.5 us of idle GPU, so no "
+                         "boundary inside the steady state); sampled = a pair on every E-th launch")
+    ap.add_argument("--event-every", type=int, default=4, help="--kernel-events sampled: every E-th launch")
     ap.add_argument("--per-step-issue", action="store_true",
                     help="diagnostics: issue each timed step from Python (one lompc_plan_run per step)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -119,6 +121,8 @@ def check_env():
 
 def main():
     args = parse()
+    if args.no_kernel_events:
+        args.kernel_events = "none"
     check_env()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
@@ -255,27 +259,32 @@ def main():
         rep, fail, inv = r["plan"].check()  # (sticky tallies: every warmup step)
         assert fail == 0 and inv == 0, (fail, inv)
     for r in runs:
-        r["plan"].profile(enable=("k_eval",) if not args.no_kernel_events else False)
+        r["plan"].profile(enable=("k_eval",) if args.kernel_events != "none" else False)
         r["plan"].profile(read=True, reset=True)
-    sets_t = sets_v = None
+    # every timed step writes its own outputs ([K][B][N] w, [K][B] cost, [K][S][...] set reductions),
+    # so every step is observable afterwards (verify_steps)
+    outs_t = outs_v = None
     if batched:
-        S_all = runs[0]["plan"].S
-        sets_t = (torch.empty((args.steps, S_all, N), dtype=torch.float64, device=dev),
-                  torch.empty((args.steps, S_all, 8), dtype=torch.float64, device=dev))
-        sets_v = tuple(torch.empty_like(x) for x in sets_t)
+        pl = runs[0]["plan"]
+        K = args.steps
+        outs_t = {k: torch.empty((K,) + tuple(v.shape), dtype=v.dtype, device=dev) for k, v in pl.out.items()
+                  if v is not None}
+        outs_v = {k: torch.empty_like(v) for k, v in outs_t.items()}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ev_every = max(1, args.event_every)
+    no_events = args.kernel_events == "none"
     t0 = time.perf_counter()
     if batched:
         r = runs[0]
         r["plan"].run_steps(r["lm_ptr"][args.warmup], r["lr_ptr"], args.steps, r["lm_stride"], 0,
-                            profile_every=0 if args.no_kernel_events else ev_every, set_out=sets_t)
+                            profile_every=0 if no_events else ev_every, out=outs_t,
+                            span_events=args.kernel_events == "span")
     else:
         for k in range(args.warmup, nsteps):
-            sample = not args.no_kernel_events and (k - args.warmup) % ev_every == 0
-            if ev_every > 1 and not args.no_kernel_events:
+            sample = not no_events and (k - args.warmup) % ev_every == 0
+            if ev_every > 1 and not no_events:
                 for r in runs:
                     r["plan"].profile(enable=("k_eval",) if sample else False)
             step(k)
@@ -295,12 +304,13 @@ def main():
         repaired += rep
     # the per-EV kernel's timing over the timed region: HIP events on its own dispatches
     k_ms, k_n, k_qps = 0.0, 0, 0
+    group = runs[0]["plan"].info()["steps_group"] if batched and args.mode == "path" else 0
     for r in runs:
         ms, n = r["plan"].profile(read=True)
         k_ms += ms
         k_n += n
-        k_qps += r["qps"] * n
-    verified = verify_steps(runs[0], args, sets_t, sets_v, torch) if batched else None
+        k_qps += r["qps"] * n * max(group, 1)  # (a stepped launch evaluates `group` steps)
+    verified = verify_steps(runs[0], args, outs_t, outs_v, torch) if batched else None
     avg_launch_s = (k_ms / 1e3) / max(k_n, 1)
     qp_per_launch = k_qps / max(k_n, 1)
     bytes_per_qp = 8 * (N + 2)
@@ -308,8 +318,8 @@ def main():
     # the stepped form (lompc_plan_run_steps, full outputs, no communicator): the timed region's
     # events sit on its k_step launches
     stepped = batched and args.mode == "path" and runs[0]["plan"].info()["cells"] % 4 == 0
-    rkernel = ("k_step (step k+1's path + step k's evaluation + step k-1's closing)" if stepped
-               else ("k_eval" if args.mode == "path" else "k_direct"))
+    rkernel = (f"k_step (the paths of a group of {group} steps + the previous group's evaluations + the "
+               "closings of the group before)" if stepped else ("k_eval" if args.mode == "path" else "k_direct"))
 
     total_qp = world * B * args.steps
     value = total_qp / dt
@@ -343,10 +353,16 @@ def main():
                                                       if sharded else "dp1")),
             "sharded_code_path": bool(sharded),
             "dist_backend": (args.dist_backend if sharded else None),
-            "launches_per_step": (("1 (k_step) + 2 for the K steps' pipeline fill and drain"
-                                   + ("; + the all-gather and the combine kernel" if comm is not None else ""))
+            "launches_per_step": ((f"1/{group} (one k_step per group of {group} steps) + 2 for the K steps' "
+                                   "pipeline fill and drain"
+                                   + ("; + per step the all-gather and the combine kernel" if comm is not None else ""))
                                   if stepped else sum(r["plan"].launches_per_run() for r in runs)),
-            "kernel_events": "none" if args.no_kernel_events else f"{rkernel.split()[0]}, 1 in {ev_every} timed steps",
+            "step_outputs": ("every step's own: w [K][B][N], cost [K][B], set reductions [K][S][...]" if batched
+                             else "shared buffers (the last step's remain)"),
+            "kernel_events": ("none" if no_events else
+                              (f"{rkernel.split()[0]}: one pair spanning {k_n} steady-state launches" if args.kernel_events == "span"
+                               else f"{rkernel.split()[0]}, 1 in {ev_every} timed launches")),
+            "steps_per_launch": group if stepped else 1,
             "issue": ("one lompc_plan_run_steps call for the K timed steps" + (" (stepped form)" if stepped else ""))
                      if batched else "per-step lompc_plan_run",
             "correctness_gate": "sticky device tallies: no failed / invalid QP in any warmup or timed step",
@@ -402,28 +418,26 @@ def main():
         sys.exit(1)  # the QP/s line is printed; a failed station leg still fails the run
 
 
-def verify_steps(run, args, sets_t, sets_v, torch):
+def verify_steps(run, args, outs_t, outs_v, torch):
     """Every timed step checked after the timed region: the same K prices re-run through
     lompc_plan_run_steps in its LOMPC_STEPS_PER_KERNEL form (the same kernels on the same arguments,
-    one part per launch: no overlap inside a launch) must give every step's set reductions (sums of
-    w, counts, sums of cost / w0 / price0, max A_bar error, tallies) and the last step's per-EV w and
-    cost bit for bit.  A mismatch fails the run."""
+    one part per launch: no overlap inside a launch) must give every step's outputs — w, cost and the
+    set reductions (sums of w, counts, sums of cost / w0 / price0, max A_bar error, tallies) — bit for
+    bit.  A mismatch fails the run."""
     plan = run["plan"]
     plan.profile(enable=False)
-    last = {k: plan.out[k].clone() for k in ("w", "cost") if plan.out.get(k) is not None}
     plan.run_steps(run["lm_ptr"][args.warmup], run["lr_ptr"], args.steps, run["lm_stride"], 0, per_kernel=True,
-                   set_out=sets_v)
+                   out=outs_v)
     rep, fail, inv = plan.check()
     assert fail == 0 and inv == 0, (fail, inv)
-    ok = [bool(torch.equal(sets_t[0][k], sets_v[0][k]) and torch.equal(sets_t[1][k], sets_v[1][k]))
-          for k in range(args.steps)]
-    rows = all(torch.equal(v, plan.out[k]) for k, v in last.items())
-    if not (all(ok) and rows):
-        raise SystemExit(f"bench.py: timed steps differ from their re-run: per-step {ok}, last rows {rows}")
-    return {"steps": sum(ok), "how": "every timed step's set reductions and the last step's w / cost re-run "
-                                     "through lompc_plan_run_steps(LOMPC_STEPS_PER_KERNEL) after the timed "
-                                     "region: bitwise equal",
-            "counts_ok": bool((sets_t[1][:, :, 0].sum(dim=1) == plan.B).all())}
+    ok = [all(bool(torch.equal(outs_t[key][k], outs_v[key][k])) for key in outs_t) for k in range(args.steps)]
+    if not all(ok):
+        raise SystemExit(f"bench.py: timed steps differ from their re-run: {ok}")
+    st = outs_t.get("set_stats")
+    return {"steps": sum(ok), "outputs": sorted(outs_t),
+            "how": "every timed step's outputs (w, cost, set reductions) re-run through "
+                   "lompc_plan_run_steps(LOMPC_STEPS_PER_KERNEL) after the timed region: bitwise equal",
+            "counts_ok": bool((st[:, :, 0].sum(dim=1) == plan.B).all()) if st is not None else None}
 
 
 def load_pmc(args, N, qp_per_launch):
@@ -525,8 +539,9 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
       algorithmic HBM bytes = gamma in = 8 B per QP;
     * ``w0`` — get_w0_price0 (price_solver.py:272-285): w0 per EV out + price0 sums: 16 B per QP.
 
-    Each reports QP/s, ms per step and the k_step launch time (HIP events on its own dispatches)
-    with its HBM roofline at that contract's bytes (latency-bound: 8-16 B per QP is far below what
+    Each reports QP/s, ms per step and the k_step launch time (one HIP-event pair over the steady-state
+    launches, each carrying the evaluations of `steps_per_launch` steps) with its HBM roofline at that
+    contract's bytes (latency-bound: 8-16 B per QP is far below what
     one launch can move; the path chain sets the launch time)."""
     from lompc_amd import BatchPlan
 
@@ -546,17 +561,18 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
         plan.profile(read=True, reset=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        plan.run_steps(lm_ptr[args.warmup], lr_ptr, K, stride, 0, profile_every=args.event_every)
+        plan.run_steps(lm_ptr[args.warmup], lr_ptr, K, stride, 0, span_events=True, per_run=True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         rep, fail, inv = plan.check()
         assert fail == 0 and inv == 0, (name, fail, inv)
         ms_e, n_e = plan.profile(read=True)
         B = plan.B
+        grp = max(plan.info()["steps_group"], 1)
         ev_us = ms_e / max(n_e, 1) * 1e3
-        gbs = bpq * B / (ev_us * 1e-6) / 1e9 if n_e else 0.0
+        gbs = bpq * B * grp / (ev_us * 1e-6) / 1e9 if n_e else 0.0
         out[name] = {"value": B * K / dt, "unit": "QP/s", "ms_per_step": dt / K * 1e3, "steps": K,
-                     "launches_per_step": "1 (k_step) + 2 for the K steps' pipeline fill and drain",
+                     "steps_per_launch": grp, "outputs": "every step's own (per-step buffers)",
                      "repaired_qps": rep, "k_step_avg_us": ev_us, "k_step_launches_timed": n_e,
                      "roofline": {"bound": "hbm", "kernel": "k_step", "bytes_per_qp": bpq,
                                   "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,

@@ -40,6 +40,8 @@ LOMPC_PLAN_SORTED_GAMMA = 16
 LOMPC_PLAN_CLOSE_IN_FINALIZE = 32
 LOMPC_PLAN_CELLS_SHIFT = 20
 LOMPC_STEPS_PER_KERNEL = 1
+LOMPC_STEPS_SPAN_EVENTS = 2
+LOMPC_STEPS_ONE_RUN_PER_LAUNCH = 4
 
 
 def LOMPC_PLAN_CELLS(g: int) -> int:
@@ -89,9 +91,9 @@ SIGNATURES = [
     ("lompc_bimpc_solve", _I, [_I, _I, _I] + [_D] * 10 + [_P] * 6 + [_D] + [_P] * 6),
     ("lompc_plan_create", _I, [_I, _P, _P, _L, _P, _P, _P, _I, _P, ctypes.POINTER(_P)]),
     ("lompc_plan_run", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
-    ("lompc_plan_run_steps", _I, [_P, _P, _L, _P, _L, _I, _I, _P, _P, _P, _P, _P, _P, _L, _L, _I, _P]),
+    ("lompc_plan_run_steps", _I, [_P, _P, _L, _P, _L, _I, _I, _P, _P, _P, _P, _P, _P, _L, _L, _L, _I, _P]),
     ("lompc_plan_status", _I, [_P, _P, _P, _P, _P]),
-    ("lompc_plan_get_info", _I, [_P, _P, _P, _P, _P]),
+    ("lompc_plan_get_info", _I, [_P, _P, _P, _P, _P, _P]),
     ("lompc_plan_update", _I, [_P, _L, _P, _P, _P, _P]),
     ("lompc_price_loop", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_plan_profile_enable", _I, [_P, _I]),

@@ -463,13 +463,14 @@ class BatchPlan:
         return self
 
     def info(self) -> dict:
-        """Batch size, parameter sets, gamma cells per set and k_eval workgroups of the plan."""
+        """Batch size, parameter sets, gamma cells per set, k_eval workgroups of the plan and the runs per
+        launch group of its last stepped run_steps call (0: none)."""
         if self.direct:
-            return {"B": self.B, "sets": self.S, "cells": 0, "workgroups": 0}
-        B, S, cells, wg = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int(0), ctypes.c_int(0)
+            return {"B": self.B, "sets": self.S, "cells": 0, "workgroups": 0, "steps_group": 0}
+        B, S, cells, wg, grp = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
         self._check_rc(self._lib.lompc_plan_get_info(self._plan, ctypes.byref(B), ctypes.byref(S), ctypes.byref(cells),
-                                                     ctypes.byref(wg)))
-        return {"B": B.value, "sets": S.value, "cells": cells.value, "workgroups": wg.value}
+                                                     ctypes.byref(wg), ctypes.byref(grp)))
+        return {"B": B.value, "sets": S.value, "cells": cells.value, "workgroups": wg.value, "steps_group": grp.value}
 
     def update(self, gamma, set_offsets, w_ref=None, validate=True) -> "BatchPlan":
         """Re-target the plan at a new batch with the same contexts and set counts (e.g. the
@@ -529,44 +530,63 @@ class BatchPlan:
         return self.out
 
     def run_steps(self, lmbd, lmbd_r, n_runs: int, lmbd_stride: int, lmbd_r_stride: int = 0,
-                  profile_every: int = 0, per_run_sets: bool = False, per_kernel: bool = False,
-                  set_out=None) -> dict:
-        """n_runs consecutive runs in ONE C-ABI call (lompc_plan_run_steps): run k at the prices
-        lmbd + k lmbd_stride, lmbd_r + k lmbd_r_stride (device pointers or tensors, strides in
-        doubles); profile_every > 0: only every E-th run carries the enabled HIP events.
-        per_run_sets: every run's set reductions are kept — the returned dict's ``set_sum_w`` /
-        ``set_stats`` are then (n_runs, S, N) / (n_runs, S, 8) tensors (fresh each call); else they
-        hold the last run's.  per_kernel: LOMPC_STEPS_PER_KERNEL (the same runs, one kernel per
-        launch, bit for bit the same outputs).  set_out: (set_sum_w, set_stats) tensors of shapes
-        (n_runs, S, N) / (n_runs, S, 8) to write every run's reductions into (implies per_run_sets)."""
+                  profile_every: int = 0, per_run_sets: bool = False, per_run: bool = False, out=None,
+                  per_kernel: bool = False, span_events: bool = False, one_run_per_launch: bool = False) -> dict:
+        """n_runs consecutive independent runs in ONE C-ABI call (lompc_plan_run_steps): run k at the
+        prices lmbd + k lmbd_stride, lmbd_r + k lmbd_r_stride (device pointers or tensors, strides in
+        doubles); profile_every > 0: only every E-th stepped launch carries the enabled HIP events.
+
+        Outputs: by default every run writes the plan's ``out`` buffers (the last run's remain).
+        per_run_sets: every run's set reductions kept — ``set_sum_w`` / ``set_stats`` of the returned
+        dict are (n_runs, S, N) / (n_runs, S, 8); per_run: every output kept per run (w (n_runs, B, N),
+        cost / w0 / status (n_runs, B), sets as above; the stepped form then overlaps two runs per
+        group).  out: a dict of preallocated per-run tensors for any of those keys (the others as the
+        flags say).  per_kernel: LOMPC_STEPS_PER_KERNEL (the same runs, one part per launch, bit for
+        bit the same outputs); span_events: one event pair over the stepped launches
+        (LOMPC_STEPS_SPAN_EVENTS); one_run_per_launch: groups of one run."""
         if self.direct:
             raise ValueError("run_steps: PATH-mode plans only")
         self._usable()
+        torch = _torch()
+        K = int(n_runs)
         pl = lmbd if isinstance(lmbd, int) else lmbd.data_ptr()
         pr = lmbd_r if isinstance(lmbd_r, int) else lmbd_r.data_ptr()
-        outs, out = list(self._outs), self.out
-        sw_stride = st_stride = 0
-        if (per_run_sets or set_out is not None) and self._want["set"]:
-            torch = _torch()
-            dev = f"cuda:{self.lompc.device}"
-            shp = ((int(n_runs), self.S, self.N), (int(n_runs), self.S, _lib.LOMPC_SET_STATS))
-            if set_out is not None:
-                sw, st = set_out
-                if (tuple(sw.shape), tuple(st.shape)) != shp or sw.dtype != torch.float64 or st.dtype != torch.float64 \
-                        or not (sw.is_contiguous() and st.is_contiguous()) or sw.device != self.out["set_sum_w"].device:
-                    raise ValueError(f"run_steps: set_out must be contiguous fp64 tensors of shapes {shp}")
-            else:
-                sw = torch.empty(shp[0], dtype=torch.float64, device=dev)
-                st = torch.empty(shp[1], dtype=torch.float64, device=dev)
-            outs[4], outs[5] = sw.data_ptr(), st.data_ptr()
-            sw_stride, st_stride = self.S * self.N, self.S * _lib.LOMPC_SET_STATS
-            out = dict(self.out, set_sum_w=sw, set_stats=st)
-        rc = self._lib.lompc_plan_run_steps(self._plan, pl, int(lmbd_stride), pr, int(lmbd_r_stride), int(n_runs),
-                                            int(profile_every), *outs, sw_stride, st_stride,
-                                            _lib.LOMPC_STEPS_PER_KERNEL if per_kernel else 0, self._stream)
+        keys = ("w", "cost", "w0", "status", "set_sum_w", "set_stats")
+        shapes = {"w": (K, self.B, self.N), "cost": (K, self.B), "w0": (K, self.B), "status": (K, self.B),
+                  "set_sum_w": (K, self.S, self.N), "set_stats": (K, self.S, _lib.LOMPC_SET_STATS)}
+        given = dict(out or {})
+        res = dict(self.out)
+        for k in keys:
+            if self.out[k] is None:
+                if given.get(k) is not None:
+                    raise ValueError(f"run_steps: the plan has no {k} output")
+                continue
+            if k in given or per_run or (per_run_sets and k in ("set_sum_w", "set_stats")):
+                t = given.get(k)
+                if t is None:
+                    t = torch.empty(shapes[k], dtype=self.out[k].dtype, device=self.out[k].device)
+                elif tuple(t.shape) != shapes[k] or t.dtype != self.out[k].dtype or not t.is_contiguous() \
+                        or t.device != self.out[k].device:
+                    raise ValueError(f"run_steps: out[{k!r}] must be a contiguous {self.out[k].dtype} tensor {shapes[k]}")
+                res[k] = t
+        per_ev = [k for k in ("w", "cost", "w0", "status") if res[k] is not None]
+        strided = [res[k].dim() == self.out[k].dim() + 1 for k in per_ev]
+        if any(strided) and not all(strided):
+            raise ValueError("run_steps: the per-EV outputs are either all per run or all shared")
+        ev_stride = self.B if per_ev and strided[0] else 0
+        sw_stride = self.S * self.N if res["set_sum_w"] is not None and res["set_sum_w"].dim() == 3 else 0
+        st_stride = self.S * _lib.LOMPC_SET_STATS if res["set_stats"] is not None and res["set_stats"].dim() == 3 else 0
+        if (res["set_sum_w"] is None) != (res["set_stats"] is None) or (sw_stride == 0) != (st_stride == 0):
+            raise ValueError("run_steps: set_sum_w and set_stats are both per run or both shared")
+        flags = ((_lib.LOMPC_STEPS_PER_KERNEL if per_kernel else 0) | (_lib.LOMPC_STEPS_SPAN_EVENTS if span_events else 0)
+                 | (_lib.LOMPC_STEPS_ONE_RUN_PER_LAUNCH if one_run_per_launch else 0))
+        ptrs = [_ptr(res[k]) for k in keys]
+        rc = self._lib.lompc_plan_run_steps(self._plan, pl, int(lmbd_stride), pr, int(lmbd_r_stride), K,
+                                            int(profile_every), *ptrs, sw_stride, st_stride, ev_stride, flags,
+                                            self._stream)
         if rc:
             self._check_rc(rc)
-        return out
+        return res
 
     def check(self) -> tuple[int, int, int]:
         """Synchronise the plan's stream; raise on uncertified QPs; returns (repaired, failed, invalid)."""

@@ -221,21 +221,31 @@ int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, d
 
 /* n_runs consecutive independent runs (as n_runs lompc_plan_run calls) at the prices
  * lmbd + k lmbd_stride and lmbd_r + k lmbd_r_stride (k = 0 .. n_runs - 1, strides in doubles).
- * Run k's set reductions go to set_sum_w + k set_sum_w_stride and set_stats + k set_stats_stride
- * (strides in doubles; 0 = every run writes the same rows, the last run's remain), so every run
- * of the call is observable; the per-EV outputs (w, cost, w0, status) end holding the last run's.
- * With profile_every > 0 only runs k = 0, E, 2E, ... carry the enabled profiling events.
+ * Run k's set reductions go to set_sum_w + k set_sum_w_stride and set_stats + k set_stats_stride,
+ * its per-EV outputs to w + k ev_stride N, cost / w0 / status + k ev_stride (strides in elements;
+ * 0 = every run writes the same rows and the last run's remain; ev_stride > 0 requires
+ * ev_stride >= B), so every run of the call can be observable.  With profile_every > 0 only every
+ * E-th launch carries the enabled profiling events.
  * One C-ABI call for a sequence of independent batches (a benchmark's timed steps).  Plans whose
- * cells fill whole path workgroups take the STEPPED form (one launch per run carries run k + 1's
- * path, run k's evaluation and run k - 1's closing); steps_flags:
- *   LOMPC_STEPS_PER_KERNEL  the same runs issued one kernel per launch, with the same evaluation
- *                           block map, so bit for bit the same outputs (verification / A-B) */
+ * cells fill whole path workgroups take the STEPPED form: one launch carries the
+ * paths of a group of runs, the evaluations of the previous group and the closings of the group
+ * before — groups of two runs when their per-EV outputs do not overlap (ev_stride > 0 or no per-EV
+ * output) and both paths fit, else of one.  steps_flags:
+ *   LOMPC_STEPS_PER_KERNEL  the same runs issued one part per launch (paths / evaluations /
+ *                           closings), with the same evaluation block map, so bit for bit the same
+ *                           outputs (verification / A-B)
+ *   LOMPC_STEPS_SPAN_EVENTS the enabled K_EVAL timing as ONE event pair from the start of the first
+ *                           full stepped launch to the end of the last, read back as that many
+ *                           launches (no per-launch event boundaries inside the timed steps)
+ *   LOMPC_STEPS_ONE_RUN_PER_LAUNCH  groups of one run (A/B) */
 #define LOMPC_STEPS_PER_KERNEL 1
+#define LOMPC_STEPS_SPAN_EVENTS 2
+#define LOMPC_STEPS_ONE_RUN_PER_LAUNCH 4
 int lompc_plan_run_steps(lompc_plan* plan, const double* lmbd, int64_t lmbd_stride,
                          const double* lmbd_r, int64_t lmbd_r_stride, int n_runs,
                          int profile_every, double* w, double* cost, double* w0, int8_t* status,
                          double* set_sum_w, double* set_stats, int64_t set_sum_w_stride,
-                         int64_t set_stats_stride, int steps_flags, void* stream);
+                         int64_t set_stats_stride, int64_t ev_stride, int steps_flags, void* stream);
 
 /* Synchronise ``stream``; EVs repaired / failed / invalid summed over EVERY run since the previous
  * lompc_plan_status call (sticky device tallies, zeroed here), so a failure in any of the runs of a
@@ -244,9 +254,11 @@ int lompc_plan_run_steps(lompc_plan* plan, const double* lmbd, int64_t lmbd_stri
 int lompc_plan_status(lompc_plan* plan, void* stream, int64_t* n_repaired,
                       int64_t* n_failed, int64_t* n_invalid);
 
-/* Batch size, total parameter sets, gamma cells per set and k_eval workgroups of the plan
- * (any pointer may be null). */
-int lompc_plan_get_info(const lompc_plan* plan, int64_t* B, int64_t* S, int* cells, int* eval_workgroups);
+/* Batch size, total parameter sets, gamma cells per set and k_eval workgroups of the plan, and the
+ * runs per launch group of its last stepped lompc_plan_run_steps call (0: none yet); any pointer may
+ * be null. */
+int lompc_plan_get_info(const lompc_plan* plan, int64_t* B, int64_t* S, int* cells, int* eval_workgroups,
+                        int* steps_group);
 
 /* HIP-event timing of the plan's kernels (hipExtLaunchKernel start/stop events on their own
  * dispatches): enable takes a mask of (1 << LOMPC_PLAN_K_*) bits (0 = off); read synchronises

@@ -2300,8 +2300,8 @@ int lq_run_steps_stepped(lompc_plan* p, int R, const double* lmbd, int64_t lmbd_
   const int64_t bytes = (int64_t)(recs.size() * sizeof(StepLaunch));
   if (!p->ev_steps) HIPCHK(p, hipEventCreateWithFlags(&p->ev_steps, hipEventDisableTiming));
   HIPCHK(p, hipEventSynchronize(p->ev_steps));  // (the staging may still feed the previous call's copy)
-  if (bytes > p->cap_steps) {
-    const int64_t c = with_slack(bytes);
+  if (bytes > p->cap_steps) {  // (room for 64 launches from the start: no allocation between calls)
+    const int64_t c = std::max<int64_t>(with_slack(bytes), 64 * 3 * (int64_t)sizeof(StepLaunch));
     if (p->h_steps) HIPCHK(p, hipHostFree(p->h_steps));
     p->h_steps = nullptr;
     HIPCHK(p, hipHostMalloc((void**)&p->h_steps, (size_t)c, hipHostMallocDefault));
@@ -2338,7 +2338,7 @@ int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
                          int64_t lmbd_r_stride, int n_runs, int profile_every, double* w, double* cost, double* w0,
                          int8_t* status, double* set_sum_w, double* set_stats, int64_t set_sum_w_stride,
                          int64_t set_stats_stride, int64_t ev_stride, int steps_flags, void* stream) {
-  constexpr int known = LOMPC_STEPS_PER_KERNEL | LOMPC_STEPS_SPAN_EVENTS | LOMPC_STEPS_ONE_RUN_PER_LAUNCH;
+  constexpr int known = LOMPC_STEPS_PER_KERNEL | LOMPC_STEPS_SPAN_EVENTS | LOMPC_STEPS_TWO_RUNS_PER_LAUNCH;
   if (!p || n_runs < 0 || profile_every < 0 || set_sum_w_stride < 0 || set_stats_stride < 0 || ev_stride < 0 ||
       (steps_flags & ~known))
     return LOMPC_ERR_INVALID_ARG;
@@ -2354,7 +2354,7 @@ int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     // two runs per group when their per-EV outputs do not overlap (per-run strides, or none) and both
     // paths fit one wave per SIMD beside the evaluation
     const int64_t cells = p->S * p->G;
-    const bool two = !(steps_flags & LOMPC_STEPS_ONE_RUN_PER_LAUNCH) && n_runs >= 2 && (!per_ev || ev_stride > 0) &&
+    const bool two = (steps_flags & LOMPC_STEPS_TWO_RUNS_PER_LAUNCH) && n_runs >= 2 && (!per_ev || ev_stride > 0) &&
                      2 * cells <= 4ll * std::max(p->n_cu, 1) * 3 / 4;
     return lq_run_steps_stepped(p, two ? 2 : 1, lmbd, lmbd_stride, lmbd_r, lmbd_r_stride, n_runs, profile_every,
                                 (steps_flags & LOMPC_STEPS_SPAN_EVENTS) != 0, w, cost, w0, status, ev_stride,

@@ -531,7 +531,7 @@ class BatchPlan:
 
     def run_steps(self, lmbd, lmbd_r, n_runs: int, lmbd_stride: int, lmbd_r_stride: int = 0,
                   profile_every: int = 0, per_run_sets: bool = False, per_run: bool = False, out=None,
-                  per_kernel: bool = False, span_events: bool = False, one_run_per_launch: bool = False) -> dict:
+                  per_kernel: bool = False, span_events: bool = False, two_runs_per_launch: bool = False) -> dict:
         """n_runs consecutive independent runs in ONE C-ABI call (lompc_plan_run_steps): run k at the
         prices lmbd + k lmbd_stride, lmbd_r + k lmbd_r_stride (device pointers or tensors, strides in
         doubles); profile_every > 0: only every E-th stepped launch carries the enabled HIP events.
@@ -539,11 +539,11 @@ class BatchPlan:
         Outputs: by default every run writes the plan's ``out`` buffers (the last run's remain).
         per_run_sets: every run's set reductions kept — ``set_sum_w`` / ``set_stats`` of the returned
         dict are (n_runs, S, N) / (n_runs, S, 8); per_run: every output kept per run (w (n_runs, B, N),
-        cost / w0 / status (n_runs, B), sets as above; the stepped form then overlaps two runs per
-        group).  out: a dict of preallocated per-run tensors for any of those keys (the others as the
+        cost / w0 / status (n_runs, B), sets as above).  out: a dict of preallocated per-run tensors for any of those keys (the others as the
         flags say).  per_kernel: LOMPC_STEPS_PER_KERNEL (the same runs, one part per launch, bit for
         bit the same outputs); span_events: one event pair over the stepped launches
-        (LOMPC_STEPS_SPAN_EVENTS); one_run_per_launch: groups of one run."""
+        (LOMPC_STEPS_SPAN_EVENTS); two_runs_per_launch: groups of two runs (LOMPC_STEPS_TWO_RUNS_PER_LAUNCH;
+        per_run or no per-EV outputs)."""
         if self.direct:
             raise ValueError("run_steps: PATH-mode plans only")
         self._usable()
@@ -579,7 +579,7 @@ class BatchPlan:
         if (res["set_sum_w"] is None) != (res["set_stats"] is None) or (sw_stride == 0) != (st_stride == 0):
             raise ValueError("run_steps: set_sum_w and set_stats are both per run or both shared")
         flags = ((_lib.LOMPC_STEPS_PER_KERNEL if per_kernel else 0) | (_lib.LOMPC_STEPS_SPAN_EVENTS if span_events else 0)
-                 | (_lib.LOMPC_STEPS_ONE_RUN_PER_LAUNCH if one_run_per_launch else 0))
+                 | (_lib.LOMPC_STEPS_TWO_RUNS_PER_LAUNCH if two_runs_per_launch else 0))
         ptrs = [_ptr(res[k]) for k in keys]
         rc = self._lib.lompc_plan_run_steps(self._plan, pl, int(lmbd_stride), pr, int(lmbd_r_stride), K,
                                             int(profile_every), *ptrs, sw_stride, st_stride, ev_stride, flags,

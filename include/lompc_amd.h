@@ -229,18 +229,19 @@ int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, d
  * One C-ABI call for a sequence of independent batches (a benchmark's timed steps).  Plans whose
  * cells fill whole path workgroups take the STEPPED form: one launch carries the
  * paths of a group of runs, the evaluations of the previous group and the closings of the group
- * before — groups of two runs when their per-EV outputs do not overlap (ev_stride > 0 or no per-EV
- * output) and both paths fit, else of one.  steps_flags:
+ * before — groups of one run, or of two on request (LOMPC_STEPS_TWO_RUNS_PER_LAUNCH, when their per-EV
+ * outputs do not overlap: ev_stride > 0 or no per-EV output; and both paths fit).  steps_flags:
  *   LOMPC_STEPS_PER_KERNEL  the same runs issued one part per launch (paths / evaluations /
  *                           closings), with the same evaluation block map, so bit for bit the same
  *                           outputs (verification / A-B)
  *   LOMPC_STEPS_SPAN_EVENTS the enabled K_EVAL timing as ONE event pair from the start of the first
  *                           full stepped launch to the end of the last, read back as that many
  *                           launches (no per-launch event boundaries inside the timed steps)
- *   LOMPC_STEPS_ONE_RUN_PER_LAUNCH  groups of one run (A/B) */
+ *   LOMPC_STEPS_TWO_RUNS_PER_LAUNCH  groups of two runs (measured no faster than one at config 3:
+ *                           the two evaluations take twice one's time) */
 #define LOMPC_STEPS_PER_KERNEL 1
 #define LOMPC_STEPS_SPAN_EVENTS 2
-#define LOMPC_STEPS_ONE_RUN_PER_LAUNCH 4
+#define LOMPC_STEPS_TWO_RUNS_PER_LAUNCH 4
 int lompc_plan_run_steps(lompc_plan* plan, const double* lmbd, int64_t lmbd_stride,
                          const double* lmbd_r, int64_t lmbd_r_stride, int n_runs,
                          int profile_every, double* w, double* cost, double* w0, int8_t* status,

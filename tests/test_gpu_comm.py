@@ -92,8 +92,9 @@ def test_plan_with_comm_equals_plain(nccl1, want_w):
     for per_kernel in (False, True):
         for per_run in (False, True):  # (per_run: two runs per launch, each with its own collective)
             o_s = shard.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, per_run=per_run,
-                                  per_kernel=per_kernel)
-            o_p = plain.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, per_run=per_run)
+                                  per_kernel=per_kernel, two_runs_per_launch=per_run)
+            o_p = plain.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, per_run=per_run,
+                                  two_runs_per_launch=per_run)
             assert shard.check()[1:] == (0, 0) and plain.check()[1:] == (0, 0)
             assert shard.info()["steps_group"] == plain.info()["steps_group"] == (2 if per_run else 1)
             for key, v in o_p.items():

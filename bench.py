@@ -404,6 +404,11 @@ def main():
         line["contracts"] = contract_legs(eng, runs[0], N, P, args, nsteps, dev, torch, comm, pmc)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(eng, N, args.cpu_seconds, args.seed)
+        if path:
+            ref = None
+            if outs_t is not None and "w" in outs_t:  # the first timed step's GPU outputs, for the parity check
+                ref = {k: outs_t[k][0].cpu().numpy() for k in ("w", "cost", "set_sum_w", "set_stats") if k in outs_t}
+            line["cpu_baseline"]["same_algorithm"] = cpu_same_algorithm(eng, N, P, args, ref)
     if path and world == 1 and not args.no_direct:
         line["direct_mode"] = direct_leg(eng, N, P, args, nsteps, dev, torch)
     if not args.no_station:
@@ -738,6 +743,57 @@ def check_station_state(st, consts):
     for key in ("Mp_s", "Mp_l"):
         if int(st.logs["statistics"][key][:, t].sum()) != st.M_2:
             raise AssertionError(f"{key} does not count every EV once")
+
+
+def cpu_same_algorithm(eng, N, P, args, ref):
+    """The PATH engine's own algorithm on this host's cores (oracle/path_cpu.cpp, C++ / OpenMP: per
+    (set, gamma cell) exact start solve + parametric active-set tracking with certified pieces, per-EV
+    lookup and row write, per-set reductions — SURVEY.md §8(d)(1)) on the SAME workload as the GPU line:
+    all 262 144 EVs of both types, 24 sets, full outputs (w, cost, set reductions), the timed steps'
+    fresh prices in turn; all host threads and one thread.  Its outputs for the first timed step are
+    compared with the GPU's (``parity``): the two implementations of one algorithm, fp64 both."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_c  # baseline only
+
+    oracle_c.build()
+    threads = oracle_c.max_threads()
+    cs = [e["c"] for e in eng]
+    off = np.concatenate([eng[0]["off"], eng[0]["M"] + eng[1]["off"][1:]])
+    g = np.concatenate([e["gamma"].cpu().numpy() for e in eng])
+    wr = np.concatenate([e["wr"].cpu().numpy() for e in eng])
+    lms = [np.concatenate([e["lm"][k].cpu().numpy() for e in eng]) for k in range(args.warmup, args.warmup + args.steps)]
+    lr = np.zeros(2 * P)
+    B = int(off[-1])
+
+    def timed(nt, budget):
+        oracle_c.path_run(N, cs, [P, P], lms[0], lr, g, off, w_ref=wr, nthreads=nt)  # warm-up (threads, pages)
+        done, t0, k = 0, time.perf_counter(), 0
+        while True:
+            o = oracle_c.path_run(N, cs, [P, P], lms[k % len(lms)], lr, g, off, w_ref=wr, nthreads=nt)
+            assert o["info"][3] == 0
+            done += B
+            k += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget:
+                return done / dt, k, dt
+
+    v, runs, dt = timed(threads, args.cpu_seconds / 2)
+    v1, runs1, dt1 = timed(1, args.cpu_seconds / 4)
+    out = {"value": v, "unit": "QP/s", "cores": threads, "kind": "port (same algorithm as the GPU path engine)",
+           "sample": f"{runs} runs x {B} EVs (horizon {N}, 24 sets, full outputs, the timed steps' prices) in {dt:.1f} s, "
+                     f"OpenMP {threads} threads (oracle/path_cpu.cpp)",
+           "single_thread": {"value": v1, "sample": f"{runs1} runs x {B} EVs in {dt1:.1f} s, 1 thread"}}
+    if ref is not None:
+        o = oracle_c.path_run(N, cs, [P, P], lms[0], lr, g, off, w_ref=wr, nthreads=threads)
+        out["parity"] = {"step": "the first timed step (all EVs)",
+                         "max_abs_dw": float(np.abs(o["w"] - ref["w"]).max()),
+                         "max_rel_dcost": float((np.abs(o["cost"] - ref["cost"]) / np.maximum(1.0, np.abs(ref["cost"]))).max()),
+                         "max_rel_dset_sum_w": float((np.abs(o["set_sum_w"] - ref["set_sum_w"])
+                                                      / np.maximum(1.0, np.abs(ref["set_sum_w"]))).max()),
+                         "counts_equal": bool(np.array_equal(o["set_stats"][:, 0], ref["set_stats"][:, 0]))}
+        if not out["parity"]["max_abs_dw"] <= 1e-9:
+            raise SystemExit(f"bench.py: CPU path engine and GPU differ: {out['parity']}")
+    return out
 
 
 def cpu_baseline(eng, N, seconds, seed=0):

@@ -14,9 +14,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SO = os.path.join(HERE, "_build", "liboracle_lompc.so")
 
 
+SO_PATH = os.path.join(HERE, "_build", "libpath_cpu.so")
+
+
 def build() -> str:
-    src = os.path.join(HERE, "lompc_oracle.c")
-    if not os.path.exists(SO) or os.path.getmtime(SO) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, f) for f in ("lompc_oracle.c", "path_cpu.cpp", "Makefile")]
+    t = max(os.path.getmtime(f) for f in srcs)
+    if any(not os.path.exists(x) or os.path.getmtime(x) < t for x in (SO, SO_PATH)):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return SO
 
@@ -56,3 +60,49 @@ def solve_batch(N, consts, lmbd, lmbd_r, gamma, nthreads=0):
 
 def max_threads() -> int:
     return int(load().oracle_max_threads())
+
+
+_plib = None
+
+
+def load_path():
+    global _plib
+    if _plib is None:
+        if not os.path.exists(SO_PATH):
+            build()
+        lib = ctypes.CDLL(SO_PATH)
+        P, I, L = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+        lib.path_cpu_run.restype = I
+        lib.path_cpu_run.argtypes = [I, I, P, P, P, P, P, L, P, P, I, P, P, P, P, I, P]
+        lib.path_cpu_max_threads.restype = I
+        _plib = lib
+    return _plib
+
+
+def path_run(N, consts, sets_per_ctx, lmbd, lmbd_r, gamma, set_off, w_ref=None, cells=0, nthreads=0, want_w=True,
+             want_cost=True):
+    """The path engine's algorithm on the host (oracle/path_cpu.cpp): B QPs grouped by set (the sets of
+    consts[0] first), lmbd (S, 3N), lmbd_r (S,), gamma (B,), set_off (S+1,).  Returns a dict of w (B, N),
+    cost (B,), set_sum_w (S, N), set_stats (S, 8) and info (pieces, certified cells, EVs solved
+    individually, EVs failed)."""
+    lib = load_path()
+    cs = np.ascontiguousarray(np.array([[c.delta, c.theta, c.y_max, c.w_max, 1.0 if c.ev_type == "small" else 0.0]
+                                        for c in consts], dtype=np.float64))
+    spc = np.ascontiguousarray(np.asarray(sets_per_ctx, dtype=np.int64))
+    lm = np.ascontiguousarray(np.asarray(lmbd, dtype=np.float64))
+    lr = np.ascontiguousarray(np.asarray(lmbd_r, dtype=np.float64))
+    g = np.ascontiguousarray(np.asarray(gamma, dtype=np.float64))
+    off = np.ascontiguousarray(np.asarray(set_off, dtype=np.int64))
+    wr = None if w_ref is None else np.ascontiguousarray(np.asarray(w_ref, dtype=np.float64))
+    S, B = off.shape[0] - 1, g.shape[0]
+    out = {"w": np.empty((B, N)) if want_w else None, "cost": np.empty(B) if want_cost else None,
+           "set_sum_w": np.empty((S, N)), "set_stats": np.empty((S, 8))}
+    info = np.zeros(4, dtype=np.int64)
+    ptr = lambda a: None if a is None else a.ctypes.data
+    rc = lib.path_cpu_run(int(N), len(consts), cs.ctypes.data, spc.ctypes.data, lm.ctypes.data, lr.ctypes.data,
+                          ptr(wr), B, g.ctypes.data, off.ctypes.data, int(cells), ptr(out["w"]), ptr(out["cost"]),
+                          out["set_sum_w"].ctypes.data, out["set_stats"].ctypes.data, int(nthreads), info.ctypes.data)
+    if rc:
+        raise ValueError(f"path_cpu_run: {rc}")
+    out["info"] = info
+    return out

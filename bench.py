@@ -261,14 +261,15 @@ def main():
     for r in runs:
         r["plan"].profile(enable=("k_eval",) if args.kernel_events != "none" else False)
         r["plan"].profile(read=True, reset=True)
-    # every timed step writes its own outputs ([K][B][N] w, [K][B] cost, [K][S][...] set reductions),
-    # so every step is observable afterwards (verify_steps)
+    # every timed step writes its own set reductions ([K][S][...]), so every step is observable afterwards
+    # (verify_steps); the per-EV outputs (w, cost) are one buffer that every step rewrites, as a price
+    # loop's iterations do (price_solver.py:203-209), the last step's remaining
     outs_t = outs_v = None
     if batched:
         pl = runs[0]["plan"]
         K = args.steps
-        outs_t = {k: torch.empty((K,) + tuple(v.shape), dtype=v.dtype, device=dev) for k, v in pl.out.items()
-                  if v is not None}
+        outs_t = {k: torch.empty((K,) + tuple(pl.out[k].shape), dtype=torch.float64, device=dev)
+                  for k in ("set_sum_w", "set_stats") if pl.out.get(k) is not None}
         outs_v = {k: torch.empty_like(v) for k, v in outs_t.items()}
     if world > 1:
         dist.barrier()
@@ -304,13 +305,17 @@ def main():
         repaired += rep
     # the per-EV kernel's timing over the timed region: HIP events on its own dispatches
     k_ms, k_n, k_qps = 0.0, 0, 0
-    group = runs[0]["plan"].info()["steps_group"] if batched and args.mode == "path" else 0
     for r in runs:
         ms, n = r["plan"].profile(read=True)
         k_ms += ms
         k_n += n
-        k_qps += r["qps"] * n * max(group, 1)  # (a stepped launch evaluates `group` steps)
+        k_qps += r["qps"] * n
     verified = verify_steps(runs[0], args, outs_t, outs_v, torch) if batched else None
+    gpu_last = None  # the last timed step's GPU outputs (host copies), for the CPU engine's parity check
+    if batched and args.mode == "path" and not args.no_cpu_baseline and runs[0]["plan"].out.get("w") is not None:
+        pl = runs[0]["plan"]
+        gpu_last = {"w": pl.out["w"].cpu().numpy(), "cost": pl.out["cost"].cpu().numpy(),
+                    "set_sum_w": outs_t["set_sum_w"][-1].cpu().numpy(), "set_stats": outs_t["set_stats"][-1].cpu().numpy()}
     avg_launch_s = (k_ms / 1e3) / max(k_n, 1)
     qp_per_launch = k_qps / max(k_n, 1)
     bytes_per_qp = 8 * (N + 2)
@@ -318,8 +323,8 @@ def main():
     # the stepped form (lompc_plan_run_steps, full outputs, no communicator): the timed region's
     # events sit on its k_step launches
     stepped = batched and args.mode == "path" and runs[0]["plan"].info()["cells"] % 4 == 0
-    rkernel = (f"k_step (the paths of a group of {group} steps + the previous group's evaluations + the "
-               "closings of the group before)" if stepped else ("k_eval" if args.mode == "path" else "k_direct"))
+    rkernel = ("k_step (step k+1's path + step k's evaluation + step k-1's closing)" if stepped
+               else ("k_eval" if args.mode == "path" else "k_direct"))
 
     total_qp = world * B * args.steps
     value = total_qp / dt
@@ -353,16 +358,14 @@ def main():
                                                       if sharded else "dp1")),
             "sharded_code_path": bool(sharded),
             "dist_backend": (args.dist_backend if sharded else None),
-            "launches_per_step": ((f"1/{group} (one k_step per group of {group} steps) + 2 for the K steps' "
-                                   "pipeline fill and drain"
+            "launches_per_step": (("1 (k_step) + 2 for the K steps' pipeline fill and drain"
                                    + ("; + per step the all-gather and the combine kernel" if comm is not None else ""))
                                   if stepped else sum(r["plan"].launches_per_run() for r in runs)),
-            "step_outputs": ("every step's own: w [K][B][N], cost [K][B], set reductions [K][S][...]" if batched
-                             else "shared buffers (the last step's remain)"),
+            "step_outputs": ("set reductions: every step's own [K][S][...]; w, cost: one buffer every step rewrites"
+                             if batched else "shared buffers (the last step's remain)"),
             "kernel_events": ("none" if no_events else
                               (f"{rkernel.split()[0]}: one pair spanning {k_n} steady-state launches" if args.kernel_events == "span"
                                else f"{rkernel.split()[0]}, 1 in {ev_every} timed launches")),
-            "steps_per_launch": group if stepped else 1,
             "issue": ("one lompc_plan_run_steps call for the K timed steps" + (" (stepped form)" if stepped else ""))
                      if batched else "per-step lompc_plan_run",
             "correctness_gate": "sticky device tallies: no failed / invalid QP in any warmup or timed step",
@@ -405,10 +408,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(eng, N, args.cpu_seconds, args.seed)
         if path:
-            ref = None
-            if outs_t is not None and "w" in outs_t:  # the first timed step's GPU outputs, for the parity check
-                ref = {k: outs_t[k][0].cpu().numpy() for k in ("w", "cost", "set_sum_w", "set_stats") if k in outs_t}
-            line["cpu_baseline"]["same_algorithm"] = cpu_same_algorithm(eng, N, P, args, ref)
+            line["cpu_baseline"]["same_algorithm"] = cpu_same_algorithm(eng, N, P, args, gpu_last)
     if path and world == 1 and not args.no_direct:
         line["direct_mode"] = direct_leg(eng, N, P, args, nsteps, dev, torch)
     if not args.no_station:
@@ -426,22 +426,23 @@ def main():
 def verify_steps(run, args, outs_t, outs_v, torch):
     """Every timed step checked after the timed region: the same K prices re-run through
     lompc_plan_run_steps in its LOMPC_STEPS_PER_KERNEL form (the same kernels on the same arguments,
-    one part per launch: no overlap inside a launch) must give every step's outputs — w, cost and the
-    set reductions (sums of w, counts, sums of cost / w0 / price0, max A_bar error, tallies) — bit for
-    bit.  A mismatch fails the run."""
+    one part per launch: no overlap inside a launch) must give every step's set reductions (sums of w,
+    counts, sums of cost / w0 / price0, max A_bar error, tallies) and the last step's per-EV w and cost
+    bit for bit.  A mismatch fails the run."""
     plan = run["plan"]
     plan.profile(enable=False)
+    last = {k: plan.out[k].clone() for k in ("w", "cost") if plan.out.get(k) is not None}
     plan.run_steps(run["lm_ptr"][args.warmup], run["lr_ptr"], args.steps, run["lm_stride"], 0, per_kernel=True,
                    out=outs_v)
     rep, fail, inv = plan.check()
     assert fail == 0 and inv == 0, (fail, inv)
     ok = [all(bool(torch.equal(outs_t[key][k], outs_v[key][k])) for key in outs_t) for k in range(args.steps)]
-    if not all(ok):
-        raise SystemExit(f"bench.py: timed steps differ from their re-run: {ok}")
+    rows = all(bool(torch.equal(v, plan.out[k])) for k, v in last.items())
+    if not (all(ok) and rows):
+        raise SystemExit(f"bench.py: timed steps differ from their re-run: per-step sets {ok}, last step's rows {rows}")
     st = outs_t.get("set_stats")
-    return {"steps": sum(ok), "outputs": sorted(outs_t),
-            "how": "every timed step's outputs (w, cost, set reductions) re-run through "
-                   "lompc_plan_run_steps(LOMPC_STEPS_PER_KERNEL) after the timed region: bitwise equal",
+    return {"steps": sum(ok), "how": "every timed step's set reductions and the last step's w / cost re-run through "
+                                     "lompc_plan_run_steps(LOMPC_STEPS_PER_KERNEL) after the timed region: bitwise equal",
             "counts_ok": bool((st[:, :, 0].sum(dim=1) == plan.B).all()) if st is not None else None}
 
 
@@ -545,8 +546,7 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
     * ``w0`` — get_w0_price0 (price_solver.py:272-285): w0 per EV out + price0 sums: 16 B per QP.
 
     Each reports QP/s, ms per step and the k_step launch time (one HIP-event pair over the steady-state
-    launches, each carrying the evaluations of `steps_per_launch` steps) with its HBM roofline at that
-    contract's bytes (latency-bound: 8-16 B per QP is far below what
+    launches) with its HBM roofline at that contract's bytes (latency-bound: 8-16 B per QP is far below what
     one launch can move; the path chain sets the launch time)."""
     from lompc_amd import BatchPlan
 
@@ -566,18 +566,17 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
         plan.profile(read=True, reset=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        plan.run_steps(lm_ptr[args.warmup], lr_ptr, K, stride, 0, span_events=True, per_run=True)
+        plan.run_steps(lm_ptr[args.warmup], lr_ptr, K, stride, 0, span_events=True, per_run_sets=True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         rep, fail, inv = plan.check()
         assert fail == 0 and inv == 0, (name, fail, inv)
         ms_e, n_e = plan.profile(read=True)
         B = plan.B
-        grp = max(plan.info()["steps_group"], 1)
         ev_us = ms_e / max(n_e, 1) * 1e3
-        gbs = bpq * B * grp / (ev_us * 1e-6) / 1e9 if n_e else 0.0
+        gbs = bpq * B / (ev_us * 1e-6) / 1e9 if n_e else 0.0
         out[name] = {"value": B * K / dt, "unit": "QP/s", "ms_per_step": dt / K * 1e3, "steps": K,
-                     "steps_per_launch": grp, "outputs": "every step's own (per-step buffers)",
+                     "outputs": "every step's set reductions its own ([K][S][...]); w0 one buffer every step rewrites",
                      "repaired_qps": rep, "k_step_avg_us": ev_us, "k_step_launches_timed": n_e,
                      "roofline": {"bound": "hbm", "kernel": "k_step", "bytes_per_qp": bpq,
                                   "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
@@ -784,8 +783,8 @@ def cpu_same_algorithm(eng, N, P, args, ref):
                      f"OpenMP {threads} threads (oracle/path_cpu.cpp)",
            "single_thread": {"value": v1, "sample": f"{runs1} runs x {B} EVs in {dt1:.1f} s, 1 thread"}}
     if ref is not None:
-        o = oracle_c.path_run(N, cs, [P, P], lms[0], lr, g, off, w_ref=wr, nthreads=threads)
-        out["parity"] = {"step": "the first timed step (all EVs)",
+        o = oracle_c.path_run(N, cs, [P, P], lms[-1], lr, g, off, w_ref=wr, nthreads=threads)
+        out["parity"] = {"step": "the last timed step (all EVs)",
                          "max_abs_dw": float(np.abs(o["w"] - ref["w"]).max()),
                          "max_rel_dcost": float((np.abs(o["cost"] - ref["cost"]) / np.maximum(1.0, np.abs(ref["cost"]))).max()),
                          "max_rel_dset_sum_w": float((np.abs(o["set_sum_w"] - ref["set_sum_w"])

@@ -80,8 +80,6 @@ struct CtxEnds {  // cumulative set counts of a plan's contexts (a kernel argume
 };
 
 // one copy of the path table (k_path writes it, k_eval / k_agg / k_finalize read it)
-#define LQ_STEPS_RMAX 2  // runs per group of the stepped run_steps (k_step's LQ_STEP_RMAX)
-
 struct PathTab {
   int* cnt = nullptr;
   double* lo = nullptr;
@@ -133,32 +131,24 @@ struct lompc_plan {
   double2* t_ab = nullptr;
   uint8_t* t_sl = nullptr;
   uint8_t* d_ws = nullptr;        // [S*G][64] working set at each cell start (warm start)
-  // lompc_plan_run_steps, stepped form (k_step: the paths of a group of R runs, the evaluations of the
-  // previous group and the closings of the group before in one launch): per run in flight a path
-  // table (2R), cell-start working sets (3R) and evaluation records (2R), and the evaluation block map
-  // sized for the slots the paths leave
+  // lompc_plan_run_steps, stepped form (k_step: run k + 1's path, run k's evaluation and run k - 1's
+  // closing in one launch): two path tables, three copies of the cell-start working sets, two sets of
+  // evaluation records and the evaluation block map sized for the slots the path leaves
   struct Stepped {
-    bool ok = false;              // built for the current prepare and R
-    int R = 0;                    // runs per group
-    int nblk = 0, np_wg = 0;      // evaluation workgroups per run, path workgroups per run
+    bool ok = false;              // built for the current prepare
+    int nblk = 0, np_wg = 0;      // evaluation workgroups, path workgroups of a launch
     char* d_map = nullptr;        // int4 blocks [nblk] | int prefix [S+1]
     char* h_map = nullptr;        // pinned staging of the map
     int64_t cap_map = 0;
-    PathTab tab[2 * LQ_STEPS_RMAX]{};
-    uint8_t* sl3 = nullptr;       // [3R][S*G][64]
+    PathTab tab[2]{};
+    uint8_t* sl3 = nullptr;       // [3][S*G][64]
     int64_t cap_cells = 0;
-    int cap_R = 0;
-    double* part[2 * LQ_STEPS_RMAX] = {};
-    int* fcnt[2 * LQ_STEPS_RMAX] = {};
-    int* fidx[2 * LQ_STEPS_RMAX] = {};
+    double* part[2] = {nullptr, nullptr};
+    int* fcnt[2] = {nullptr, nullptr};
+    int* fidx[2] = {nullptr, nullptr};
     int64_t cap_blk = 0;
-    int cap_blk_R = 0;
     int occ = 0, occ_N = -1;      // k_step workgroups per CU (occupancy query) and its horizon
   } stp;
-  char* d_steps = nullptr;        // the stepped form's launch records of the current call (device)
-  char* h_steps = nullptr;        // ... their pinned staging
-  int64_t cap_steps = 0;
-  hipEvent_t ev_steps = nullptr;  // the staging's copy has run
   int* d_errflag = nullptr;
   unsigned long long* d_tally = nullptr;  // [3] EVs repaired / failed / invalid over every run since
                                           // the last lompc_plan_status (sticky, read and zeroed there)

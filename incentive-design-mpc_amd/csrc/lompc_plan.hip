@@ -1275,46 +1275,20 @@ EvalKernel eval_kernel(int N) {
   }
 }
 
-// lompc_plan_run_steps, stepped form: ONE launch carries the paths of up to LQ_STEP_RMAX runs
-// (workgroups of LQ_STEP_CELLS cells of one set, one per wave), the evaluations of the previous group
-// of runs (k_eval's block, the per-run block map sized for the slots the paths leave) and the closings
-// of the group before (one workgroup per set).  All of them are independent (separate path tables,
-// records and cell-start working sets per run in flight), so the latency-bound path chains run beside
-// the bandwidth-bound evaluations instead of before them.  Arguments per run part; a part's runs are
-// [0, rp) / [0, re) / [0, rf) of its arrays.
-#define LQ_STEP_RMAX LQ_STEPS_RMAX
-// element r (workgroup-uniform) of an argument array in device memory, read through the constant
-// address space (scalar loads, as set_consts): the launch records of the stepped form live in a
-// device buffer (one H2D copy per lompc_plan_run_steps call), so a workgroup picks its run's record
-// by a computed address — the same record as a kernel argument would make the compiler copy it
-template <typename T>
-__device__ __forceinline__ const T& kmem_at(const T* base, int r) {
-  typedef const __attribute__((address_space(4))) T KT;
-  r = __builtin_amdgcn_readfirstlane(r);
-  KT* p = (KT*)(uintptr_t)base + r;
-  return *(const T*)p;
-}
-struct StepLaunch {
-  PathArgs pa[LQ_STEP_RMAX];
-  EvalArgs ea[LQ_STEP_RMAX];
-  FinalArgs ff[LQ_STEP_RMAX];
-  int np1, rp;  // path workgroups per run, runs with a path part
-  int nb1, re;  // evaluation workgroups per run, runs with an evaluation part
-  int nf1, rf;  // closing workgroups per run (S), runs with a closing part
-};
-
+// lompc_plan_run_steps, stepped form: ONE launch carries run k + 1's path (workgroups [0, np_wg):
+// LQ_STEP_CELLS cells of one set each, one per wave), run k's evaluation (the next ne workgroups,
+// k_eval's block; the block map sized for the slots the path leaves) and run k - 1's closing (nf
+// workgroups, one per set).  The three are independent (separate path tables, records and cell-start
+// working sets per run in flight), so the latency-bound path chain runs beside the bandwidth-bound
+// evaluation instead of before it.  (The arguments stay kernel arguments: preloaded, where a record in
+// memory would add a dependent load round at the start of every workgroup.)
 template <int NT>
-__global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_step(const StepLaunch* __restrict__ rec) {
+__global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_step(PathArgs pa, EvalArgs ea, FinalArgs ff, int np_wg,
+                                                                    int ne, int nf) {
   extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
-  const StepLaunch& A = kmem_at(rec, 0);
   int b = (int)blockIdx.x;
-  static_assert(LQ_STEP_RMAX == 2, "k_step selects between two runs");
-  // (the run r of a workgroup: its argument record read through the constant address space at a
-  // computed offset — scalar loads; a select between two records makes the compiler copy them)
-  if (b < A.np1 * A.rp) {  // (G % LQ_STEP_CELLS == 0: every cell of a workgroup in one set)
-    const int r = b / A.np1;
-    const PathArgs& pa = kmem_at(A.pa, r);
-    const int c0 = (b - r * A.np1) * LQ_STEP_CELLS;
+  if (b < np_wg) {
+    const int c0 = b * LQ_STEP_CELLS;  // (G % LQ_STEP_CELLS == 0: every cell of the workgroup in one set)
     lq_tab_init(set_consts(pa.qd, pa.ce, c0 / pa.G));
     const int wv = (int)(threadIdx.x >> 6), cell = c0 + wv;
     // the path chain is the launch's critical path: its waves issue first on a SIMD they share
@@ -1323,21 +1297,19 @@ __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_step(const StepLau
     if (wv < LQ_STEP_CELLS && cell < pa.S * pa.G) path_cell<NT, false>(pa, cell);
     return;
   }
-  b -= A.np1 * A.rp;
-  if (b < A.nb1 * A.re) {
-    const int r = b / A.nb1;
-    eval_block<NT, false>(kmem_at(A.ea, r), b - r * A.nb1);
+  b -= np_wg;
+  if (b < ne) {
+    eval_block<NT, false>(ea, b);
     return;
   }
-  b -= A.nb1 * A.re;
-  if (b < A.nf1 * A.rf) {
-    const int r = b / A.nf1;
+  b -= ne;
+  if (b < nf) {
     double (*red)[FIN_W] = reinterpret_cast<double (*)[FIN_W]>(s_dyn);
-    finalize_set<EVAL_WAVES, false>(kmem_at(A.ff, r), b - r * A.nf1, red, red + EVAL_WAVES);
+    finalize_set<EVAL_WAVES, false>(ff, b, red, red + EVAL_WAVES);
   }
 }
 
-typedef void (*StepKernel)(const StepLaunch*);
+typedef void (*StepKernel)(PathArgs, EvalArgs, FinalArgs, int, int, int);
 StepKernel step_kernel(int N) {
   switch (N) {
     case 12: return k_step<12>;
@@ -1880,7 +1852,7 @@ void lq_plan_free(lompc_plan* p) {
     if (x) (void)hipFree(x);
   {
     auto& z = p->stp;
-    for (int k = 0; k < 2 * LQ_STEPS_RMAX; ++k) {
+    for (int k = 0; k < 2; ++k) {
       void* zs[] = {z.tab[k].cnt, z.tab[k].lo, z.tab[k].ge, z.tab[k].cf, z.tab[k].ab, z.part[k], z.fcnt[k], z.fidx[k]};
       for (void* x : zs)
         if (x) (void)hipFree(x);
@@ -1890,9 +1862,7 @@ void lq_plan_free(lompc_plan* p) {
     if (z.h_map) (void)hipHostFree(z.h_map);
   }
   if (p->h_buf) (void)hipHostFree(p->h_buf);
-  if (p->h_steps) (void)hipHostFree(p->h_steps);
-  if (p->d_steps) (void)hipFree(p->d_steps);
-  if (p->ev_steps) (void)hipEventDestroy(p->ev_steps);
+
   if (p->h_loop) (void)hipHostFree(p->h_loop);
   if (p->h_dec) (void)hipHostFree(p->h_dec);
   if (p->ev_stage) (void)hipEventDestroy(p->ev_stage);
@@ -2094,10 +2064,10 @@ int lq_price_loop_host(lompc_plan* p, const lompc_price_loop_args* a, double* lm
   return LOMPC_OK;
 }
 
-// The stepped form's block map, tables and records (once per prepare and group size R).  The paths
-// of a group take R np_wg of the k_step workgroup slots for the whole launch, so the evaluation blocks
-// of the group's R runs are sized to fill the rest once (or a whole number of times for big batches).
-int stepped_setup(lompc_plan* p, int R, hipStream_t st) {
+// The stepped form's block map, tables and records (once per prepare).  The path takes np_wg of the
+// k_step workgroup slots for the whole launch, so the evaluation blocks are sized to fill the rest once
+// (or a whole number of times for big batches).
+int stepped_setup(lompc_plan* p, hipStream_t st) {
   auto& z = p->stp;
   const int N = p->N;
   const int64_t S = p->S, G = p->G, ncell = S * G, B = p->B;
@@ -2109,19 +2079,18 @@ int stepped_setup(lompc_plan* p, int R, hipStream_t st) {
   }
   z.np_wg = (int)((ncell + LQ_STEP_CELLS - 1) / LQ_STEP_CELLS);
   const int64_t slots = (int64_t)p->n_cu * z.occ;
-  const int64_t free1 = std::max<int64_t>(slots - R * z.np_wg, slots / 2);  // the first round, beside the paths
-  const int64_t BR = R * B;
-  const int64_t rounds = std::max<int64_t>(1, (10 * BR + 9ll * slots * EVAL_MAXB - 1) / (9ll * slots * EVAL_MAXB));
+  const int64_t free1 = std::max<int64_t>(slots - z.np_wg, slots / 2);  // the first round, beside the path
+  const int64_t rounds = std::max<int64_t>(1, (10 * B + 9ll * slots * EVAL_MAXB - 1) / (9ll * slots * EVAL_MAXB));
   const int64_t target = free1 + (rounds - 1) * slots;
   std::vector<int64_t> off(S + 1);
   {  // the set offsets from the prepared map (host copy kept in the pinned metadata)
     const int64_t* hoff = reinterpret_cast<const int64_t*>(p->h_buf + p->h_off_at);
     for (int64_t s = 0; s <= S; ++s) off[s] = hoff[s];
   }
-  auto blocks_of = [&](int64_t m) -> int64_t {  // (of one run: R runs share the target)
+  auto blocks_of = [&](int64_t m) -> int64_t {
     if (m <= 0) return 0;
     const int64_t lo = (m + EVAL_MAXB - 1) / EVAL_MAXB, hi = (m + 255) / 256;
-    return std::max<int64_t>(lo, std::min<int64_t>(hi, m * target / std::max<int64_t>(BR, 1)));
+    return std::max<int64_t>(lo, std::min<int64_t>(hi, m * target / std::max<int64_t>(B, 1)));
   };
   int64_t nblk = 0;
   for (int64_t s = 0; s < S; ++s) nblk += blocks_of(off[s + 1] - off[s]);
@@ -2147,78 +2116,73 @@ int stepped_setup(lompc_plan* p, int R, hipStream_t st) {
   }
   HIPCHK(p, hipMemcpyAsync(z.d_map, z.h_map, bytes, hipMemcpyHostToDevice, st));
   z.nblk = (int)nblk;
-  if (ncell > z.cap_cells || R > z.cap_R) {
-    for (int k = 0; k < 2 * R; ++k) {
+  if (ncell > z.cap_cells) {
+    for (int k = 0; k < 2; ++k) {
       auto& t = z.tab[k];
       if ((rc = grow(p, &t.cnt, ncell)) || (rc = grow(p, &t.lo, ncell)) || (rc = grow(p, &t.ge, ncell * LQ_PPL)) ||
           (rc = grow(p, &t.cf, ncell * LQ_PPL * 8)) || (rc = grow(p, &t.ab, ncell * LQ_PPL * N)))
         return rc;
     }
-    if ((rc = grow(p, &z.sl3, 3 * (size_t)R * ncell * 64))) return rc;
+    if ((rc = grow(p, &z.sl3, 3 * (size_t)ncell * 64))) return rc;
     z.cap_cells = ncell;
-    z.cap_R = R;
   }
-  if (nblk > z.cap_blk || R > z.cap_blk_R) {
-    for (int k = 0; k < 2 * R; ++k)
+  if (nblk > z.cap_blk) {
+    for (int k = 0; k < 2; ++k)
       if ((rc = grow(p, &z.part[k], (size_t)nblk * (N + NPX))) || (rc = grow(p, &z.fcnt[k], (size_t)nblk * EVAL_WAVES)) ||
           (rc = grow(p, &z.fidx[k], (size_t)nblk * EVAL_MAXB)))
         return rc;
     z.cap_blk = nblk;
-    z.cap_blk_R = R;
   }
-  z.R = R;
   z.ok = true;
   return LOMPC_OK;
 }
 
-// K >= 1 independent runs, stepped, in groups of R (run j in group g = j / R): launch 0 = the paths of
-// group 0; launch L (1 <= L <= ng) = k_step(paths of group L (L < ng), evaluations of group L - 1,
-// closings of group L - 2 (L >= 2)); launch ng + 1 = the closings of the last group (ng groups).  Run j
-// uses path table 2R ((g % 2) + ...) and records of the same index, cell-start working sets j's slot of
-// 3R.  Per-EV outputs: run k writes w + k ev_stride N (cost, w0, status + k ev_stride); with
-// ev_stride = 0 every run writes the same rows (R = 1 then, and only the LAST run's closing writes
-// per-EV outputs: every earlier closing shares its launch with a later run's evaluation, whose rows must
-// win).  Set outputs of run k at the per-run strides.  With a communicator, run j's closing fills send
-// slot j % 2R and its all-gather + combine follow the launch that carried it, on the same stream (one
-// collective per run).
-// split (LOMPC_STEPS_PER_KERNEL): every launch above issued as one launch per part (paths /
-// evaluations / closings), in that order — the same kernels on the same arguments without the overlap,
-// so the same bits (what the bench's verification compares).
-int lq_run_steps_stepped(lompc_plan* p, int R, const double* lmbd, int64_t lmbd_stride, const double* lmbd_r,
+// K >= 1 independent runs, stepped: launch 0 = run 0's path; launch k (1 <= k <= K) = k_step(run k's
+// path (k < K), run k - 1's evaluation, run k - 2's closing (k >= 2)); launch K + 1 = run K - 1's
+// closing.  Run j uses path table j % 2, records j % 2 and cell-start working sets j % 3.  Per-EV
+// outputs: run k writes w + k ev_stride N (cost, w0, status + k ev_stride); with ev_stride = 0 every
+// run writes the same rows and only the LAST run's closing writes per-EV outputs (every earlier closing
+// shares its launch with a later run's evaluation, whose rows must win).  Set outputs of run k at the
+// per-run strides.  With a communicator, run j's closing fills send slot j % 2 and its all-gather +
+// combine follow the launch that carried it, on the same stream (one collective per run).
+// split (LOMPC_STEPS_PER_KERNEL): every launch above issued as one launch per part (path / evaluation
+// / closing), in that order — the same kernels on the same arguments without the overlap, so the same
+// bits (what the bench's verification compares).  span: one event pair from the start of launch 1's
+// dispatch to the end of launch K - 1's (hipExtLaunchKernel events), read as K - 1 launches.
+int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride, const double* lmbd_r,
                          int64_t lmbd_r_stride, int n_runs, int profile_every, bool span_events, double* w, double* cost,
                          double* w0, int8_t* status, int64_t ev_stride, double* set_sum_w, int64_t sw_stride,
                          double* set_stats, int64_t st_stride, bool split, hipStream_t st) {
   auto& z = p->stp;
   int rc;
-  if ((!z.ok || z.R != R) && (rc = stepped_setup(p, R, st))) return rc;
+  if (!z.ok && (rc = stepped_setup(p, st))) return rc;
   const int N = p->N;
   const int64_t ncell = p->S * p->G, L = p->S * (N + LOMPC_SET_STATS);
   const bool xr = p->comm != nullptr;
-  if (xr && (rc = lq_xbufs(p, 2 * R))) return rc;
-  const int K = n_runs, ng = (K + R - 1) / R;
-  auto slot = [&](int j) { return ((j / R) & 1) * R + j % R; };  // path table / records of run j
+  if (xr && (rc = lq_xbufs(p, 2))) return rc;
+  const int K = n_runs;
   auto tab = [&](int j) {
-    PathTab t = z.tab[slot(j)];
-    t.sl = z.sl3 + (size_t)(((j / R) % 3) * R + j % R) * ncell * 64;
+    PathTab t = z.tab[j & 1];
+    t.sl = z.sl3 + (size_t)(j % 3) * ncell * 64;
     return t;
   };
   auto lm = [&](int j) { return lmbd + (size_t)j * lmbd_stride; };
   auto lr = [&](int j) { return lmbd_r + (size_t)j * lmbd_r_stride; };
   auto sw_of = [&](int j) { return set_sum_w ? set_sum_w + (size_t)j * sw_stride : nullptr; };
   auto st_of = [&](int j) { return set_stats ? set_stats + (size_t)j * st_stride : nullptr; };
-  auto xsend = [&](int j) { return p->d_xsend + (size_t)(j % (2 * R)) * L; };
+  auto xsend = [&](int j) { return p->d_xsend + (size_t)(j & 1) * L; };
   auto args = [&](int j, EvalArgs& a, FinalArgs& r) {
     const size_t eo = (size_t)j * ev_stride;
     eval_args(p, lm(j), lr(j), w ? w + eo * N : nullptr, cost ? cost + eo : nullptr, w0 ? w0 + eo : nullptr,
               status ? status + eo : nullptr, tab(j), a, r);
     a.blk = reinterpret_cast<const int4*>(z.d_map);
     a.nblk = z.nblk;
-    a.partial = z.part[slot(j)];
-    r.partial = z.part[slot(j)];
-    a.fail_cnt = z.fcnt[slot(j)];
-    r.fail_cnt = z.fcnt[slot(j)];
-    a.fail_idx = z.fidx[slot(j)];
-    r.fail_idx = z.fidx[slot(j)];
+    a.partial = z.part[j & 1];
+    r.partial = z.part[j & 1];
+    a.fail_cnt = z.fcnt[j & 1];
+    r.fail_cnt = z.fcnt[j & 1];
+    a.fail_idx = z.fidx[j & 1];
+    r.fail_idx = z.fidx[j & 1];
     r.blk_prefix = reinterpret_cast<const int*>(z.d_map + (((size_t)z.nblk * sizeof(int4) + 15) & ~(size_t)15));
     r.set_sum_w = xr ? xsend(j) : sw_of(j);
     r.set_stats = xr ? xsend(j) + p->S * N : st_of(j);
@@ -2230,97 +2194,56 @@ int lq_run_steps_stepped(lompc_plan* p, int R, const double* lmbd, int64_t lmbd_
   const int cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
   const size_t lds = eval_lds(N, p->G, cap);
   const StepKernel kern = step_kernel(N);
-  // span: ONE event pair, the start of the first steady-state launch's dispatch and the end of the
-  // last one's (hipExtLaunchKernel events), read as ng - 1 launches of the average duration
   hipEvent_t span0 = nullptr, span1 = nullptr;
-  if (span_events && ng >= 2 && plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &span0, &span1)) return fail_arg(p, "profiling events");
-  // one k_step launch of the parts in A (rp / re / rf runs); prof: its own event pair
-  // (1) every launch's record, (2) one copy of them to the device, (3) the launches
-  struct Item {
-    int rec, nwg, x0, nx;  // record, workgroups, the runs whose exchange follows it: [x0, x0 + nx)
-    bool prof;
-    hipEvent_t s0, s1;     // span events (start of this dispatch / end of it)
+  if (span_events && K >= 2 && plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &span0, &span1)) return fail_arg(p, "profiling events");
+  // one k_step launch of (npw path, ne evaluation, nf closing workgroups); prof: its own event pair
+  auto launch = [&](const PathArgs& pa, const EvalArgs& ea, const FinalArgs& ff, int npw, int ne, int nf, bool prof,
+                    hipEvent_t s0, hipEvent_t s1) -> int {
+    if (npw + ne + nf == 0) return LOMPC_OK;
+    hipEvent_t e0 = s0, e1 = s1;
+    if (prof && plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1)) return fail_arg(p, "profiling events");
+    hipExtLaunchKernelGGL(kern, dim3((unsigned)(npw + ne + nf)), dim3(EVAL_EVS), lds, st, e0, e1, 0, pa, ea, ff, npw, ne,
+                          nf);
+    HIPCHK(p, hipGetLastError());
+    if (prof) plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
+    return LOMPC_OK;
   };
-  std::vector<StepLaunch> recs;
-  std::vector<Item> items;
-  recs.reserve(3 * (size_t)(ng + 2));
-  auto add = [&](const StepLaunch& A, bool prof, hipEvent_t s0, hipEvent_t s1) {
-    const int nwg = A.np1 * A.rp + A.nb1 * A.re + A.nf1 * A.rf;
-    if (nwg == 0) return;
-    recs.push_back(A);
-    items.push_back(Item{(int)recs.size() - 1, nwg, 0, 0, prof, s0, s1});
-  };
-  for (int Lc = 0; Lc <= ng + 1; ++Lc) {
-    StepLaunch A{};
-    A.np1 = z.np_wg;
-    A.nb1 = z.nblk;
-    A.nf1 = (int)p->S;
-    // paths of group Lc, evaluations of group Lc - 1, closings of group Lc - 2
-    for (int i = 0; i < R; ++i) {
-      const int jp = Lc * R + i, je = (Lc - 1) * R + i, jf = (Lc - 2) * R + i;
-      if (Lc < ng && jp < K) A.pa[A.rp++] = path_args(p, lm(jp), lr(jp), tab(jp));
-      if (Lc >= 1 && Lc - 1 < ng && je < K) {
-        FinalArgs unused;
-        args(je, A.ea[A.re++], unused);
-      }
-      if (Lc >= 2 && jf < K) {
-        EvalArgs unused;
-        args(jf, unused, A.ff[A.rf++]);
-      }
+  for (int k = 0; k <= K + 1; ++k) {
+    const PathArgs pa = k < K ? path_args(p, lm(k), lr(k), tab(k)) : PathArgs{};
+    const int npw = k < K ? z.np_wg : 0;
+    EvalArgs ea{}, unused_e;
+    FinalArgs ff{}, unused_f;
+    int ne = 0, nf = 0;
+    if (k >= 1 && k - 1 < K) {
+      args(k - 1, ea, unused_f);
+      ne = z.nblk;
     }
+    if (k >= 2) {
+      args(k - 2, unused_e, ff);
+      nf = (int)p->S;
+    }
+    int npw_l = npw;
 #ifdef LQ_STEP_DIAG
     // diagnostic builds only (-DLQ_STEP_DIAG=1 / 2, timing of the launch's parts): from launch 3 on,
     // 1 drops the path workgroups, 2 the evaluation and closing workgroups; outputs are not the runs'
-    if (Lc >= 3 && Lc < ng) {
-      if (LQ_STEP_DIAG == 1) A.rp = 0;
-      if (LQ_STEP_DIAG == 2) A.re = A.rf = 0;
+    if (k >= 3 && k < K) {
+      if (LQ_STEP_DIAG == 1) npw_l = 0;
+      if (LQ_STEP_DIAG == 2) ne = nf = 0;
     }
 #endif
-    // the full k_step launches (1 .. ng - 1) carry the events: sampled per launch, or one pair
-    // around all of them (span: no event boundary inside the steady state)
-    const bool steady = Lc >= 1 && Lc < ng;
-    const bool prof = !span_events && steady && (profile_every <= 0 || (Lc - 1) % profile_every == 0);
-    hipEvent_t s0 = (span0 && Lc == 1) ? span0 : nullptr, s1 = (span0 && Lc == ng - 1) ? span1 : nullptr;
+    // the full k_step launches (1 .. K - 1) carry the events: sampled, or one pair around all of them
+    const bool steady = k >= 1 && k < K;
+    const bool prof = !span_events && steady && (profile_every <= 0 || (k - 1) % profile_every == 0);
+    const hipEvent_t s0 = (span0 && k == 1) ? span0 : nullptr, s1 = (span0 && k == K - 1) ? span1 : nullptr;
     if (split) {  // the same parts, one launch each (no overlap)
-      StepLaunch P = A, E = A, F = A;
-      P.re = P.rf = 0;
-      E.rp = E.rf = 0;
-      F.rp = F.re = 0;
-      add(P, false, nullptr, nullptr);
-      add(E, prof, s0, s1);
-      add(F, false, nullptr, nullptr);
-    } else {
-      add(A, prof, s0, s1);
+      if ((rc = launch(pa, ea, ff, npw_l, 0, 0, false, nullptr, nullptr)) ||
+          (rc = launch(pa, ea, ff, 0, ne, 0, prof, s0, s1)) || (rc = launch(pa, ea, ff, 0, 0, nf, false, nullptr, nullptr)))
+        return rc;
+    } else if ((rc = launch(pa, ea, ff, npw_l, ne, nf, prof, s0, s1))) {
+      return rc;
     }
-    if (xr && A.rf > 0) {
-      items.back().x0 = (Lc - 2) * R;
-      items.back().nx = A.rf;
-    }
-  }
-  const int64_t bytes = (int64_t)(recs.size() * sizeof(StepLaunch));
-  if (!p->ev_steps) HIPCHK(p, hipEventCreateWithFlags(&p->ev_steps, hipEventDisableTiming));
-  HIPCHK(p, hipEventSynchronize(p->ev_steps));  // (the staging may still feed the previous call's copy)
-  if (bytes > p->cap_steps) {  // (room for 64 launches from the start: no allocation between calls)
-    const int64_t c = std::max<int64_t>(with_slack(bytes), 64 * 3 * (int64_t)sizeof(StepLaunch));
-    if (p->h_steps) HIPCHK(p, hipHostFree(p->h_steps));
-    p->h_steps = nullptr;
-    HIPCHK(p, hipHostMalloc((void**)&p->h_steps, (size_t)c, hipHostMallocDefault));
-    if ((rc = grow(p, &p->d_steps, (size_t)c))) return rc;
-    p->cap_steps = c;
-  }
-  memcpy(p->h_steps, recs.data(), (size_t)bytes);
-  HIPCHK(p, hipMemcpyAsync(p->d_steps, p->h_steps, (size_t)bytes, hipMemcpyHostToDevice, st));
-  HIPCHK(p, hipEventRecord(p->ev_steps, st));
-  const StepLaunch* d_rec = reinterpret_cast<const StepLaunch*>(p->d_steps);
-  for (const Item& it : items) {
-    hipEvent_t e0 = it.s0, e1 = it.s1;
-    if (it.prof && plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1)) return fail_arg(p, "profiling events");
-    hipExtLaunchKernelGGL(kern, dim3((unsigned)it.nwg), dim3(EVAL_EVS), lds, st, e0, e1, 0, d_rec + it.rec);
-    HIPCHK(p, hipGetLastError());
-    if (it.prof) plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
-    if (it.s1) plan_prof_end(p, LOMPC_PLAN_K_EVAL, span0, span1, ng - 1);
-    for (int j = it.x0; j < it.x0 + it.nx; ++j)
-      if ((rc = lq_exchange(p, xsend(j), sw_of(j), st_of(j), st))) return rc;
+    if (s1) plan_prof_end(p, LOMPC_PLAN_K_EVAL, span0, span1, K - 1);
+    if (xr && nf && (rc = lq_exchange(p, xsend(k - 2), sw_of(k - 2), st_of(k - 2), st))) return rc;
   }
   return LOMPC_OK;
 }
@@ -2338,7 +2261,7 @@ int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
                          int64_t lmbd_r_stride, int n_runs, int profile_every, double* w, double* cost, double* w0,
                          int8_t* status, double* set_sum_w, double* set_stats, int64_t set_sum_w_stride,
                          int64_t set_stats_stride, int64_t ev_stride, int steps_flags, void* stream) {
-  constexpr int known = LOMPC_STEPS_PER_KERNEL | LOMPC_STEPS_SPAN_EVENTS | LOMPC_STEPS_TWO_RUNS_PER_LAUNCH;
+  constexpr int known = LOMPC_STEPS_PER_KERNEL | LOMPC_STEPS_SPAN_EVENTS;
   if (!p || n_runs < 0 || profile_every < 0 || set_sum_w_stride < 0 || set_stats_stride < 0 || ev_stride < 0 ||
       (steps_flags & ~known))
     return LOMPC_ERR_INVALID_ARG;
@@ -2350,17 +2273,11 @@ int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   // sums the rows it does not store)
   const bool per_ev = w || cost || w0 || status;
   const bool agg = p->sorted && !per_ev;
-  if (n_runs >= 1 && !p->skip && !agg && !p->close && p->nblk > 0 && p->G % LQ_STEP_CELLS == 0) {
-    // two runs per group when their per-EV outputs do not overlap (per-run strides, or none) and both
-    // paths fit one wave per SIMD beside the evaluation
-    const int64_t cells = p->S * p->G;
-    const bool two = (steps_flags & LOMPC_STEPS_TWO_RUNS_PER_LAUNCH) && n_runs >= 2 && (!per_ev || ev_stride > 0) &&
-                     2 * cells <= 4ll * std::max(p->n_cu, 1) * 3 / 4;
-    return lq_run_steps_stepped(p, two ? 2 : 1, lmbd, lmbd_stride, lmbd_r, lmbd_r_stride, n_runs, profile_every,
+  if (n_runs >= 1 && !p->skip && !agg && !p->close && p->nblk > 0 && p->G % LQ_STEP_CELLS == 0)
+    return lq_run_steps_stepped(p, lmbd, lmbd_stride, lmbd_r, lmbd_r_stride, n_runs, profile_every,
                                 (steps_flags & LOMPC_STEPS_SPAN_EVENTS) != 0, w, cost, w0, status, ev_stride,
                                 set_sum_w, set_sum_w_stride, set_stats, set_stats_stride,
                                 (steps_flags & LOMPC_STEPS_PER_KERNEL) != 0, st);
-  }
   const int mask = p->prof;
   int rc = LOMPC_OK;
   // run k's closing (k_finalize) rides in run k + 1's path launch (k_path_fin); the last run's
@@ -2410,7 +2327,7 @@ int lompc_plan_status(lompc_plan* p, void* stream, int64_t* n_repaired, int64_t*
 int lompc_plan_get_info(const lompc_plan* p, int64_t* B, int64_t* S, int* cells, int* eval_workgroups,
                         int* steps_group) {
   if (!p) return LOMPC_ERR_INVALID_ARG;
-  if (steps_group) *steps_group = p->stp.ok ? p->stp.R : 0;
+  if (steps_group) *steps_group = p->stp.ok ? 1 : 0;
   if (B) *B = p->B;
   if (S) *S = p->S;
   if (cells) *cells = p->G;

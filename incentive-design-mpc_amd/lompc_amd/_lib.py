@@ -41,7 +41,6 @@ LOMPC_PLAN_CLOSE_IN_FINALIZE = 32
 LOMPC_PLAN_CELLS_SHIFT = 20
 LOMPC_STEPS_PER_KERNEL = 1
 LOMPC_STEPS_SPAN_EVENTS = 2
-LOMPC_STEPS_TWO_RUNS_PER_LAUNCH = 4
 
 
 def LOMPC_PLAN_CELLS(g: int) -> int:

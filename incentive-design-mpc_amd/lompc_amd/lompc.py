@@ -464,7 +464,7 @@ class BatchPlan:
 
     def info(self) -> dict:
         """Batch size, parameter sets, gamma cells per set, k_eval workgroups of the plan and the runs per
-        launch group of its last stepped run_steps call (0: none)."""
+        stepped run_steps launch (1 once the stepped form has run, else 0)."""
         if self.direct:
             return {"B": self.B, "sets": self.S, "cells": 0, "workgroups": 0, "steps_group": 0}
         B, S, cells, wg, grp = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
@@ -531,7 +531,7 @@ class BatchPlan:
 
     def run_steps(self, lmbd, lmbd_r, n_runs: int, lmbd_stride: int, lmbd_r_stride: int = 0,
                   profile_every: int = 0, per_run_sets: bool = False, per_run: bool = False, out=None,
-                  per_kernel: bool = False, span_events: bool = False, two_runs_per_launch: bool = False) -> dict:
+                  per_kernel: bool = False, span_events: bool = False) -> dict:
         """n_runs consecutive independent runs in ONE C-ABI call (lompc_plan_run_steps): run k at the
         prices lmbd + k lmbd_stride, lmbd_r + k lmbd_r_stride (device pointers or tensors, strides in
         doubles); profile_every > 0: only every E-th stepped launch carries the enabled HIP events.
@@ -542,8 +542,7 @@ class BatchPlan:
         cost / w0 / status (n_runs, B), sets as above).  out: a dict of preallocated per-run tensors for any of those keys (the others as the
         flags say).  per_kernel: LOMPC_STEPS_PER_KERNEL (the same runs, one part per launch, bit for
         bit the same outputs); span_events: one event pair over the stepped launches
-        (LOMPC_STEPS_SPAN_EVENTS); two_runs_per_launch: groups of two runs (LOMPC_STEPS_TWO_RUNS_PER_LAUNCH;
-        per_run or no per-EV outputs)."""
+        (LOMPC_STEPS_SPAN_EVENTS)."""
         if self.direct:
             raise ValueError("run_steps: PATH-mode plans only")
         self._usable()
@@ -578,8 +577,7 @@ class BatchPlan:
         st_stride = self.S * _lib.LOMPC_SET_STATS if res["set_stats"] is not None and res["set_stats"].dim() == 3 else 0
         if (res["set_sum_w"] is None) != (res["set_stats"] is None) or (sw_stride == 0) != (st_stride == 0):
             raise ValueError("run_steps: set_sum_w and set_stats are both per run or both shared")
-        flags = ((_lib.LOMPC_STEPS_PER_KERNEL if per_kernel else 0) | (_lib.LOMPC_STEPS_SPAN_EVENTS if span_events else 0)
-                 | (_lib.LOMPC_STEPS_TWO_RUNS_PER_LAUNCH if two_runs_per_launch else 0))
+        flags = (_lib.LOMPC_STEPS_PER_KERNEL if per_kernel else 0) | (_lib.LOMPC_STEPS_SPAN_EVENTS if span_events else 0)
         ptrs = [_ptr(res[k]) for k in keys]
         rc = self._lib.lompc_plan_run_steps(self._plan, pl, int(lmbd_stride), pr, int(lmbd_r_stride), K,
                                             int(profile_every), *ptrs, sw_stride, st_stride, ev_stride, flags,

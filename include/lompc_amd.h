@@ -228,20 +228,15 @@ int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, d
  * E-th launch carries the enabled profiling events.
  * One C-ABI call for a sequence of independent batches (a benchmark's timed steps).  Plans whose
  * cells fill whole path workgroups take the STEPPED form: one launch carries the
- * paths of a group of runs, the evaluations of the previous group and the closings of the group
- * before — groups of one run, or of two on request (LOMPC_STEPS_TWO_RUNS_PER_LAUNCH, when their per-EV
- * outputs do not overlap: ev_stride > 0 or no per-EV output; and both paths fit).  steps_flags:
+ * path of run k + 1, the evaluation of run k and the closing of run k - 1.  steps_flags:
  *   LOMPC_STEPS_PER_KERNEL  the same runs issued one part per launch (paths / evaluations /
  *                           closings), with the same evaluation block map, so bit for bit the same
  *                           outputs (verification / A-B)
  *   LOMPC_STEPS_SPAN_EVENTS the enabled K_EVAL timing as ONE event pair from the start of the first
  *                           full stepped launch to the end of the last, read back as that many
- *                           launches (no per-launch event boundaries inside the timed steps)
- *   LOMPC_STEPS_TWO_RUNS_PER_LAUNCH  groups of two runs (measured no faster than one at config 3:
- *                           the two evaluations take twice one's time) */
+ *                           launches (no per-launch event boundaries inside the timed steps) */
 #define LOMPC_STEPS_PER_KERNEL 1
 #define LOMPC_STEPS_SPAN_EVENTS 2
-#define LOMPC_STEPS_TWO_RUNS_PER_LAUNCH 4
 int lompc_plan_run_steps(lompc_plan* plan, const double* lmbd, int64_t lmbd_stride,
                          const double* lmbd_r, int64_t lmbd_r_stride, int n_runs,
                          int profile_every, double* w, double* cost, double* w0, int8_t* status,
@@ -256,8 +251,8 @@ int lompc_plan_status(lompc_plan* plan, void* stream, int64_t* n_repaired,
                       int64_t* n_failed, int64_t* n_invalid);
 
 /* Batch size, total parameter sets, gamma cells per set and k_eval workgroups of the plan, and the
- * runs per launch group of its last stepped lompc_plan_run_steps call (0: none yet); any pointer may
- * be null. */
+ * runs per stepped launch of its lompc_plan_run_steps calls (1 once the stepped form has run, else 0);
+ * any pointer may be null. */
 int lompc_plan_get_info(const lompc_plan* plan, int64_t* B, int64_t* S, int* cells, int* eval_workgroups,
                         int* steps_group);
 

@@ -58,8 +58,7 @@ def test_header_constants_match_python():
                  "LOMPC_PLAN_CLOSE_IN_EVAL", "LOMPC_PLAN_SORTED_GAMMA", "LOMPC_COMM_ID_BYTES", "LOMPC_LOOP_PROF_ITERS", "LOMPC_LOOP_PROF_WALL",
                  "LOMPC_LOOP_PROF_ISSUE", "LOMPC_LOOP_PROF_WAIT", "LOMPC_LOOP_PROF_GPU", "LOMPC_LOOP_PROF_STEP",
                  "LOMPC_LOOP_PROF_HOST", "LOMPC_LOOP_PROF", "LOMPC_LOOP_AHEAD", "LOMPC_PLAN_CLOSE_IN_FINALIZE",
-                 "LOMPC_PLAN_CELLS_SHIFT", "LOMPC_STEPS_PER_KERNEL", "LOMPC_STEPS_SPAN_EVENTS",
-                 "LOMPC_STEPS_TWO_RUNS_PER_LAUNCH"):
+                 "LOMPC_PLAN_CELLS_SHIFT", "LOMPC_STEPS_PER_KERNEL", "LOMPC_STEPS_SPAN_EVENTS"):
         m = re.search(rf"#define {name}\s+(\d+)", src)
         attr = "ABI_VERSION" if name == "LOMPC_ABI_VERSION" else name
         assert m and int(m.group(1)) == getattr(_lib, attr), name

@@ -90,13 +90,12 @@ def test_plan_with_comm_equals_plain(nccl1, want_w):
     # the stepped run_steps with the communicator (one all-gather + combine per run, after the launch
     # that closed it), every run's records kept: the plain plan's, both issue forms
     for per_kernel in (False, True):
-        for per_run in (False, True):  # (per_run: two runs per launch, each with its own collective)
+        for per_run in (False, True):  # (per_run: every output per run)
             o_s = shard.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, per_run=per_run,
-                                  per_kernel=per_kernel, two_runs_per_launch=per_run)
-            o_p = plain.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, per_run=per_run,
-                                  two_runs_per_launch=per_run)
+                                  per_kernel=per_kernel)
+            o_p = plain.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, per_run=per_run)
             assert shard.check()[1:] == (0, 0) and plain.check()[1:] == (0, 0)
-            assert shard.info()["steps_group"] == plain.info()["steps_group"] == (2 if per_run else 1)
+            assert shard.info()["steps_group"] == plain.info()["steps_group"] == 1
             for key, v in o_p.items():
                 if v is not None:
                     assert torch.equal(v, o_s[key]), (per_kernel, per_run, key)

@@ -454,25 +454,23 @@ def test_run_steps_matches_single_runs(gpu, want_w, K):
         for key in ("w", "cost", "status", "set_sum_w", "set_stats"):
             if out.get(key) is not None:
                 assert torch.equal(out[key], out_s[key]), key
-        # every output per run, groups of one or two runs per launch (K = 3, 7: a last group of one): every
-        # run's outputs those of its single run; the span events count the steady-state launches
-        for two, split in ((True, False), (True, True), (False, False)):
+        # every output per run (per-EV outputs at a per-run stride, every closing writes its run's
+        # re-solved rows): every run's outputs those of its single run; the span events count the
+        # steady-state launches
+        for split in (False, True):
             pr = BatchPlan(lompcs, g, off, **kw)
             pr.profile(enable=("k_eval",))
             pr.profile(read=True, reset=True)
-            o = pr.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run=True, per_kernel=split,
-                             two_runs_per_launch=two, span_events=True)
+            o = pr.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run=True, per_kernel=split, span_events=True)
             assert pr.check()[1:] == (0, 0)
-            grp = pr.info()["steps_group"]
             if cells is None:
-                assert grp == (2 if two and K >= 2 else 1)
-                ng = (K + grp - 1) // grp
+                assert pr.info()["steps_group"] == 1
                 ms, n = pr.profile(read=True)
-                assert n == (ng - 1 if ng >= 2 else 0) and (ms > 0.0) == (n > 0)
+                assert n == K - 1 and (ms > 0.0) == (n > 0)
             for k in range(K):
                 for key in ("w", "cost", "status", "set_sum_w", "set_stats"):
                     if o.get(key) is not None:
-                        assert torch.equal(o[key][k], runs[k][key]), (cells, two, split, k, key)
+                        assert torch.equal(o[key][k], runs[k][key]), (cells, split, k, key)
     if K != 7 or not want_w:
         return
     # every run vs the oracle: per-set sums of the per-EV optima

@@ -1288,13 +1288,15 @@ __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_step(PathArgs pa, 
   extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
   int b = (int)blockIdx.x;
   if (b < np_wg) {
-    const int c0 = b * LQ_STEP_CELLS;  // (G % LQ_STEP_CELLS == 0: every cell of the workgroup in one set)
-    lq_tab_init(set_consts(pa.qd, pa.ce, c0 / pa.G));
-    const int wv = (int)(threadIdx.x >> 6), cell = c0 + wv;
+    // (G % LQ_STEP_CELLS == 0: every cell of the workgroup in one set).  The waves without a cell exit
+    // here; the path waves initialise the set's box table inside path_cell, after their price loads
+    // are issued (the barrier overlaps them, as in k_path)
+    const int wv = (int)(threadIdx.x >> 6), cell = b * LQ_STEP_CELLS + wv;
+    if (wv >= LQ_STEP_CELLS || cell >= pa.S * pa.G) return;
     // the path chain is the launch's critical path: its waves issue first on a SIMD they share
     // with evaluation waves (which mostly wait on memory)
     if (LQ_STEP_PRIO) __builtin_amdgcn_s_setprio(3);
-    if (wv < LQ_STEP_CELLS && cell < pa.S * pa.G) path_cell<NT, false>(pa, cell);
+    path_cell<NT, true>(pa, cell);
     return;
   }
   b -= np_wg;

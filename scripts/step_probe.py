@@ -1,0 +1,80 @@
+"""Diagnostics: the stepped run_steps at config 3 on one or several library builds, one process.
+
+    python scripts/step_probe.py [lib.so ...] [--cells G] [--steps K] [--reps R] [--outputs full|set]
+
+For every in-tree library (lompc_amd/<lib>.so, default the product library; variants are -D builds
+made by scripts/build_variant.py) and every cell count: K steps per lompc_plan_run_steps call with
+per-step set outputs, R calls; prints the per-step wall time (median over the calls), the k_step
+average from one HIP-event pair spanning the steady-state launches, and the standalone kernels
+(k_path / k_eval / k_finalize as their own launches, 20 single runs).  Not a measurement of record:
+bench.py is (it refuses variant libraries).
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "incentive-design-mpc_amd"))
+ap = argparse.ArgumentParser()
+ap.add_argument("libs", nargs="*", default=["liblompc_amd.so"])
+ap.add_argument("--cells", type=int, nargs="*", default=[0])
+ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--outputs", default="full")
+ap.add_argument("--horizon", type=int, default=24)
+args = ap.parse_args()
+
+import torch  # noqa: E402
+
+from lompc_amd import _lib  # noqa: E402
+
+N, P, B = args.horizon, 12, 262144
+for libname in args.libs:
+    lib = _lib.load(os.path.join(ROOT, "incentive-design-mpc_amd", "lompc_amd", libname))
+    _lib._lib = lib
+    from lompc_amd import BatchPlan, LoMPC, LoMPCConstants  # noqa: E402
+
+    rng = np.random.default_rng(0)
+    cs = [LoMPCConstants(0.05, 10.0, 0.9, 0.25, "small"), LoMPCConstants(0.025, 50.0, 0.9, 0.15, "large")]
+    lompcs = [LoMPC(N, c, device=0) for c in cs]
+    M = B // 2
+    off1 = np.array([(M * p) // P for p in range(P + 1)], dtype=np.int64)
+    off = np.concatenate([off1, M + off1[1:]])
+    g = torch.as_tensor(np.concatenate([c.y_max - (0.3 + 0.2 * rng.random(M)) for c in cs]), device="cuda")
+    K = args.steps
+    lm = torch.as_tensor(np.stack([np.concatenate([c.theta * rng.random((P, 3 * N)) for c in cs]) for _ in range(K)]),
+                         device="cuda")
+    lr = torch.zeros((K, 2 * P), dtype=torch.float64, device="cuda")
+    wr = torch.as_tensor(np.concatenate([c.w_max * rng.random((P, N)) for c in cs]), device="cuda")
+    for cells in args.cells:
+        plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], w_ref=wr, want_w=args.outputs == "full",
+                         want_cost=args.outputs != "set", cells=cells or None)
+        plan.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True)
+        plan.check()
+        walls, ks = [], []
+        for _ in range(args.reps):
+            plan.profile(enable=("k_eval",))
+            plan.profile(read=True, reset=True)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            plan.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, span_events=True)
+            torch.cuda.synchronize()
+            walls.append((time.perf_counter() - t0) / K * 1e6)
+            ms, n = plan.profile(read=True)
+            ks.append(ms / max(n, 1) * 1e3)
+            plan.check()
+        plan.profile(enable=("k_path", "k_eval", "k_finalize"))
+        for k in ("k_path", "k_eval", "k_finalize"):
+            plan.profile(read=True, reset=True, kernel=k)
+        for j in range(20):
+            plan.run(lm[j % K], lr[j % K])
+        plan.check()
+        alone = {k: plan.profile(read=True, kernel=k) for k in ("k_path", "k_eval", "k_finalize")}
+        plan.profile(enable=False)
+        print(f"{libname} cells {plan.cells} {args.outputs}: per step {np.median(walls):6.2f} us (min {min(walls):6.2f})"
+              f"  k_step {np.median(ks):6.2f} us  alone: " +
+              "  ".join(f"{k} {ms / max(n, 1) * 1e3:6.2f}" for k, (ms, n) in alone.items()), flush=True)
+        del plan

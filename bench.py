@@ -659,6 +659,17 @@ def station_leg(args, world, dev, sharded=False):
         it = np.concatenate([stats["niter_s"][:, warm:warm + steps].ravel(), stats["niter_l"][:, warm:warm + steps].ravel()])
         ncalls = calls() - c0
         ms = np.asarray(per_step) * 1e3
+        # the step-to-step spread: a step's time against its price iterations (both types, all
+        # partitions) — a least-squares line ms = fixed + per_iteration * iterations
+        its = np.zeros(steps)
+        for key in ("niter_s", "niter_l"):
+            a = np.asarray(stats[key][:, warm:warm + steps], dtype=np.float64)
+            its += np.where(a >= 0, a, 0).sum(axis=0)
+        spread = {"ms": [round(float(v), 3) for v in ms], "price_iterations": [int(v) for v in its]}
+        if steps >= 3 and np.ptp(its) > 0:
+            b, a0 = np.polyfit(its, ms, 1)
+            r = np.corrcoef(its, ms)[0, 1]
+            spread.update({"fit_ms_fixed": float(a0), "fit_us_per_iteration": float(b * 1e3), "fit_r2": float(r * r)})
         info = st.bimpc.last_info or {}
         loop = price_loop_breakdown(st, args.station_prof_steps, consts, torch)
         out.update({"value": steps / dt, "ms_per_step": dt / steps * 1e3,
@@ -666,6 +677,7 @@ def station_leg(args, world, dev, sharded=False):
                     "ms_per_step_max": float(ms.max()),
                     "price_iterations_per_step": float(np.sum(it[it >= 0])) / steps,
                     "engine_calls_per_step": ncalls / steps,
+                    "per_step": spread,
                     "lompc_qps_per_sec_est": (ncalls + 2 * P * steps) * M_2 / P / dt,
                     "checks": {"storage_x_final": float(st.x), "x_max": float(consts.bimpc_consts.x_max),
                                "bimpc_iterations_last": info.get("iterations"),

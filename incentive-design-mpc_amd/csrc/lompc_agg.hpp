@@ -250,211 +250,271 @@ __device__ __forceinline__ int agg_search(const double* __restrict__ g, int a, i
 }
 
 constexpr int LQ_AGG_W = 16;  // k_agg: waves per workgroup (cells per pass)
+constexpr int LQ_AGG_REC = LOMPC_MAX_N + 8;  // k_loop_iter: doubles per cell record (sums of w | 5 scalars)
 
+// a set's run-wide values (every wave of the set's cells)
+struct AggSet {
+  const QPConst* q;
+  int N, G, KF, n_s;
+  int4 si;
+  bool order_ok;
+  const double* g;
+  const unsigned long long *P1, *PH, *PL;
+  const int* ps;
+  double wlo, h1, fs;
+  const double* L;
+  double lr, l1, l2, l3, tt, wm;
+};
+
+template <int NT>
+__device__ __forceinline__ AggSet agg_set_init(const AggArgs& r, const int s) {
+  AggSet z;
+  z.N = NT ? NT : r.N;
+  z.G = r.G;
+  z.KF = r.F / r.G;
+  z.q = &set_consts(r.qd, r.ce, s);
+  const int64_t so = r.set_off[s];
+  z.n_s = (int)(r.set_off[s + 1] - so);
+  z.si = r.sinfo[s];
+  z.order_ok = z.si.y != 0;
+  z.g = r.gamma + so;
+  z.P1 = r.P + so + s;
+  z.PH = z.P1 + r.PB;
+  z.PL = z.P1 + 2 * r.PB;
+  z.ps = r.pos + (size_t)s * (r.F + 1);
+  z.wlo = r.window[2 * s];
+  const double W = r.window[2 * s + 1] - z.wlo;
+  z.h1 = W * 0x1p-40;
+  z.fs = (double)r.F / W;
+  z.L = r.lmbd + (size_t)s * 3 * z.N;
+  z.lr = r.lmbd_r[s];
+  z.l1 = z.L[0];
+  z.l2 = z.L[z.N];
+  z.l3 = z.L[2 * z.N];
+  z.tt = z.q->theta * z.q->theta;
+  z.wm = z.q->w_max;
+  return z;
+}
+
+// a wave's partial sums over its cells (per lane: stage sums of w; lane 0 / wave-reduced: scalars)
+struct AggPart {
+  double accw = 0.0, acost = 0.0, ap0 = 0.0, aerr = 0.0;
+  int nrep = 0, nfail = 0;
+};
+
+// Cell c of set s by one wave, into the wave's partials.  COH: the cell's tables were written in
+// this launch (by this wave: k_loop_iter) — device-coherent loads (the scalar cache and the L1
+// hold no copy of them).
+template <int NT, bool COH>
+__device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, const int s, const int c, const int lane,
+                                         AggPart& a) {
+  const int N = NT ? NT : z.N, G = z.G, KF = z.KF;
+  const QPConst& q = *z.q;
+  const double* __restrict__ g = z.g;
+  const int* ps = z.ps;
+  const double wlo = z.wlo, h1 = z.h1, fs = z.fs;
+  const double l1 = z.l1, l2 = z.l2, l3 = z.l3, lr = z.lr, tt = z.tt, wm = z.wm;
+  const int cell = s * G + c;
+  const size_t sb = (size_t)cell * LQ_PPL;
+  // one memory round: the cell's sorted positions, its piece count and coverage start, and
+  // every piece slot (whatever the count: no round waits on it) — piece ends and coefficients
+  // on lane k, rows on lane t
+  const int cs = ps[c * KF], ce = ps[(c + 1) * KF];
+  const int cnt_l = ld_t<COH>(r.t_cnt + cell);
+  const double lo = ld_t<COH>(r.t_lo + cell);
+  const double ge_l = lane < LQ_PPL ? ld_t<COH>(r.t_ge + sb + lane) : INFINITY;
+  double cf[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) cf[k] = lane < LQ_PPL ? ld_t<COH>(r.t_cf + (sb + lane) * 8 + k) : 0.0;
+  double2 ab[LQ_PPL];
+#pragma unroll
+  for (int k = 0; k < LQ_PPL; ++k) ab[k] = lane < N ? ld_t<COH>(r.t_ab + (sb + k) * N + lane) : make_double2(0.0, 0.0);
+  if (ce <= cs) return;
+  const int cnt = min(max(cnt_l, 0), LQ_PPL);
+  const double ge = lane < cnt ? ge_l : INFINITY;
+#pragma unroll
+  for (int k = 0; k < LQ_PPL; ++k) ab[k] = k < cnt ? ab[k] : make_double2(0.0, 0.0);
+  // boundary j (lane j <= cnt): j = 0 the coverage start (first gamma >= lo), j >= 1 the end of
+  // piece j - 1 (first gamma > ge_{j-1}); its fine bucket clamped to the cell's
+  const double gprev = __shfl(ge, max(lane - 1, 0), 64);  // (every lane: no read of an inactive lane)
+  const double vb = lane == 0 ? lo : gprev;
+  const int fb = min(max(agg_fine(vb, wlo, fs, r.F), c * KF), (c + 1) * KF - 1);
+  int qa = lane <= cnt ? ps[fb] : 0, qb = lane <= cnt ? ps[fb + 1] : 0;
+  qa = min(max(qa, cs), ce);
+  qb = min(max(qb, cs), ce);
+  int qpos = cs;
+  {
+    // every boundary's candidates in flight together (one memory round, not one per boundary);
+    // a bucket wider than 64 EVs falls back to agg_search's binary search
+    double xg[LQ_PPL + 1];
+#pragma unroll
+    for (int j = 0; j <= LQ_PPL; ++j) {
+      const int a0 = lqw::readlane_i(qa, j), b0 = lqw::readlane_i(qb, j);  // (j wave-uniform)
+      xg[j] = (j <= cnt && b0 - a0 <= 64 && a0 + lane < b0) ? g[a0 + lane] : INFINITY;
+    }
+#pragma unroll
+    for (int j = 0; j <= LQ_PPL; ++j) {
+      if (j > cnt) continue;  // (wave-uniform)
+      const int a0 = lqw::readlane_i(qa, j), b0 = lqw::readlane_i(qb, j);
+      const double v = lqw::readlane_d(vb, j);
+      int pj;
+      if (b0 - a0 <= 64) {
+        const bool before = j == 0 ? (xg[j] < v) : (xg[j] <= v);
+        pj = a0 + (int)__popcll(__ballot(before && a0 + lane < b0));
+      } else {
+        pj = agg_search(g, a0, b0, v, j == 0, lane);
+      }
+      if (lane == j) qpos = pj;
+    }
+  }
+  if (cnt == 0) qpos = ce;
+  // per piece k = lane: [qpos_k, qpos_{k+1})
+  const int qn = __shfl(qpos, min(lane + 1, 63), 64);
+  const bool pk = lane < cnt;
+  const int na = pk ? qpos : 0, nb = pk ? max(qn, qpos) : 0;
+  const double n = (double)(nb - na);
+  unsigned long long d1 = 0, dh = 0, dl = 0;
+  double gf = 0.0, gl = 0.0;
+  if (pk && nb > na) {
+    d1 = z.P1[nb] - z.P1[na];
+    dh = z.PH[nb] - z.PH[na];
+    dl = z.PL[nb] - z.PL[na];
+    gf = g[na];
+    gl = g[nb - 1];
+  }
+  const double X1 = (double)d1;
+  const double X2 = fma((double)dh, 0x1p40, (double)dl);
+  const double Gm = fma(h1, X1, n * wlo);                                 // sum gamma
+  const double G2 = fma(h1 * h1, X2, fma(2.0 * wlo * h1, X1, n * wlo * wlo));  // sum gamma^2
+  if (pk && nb > na) {
+    a.acost += fma(cf[2], G2, fma(cf[1], Gm, cf[0] * n));
+    const double e_f = fma(fma(cf[5], gf, cf[4]), gf, cf[3]), e_l = fma(fma(cf[5], gl, cf[4]), gl, cf[3]);
+    a.aerr = fmax(a.aerr, fmax(fmax(e_f, e_l), 0.0));
+    const double a0 = cf[6], b0 = cf[7];
+    const double sw0 = fma(b0, Gm, a0 * n), sw02 = fma(b0 * b0, G2, fma(2.0 * a0 * b0, Gm, a0 * a0 * n));
+    a.ap0 += q.theta * fma(l1, sw0, l2 * fma(wm, n, -sw0)) + fma(q.q_scale, l3, tt * lr) * sw02;  // lompc.py:164-170
+  }
+  // per-stage sums of w: sum over pieces of n_k a_kt + Gamma_k b_kt (lane t)
+#pragma unroll
+  for (int k = 0; k < LQ_PPL; ++k) {
+    const double nk = lqw::readlane_d(n, k), gk = lqw::readlane_d(Gm, k);
+    a.accw = fma(gk, ab[k].y, fma(nk, ab[k].x, a.accw));  // (slots past cnt: n = 0, Gamma = 0)
+  }
+  // EVs of the cell outside its certified coverage: re-solved one by one (k_finalize's method)
+  const int u0 = cs, u1 = lqw::readlane_i(qpos, 0), v0 = lqw::readlane_i(qpos, cnt), v1 = ce;
+  if (u1 > u0 || v1 > v0) {
+    lqw::WaveSet ws;
+    double l2w;
+    bool bad;
+    load_set(q, z.L, lr, N, lane, ws, l2w, bad);
+    const double c0 = q.theta * q.w_max * lqw::wave_sum(l2w, N);
+    const double kappa = lr / q.delta;
+    const double l0[3] = {l1, l2, l3};
+    const double wr = (r.w_ref && lane < N) ? r.w_ref[(size_t)s * N + lane] : 0.0;
+    for (int part = 0; part < 2; ++part) {
+      const int e0 = part ? v0 : u0, e1 = part ? v1 : u1;
+      for (int j = e0; j < e1; ++j) {
+        const double gj = g[j];
+        int sl = lane < N ? (int)r.t_sl[(size_t)cell * 64 + lane] : 0;  // (COH: this lane's own store)
+        double wl = 0.0, rl = 0.0;
+        const bool okk = lqw::wave_solve(q, ws, gj, sl, wl, rl);
+        double co, eo, po;
+        wave_ev_outputs(q, ws, c0, kappa, l0, lr, wr, gj, wl, co, eo, po);
+        a.accw += lane < N ? wl : 0.0;
+        if (lane == 0) {
+          a.acost += co;
+          a.ap0 += po;
+          a.aerr = fmax(a.aerr, eo * eo);
+          a.nrep += okk ? 1 : 0;
+          a.nfail += okk ? 0 : 1;
+        }
+      }
+    }
+  }
+}
+
+// the wave's record: lane t < N its stage sum; x0..x4 cost, price0, max err^2, repaired, failed
+struct AggRec {
+  double x0, x1, x2, x3, x4;
+  __device__ __forceinline__ double pick(const int j) const {  // (selects: no private array)
+    return j == 0 ? x0 : (j == 1 ? x1 : (j == 2 ? x2 : (j == 3 ? x3 : x4)));
+  }
+};
+__device__ __forceinline__ AggRec agg_wave_record(const AggPart& a) {
+  double xs[4] = {a.acost, a.ap0, 0.0, 0.0};
+  lqw::wave_totals(xs, 64);
+  return AggRec{xs[0], xs[1], lqw::wave_max(a.aerr, 64), (double)lqw::readlane_i(a.nrep, 0),
+                (double)lqw::readlane_i(a.nfail, 0)};
+}
+
+// Set s's closing from nrec wave records, combined in record order, by ONE wave (lane = stage):
+// wrec(k) lane t's stage sum of record k, xrec(k, j) its scalar j.  WT: set outputs written
+// through to L2, complete when this returns.
+template <bool WT, class FW, class FX>
+__device__ __forceinline__ void agg_finish(const AggArgs& r, const AggSet& z, const int s, const int lane, const int nrec,
+                                           FW wrec, FX xrec) {
+  const int N = z.N, n_s = z.n_s;
+  double v = 0.0;
+  if (lane < N)
+    for (int k = 0; k < nrec; ++k) v += wrec(k);
+  if (lane < N && r.set_sum_w) {
+    if (WT) st_wt8(r.set_sum_w + (size_t)s * N + lane, v);
+    else r.set_sum_w[(size_t)s * N + lane] = v;
+  }
+  const double sw0 = lqw::readlane_d(v, 0);  // (sum of w0)
+  double c = 0.0, p0 = 0.0, e = 0.0, rr = 0.0, ff = 0.0;  // (every lane, the same order)
+  for (int k = 0; k < nrec; ++k) {
+    c += xrec(k, 0);
+    p0 += xrec(k, 1);
+    e = fmax(e, xrec(k, 2));
+    rr += xrec(k, 3);
+    ff += xrec(k, 4);
+  }
+  if (!z.order_ok) ff = (double)n_s;  // gamma not ascending: every EV reported failed, nothing summed
+  const double ni = (double)(n_s - (z.order_ok ? z.si.x : n_s));  // invalid gamma: after the valid ones
+  if (lane < LOMPC_SET_STATS) {
+    double x = 0.0;
+    switch (lane) {
+      case LOMPC_STAT_COUNT: x = (double)n_s; break;
+      case LOMPC_STAT_SUM_W0: x = sw0; break;
+      case LOMPC_STAT_SUM_PRICE0: x = p0; break;
+      case LOMPC_STAT_MAX_ERR: x = sqrt(e); break;
+      case LOMPC_STAT_SUM_COST: x = c; break;
+      case LOMPC_STAT_N_REPAIRED: x = rr; break;
+      case LOMPC_STAT_N_FAILED: x = ff; break;
+      default: x = ni; break;
+    }
+    if (r.set_stats) {
+      if (WT) st_wt8(r.set_stats + (size_t)s * LOMPC_SET_STATS + lane, x);
+      else r.set_stats[(size_t)s * LOMPC_SET_STATS + lane] = x;
+    }
+    r.stats[(size_t)s * LOMPC_SET_STATS + lane] = x;
+  }
+  if (lane == 0 && r.tally) {
+    if (rr > 0.0) __hip_atomic_fetch_add(r.tally + 0, (unsigned long long)rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ff > 0.0) __hip_atomic_fetch_add(r.tally + 1, (unsigned long long)ff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ni > 0.0) __hip_atomic_fetch_add(r.tally + 2, (unsigned long long)ni, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (WT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the set outputs have reached L2
+}
+
+// one workgroup per set, wave wv: cells wv, wv + nw, ...; the waves' records combined in wave order
 template <int NT>
 __global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
   __shared__ double s_w[LQ_AGG_W][LOMPC_MAX_N];
   __shared__ double s_x[LQ_AGG_W][8];  // cost, price0, max err^2, repaired, failed
-  __shared__ double s_fin[8];          // the set's scalars
   if (r.skip && *r.skip) return;
   const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
-  const int N = NT ? NT : r.N, G = r.G, KF = r.F / G;
-  const QPConst& q = set_consts(r.qd, r.ce, s);
-  lq_tab_init(q);  // (the individual re-solves' box table)
-  const int64_t so = r.set_off[s];
-  const int n_s = (int)(r.set_off[s + 1] - so);
-  const int4 si = r.sinfo[s];
-  const double* __restrict__ g = r.gamma + so;
-  const unsigned long long* P1 = r.P + so + s;
-  const unsigned long long* PH = P1 + r.PB;
-  const unsigned long long* PL = P1 + 2 * r.PB;
-  const int* ps = r.pos + (size_t)s * (r.F + 1);
-  const double wlo = r.window[2 * s], W = r.window[2 * s + 1] - wlo;
-  const double h1 = W * 0x1p-40, fs = (double)r.F / W;
-  const double* __restrict__ L = r.lmbd + (size_t)s * 3 * N;
-  const double lr = r.lmbd_r[s];
-  const double l1 = L[0], l2 = L[N], l3 = L[2 * N];
-  const double tt = q.theta * q.theta, wm = q.w_max;
-  double accw = 0.0, acost = 0.0, ap0 = 0.0, aerr = 0.0;
-  int nrep = 0, nfail = 0;
-  const bool order_ok = si.y != 0;
-  for (int c = wv; order_ok && c < G; c += nw) {
-    const int cell = s * G + c;
-    const size_t sb = (size_t)cell * LQ_PPL;
-    // one memory round: the cell's sorted positions, its piece count and coverage start, and
-    // every piece slot (whatever the count: no round waits on it) — piece ends and coefficients
-    // on lane k, rows on lane t
-    const int cs = ps[c * KF], ce = ps[(c + 1) * KF];
-    const int cnt_l = r.t_cnt[cell];
-    const double lo = r.t_lo[cell];
-    const double ge_l = lane < LQ_PPL ? r.t_ge[sb + lane] : INFINITY;
-    double cf[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) cf[k] = lane < LQ_PPL ? r.t_cf[(sb + lane) * 8 + k] : 0.0;
-    double2 ab[LQ_PPL];
-#pragma unroll
-    for (int k = 0; k < LQ_PPL; ++k) ab[k] = lane < N ? r.t_ab[(sb + k) * N + lane] : make_double2(0.0, 0.0);
-    if (ce <= cs) continue;
-    const int cnt = min(max(cnt_l, 0), LQ_PPL);
-    const double ge = lane < cnt ? ge_l : INFINITY;
-#pragma unroll
-    for (int k = 0; k < LQ_PPL; ++k) ab[k] = k < cnt ? ab[k] : make_double2(0.0, 0.0);
-    // boundary j (lane j <= cnt): j = 0 the coverage start (first gamma >= lo), j >= 1 the end of
-    // piece j - 1 (first gamma > ge_{j-1}); its fine bucket clamped to the cell's
-    const double gprev = __shfl(ge, max(lane - 1, 0), 64);  // (every lane: no read of an inactive lane)
-    const double vb = lane == 0 ? lo : gprev;
-    const int fb = min(max(agg_fine(vb, wlo, fs, r.F), c * KF), (c + 1) * KF - 1);
-    int qa = lane <= cnt ? ps[fb] : 0, qb = lane <= cnt ? ps[fb + 1] : 0;
-    qa = min(max(qa, cs), ce);
-    qb = min(max(qb, cs), ce);
-    int qpos = cs;
-    {
-      // every boundary's candidates in flight together (one memory round, not one per boundary);
-      // a bucket wider than 64 EVs falls back to agg_search's binary search
-      double xg[LQ_PPL + 1];
-#pragma unroll
-      for (int j = 0; j <= LQ_PPL; ++j) {
-        const int a = lqw::readlane_i(qa, j), b = lqw::readlane_i(qb, j);  // (j wave-uniform)
-        xg[j] = (j <= cnt && b - a <= 64 && a + lane < b) ? g[a + lane] : INFINITY;
-      }
-#pragma unroll
-      for (int j = 0; j <= LQ_PPL; ++j) {
-        if (j > cnt) continue;  // (wave-uniform)
-        const int a = lqw::readlane_i(qa, j), b = lqw::readlane_i(qb, j);
-        const double v = lqw::readlane_d(vb, j);
-        int pj;
-        if (b - a <= 64) {
-          const bool before = j == 0 ? (xg[j] < v) : (xg[j] <= v);
-          pj = a + (int)__popcll(__ballot(before && a + lane < b));
-        } else {
-          pj = agg_search(g, a, b, v, j == 0, lane);
-        }
-        if (lane == j) qpos = pj;
-      }
-    }
-    if (cnt == 0) qpos = ce;
-    // per piece k = lane: [qpos_k, qpos_{k+1})
-    const int qn = __shfl(qpos, min(lane + 1, 63), 64);
-    const bool pk = lane < cnt;
-    const int na = pk ? qpos : 0, nb = pk ? max(qn, qpos) : 0;
-    const double n = (double)(nb - na);
-    unsigned long long d1 = 0, dh = 0, dl = 0;
-    double gf = 0.0, gl = 0.0;
-    if (pk && nb > na) {
-      d1 = P1[nb] - P1[na];
-      dh = PH[nb] - PH[na];
-      dl = PL[nb] - PL[na];
-      gf = g[na];
-      gl = g[nb - 1];
-    }
-    const double X1 = (double)d1;
-    const double X2 = fma((double)dh, 0x1p40, (double)dl);
-    const double Gm = fma(h1, X1, n * wlo);                                 // sum gamma
-    const double G2 = fma(h1 * h1, X2, fma(2.0 * wlo * h1, X1, n * wlo * wlo));  // sum gamma^2
-    if (pk && nb > na) {
-      acost += fma(cf[2], G2, fma(cf[1], Gm, cf[0] * n));
-      const double e_f = fma(fma(cf[5], gf, cf[4]), gf, cf[3]), e_l = fma(fma(cf[5], gl, cf[4]), gl, cf[3]);
-      aerr = fmax(aerr, fmax(fmax(e_f, e_l), 0.0));
-      const double a0 = cf[6], b0 = cf[7];
-      const double sw0 = fma(b0, Gm, a0 * n), sw02 = fma(b0 * b0, G2, fma(2.0 * a0 * b0, Gm, a0 * a0 * n));
-      ap0 += q.theta * fma(l1, sw0, l2 * fma(wm, n, -sw0)) + fma(q.q_scale, l3, tt * lr) * sw02;  // lompc.py:164-170
-    }
-    // per-stage sums of w: sum over pieces of n_k a_kt + Gamma_k b_kt (lane t)
-#pragma unroll
-    for (int k = 0; k < LQ_PPL; ++k) {
-      const double nk = lqw::readlane_d(n, k), gk = lqw::readlane_d(Gm, k);
-      accw = fma(gk, ab[k].y, fma(nk, ab[k].x, accw));  // (slots past cnt: n = 0, Gamma = 0)
-    }
-    // EVs of the cell outside its certified coverage: re-solved one by one (k_finalize's method)
-    const int u0 = cs, u1 = lqw::readlane_i(qpos, 0), v0 = lqw::readlane_i(qpos, cnt), v1 = ce;
-    if (u1 > u0 || v1 > v0) {
-      lqw::WaveSet ws;
-      double l2w;
-      bool bad;
-      load_set(q, L, lr, N, lane, ws, l2w, bad);
-      const double c0 = q.theta * q.w_max * lqw::wave_sum(l2w, N);
-      const double kappa = lr / q.delta;
-      const double l0[3] = {l1, l2, l3};
-      const double wr = (r.w_ref && lane < N) ? r.w_ref[(size_t)s * N + lane] : 0.0;
-      for (int part = 0; part < 2; ++part) {
-        const int e0 = part ? v0 : u0, e1 = part ? v1 : u1;
-        for (int j = e0; j < e1; ++j) {
-          const double gj = g[j];
-          int sl = lane < N ? (int)r.t_sl[(size_t)cell * 64 + lane] : 0;
-          double wl = 0.0, rl = 0.0;
-          const bool okk = lqw::wave_solve(q, ws, gj, sl, wl, rl);
-          double co, eo, po;
-          wave_ev_outputs(q, ws, c0, kappa, l0, lr, wr, gj, wl, co, eo, po);
-          accw += lane < N ? wl : 0.0;
-          if (lane == 0) {
-            acost += co;
-            ap0 += po;
-            aerr = fmax(aerr, eo * eo);
-            nrep += okk ? 1 : 0;
-            nfail += okk ? 0 : 1;
-          }
-        }
-      }
-    }
-  }
-  // the waves' partials, combined in wave order
-  double xs[4] = {acost, ap0, 0.0, 0.0};
-  lqw::wave_totals(xs, 64);
-  const double emx = lqw::wave_max(aerr, 64);
-  const int rp = lqw::readlane_i(nrep, 0), fl = lqw::readlane_i(nfail, 0);
-  if (lane < N) s_w[wv][lane] = accw;
-  if (lane == 0) {
-    s_x[wv][0] = xs[0];
-    s_x[wv][1] = xs[1];
-    s_x[wv][2] = emx;
-    s_x[wv][3] = (double)rp;
-    s_x[wv][4] = (double)fl;
-  }
+  const AggSet z = agg_set_init<NT>(r, s);
+  lq_tab_init(*z.q);  // (the individual re-solves' box table)
+  AggPart a;
+  for (int c = wv; z.order_ok && c < z.G; c += nw) agg_cell<NT, false>(r, z, s, c, lane, a);
+  const AggRec x = agg_wave_record(a);
+  if (lane < z.N) s_w[wv][lane] = a.accw;
+  if (lane < 5) s_x[wv][lane] = x.pick(lane);
   __syncthreads();
-  if (tid < N) {
-    double v = 0.0;
-    for (int k = 0; k < nw; ++k) v += s_w[k][tid];
-    if (r.set_sum_w) r.set_sum_w[(size_t)s * N + tid] = v;
-    if (tid == 0) s_fin[5] = v;  // (sum of w0)
-  }
-  if (tid == 0) {  // (after its own sum above)
-    double c = 0.0, p0 = 0.0, e = 0.0, rr = 0.0, ff = 0.0;
-    for (int k = 0; k < nw; ++k) {
-      c += s_x[k][0];
-      p0 += s_x[k][1];
-      e = fmax(e, s_x[k][2]);
-      rr += s_x[k][3];
-      ff += s_x[k][4];
-    }
-    if (!order_ok) ff = (double)n_s;  // gamma not ascending: every EV reported failed, nothing summed
-    s_fin[0] = c;
-    s_fin[1] = p0;
-    s_fin[2] = sqrt(e);
-    s_fin[3] = rr;
-    s_fin[4] = ff;
-  }
-  __syncthreads();
-  if (tid < LOMPC_SET_STATS) {
-    double v = 0.0;
-    switch (tid) {
-      case LOMPC_STAT_COUNT: v = (double)n_s; break;
-      case LOMPC_STAT_SUM_W0: v = s_fin[5]; break;
-      case LOMPC_STAT_SUM_PRICE0: v = s_fin[1]; break;
-      case LOMPC_STAT_MAX_ERR: v = s_fin[2]; break;
-      case LOMPC_STAT_SUM_COST: v = s_fin[0]; break;
-      case LOMPC_STAT_N_REPAIRED: v = s_fin[3]; break;
-      case LOMPC_STAT_N_FAILED: v = s_fin[4]; break;
-      default: v = (double)(n_s - (order_ok ? si.x : n_s)); break;  // invalid gamma: after the valid ones
-    }
-    if (r.set_stats) r.set_stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
-    r.stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
-  }
-  if (tid == 0 && r.tally) {
-    const double nr = s_fin[3], nf = s_fin[4], ni = (double)(n_s - (order_ok ? si.x : n_s));
-    if (nr > 0.0) __hip_atomic_fetch_add(r.tally + 0, (unsigned long long)nr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (nf > 0.0) __hip_atomic_fetch_add(r.tally + 1, (unsigned long long)nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (ni > 0.0) __hip_atomic_fetch_add(r.tally + 2, (unsigned long long)ni, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (wv == 0)
+    agg_finish<false>(r, z, s, lane, nw, [&](int k) { return s_w[k][lane]; }, [&](int k, int j) { return s_x[k][j]; });
 }
 
 typedef void (*AggKernel)(AggArgs);

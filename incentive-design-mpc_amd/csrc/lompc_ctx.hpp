@@ -165,6 +165,8 @@ struct lompc_plan {
   struct lq_host_loop* h_loop = nullptr;  // pinned: progress / done / results, written by k_loop_step
   double* h_dec = nullptr;        // pinned [2][max_iter]: dual cost decreases (actual, predicted)
   int cap_loop_iter = 0;
+  double* d_aggrec = nullptr;     // [S * G][LQ_AGG_REC] k_loop_iter's cell records
+  int64_t cap_aggrec = 0;
   // gamma-sorted sets (LOMPC_PLAN_SORTED_GAMMA, lompc_agg.hpp): runs without per-EV outputs
   // aggregate per piece from prefix sums built at prepare (k_agg) instead of k_eval
   bool sorted = false;
@@ -241,5 +243,11 @@ int lq_comm_allgather(lompc_comm* c, const double* send, double* recv, size_t co
 
 // price loops (lompc_plan.hip: host form; lompc_loop.hip: device-resident form and the C-ABI entry)
 const char* lq_failed_text(lompc_plan* p, hipStream_t st);
+// one device-loop iteration as ONE launch (k_loop_iter: path + aggregation + the loop step) when
+// the plan allows it (gamma-sorted sets, no communicator, at most LQ_AGG_W cells per set)
+struct StepArgs;
+bool lq_loop_fusable(const lompc_plan* p);
+int lq_launch_loop_iter(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,
+                        const StepArgs& sa, int m, hipStream_t st);
 int lq_price_loop_host(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd, double* w_k, double* dual_cost,
                        double* dec_actual, double* dec_pred, int* iterations, double* errs, hipStream_t st);

@@ -38,6 +38,7 @@
 #include <type_traits>
 
 #include "lompc_ctx.hpp"
+#include "lompc_loopstep.hpp"
 #include "lompc_wave.hpp"
 
 #ifdef LOMPC_STAMPS
@@ -1324,6 +1325,88 @@ StepKernel step_kernel(int N) {
 
 #include "lompc_agg.hpp"
 
+// ---------------------------------------------------------------- k_loop_iter
+// One iteration of the device-resident price loop over gamma-sorted sets (lompc_loop.hip) in ONE
+// launch, one wave per (set, cell) as k_path: the wave tracks its cell's path (path_cell), then
+// aggregates the same cell from the tables it has just written (agg_cell, coherent loads) into a
+// cell record (write-through); the set's last arriving cell closes the set from its G records in
+// cell order (agg_finish: k_agg's arithmetic, whose wave c holds cell c for G <= LQ_AGG_W — the
+// same bits), and the last set to close runs the loop step (lompc_loopstep.hpp) on the engine
+// call's set outputs.  The unfused form's three launches (k_path, k_agg, k_loop_step) and two
+// kernel boundaries become one launch and two arrival counters (ctl[1 + s] per set, ctl[3]).
+#ifdef LOMPC_STAMPS
+// diagnostic build: per k_loop_iter wave (blk < 64) the phases' s_memrealtime ticks summed over the
+// launches: [0] path, [1] aggregation, [2] record + arrival, [3] set closing, [4] loop step,
+// [5] launches, [6] closings, [7] steps (scripts/loop_stamps.py)
+__device__ unsigned long long g_lstamps[64 * 8];
+#define LQ_LSTAMP(k)                                                                                 \
+  do {                                                                                               \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                 \
+    const long long t__ = __builtin_amdgcn_s_memrealtime();                                          \
+    if (lane == 0 && blk < 64) {                                                                     \
+      __hip_atomic_fetch_add(g_lstamps + blk * 8 + (k), (unsigned long long)(t__ - tl__), __ATOMIC_RELAXED, \
+                             __HIP_MEMORY_SCOPE_AGENT);                                              \
+      __hip_atomic_fetch_add(g_lstamps + blk * 8 + 5 + ((k) >= 3 ? (k) - 2 : 0), (k) == 0 || (k) >= 3 ? 1ull : 0ull, \
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                            \
+    }                                                                                                \
+    tl__ = t__;                                                                                      \
+  } while (0)
+#else
+#define LQ_LSTAMP(k)
+#endif
+
+template <int NT>
+__global__ __launch_bounds__(64) void k_loop_iter(PathArgs pa, AggArgs ga, StepArgs sa, double* rec, int m) {
+  if (sa.ctl[0]) return;  // finished: a call enqueued ahead of the convergence (every workgroup)
+  const int blk = (int)blockIdx.x, lane = (int)threadIdx.x, G = pa.G;
+  const int s = blk / G, c = blk - s * G;
+#ifdef LOMPC_STAMPS
+  long long tl__ = __builtin_amdgcn_s_memrealtime();
+#endif
+  path_cell<NT, true>(pa, blk);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the cell's tables have reached L2
+  LQ_LSTAMP(0);
+  const AggSet z = agg_set_init<NT>(ga, s);
+  AggPart ap;
+  if (z.order_ok) agg_cell<NT, true>(ga, z, s, c, lane, ap);
+  LQ_LSTAMP(1);
+  const AggRec x = agg_wave_record(ap);
+  double* rc = rec + (size_t)blk * LQ_AGG_REC;
+  if (lane < z.N) st_wt8(rc + lane, ap.accw);
+  if (lane < 5) st_wt8(rc + LOMPC_MAX_N + lane, x.pick(lane));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0) {
+    old = __hip_atomic_fetch_add(sa.ctl + 1 + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == G - 1) __hip_atomic_store(sa.ctl + 1 + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  LQ_LSTAMP(2);
+  if (lqw::readlane_i(old, 0) != G - 1) return;
+  const double* rs = rec + (size_t)s * G * LQ_AGG_REC;
+  agg_finish<true>(ga, z, s, lane, G, [&](int k) { return ld_t<true>(rs + (size_t)k * LQ_AGG_REC + lane); },
+                   [&](int k, int j) { return ld_t<true>(rs + (size_t)k * LQ_AGG_REC + LOMPC_MAX_N + j); });
+  LQ_LSTAMP(3);
+  old = 0;
+  if (lane == 0) {
+    old = __hip_atomic_fetch_add(sa.ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == pa.S - 1) __hip_atomic_store(sa.ctl + 3, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (lqw::readlane_i(old, 0) != pa.S - 1) return;
+  loop_step<true>(sa, m, lane);
+  LQ_LSTAMP(4);
+}
+
+typedef void (*LoopIterKernel)(PathArgs, AggArgs, StepArgs, double*, int);
+LoopIterKernel loop_iter_kernel(int N) {
+  switch (N) {
+    case 12: return k_loop_iter<12>;
+    case 16: return k_loop_iter<16>;
+    case 24: return k_loop_iter<24>;
+    case 48: return k_loop_iter<48>;
+    default: return k_loop_iter<0>;
+  }
+}
+
 // ---------------------------------------------------------------- host helpers
 
 // capacities of the buffers a re-targeted plan (lompc_plan_update) may outgrow: 1/4 headroom, so a
@@ -1842,13 +1925,41 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   return lq_launch_eval(p, lmbd, lmbd_r, w, cost, w0, status, set_sum_w, set_stats, tb, st, prof_ctx);
 }
 
+bool lq_loop_fusable(const lompc_plan* p) {  // (S = 2: the loop's sets; ctl holds 2 set counters)
+  return p->sorted && !p->comm && p->nblk > 0 && p->S == 2 && p->G >= 1 && p->G <= LQ_AGG_W;
+}
+
+int lq_launch_loop_iter(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,
+                        const StepArgs& sa, int m, hipStream_t st) {
+  if (!lq_loop_fusable(p)) return fail_arg(p, "k_loop_iter: plan not fusable");
+  const int N = p->N;
+  const int64_t nrec = p->S * p->G * (int64_t)LQ_AGG_REC;
+  if (nrec > p->cap_aggrec) {
+    const int rc = grow(p, &p->d_aggrec, nrec);
+    if (rc) return rc;
+    p->cap_aggrec = nrec;
+  }
+  const PathTab tb = own_tab(p);
+  const PathArgs pa = path_args(p, lmbd, lmbd_r, tb);
+  AggArgs ga{(int)p->S, p->G, N, p->aggF, p->d_q, p->ce, p->d_set_off, p->d_window, p->gamma, lmbd, lmbd_r,
+             p->w_ref, tb.cnt, tb.lo, tb.sl, tb.ge, tb.cf, tb.ab, p->d_P, p->B + p->S, p->d_pos,
+             p->d_sinfo, set_sum_w, set_stats, p->d_stats, p->d_tally, p->skip};
+  hipEvent_t e0 = nullptr, e1 = nullptr;  // (timed as k_path)
+  if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
+  hipExtLaunchKernelGGL(loop_iter_kernel(N), dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa, ga, sa,
+                        p->d_aggrec, m);
+  HIPCHK(p, hipGetLastError());
+  plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
+  return LOMPC_OK;
+}
+
 void lq_plan_free(lompc_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
   (void)hipDeviceSynchronize();
   void* ptrs[] = {p->d_meta,  p->d_stats_own, p->d_window, p->d_partial, p->t_cnt,     p->t_lo,      p->t_ge,         p->t_cf,
                   p->t_ab,    p->t_sl,        p->d_ws,      p->d_errflag,
-                  p->d_fail_cnt, p->d_fail_idx, p->d_tally, p->d_wacc, p->d_arrive, p->d_xsend, p->d_xrecv, p->d_loop,
+                  p->d_fail_cnt, p->d_fail_idx, p->d_tally, p->d_wacc, p->d_arrive, p->d_xsend, p->d_xrecv, p->d_loop, p->d_aggrec,
                   p->d_bsum, p->d_P, p->d_pos, p->d_sinfo};
   for (void* x : ptrs)
     if (x) (void)hipFree(x);
@@ -1882,6 +1993,16 @@ int lompc_debug_wstart(long long* host, int n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wstart), sizeof(long long) * n, 0, hipMemcpyDeviceToHost) == hipSuccess
              ? LOMPC_OK
              : LOMPC_ERR_HIP;
+}
+int lompc_debug_loopstamps(unsigned long long* host, int reset) {  // [64][8] (g_lstamps)
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lstamps), sizeof(g_lstamps), 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return LOMPC_ERR_HIP;
+  if (reset) {
+    static const unsigned long long z[64 * 8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lstamps), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
+      return LOMPC_ERR_HIP;
+  }
+  return LOMPC_OK;
 }
 int lompc_debug_stamps(long long* host, int n) {
   if (n > 65536 * 8) n = 65536 * 8;

@@ -25,6 +25,7 @@ for s in $STEPS; do
     pipetest) run pipetest 600 $PYT tests/test_gpu_pipeline.py -m gpu -k run_steps ;;
     comm) run comm 600 $PYT tests/test_gpu_comm.py -m gpu ;;
     c5test) run c5test 600 $PYT tests/test_gpu_example.py -m gpu -k config5 ;;
+    loop) run loop 600 $PYT tests/test_gpu_price_solver.py tests/test_gpu_station.py -m gpu ;;
     qnew) run qnew 600 $PYT tests/test_gpu_example.py tests/test_gpu_station.py -m gpu ;;
     bench) run bench 600 python bench.py ;;
     bench20) run bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
@@ -41,6 +42,8 @@ for s in $STEPS; do
     bimpc) run bimpc 300 python scripts/bimpc_timing.py ;;
     benchdirect) run bench_direct 600 python bench.py --mode direct --no-cpu-baseline ;;
     stamps) run stamps 300 python scripts/kstamps.py ;;
+    lstamps) run lstamps 300 python scripts/loop_stamps.py 48 ;;
+    stampsrt) run stampsrt 300 env KS_RT=1 KS_VARIANT=rt python scripts/kstamps.py 24 ;;
     # the driver's exact command under the kernel trace: where the wall time per step goes
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-station --no-direct ;;
     *) echo "unknown step $s" ;;

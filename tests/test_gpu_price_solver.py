@@ -145,3 +145,37 @@ def test_device_loop_matches_host_loop(gpu, monkeypatch, ev, price_type, N):
             np.testing.assert_allclose(sd[k], sh[k], rtol=1e-8, atol=1e-8 * np.max(np.abs(sh[k]), initial=1.0), err_msg=k)
         for k in ("price_before_reg", "price_after_reg"):
             assert abs(sd[k] - sh[k]) <= 1e-9 * max(1.0, abs(sh[k])), k
+
+
+@pytest.mark.parametrize("N", [12, 48])
+def test_device_loop_is_one_launch_per_iteration(gpu, monkeypatch, N):
+    """Over a gamma-sorted loop plan the device loop runs each iteration as ONE launch
+    (k_loop_iter: path, aggregation and loop step; timed as k_path): no k_eval / k_agg launch, one
+    launch per engine call (+ at most LOMPC_LOOP_AHEAD enqueued past the convergence), and the
+    same iterations and prices as the host loop (which runs k_path + k_agg + the host step)."""
+    from lompc_amd import _lib
+
+    monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
+    c, lc = consts("large")
+    rng = np.random.default_rng(5 + N)
+    y0 = 0.3 + 0.05 * c.y_max * rng.random(20000)
+    w_ref = c.w_max * (0.2 + 0.6 * rng.random(N))
+    res = {}
+    for mode in ("device", "host"):
+        ps = PriceSolver(N, lc, "linear-convex", device=0)
+        ps.device_loop = mode == "device"
+        ps.set_charge_levels(y0)
+        plan = ps._plan
+        plan.profile(enable=("k_path", "k_eval"))
+        for k in ("k_path", "k_eval"):
+            plan.profile(read=True, reset=True, kernel=k)
+        lm, st = ps.compute_optimal_prices(w_ref, 0.0)
+        n = {k: plan.profile(read=True, kernel=k)[1] for k in ("k_path", "k_eval")}
+        plan.profile(enable=False)
+        res[mode] = (lm.copy(), st, n)
+    (ld, sd, nd), (lh, sh, nh) = res["device"], res["host"]
+    assert sd["iter"] == sh["iter"]
+    assert nd["k_eval"] == 0, nd
+    assert sd["iter"] + 1 <= nd["k_path"] <= sd["iter"] + 1 + _lib.LOMPC_LOOP_AHEAD, nd
+    assert nh["k_eval"] == nh["k_path"] == sh["iter"] + 1, nh
+    np.testing.assert_allclose(ld, lh, rtol=0, atol=1e-9 * c.theta)

@@ -305,9 +305,14 @@ struct AggPart {
 // Cell c of set s by one wave, into the wave's partials.  COH: the cell's tables were written in
 // this launch (by this wave: k_loop_iter) — device-coherent loads (the scalar cache and the L1
 // hold no copy of them).
+// the cell's sorted positions [cs, ce)
+__device__ __forceinline__ int2 agg_cell_range(const AggSet& z, const int c) {
+  return make_int2(z.ps[c * z.KF], z.ps[(c + 1) * z.KF]);
+}
+
 template <int NT, bool COH>
-__device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, const int s, const int c, const int lane,
-                                         AggPart& a) {
+__device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, const int s, const int c, const int2 rng,
+                                         const int lane, AggPart& a) {
   const int N = NT ? NT : z.N, G = z.G, KF = z.KF;
   const QPConst& q = *z.q;
   const double* __restrict__ g = z.g;
@@ -319,16 +324,26 @@ __device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, cons
   // one memory round: the cell's sorted positions, its piece count and coverage start, and
   // every piece slot (whatever the count: no round waits on it) — piece ends and coefficients
   // on lane k, rows on lane t
-  const int cs = ps[c * KF], ce = ps[(c + 1) * KF];
+  const int cs = rng.x, ce = rng.y;
   const int cnt_l = ld_t<COH>(r.t_cnt + cell);
   const double lo = ld_t<COH>(r.t_lo + cell);
-  const double ge_l = lane < LQ_PPL ? ld_t<COH>(r.t_ge + sb + lane) : INFINITY;
+  // (every lane loads an in-range slot and the unused ones are masked after: no per-load branch,
+  // which the device-coherent loads would otherwise each get)
+  const int pl = lane & (LQ_PPL - 1), tl = min(lane, N - 1);
+  const double ge_v = ld_t<COH>(r.t_ge + sb + pl);
+  const double ge_l = lane < LQ_PPL ? ge_v : INFINITY;
   double cf[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) cf[k] = lane < LQ_PPL ? ld_t<COH>(r.t_cf + (sb + lane) * 8 + k) : 0.0;
+  for (int k = 0; k < 8; ++k) {
+    const double v = ld_t<COH>(r.t_cf + (sb + pl) * 8 + k);
+    cf[k] = lane < LQ_PPL ? v : 0.0;
+  }
   double2 ab[LQ_PPL];
 #pragma unroll
-  for (int k = 0; k < LQ_PPL; ++k) ab[k] = lane < N ? ld_t<COH>(r.t_ab + (sb + k) * N + lane) : make_double2(0.0, 0.0);
+  for (int k = 0; k < LQ_PPL; ++k) {
+    const double2 v = ld_t<COH>(r.t_ab + (sb + k) * N + tl);
+    ab[k] = lane < N ? v : make_double2(0.0, 0.0);
+  }
   if (ce <= cs) return;
   const int cnt = min(max(cnt_l, 0), LQ_PPL);
   const double ge = lane < cnt ? ge_l : INFINITY;
@@ -447,33 +462,45 @@ __device__ __forceinline__ AggRec agg_wave_record(const AggPart& a) {
                 (double)lqw::readlane_i(a.nfail, 0)};
 }
 
+// a set's closed outputs on the closing wave: lane t < N the stage sum of w, lane j < 8 stat j
+struct AggSetOut {
+  double sumw, stat;
+};
+
 // Set s's closing from nrec wave records, combined in record order, by ONE wave (lane = stage):
-// wrec(k) lane t's stage sum of record k, xrec(k, j) its scalar j.  WT: set outputs written
-// through to L2, complete when this returns.
-template <bool WT, class FW, class FX>
-__device__ __forceinline__ void agg_finish(const AggArgs& r, const AggSet& z, const int s, const int lane, const int nrec,
-                                           FW wrec, FX xrec) {
+// wrec(k) lane t's stage sum of record k, xlane(k) on lane j < 5 its scalar j (each lane combines
+// one scalar over the records).  WT: set outputs written through to L2, complete when this returns.
+// PADDED: records nrec .. LQ_AGG_W - 1 exist and are zero (sums and maxima of nonnegative
+// errors unchanged: no per-record condition)
+template <bool WT, bool PADDED, class FW, class FX>
+__device__ __forceinline__ AggSetOut agg_finish(const AggArgs& r, const AggSet& z, const int s, const int lane, const int nrec,
+                                           FW wrec, FX xlane) {
   const int N = z.N, n_s = z.n_s;
-  double v = 0.0;
-  if (lane < N)
-    for (int k = 0; k < nrec; ++k) v += wrec(k);
+  // (nrec <= LQ_AGG_W: unrolled, so register-held records stay in registers; lanes >= N sum
+  // whatever they hold, unread)
+  double v = 0.0, xs = 0.0, xm = 0.0;  // lane j < 5: scalar j summed / maximised over the records in order
+#pragma unroll
+  for (int k = 0; k < LQ_AGG_W; ++k) {
+    if (PADDED || k < nrec) {  // (no early exit: it would leave the records' registers to a stack array)
+      v += wrec(k);
+      const double xv = xlane(k);
+      xs += xv;
+      xm = fmax(xm, xv);
+    }
+  }
+  const double xa = lane == 2 ? xm : xs;  // (scalar 2, the max error: a max)
   if (lane < N && r.set_sum_w) {
     if (WT) st_wt8(r.set_sum_w + (size_t)s * N + lane, v);
     else r.set_sum_w[(size_t)s * N + lane] = v;
   }
   const double sw0 = lqw::readlane_d(v, 0);  // (sum of w0)
-  double c = 0.0, p0 = 0.0, e = 0.0, rr = 0.0, ff = 0.0;  // (every lane, the same order)
-  for (int k = 0; k < nrec; ++k) {
-    c += xrec(k, 0);
-    p0 += xrec(k, 1);
-    e = fmax(e, xrec(k, 2));
-    rr += xrec(k, 3);
-    ff += xrec(k, 4);
-  }
+  const double c = lqw::readlane_d(xa, 0), p0 = lqw::readlane_d(xa, 1), e = lqw::readlane_d(xa, 2);
+  const double rr = lqw::readlane_d(xa, 3);
+  double ff = lqw::readlane_d(xa, 4);
   if (!z.order_ok) ff = (double)n_s;  // gamma not ascending: every EV reported failed, nothing summed
   const double ni = (double)(n_s - (z.order_ok ? z.si.x : n_s));  // invalid gamma: after the valid ones
+  double x = 0.0;
   if (lane < LOMPC_SET_STATS) {
-    double x = 0.0;
     switch (lane) {
       case LOMPC_STAT_COUNT: x = (double)n_s; break;
       case LOMPC_STAT_SUM_W0: x = sw0; break;
@@ -496,6 +523,7 @@ __device__ __forceinline__ void agg_finish(const AggArgs& r, const AggSet& z, co
     if (ni > 0.0) __hip_atomic_fetch_add(r.tally + 2, (unsigned long long)ni, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (WT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the set outputs have reached L2
+  return AggSetOut{v, x};
 }
 
 // one workgroup per set, wave wv: cells wv, wv + nw, ...; the waves' records combined in wave order
@@ -508,13 +536,13 @@ __global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
   const AggSet z = agg_set_init<NT>(r, s);
   lq_tab_init(*z.q);  // (the individual re-solves' box table)
   AggPart a;
-  for (int c = wv; z.order_ok && c < z.G; c += nw) agg_cell<NT, false>(r, z, s, c, lane, a);
+  for (int c = wv; z.order_ok && c < z.G; c += nw) agg_cell<NT, false>(r, z, s, c, agg_cell_range(z, c), lane, a);
   const AggRec x = agg_wave_record(a);
   if (lane < z.N) s_w[wv][lane] = a.accw;
   if (lane < 5) s_x[wv][lane] = x.pick(lane);
   __syncthreads();
   if (wv == 0)
-    agg_finish<false>(r, z, s, lane, nw, [&](int k) { return s_w[k][lane]; }, [&](int k, int j) { return s_x[k][j]; });
+    agg_finish<false, false>(r, z, s, lane, nw, [&](int k) { return s_w[k][lane]; }, [&](int k) { return s_x[k][min(lane, 7)]; });
 }
 
 typedef void (*AggKernel)(AggArgs);

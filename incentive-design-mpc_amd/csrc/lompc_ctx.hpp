@@ -167,6 +167,7 @@ struct lompc_plan {
   int cap_loop_iter = 0;
   double* d_aggrec = nullptr;     // [S * G][LQ_AGG_REC] k_loop_iter's cell records
   int64_t cap_aggrec = 0;
+  int64_t aggrec_zero = -1;       // offset of its zeroed padding record (-1: none yet)
   // gamma-sorted sets (LOMPC_PLAN_SORTED_GAMMA, lompc_agg.hpp): runs without per-EV outputs
   // aggregate per piece from prefix sums built at prepare (k_agg) instead of k_eval
   bool sorted = false;

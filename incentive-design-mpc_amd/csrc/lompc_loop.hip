@@ -80,7 +80,8 @@ int lq_price_loop_device(lompc_plan* p, const lompc_price_loop_args* a, double* 
   h->conv_at = -1;
   StepArgs sa{N,        a->r,        MI,       a->tol_avg, a->theta, a->w_max, a->m,
               a->kappa, a->eps_reg,  a->tol,   a->n_evs,   a->dev_sw, a->dev_st, a->dev_in,
-              p->d_loop, reinterpret_cast<double*>(reinterpret_cast<char*>(p->d_loop) + 16), d_h, d_dec};
+              p->d_loop, reinterpret_cast<double*>(reinterpret_cast<char*>(p->d_loop) + 16),
+              reinterpret_cast<double*>(reinterpret_cast<char*>(p->d_loop) + LQ_LOOP_TRI), d_h, d_dec};
   const int ahead = LOMPC_LOOP_AHEAD;
   const bool fused = lq_loop_fusable(p);
   auto done = [&]() { return __atomic_load_n(const_cast<long long*>(&h->done), __ATOMIC_ACQUIRE) != 0; };

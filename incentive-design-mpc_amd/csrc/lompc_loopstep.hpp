@@ -19,8 +19,10 @@ struct lq_host_loop {
 };
 
 // d_loop: int ctl[4] (ctl[0]: finished = the plan kernels' skip flag; ctl[1]: k_loop_iter's
-// arrived workgroups, zero between calls) | double state[4]
-constexpr int LQ_LOOP_BYTES = 64;
+// arrived workgroups, zero between calls) | double state[4] | pad | the A_bar factor of the loop
+// (lqp::Tri per lane: Q[64] iv[64] d[64] K[64], written by the first step)
+constexpr int LQ_LOOP_TRI = 64;  // byte offset of the factor
+constexpr int LQ_LOOP_BYTES = LQ_LOOP_TRI + 4 * 64 * 8;
 
 struct StepArgs {
   int N, r, max_iter, tol_avg;
@@ -30,6 +32,7 @@ struct StepArgs {
   double* dev_in;    // [2][3N] prices | [2] lmbd_r | [2][N] w_ref   (the plan's price buffer)
   int* ctl;
   double* state;     // [0] dual cost of the previous call, [1] price term of dec_actual[0]
+  double* tri;       // [4][64] the A_bar factor (valid from the loop's second step)
   lq_host_loop* h;
   double* h_dec;     // [2][max_iter] pinned: dec_actual | dec_pred
 };
@@ -45,6 +48,13 @@ __device__ __forceinline__ void sys_release(long long* p, long long v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// publish v at p for the host behind every earlier store of the loop (the finishing step: the host
+// reads the results once it sees `done`)
+__device__ __forceinline__ void lq_publish(long long* p, long long v) {
+  __threadfence_system();
+  sys_release(p, v);
+}
+
 // loads of the engine call's set outputs: plain after a kernel boundary (k_loop_step),
 // device-coherent when workgroups of the same launch wrote them (k_loop_iter)
 template <bool COH>
@@ -53,25 +63,54 @@ __device__ __forceinline__ double lq_ld_set(const double* p) {
   else return *p;
 }
 
-// Engine call m of the loop has run (its set sums / stats in a.sw, a.st, at the prices in
-// a.dev_in); one wave, lane = stage.
-template <bool COH>
-__device__ __forceinline__ void loop_step(const StepArgs& a, const int m, const int lane) {
+// the engine call's outputs the step reads (lane t: stage t of the sums of w)
+struct StepIn {
+  double s0;      // set 0 (the partition's EVs): sum of w_t
+  double wk;      // set 1 = the central QP: its sum of w is its w
+  double emax;    // set 0's max A_bar error
+  double cost_c;  // set 1's cost
+  double n_inv, n_fail;
+  // the call's own inputs (step_prices: loadable before the engine call has run)
+  double lm[3];       // lane t: prices t, N + t, 2N + t
+  double wr;          // lane t: w_ref_t
+  double dc, dterm;   // state[0], state[1]
+  lqp::Tri ab;        // the A_bar factor (the loop's first step computes it)
+};
+
+// the step's inputs that do not depend on the engine call's outputs (the prices it ran at, w_ref,
+// the loop state): k_loop_iter loads them at its start, before its path
+__device__ __forceinline__ void step_prices(const StepArgs& a, const int lane, StepIn& in) {
   const int N = a.N, N3 = 3 * N;
   const bool act = lane < N;
-  const double s0 = act ? lq_ld_set<COH>(a.sw + lane) : 0.0;
-  const double wk = act ? lq_ld_set<COH>(a.sw + N + lane) : 0.0;  // set 1 = the central QP: its sum of w is its w
-  const double wr = act ? a.dev_in[2 * N3 + 2 + lane] : 0.0;
-  double lm[3];
+  in.wr = act ? a.dev_in[2 * N3 + 2 + lane] : 0.0;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) lm[k] = act ? a.dev_in[k * N + lane] : 0.0;
-  const double emax = lq_ld_set<COH>(a.st + LOMPC_STAT_MAX_ERR);
-  const double cost_c = lq_ld_set<COH>(a.st + LOMPC_SET_STATS + LOMPC_STAT_SUM_COST);
-  const double n_inv = lq_ld_set<COH>(a.st + LOMPC_STAT_N_INVALID) +
-                       lq_ld_set<COH>(a.st + LOMPC_SET_STATS + LOMPC_STAT_N_INVALID);
-  const double n_fail = lq_ld_set<COH>(a.st + LOMPC_STAT_N_FAILED) +
-                        lq_ld_set<COH>(a.st + LOMPC_SET_STATS + LOMPC_STAT_N_FAILED);
-  const double dc = a.state[0], dterm = a.state[1];
+  for (int k = 0; k < 3; ++k) in.lm[k] = act ? a.dev_in[k * N + lane] : 0.0;
+  in.dc = a.state[0];
+  in.dterm = a.state[1];
+  in.ab.Q = a.tri[lane];
+  in.ab.iv = a.tri[64 + lane];
+  in.ab.d = a.tri[128 + lane];
+  in.ab.K = a.tri[192 + lane];
+}
+
+// Engine call m of the loop has run (its set sums / stats in `in`, at the prices in a.dev_in);
+// one wave, lane = stage.
+struct NoStamp {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+// (ST: a diagnostic build's phase stamp, called with 8 after the inputs and the error metric, 9
+// after the price QP)
+template <class ST = NoStamp>
+__device__ __forceinline__ void loop_step_core(const StepArgs& a, const int m, const int lane, const StepIn& in,
+                                               const ST& stamp = ST{}) {
+  const int N = a.N, N3 = 3 * N;
+  const bool act = lane < N;
+  const double s0 = act ? in.s0 : 0.0, wk = act ? in.wk : 0.0;
+  const double emax = in.emax, cost_c = in.cost_c, n_inv = in.n_inv, n_fail = in.n_fail;
+  const double wr = in.wr;
+  double lm[3] = {in.lm[0], in.lm[1], in.lm[2]};
+  const double dc = in.dc, dterm = in.dterm;
   long long err = n_inv > 0.0 ? 1 : (n_fail > 0.0 ? 2 : 0);
   // price_solver.py:210-214: w_avg error in the A_bar = A'A + kappa I metric, w0 error, max error
   const double d = act ? s0 / a.n_evs - wr : 0.0;
@@ -84,12 +123,19 @@ __device__ __forceinline__ void loop_step(const StepArgs& a, const int m, const 
   // lmbd_k_new aliasing keeps the price term only for the first step)
   if (m > 0 && lane == 0) sys_st(a.h_dec + (m - 1), cost_c - dc + dterm);
   const bool conv = (a.tol_avg ? e2 : e0) <= a.tol;
+  stamp(8);
   double x[3] = {0.0, 0.0, 0.0};
   double dec = 0.0;
   if (!err && !conv && m < a.max_iter) {
     // the price-gradient step at (w_k, lmbd) (lompc_price_step)
     lqp::PriceQPW P;
-    P.init(N, a.r, a.theta, a.w_max, a.m, a.kappa, a.eps_reg, wk);
+    P.init(N, a.r, a.theta, a.w_max, a.m, a.kappa, a.eps_reg, wk, m > 0 ? &in.ab : nullptr);
+    if (m == 0) {  // the loop's A_bar factor for its later steps
+      a.tri[lane] = P.Ab.Q;
+      a.tri[64 + lane] = P.Ab.iv;
+      a.tri[128 + lane] = P.Ab.d;
+      a.tri[192 + lane] = P.Ab.K;
+    }
     const double q_s = 3.0 * a.theta / (4.0 * a.w_max);
     double Ql[3], q[3];
     P.mulQ(lm, Ql);
@@ -104,16 +150,17 @@ __device__ __forceinline__ void loop_step(const StepArgs& a, const int m, const 
     }
     qmax = lqw::wave_max(qmax, 64);
     dual = lqw::wave_sum(dual, 64);
-    if (lqp::nnqp_wave(P, q, lm, x, 1e-11 * (1.0 + qmax))) {
-      double Qx[3], cn = 0.0;
-      P.mulQ(x, Qx);
+    double mu[3];
+    if (lqp::nnqp_wave(P, q, lm, x, 1e-11 * (1.0 + qmax), mu)) {
+      double cn = 0.0;  // 1/2 x'Qx + q'x with Qx = mu - q from the certificate
 #pragma unroll
-      for (int k = 0; k < 3; ++k) cn += P.has(k) ? x[k] * fma(0.5, Qx[k], q[k]) : 0.0;
+      for (int k = 0; k < 3; ++k) cn += P.has(k) ? x[k] * fma(0.5, mu[k] - q[k], q[k]) : 0.0;
       dec = dual - lqw::wave_sum(cn, 64);
     } else {
       err = 3;
     }
   }
+  stamp(9);
   if (err || conv || m >= a.max_iter) {  // finished: the results to the host, then the flags
     if (act) {
 #pragma unroll
@@ -128,9 +175,8 @@ __device__ __forceinline__ void loop_step(const StepArgs& a, const int m, const 
       sys_st(&a.h->conv_at, (long long)m);
       sys_st(&a.h->err, err);
       __hip_atomic_store(a.ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the later calls skip
-      __threadfence_system();
-      sys_release(&a.h->done, 1);
-      sys_release(&a.h->progress, (long long)m + 1);
+      lq_publish(&a.h->done, 1);
+      lq_publish(&a.h->progress, (long long)m + 1);
     }
     return;
   }
@@ -152,7 +198,24 @@ __device__ __forceinline__ void loop_step(const StepArgs& a, const int m, const 
     sys_st(a.h_dec + a.max_iter + m, dec);
     a.state[0] = cost_c;
     a.state[1] = m == 0 ? dt : 0.0;
-    __threadfence_system();
-    sys_release(&a.h->progress, (long long)m + 1);
+    // (an unfinished step's progress orders nothing for the host — it only paces the enqueueing;
+    // h_dec is read after `done`, which the finishing step publishes behind every earlier store)
+    sys_st(&a.h->progress, (long long)m + 1);
   }
+}
+
+// the step with the engine call's outputs read from a.sw / a.st
+template <bool COH>
+__device__ __forceinline__ void loop_step(const StepArgs& a, const int m, const int lane) {
+  const int N = a.N;
+  const bool act = lane < N;
+  StepIn in;
+  step_prices(a, lane, in);
+  in.s0 = act ? lq_ld_set<COH>(a.sw + lane) : 0.0;
+  in.wk = act ? lq_ld_set<COH>(a.sw + N + lane) : 0.0;
+  in.emax = lq_ld_set<COH>(a.st + LOMPC_STAT_MAX_ERR);
+  in.cost_c = lq_ld_set<COH>(a.st + LOMPC_SET_STATS + LOMPC_STAT_SUM_COST);
+  in.n_inv = lq_ld_set<COH>(a.st + LOMPC_STAT_N_INVALID) + lq_ld_set<COH>(a.st + LOMPC_SET_STATS + LOMPC_STAT_N_INVALID);
+  in.n_fail = lq_ld_set<COH>(a.st + LOMPC_STAT_N_FAILED) + lq_ld_set<COH>(a.st + LOMPC_SET_STATS + LOMPC_STAT_N_FAILED);
+  loop_step_core(a, m, lane, in);
 }

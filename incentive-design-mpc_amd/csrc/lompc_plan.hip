@@ -49,7 +49,8 @@
 #define __builtin_amdgcn_s_memtime __builtin_amdgcn_s_memrealtime
 #endif
 __device__ long long g_stamps[65536 * 8];
-__device__ long long g_wstart[32768 * 8];  // k_eval: start of wave w of workgroup b at [b * 8 + w]
+__device__ long long g_wstart[32768 * 8];
+__device__ unsigned long long g_lstamps[64 * 16];  // k_loop_iter's phase sums (LQ_LSTAMP)  // k_eval: start of wave w of workgroup b at [b * 8 + w]
 #define LQ_WSTART()                                                                              \
   do {                                                                                           \
     const long long t__ = __builtin_amdgcn_s_memtime();                                          \
@@ -1329,25 +1330,26 @@ StepKernel step_kernel(int N) {
 // One iteration of the device-resident price loop over gamma-sorted sets (lompc_loop.hip) in ONE
 // launch, one wave per (set, cell) as k_path: the wave tracks its cell's path (path_cell), then
 // aggregates the same cell from the tables it has just written (agg_cell, coherent loads) into a
-// cell record (write-through); the set's last arriving cell closes the set from its G records in
-// cell order (agg_finish: k_agg's arithmetic, whose wave c holds cell c for G <= LQ_AGG_W — the
-// same bits), and the last set to close runs the loop step (lompc_loopstep.hpp) on the engine
-// call's set outputs.  The unfused form's three launches (k_path, k_agg, k_loop_step) and two
-// kernel boundaries become one launch and two arrival counters (ctl[1 + s] per set, ctl[3]).
+// cell record (write-through).  The last of the S * G cells to arrive closes both sets from their
+// records in cell order (agg_finish: k_agg's arithmetic, whose wave c holds cell c for G <=
+// LQ_AGG_W — the same bits) and runs the loop step (lompc_loopstep.hpp) on the closed outputs in
+// its registers.  The unfused form's three launches (k_path, k_agg, k_loop_step) and two kernel
+// boundaries become one launch and one arrival counter (ctl[1]).
 #ifdef LOMPC_STAMPS
 // diagnostic build: per k_loop_iter wave (blk < 64) the phases' s_memrealtime ticks summed over the
-// launches: [0] path, [1] aggregation, [2] record + arrival, [3] set closing, [4] loop step,
-// [5] launches, [6] closings, [7] steps (scripts/loop_stamps.py)
-__device__ unsigned long long g_lstamps[64 * 8];
+// launches: [0] path, [1] aggregation, [2] record + arrival, [3] both sets' closing, [4] loop step,
+// [5] launches, [6] closings, [7] steps; sub-phases of [3] and [4]: [10] the records' load round,
+// [8] the step's inputs and error metric, [9] the price QP (scripts/loop_stamps.py)
 #define LQ_LSTAMP(k)                                                                                 \
   do {                                                                                               \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                 \
     const long long t__ = __builtin_amdgcn_s_memrealtime();                                          \
     if (lane == 0 && blk < 64) {                                                                     \
-      __hip_atomic_fetch_add(g_lstamps + blk * 8 + (k), (unsigned long long)(t__ - tl__), __ATOMIC_RELAXED, \
+      __hip_atomic_fetch_add(g_lstamps + blk * 16 + (k), (unsigned long long)(t__ - tl__), __ATOMIC_RELAXED, \
                              __HIP_MEMORY_SCOPE_AGENT);                                              \
-      __hip_atomic_fetch_add(g_lstamps + blk * 8 + 5 + ((k) >= 3 ? (k) - 2 : 0), (k) == 0 || (k) >= 3 ? 1ull : 0ull, \
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                            \
+      if ((k) == 0 || (k) == 3 || (k) == 4)                                                          \
+        __hip_atomic_fetch_add(g_lstamps + blk * 16 + 5 + ((k) >= 3 ? (k) - 2 : 0), 1ull, __ATOMIC_RELAXED, \
+                               __HIP_MEMORY_SCOPE_AGENT);                                            \
     }                                                                                                \
     tl__ = t__;                                                                                      \
   } while (0)
@@ -1357,42 +1359,87 @@ __device__ unsigned long long g_lstamps[64 * 8];
 
 template <int NT>
 __global__ __launch_bounds__(64) void k_loop_iter(PathArgs pa, AggArgs ga, StepArgs sa, double* rec, int m) {
+  constexpr int S = 2;  // (lq_loop_fusable: the loop's two sets)
   if (sa.ctl[0]) return;  // finished: a call enqueued ahead of the convergence (every workgroup)
   const int blk = (int)blockIdx.x, lane = (int)threadIdx.x, G = pa.G;
   const int s = blk / G, c = blk - s * G;
 #ifdef LOMPC_STAMPS
   long long tl__ = __builtin_amdgcn_s_memrealtime();
 #endif
+  StepIn in;
+  step_prices(sa, lane, in);  // (every wave: the one that runs the step has them when it arrives last)
+  // the sets' sizes and order flags for the closing, loaded now (scalar loads are otherwise issued
+  // at their first use: a memory round on the closing's critical path)
+  int cl_n[S], cl_v[S], cl_ok[S];
+#pragma unroll
+  for (int t = 0; t < S; ++t) {
+    const int4 si = ga.sinfo[t];
+    cl_n[t] = (int)(ga.set_off[t + 1] - ga.set_off[t]);
+    cl_v[t] = si.x;
+    cl_ok[t] = si.y;
+    asm volatile("" : "+v"(cl_n[t]), "+v"(cl_v[t]), "+v"(cl_ok[t]));  // (held in VGPRs: SGPRs are scarce here)
+  }
   path_cell<NT, true>(pa, blk);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the cell's tables have reached L2
   LQ_LSTAMP(0);
-  const AggSet z = agg_set_init<NT>(ga, s);
-  AggPart ap;
-  if (z.order_ok) agg_cell<NT, true>(ga, z, s, c, lane, ap);
-  LQ_LSTAMP(1);
-  const AggRec x = agg_wave_record(ap);
-  double* rc = rec + (size_t)blk * LQ_AGG_REC;
-  if (lane < z.N) st_wt8(rc + lane, ap.accw);
-  if (lane < 5) st_wt8(rc + LOMPC_MAX_N + lane, x.pick(lane));
+  {
+    const AggSet z = agg_set_init<NT>(ga, s);
+    AggPart ap;
+    if (z.order_ok) agg_cell<NT, true>(ga, z, s, c, agg_cell_range(z, c), lane, ap);
+    LQ_LSTAMP(1);
+    const AggRec x = agg_wave_record(ap);
+    double* rc = rec + (size_t)blk * LQ_AGG_REC;
+    if (lane < z.N) st_wt8(rc + lane, ap.accw);
+    if (lane < 5) st_wt8(rc + LOMPC_MAX_N + lane, x.pick(lane));
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int old = 0;
   if (lane == 0) {
-    old = __hip_atomic_fetch_add(sa.ctl + 1 + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == G - 1) __hip_atomic_store(sa.ctl + 1 + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __hip_atomic_fetch_add(sa.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == S * G - 1) __hip_atomic_store(sa.ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   LQ_LSTAMP(2);
-  if (lqw::readlane_i(old, 0) != G - 1) return;
-  const double* rs = rec + (size_t)s * G * LQ_AGG_REC;
-  agg_finish<true>(ga, z, s, lane, G, [&](int k) { return ld_t<true>(rs + (size_t)k * LQ_AGG_REC + lane); },
-                   [&](int k, int j) { return ld_t<true>(rs + (size_t)k * LQ_AGG_REC + LOMPC_MAX_N + j); });
-  LQ_LSTAMP(3);
-  old = 0;
-  if (lane == 0) {
-    old = __hip_atomic_fetch_add(sa.ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == pa.S - 1) __hip_atomic_store(sa.ctl + 3, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lqw::readlane_i(old, 0) != S * G - 1) return;
+  // the last arriver: every record of both sets in flight at once (one memory round), each set
+  // closed in cell order, then the loop step on the closed outputs
+  AggSet zs[S];  // (agg_finish reads N and the sizes / order flags loaded at the start)
+#pragma unroll
+  for (int t = 0; t < S; ++t) {
+    zs[t].N = NT ? NT : ga.N;
+    zs[t].n_s = cl_n[t];
+    zs[t].si = make_int4(cl_v[t], cl_ok[t], 0, 0);
+    zs[t].order_ok = cl_ok[t] != 0;
   }
-  if (lqw::readlane_i(old, 0) != pa.S - 1) return;
-  loop_step<true>(sa, m, lane);
+  const int N = zs[0].N;
+  // (records k >= G read the zero record past the S * G real ones: no per-load branch or mask)
+  double rw[S][LQ_AGG_W], rx[S][LQ_AGG_W];
+  const int tl = min(lane, N - 1), xl = min(lane, 4);
+#pragma unroll
+  for (int t = 0; t < S; ++t)
+#pragma unroll
+    for (int k = 0; k < LQ_AGG_W; ++k) {
+      const double* rk = rec + (size_t)(k < G ? t * G + k : S * G) * LQ_AGG_REC;
+      rw[t][k] = ld_t<true>(rk + tl);
+      rx[t][k] = ld_t<true>(rk + LOMPC_MAX_N + xl);
+    }
+  LQ_LSTAMP(10);
+  AggSetOut o[S];
+#pragma unroll
+  for (int t = 0; t < S; ++t)
+    o[t] = agg_finish<false, true>(ga, zs[t], t, lane, G, [&](int k) { return rw[t][k]; },
+                             [&](int k) { return rx[t][k]; });
+  LQ_LSTAMP(3);
+  in.s0 = o[0].sumw;
+  in.wk = o[1].sumw;
+  in.emax = lqw::readlane_d(o[0].stat, LOMPC_STAT_MAX_ERR);
+  in.cost_c = lqw::readlane_d(o[1].stat, LOMPC_STAT_SUM_COST);
+  in.n_inv = lqw::readlane_d(o[0].stat, LOMPC_STAT_N_INVALID) + lqw::readlane_d(o[1].stat, LOMPC_STAT_N_INVALID);
+  in.n_fail = lqw::readlane_d(o[0].stat, LOMPC_STAT_N_FAILED) + lqw::readlane_d(o[1].stat, LOMPC_STAT_N_FAILED);
+#ifdef LOMPC_STAMPS
+  loop_step_core(sa, m, lane, in, [&](int k) { LQ_LSTAMP(k); });
+#else
+  loop_step_core(sa, m, lane, in);
+#endif
   LQ_LSTAMP(4);
 }
 
@@ -1933,11 +1980,16 @@ int lq_launch_loop_iter(lompc_plan* p, const double* lmbd, const double* lmbd_r,
                         const StepArgs& sa, int m, hipStream_t st) {
   if (!lq_loop_fusable(p)) return fail_arg(p, "k_loop_iter: plan not fusable");
   const int N = p->N;
-  const int64_t nrec = p->S * p->G * (int64_t)LQ_AGG_REC;
+  const int64_t nrec = (p->S * p->G + 1) * (int64_t)LQ_AGG_REC;  // + the zero record (k_loop_iter's padding)
   if (nrec > p->cap_aggrec) {
     const int rc = grow(p, &p->d_aggrec, nrec);
     if (rc) return rc;
     p->cap_aggrec = nrec;
+    p->aggrec_zero = -1;
+  }
+  if (p->aggrec_zero != nrec - LQ_AGG_REC) {  // (the cell records never reach it: zeroed once per layout)
+    HIPCHK(p, hipMemsetAsync(p->d_aggrec + (nrec - LQ_AGG_REC), 0, LQ_AGG_REC * sizeof(double), st));
+    p->aggrec_zero = nrec - LQ_AGG_REC;
   }
   const PathTab tb = own_tab(p);
   const PathArgs pa = path_args(p, lmbd, lmbd_r, tb);
@@ -1994,11 +2046,11 @@ int lompc_debug_wstart(long long* host, int n) {
              ? LOMPC_OK
              : LOMPC_ERR_HIP;
 }
-int lompc_debug_loopstamps(unsigned long long* host, int reset) {  // [64][8] (g_lstamps)
+int lompc_debug_loopstamps(unsigned long long* host, int reset) {  // [64][16] (g_lstamps)
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lstamps), sizeof(g_lstamps), 0, hipMemcpyDeviceToHost) != hipSuccess)
     return LOMPC_ERR_HIP;
   if (reset) {
-    static const unsigned long long z[64 * 8] = {};
+    static const unsigned long long z[64 * 16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_lstamps), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
       return LOMPC_ERR_HIP;
   }

@@ -28,43 +28,41 @@ using lqw::Mob;
 //                                                      the pivot form a_t - E_t^2 / d_{t-1} loses ~1e-11)
 //   p_t = E_t iv_t p_{t+1} + b_t Q_t iv_t,  Q_t = c + P_{t+1},  iv_t = 1 / (Q_t + E_t)
 //   x_t = K_t y_{t-1} + k_t,  K_t = -Q_t iv_t,  k_t = (b_t - p_{t+1}) iv_t
-// P and p are reversed-layout scans (lane l = stage N-1-l), y a natural-layout scan.
+// All in the natural layout (lane t = stage t): P and p are suffix scans (lqw::wave_scan_rev: DPP
+// inside the 16-lane rows, row totals by v_readlane), y a prefix scan — no lane reversal through LDS.
 struct Tri {
-  double Q, iv, d;  // reversed layout: Q_t, iv_t, E_t of stage N-1-lane
-  double K;         // natural layout: K_t
+  double Q, iv, d;  // Q_t, iv_t, E_t
+  double K;         // K_t
 };
 
 __device__ __forceinline__ Tri tri_factor(double c, double E, int N, int lane) {
   const bool act = lane < N;
-  const int rs = act ? N - 1 - lane : lane;
-  const double d = act ? lqw::bperm(rs, E) : 0.0;
+  const double d = act ? E : 0.0;
   Mob f = Mob::identity();
   if (act) {  // P -> d (c + P) / (c + P + d), scaled to d-entry 1
     const double u = 1.0 / (c + d);
     f = {d * u, d * c * u, u, 1.0};
   }
-  const Mob T = lqw::wave_scan(f, N);
-  const double Pn = lqw::shr1(0.0, T.b / T.d);  // P_{t+1} (P_N = 0)
+  const Mob T = lqw::wave_scan_rev(f, N);
+  const double Pn = lqw::shl1(0.0, T.b / T.d);  // P_{t+1} (P_N = 0: lane N holds the identity, or lane 63's old)
   Tri t;
   t.Q = c + Pn;
   t.iv = 1.0 / (t.Q + d);
   t.d = d;
-  t.K = act ? lqw::bperm(rs, -t.Q * t.iv) : 0.0;
+  t.K = act ? -t.Q * t.iv : 0.0;
   return t;
 }
 
 // x = (c A'A + diag(E))^-1 b
 __device__ __forceinline__ double tri_solve(const Tri& T, double b, int N, int lane) {
   const bool act = lane < N;
-  const int rs = act ? N - 1 - lane : lane;
-  const double br = act ? lqw::bperm(rs, b) : 0.0;
   Aff<1> g = Aff<1>::identity();
   if (act) {
     g.A = T.d * T.iv;
-    g.B[0] = br * T.Q * T.iv;
+    g.B[0] = b * T.Q * T.iv;
   }
-  const double pn = lqw::shr1(0.0, lqw::wave_scan(g, N).B[0]);  // p_{t+1}
-  const double k = act ? lqw::bperm(rs, (br - pn) * T.iv) : 0.0;
+  const double pn = lqw::shl1(0.0, lqw::wave_scan_rev(g, N).B[0]);  // p_{t+1}
+  const double k = act ? (b - pn) * T.iv : 0.0;
   Aff<1> h = Aff<1>::identity();
   if (act) {
     h.A = 1.0 + T.K;
@@ -81,8 +79,10 @@ struct PriceQPW {
   double eps, m, kappa;
   Tri Ab;  // factor of A_bar = A'A + kappa I
 
+  // ab: the factor of A_bar = A'A + kappa I when known (it depends on kappa and N only: the device
+  // loop computes it at its first step and keeps it), else null
   __device__ __forceinline__ void init(int N_, int r, double theta, double w_max, double m_, double kappa_,
-                                       double eps_, double w) {
+                                       double eps_, double w, const Tri* ab = nullptr) {
     N = N_;
     nb = r / N_;
     lane = (int)threadIdx.x & 63;
@@ -94,7 +94,7 @@ struct PriceQPW {
     u[0] = act ? theta : 0.0;   // Dphi rows, lompc.py:179-187
     u[1] = act ? -theta : 0.0;
     u[2] = (act && nb > 2) ? 2.0 * q_s * w : 0.0;
-    Ab = tri_factor(1.0, kappa, N, lane);
+    Ab = ab ? *ab : tri_factor(1.0, kappa, N, lane);
   }
   __device__ __forceinline__ bool has(int k) const { return lane < N && k < nb; }
 
@@ -159,13 +159,14 @@ __device__ __forceinline__ bool row_argmin(const PriceQPW& P, const double (&v)[
 }
 
 // exact non-negative QP (lompc_price.cpp nnqp): PDAS from the warm free set, primal active set
-// from x = 0 as the fallback.  Returns false when neither certifies (LOMPC_ERR_NOT_CONVERGED).
+// from x = 0 as the fallback.  Returns false when neither certifies (LOMPC_ERR_NOT_CONVERGED);
+// on success mu = Q x + q (the certificate's multipliers).
 __device__ __forceinline__ bool nnqp_wave(const PriceQPW& P, const double (&q)[3], const double (&xw)[3], double (&x)[3],
-                                          double tol) {
+                                          double tol, double (&mu)[3]) {
   bool F[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) F[k] = P.has(k) && xw[k] > 0.0;
-  double z[3], mu[3];
+  double z[3];
   for (int it = 0; it < 64; ++it) {
     P.solveF(F, q, z);
     P.mulQ(z, mu);

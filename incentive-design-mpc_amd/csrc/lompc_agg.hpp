@@ -470,17 +470,17 @@ struct AggSetOut {
 // Set s's closing from nrec wave records, combined in record order, by ONE wave (lane = stage):
 // wrec(k) lane t's stage sum of record k, xlane(k) on lane j < 5 its scalar j (each lane combines
 // one scalar over the records).  WT: set outputs written through to L2, complete when this returns.
-// PADDED: records nrec .. LQ_AGG_W - 1 exist and are zero (sums and maxima of nonnegative
-// errors unchanged: no per-record condition)
-template <bool WT, bool PADDED, class FW, class FX>
+// PADDED: records nrec .. MAXREC - 1 exist and are zero (sums and maxima of nonnegative errors
+// unchanged: no per-record condition)
+template <bool WT, bool PADDED, int MAXREC, class FW, class FX>
 __device__ __forceinline__ AggSetOut agg_finish(const AggArgs& r, const AggSet& z, const int s, const int lane, const int nrec,
                                            FW wrec, FX xlane) {
   const int N = z.N, n_s = z.n_s;
-  // (nrec <= LQ_AGG_W: unrolled, so register-held records stay in registers; lanes >= N sum
+  // (nrec <= MAXREC: unrolled, so register-held records stay in registers; lanes >= N sum
   // whatever they hold, unread)
   double v = 0.0, xs = 0.0, xm = 0.0;  // lane j < 5: scalar j summed / maximised over the records in order
 #pragma unroll
-  for (int k = 0; k < LQ_AGG_W; ++k) {
+  for (int k = 0; k < MAXREC; ++k) {
     if (PADDED || k < nrec) {  // (no early exit: it would leave the records' registers to a stack array)
       v += wrec(k);
       const double xv = xlane(k);
@@ -542,7 +542,7 @@ __global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
   if (lane < 5) s_x[wv][lane] = x.pick(lane);
   __syncthreads();
   if (wv == 0)
-    agg_finish<false, false>(r, z, s, lane, nw, [&](int k) { return s_w[k][lane]; }, [&](int k) { return s_x[k][min(lane, 7)]; });
+    agg_finish<false, false, LQ_AGG_W>(r, z, s, lane, nw, [&](int k) { return s_w[k][lane]; }, [&](int k) { return s_x[k][min(lane, 7)]; });
 }
 
 typedef void (*AggKernel)(AggArgs);

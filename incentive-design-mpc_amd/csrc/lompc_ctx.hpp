@@ -245,7 +245,7 @@ int lq_comm_allgather(lompc_comm* c, const double* send, double* recv, size_t co
 // price loops (lompc_plan.hip: host form; lompc_loop.hip: device-resident form and the C-ABI entry)
 const char* lq_failed_text(lompc_plan* p, hipStream_t st);
 // one device-loop iteration as ONE launch (k_loop_iter: path + aggregation + the loop step) when
-// the plan allows it (gamma-sorted sets, no communicator, at most LQ_AGG_W cells per set)
+// the plan allows it (gamma-sorted sets, no communicator, at most LQ_LOOP_G cells per set)
 struct StepArgs;
 bool lq_loop_fusable(const lompc_plan* p);
 int lq_launch_loop_iter(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,

@@ -14,7 +14,7 @@
 // stores (no copy, no stream sync per iteration); calls enqueued past the convergence find the
 // loop's finished flag and return at once.  The enqueue rule depends only on the iteration at
 // which the loop finished, so every rank of a sharded plan issues the same collectives.
-// Fused form (gamma-sorted sets, one rank, <= LQ_AGG_W cells per set): the engine call and the
+// Fused form (gamma-sorted sets, one rank, <= LQ_LOOP_G cells per set): the engine call and the
 // step are ONE launch, k_loop_iter (lompc_plan.hip) — path, aggregation and step without the two
 // kernel boundaries between them.
 #include <hip/hip_runtime.h>

@@ -97,6 +97,9 @@ __device__ unsigned long long g_lstamps[64 * 16];  // k_loop_iter's phase sums (
 #ifndef LQ_STEP_PRIO
 #define LQ_STEP_PRIO 1                     // k_step: path waves at raised issue priority
 #endif
+#ifndef LQ_WARM_FP64
+#define LQ_WARM_FP64 1                     // k_path with a warm start: fp64 PDAS straight from the stored set
+#endif
 #define LQ_DROP_OFF 0x7fff0000             // k_eval: a store offset past any w descriptor's range (dropped)
 
 namespace {
@@ -319,18 +322,20 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
   int sl0 = lane < N ? 1 : 0;
   if (!(a.flags & LOMPC_PLAN_DIAG_REPAIR)) {
     int sl = sl0;
+    bool warm = false;
     if (a.ws) {
       const int v = a.ws[(size_t)blk * 64 + lane];
       sl = (lane < N && v >= 0 && v <= 2 * q.m) ? v : sl0;
+      warm = LQ_WARM_FP64 && __all(lane >= N || v <= 2 * q.m);  // (a stored set on every stage: wave-uniform)
     }
     lqw::StageSol<2> sol;
     bool has_sol = false;
 #ifdef LOMPC_STAMPS
     int nit = 0;
-    const bool solved = lqw::wave_solve_path(q, ws, glo, sl, sol, has_sol, &nit);
+    const bool solved = lqw::wave_solve_path(q, ws, glo, sl, sol, has_sol, &nit, warm);
     if (lane == 0 && blk < 32768) g_stamps[blk * 8 + 4] = nit;
 #else
-    const bool solved = lqw::wave_solve_path(q, ws, glo, sl, sol, has_sol);
+    const bool solved = lqw::wave_solve_path(q, ws, glo, sl, sol, has_sol, nullptr, warm);
 #endif
     LQ_STAMP(2);
     if (solved) {
@@ -1331,10 +1336,12 @@ StepKernel step_kernel(int N) {
 // launch, one wave per (set, cell) as k_path: the wave tracks its cell's path (path_cell), then
 // aggregates the same cell from the tables it has just written (agg_cell, coherent loads) into a
 // cell record (write-through).  The last of the S * G cells to arrive closes both sets from their
-// records in cell order (agg_finish: k_agg's arithmetic, whose wave c holds cell c for G <=
-// LQ_AGG_W — the same bits) and runs the loop step (lompc_loopstep.hpp) on the closed outputs in
-// its registers.  The unfused form's three launches (k_path, k_agg, k_loop_step) and two kernel
+// records in cell order (agg_finish: k_agg's arithmetic — the same bits for G <= LQ_AGG_W, where
+// k_agg's wave c holds cell c; G <= LQ_LOOP_G) and runs the loop step (lompc_loopstep.hpp) on the
+// closed outputs in its registers.  The unfused form's three launches (k_path, k_agg, k_loop_step) and two kernel
 // boundaries become one launch and one arrival counter (ctl[1]).
+constexpr int LQ_LOOP_G = 16;  // k_loop_iter: at most this many cells per set (its closing's records in registers)
+
 #ifdef LOMPC_STAMPS
 // diagnostic build: per k_loop_iter wave (blk < 64) the phases' s_memrealtime ticks summed over the
 // launches: [0] path, [1] aggregation, [2] record + arrival, [3] both sets' closing, [4] loop step,
@@ -1412,12 +1419,12 @@ __global__ __launch_bounds__(64) void k_loop_iter(PathArgs pa, AggArgs ga, StepA
   }
   const int N = zs[0].N;
   // (records k >= G read the zero record past the S * G real ones: no per-load branch or mask)
-  double rw[S][LQ_AGG_W], rx[S][LQ_AGG_W];
+  double rw[S][LQ_LOOP_G], rx[S][LQ_LOOP_G];
   const int tl = min(lane, N - 1), xl = min(lane, 4);
 #pragma unroll
   for (int t = 0; t < S; ++t)
 #pragma unroll
-    for (int k = 0; k < LQ_AGG_W; ++k) {
+    for (int k = 0; k < LQ_LOOP_G; ++k) {
       const double* rk = rec + (size_t)(k < G ? t * G + k : S * G) * LQ_AGG_REC;
       rw[t][k] = ld_t<true>(rk + tl);
       rx[t][k] = ld_t<true>(rk + LOMPC_MAX_N + xl);
@@ -1426,7 +1433,7 @@ __global__ __launch_bounds__(64) void k_loop_iter(PathArgs pa, AggArgs ga, StepA
   AggSetOut o[S];
 #pragma unroll
   for (int t = 0; t < S; ++t)
-    o[t] = agg_finish<false, true>(ga, zs[t], t, lane, G, [&](int k) { return rw[t][k]; },
+    o[t] = agg_finish<false, true, LQ_LOOP_G>(ga, zs[t], t, lane, G, [&](int k) { return rw[t][k]; },
                              [&](int k) { return rx[t][k]; });
   LQ_LSTAMP(3);
   in.s0 = o[0].sumw;
@@ -1622,7 +1629,8 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     p->cap_cells = ncell;
     fresh_ws = true;
   }
-  if (warm && (fresh_ws || p->G != G || p->S != S)) HIPCHK(p, hipMemsetAsync(p->d_ws, 1, (size_t)ncell * 64, st));
+  // (0xff: no stored set — a cell's first run starts cold, from "all free", and its later runs warm)
+  if (warm && (fresh_ws || p->G != G || p->S != S)) HIPCHK(p, hipMemsetAsync(p->d_ws, 0xff, (size_t)ncell * 64, st));
   if (!p->d_tally) {
     if ((rc = grow(p, &p->d_tally, 3))) return rc;
     HIPCHK(p, hipMemsetAsync(p->d_tally, 0, 3 * sizeof(unsigned long long), st));
@@ -1973,7 +1981,7 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
 }
 
 bool lq_loop_fusable(const lompc_plan* p) {  // (S = 2: the loop's sets; ctl holds 2 set counters)
-  return p->sorted && !p->comm && p->nblk > 0 && p->S == 2 && p->G >= 1 && p->G <= LQ_AGG_W;
+  return p->sorted && !p->comm && p->nblk > 0 && p->S == 2 && p->G >= 1 && p->G <= LQ_LOOP_G;
 }
 
 int lq_launch_loop_iter(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,

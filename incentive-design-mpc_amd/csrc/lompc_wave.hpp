@@ -606,10 +606,12 @@ __device__ __forceinline__ bool wave_solve(const QPConst& q, const WaveSet& ws, 
 // already holds w(g) = a + b g and r(g) of the final working set for the path tracking (one
 // sub-problem solve fewer per path).  has_sol is false when the primal active set had to take
 // over (the caller then solves the final working set itself).
+// warm: s is the previous run's working set at this point (a price loop's next iteration: at most a
+// few coordinates move) — the fp64 PDAS starts from it directly, no fp32 search first
 __device__ __forceinline__ bool wave_solve_path(const QPConst& q, const WaveSet& ws, double gamma, int& s,
-                                                StageSol<2>& sol, bool& has_sol, int* nit = nullptr) {
+                                                StageSol<2>& sol, bool& has_sol, int* nit = nullptr, bool warm = false) {
   int n32 = 0, n64 = 0;
-  if (LQ_F32_IT > 0) n32 = wave_pdas_f32(q, ws, gamma, s, LQ_F32_IT);
+  if (LQ_F32_IT > 0 && !warm) n32 = wave_pdas_f32(q, ws, gamma, s, LQ_F32_IT);
   const int max_it = min(4 * ws.N + 8, LQ_PDAS_CAP);
   bool ok = false;
   double w = 0.0, r = 0.0;

@@ -43,6 +43,8 @@ for s in $STEPS; do
     benchdirect) run bench_direct 600 python bench.py --mode direct --no-cpu-baseline ;;
     stamps) run stamps 300 python scripts/kstamps.py ;;
     lstamps) run lstamps 300 python scripts/loop_stamps.py station ;;
+    lstamps32) run lstamps32 300 python scripts/loop_stamps.py station --cells 32 ;;
+    lstamps8) run lstamps8 300 python scripts/loop_stamps.py station --cells 8 ;;
     stampsrt) run stampsrt 300 env KS_RT=1 KS_VARIANT=rt python scripts/kstamps.py 24 ;;
     # the driver's exact command under the kernel trace: where the wall time per step goes
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-station --no-direct ;;

@@ -25,6 +25,11 @@ LIB = sys.argv[sys.argv.index("--lib") + 1] if "--lib" in sys.argv else "lstamps
 if "--lib" in sys.argv:
     i = sys.argv.index("--lib")
     del sys.argv[i:i + 2]
+CELLS = None  # --cells G: the station's loop plans with G path cells per set
+if "--cells" in sys.argv:
+    i = sys.argv.index("--cells")
+    CELLS = int(sys.argv[i + 1])
+    del sys.argv[i:i + 2]
 DBG = os.path.join(ROOT, "incentive-design-mpc_amd", "lompc_amd", f"liblompc_amd_{LIB}.so")
 if "--build" in sys.argv:
     print(build.build(force=True, out=DBG, defines=("LOMPC_STAMPS", "LOMPC_STAMPS_RT")))
@@ -56,6 +61,7 @@ if mode == "station":
                             demand_scale=DEMAND_SCALE * M_2 / NUM_EVS_PER_EV_TYPE, u_b_max=0.5, x_max=0.5)
     np.random.seed(0)
     st = ChargingStation(consts, device=0)
+    st.price_solver_s.loop_cells = st.price_solver_l.loop_cells = CELLS
     st._step()
     torch.cuda.synchronize()
     assert lib.lompc_debug_loopstamps(buf.ctypes.data, 1) == 0
@@ -90,6 +96,7 @@ else:
     lc = LoMPCConstants(0.025, 50.0, 0.9, 0.15, "large")
     rng = np.random.default_rng(3)
     ps = PriceSolver(N, lc, "linear-convex", device=0)
+    ps.loop_cells = CELLS
     iters = 0
     for call in range(6):
         ps.set_charge_levels(0.3 + 0.3 * lc.y_max * rng.random(EVS))

@@ -1,6 +1,7 @@
 """profiles/pmc.json from a PMC session (scripts/pmc_session.sh: one rocprofv3 --pmc pass per
 counter group over `bench.py --steps 3 --warmup 2`), per plan kernel, per dispatch:
 
+* k_step: the launches that carry an evaluation (the fill / drain launches of a call excluded);
 * k_eval HBM traffic = 2 x FETCH_SIZE (gfx950 reports half of the bytes of wide coalesced
   reads, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both KiB per dispatch -> bytes;
 * SQ counters (SQ_WAVE_CYCLES, SQ_ACTIVE_INST_* and SQ_WAIT_* count quad-cycles): the VALU-issue
@@ -27,6 +28,18 @@ for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
         for k in KERNELS:
             if name.startswith(k + "(") or name.startswith(k + "<"):  # (exact-N template instances)
                 vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+
+
+# k_step: only the steady-state launches (an evaluation's rows written: WRITE_SIZE at least half the
+# largest); a run_steps call's first launch (path only) and last (closing only) write almost
+# nothing.  Every pass runs the same dispatch sequence, so one mask selects the same launches in each
+ws_k = vals["k_step"].get("WRITE_SIZE")
+if ws_k:
+    top = max(ws_k)
+    mask = [w >= 0.5 * top for w in ws_k]
+    for c, v in list(vals["k_step"].items()):
+        if len(v) % len(mask) == 0:  # (a counter collected in several passes: the passes in order)
+            vals["k_step"][c] = [x for x, m in zip(v, mask * (len(v) // len(mask))) if m]
 
 
 def mean(k, c):

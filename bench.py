@@ -16,10 +16,10 @@ combine_set_results, rank-ordered local sum / max).  Weak scaling:
 A plan run is three kernels: k_path (per (set, gamma cell) solution paths), k_eval (per-EV
 evaluation + rows) and k_finalize (per-set reductions and any individual re-solve).  The K timed
 steps are independent runs (fresh prices each), issued by ONE lompc_plan_run_steps call in its
-stepped form: one k_step launch per step carries step k+1's path, step k's evaluation and step
-k-1's closing (the latency-bound path chain runs beside the bandwidth-bound evaluation), plus
-three launches after the last step; every step's work is done in full, the results equal the
-launch-per-kernel form bit for bit.
+wide form: the K steps' paths in one k_paths launch (thousands of independent latency-bound
+chains at once), then one k_step launch per step carrying step k's evaluation and step k-1's
+closing, plus one closing launch after the last step; every step's work is done in full inside
+the timed region, and the results equal the launch-per-kernel form bit for bit.
 
 Rank 0 prints ONE JSON line.  ``roofline`` prices the launch that carries the per-EV work
 (k_step; k_eval when the stepped form does not apply) by the evaluation's algorithmic bytes
@@ -323,8 +323,9 @@ def main():
     # the stepped form (lompc_plan_run_steps, full outputs, no communicator): the timed region's
     # events sit on its k_step launches
     stepped = batched and args.mode == "path" and runs[0]["plan"].info()["cells"] % 4 == 0
-    rkernel = ("k_step (step k+1's path + step k's evaluation + step k-1's closing)" if stepped
-               else ("k_eval" if args.mode == "path" else "k_direct"))
+    rkernel = (("k_step (step k+1's path + step k's evaluation + step k-1's closing)" if args.warm else
+                "k_step (step k's evaluation + step k-1's closing; the K steps' paths in one k_paths launch before)")
+               if stepped else ("k_eval" if args.mode == "path" else "k_direct"))
 
     total_qp = world * B * args.steps
     value = total_qp / dt
@@ -536,9 +537,9 @@ def direct_leg(eng, N, P, args, nsteps, dev, torch):
 
 def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
     """The per-iteration contracts the reference actually runs on the same batch (both EV types,
-    2P sets, fresh prices every step), each K steps in one lompc_plan_run_steps call (the stepped
-    form: one k_step launch per step carries step k+1's path, step k's evaluation — lookups and the
-    per-stage row sums, no rows stored — and step k-1's closing):
+    2P sets, fresh prices every step), each K steps in one lompc_plan_run_steps call (the wide
+    form: the K paths in one launch, then one k_step launch per step carrying step k's evaluation —
+    lookups and the per-stage row sums, no rows stored — and step k-1's closing):
 
     * ``reductions`` — PriceSolver._get_w_err (price_solver.py:196-214): only the per-set sums of
       w, the max A_bar error and the counts leave the engine (the reference drops w0, :206);

@@ -148,6 +148,9 @@ struct lompc_plan {
     int* fidx[2] = {nullptr, nullptr};
     int64_t cap_blk = 0;
     int occ = 0, occ_N = -1;      // k_step workgroups per CU (occupancy query) and its horizon
+    bool wide = false;            // the map is the wide form's (no path workgroups in its launches)
+    PathTab wt{};                 // wide form: a ring of per-run path tables, slot-major
+    int64_t cap_wt = 0;           // its capacity in cells (slots x S x G)
   } stp;
   int* d_errflag = nullptr;
   unsigned long long* d_tally = nullptr;  // [3] EVs repaired / failed / invalid over every run since

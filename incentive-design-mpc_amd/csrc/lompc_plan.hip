@@ -1329,6 +1329,39 @@ StepKernel step_kernel(int N) {
   }
 }
 
+// The wide form's path launch (lompc_plan_run_steps without warm starts): the paths of runs run0 ..
+// run0 + nruns - 1 in ONE launch, one wave per (run, set, cell) — thousands of independent
+// latency-bound chains at once instead of one run's 384 beside an evaluation; run j's prices at
+// lmbd + j lm_stride, its tables in ring slot j % slots
+template <int NT>
+__global__ __launch_bounds__(64) void k_paths(PathArgs a, int64_t lm_stride, int64_t lr_stride, int run0, int slots) {
+  const int SG = a.S * a.G;
+  const int r = (int)blockIdx.x / SG, cell = (int)blockIdx.x - r * SG;
+  const int j = run0 + r;
+  const int64_t o = (int64_t)(j % slots) * SG;
+  PathArgs b = a;
+  b.lmbd = a.lmbd + (size_t)j * lm_stride;
+  b.lmbd_r = a.lmbd_r + (size_t)j * lr_stride;
+  b.t_cnt = a.t_cnt + o;
+  b.t_lo = a.t_lo + o;
+  b.t_sl = a.t_sl + o * 64;
+  b.t_ge = a.t_ge + o * LQ_PPL;
+  b.t_cf = a.t_cf + o * LQ_PPL * 8;
+  b.t_ab = a.t_ab + o * LQ_PPL * a.N;
+  path_cell<NT, true>(b, cell);
+}
+
+typedef void (*PathsKernel)(PathArgs, int64_t, int64_t, int, int);
+PathsKernel paths_kernel(int N) {
+  switch (N) {
+    case 12: return k_paths<12>;
+    case 16: return k_paths<16>;
+    case 24: return k_paths<24>;
+    case 48: return k_paths<48>;
+    default: return k_paths<0>;
+  }
+}
+
 #include "lompc_agg.hpp"
 
 // ---------------------------------------------------------------- k_loop_iter
@@ -2030,7 +2063,8 @@ void lq_plan_free(lompc_plan* p) {
       for (void* x : zs)
         if (x) (void)hipFree(x);
     }
-    for (void* x : {(void*)z.d_map, (void*)z.sl3})
+    for (void* x : {(void*)z.d_map, (void*)z.sl3, (void*)z.wt.cnt, (void*)z.wt.lo, (void*)z.wt.ge, (void*)z.wt.cf,
+                    (void*)z.wt.ab, (void*)z.wt.sl})
       if (x) (void)hipFree(x);
     if (z.h_map) (void)hipHostFree(z.h_map);
   }
@@ -2250,7 +2284,7 @@ int lq_price_loop_host(lompc_plan* p, const lompc_price_loop_args* a, double* lm
 // The stepped form's block map, tables and records (once per prepare).  The path takes np_wg of the
 // k_step workgroup slots for the whole launch, so the evaluation blocks are sized to fill the rest once
 // (or a whole number of times for big batches).
-int stepped_setup(lompc_plan* p, hipStream_t st) {
+int stepped_setup(lompc_plan* p, hipStream_t st, bool wide) {
   auto& z = p->stp;
   const int N = p->N;
   const int64_t S = p->S, G = p->G, ncell = S * G, B = p->B;
@@ -2260,7 +2294,7 @@ int stepped_setup(lompc_plan* p, hipStream_t st) {
     z.occ = std::max(z.occ, 1);
     z.occ_N = N;
   }
-  z.np_wg = (int)((ncell + LQ_STEP_CELLS - 1) / LQ_STEP_CELLS);
+  z.np_wg = wide ? 0 : (int)((ncell + LQ_STEP_CELLS - 1) / LQ_STEP_CELLS);  // (wide: the paths have their own launch)
   const int64_t slots = (int64_t)p->n_cu * z.occ;
   const int64_t free1 = std::max<int64_t>(slots - z.np_wg, slots / 2);  // the first round, beside the path
   const int64_t rounds = std::max<int64_t>(1, (10 * B + 9ll * slots * EVAL_MAXB - 1) / (9ll * slots * EVAL_MAXB));
@@ -2317,34 +2351,67 @@ int stepped_setup(lompc_plan* p, hipStream_t st) {
     z.cap_blk = nblk;
   }
   z.ok = true;
+  z.wide = wide;
   return LOMPC_OK;
 }
 
-// K >= 1 independent runs, stepped: launch 0 = run 0's path; launch k (1 <= k <= K) = k_step(run k's
-// path (k < K), run k - 1's evaluation, run k - 2's closing (k >= 2)); launch K + 1 = run K - 1's
-// closing.  Run j uses path table j % 2, records j % 2 and cell-start working sets j % 3.  Per-EV
-// outputs: run k writes w + k ev_stride N (cost, w0, status + k ev_stride); with ev_stride = 0 every
-// run writes the same rows and only the LAST run's closing writes per-EV outputs (every earlier closing
-// shares its launch with a later run's evaluation, whose rows must win).  Set outputs of run k at the
-// per-run strides.  With a communicator, run j's closing fills send slot j % 2 and its all-gather +
-// combine follow the launch that carried it, on the same stream (one collective per run).
+#define LQ_WIDE_RUNS 32  // wide form: runs per path launch (its table ring holds one more)
+
+// K >= 1 independent runs.  Two schedules, one per plan kind:
+// * wide (no warm start — every run's path depends on its own prices only): the paths of up to
+//   LQ_WIDE_RUNS runs in ONE k_paths launch, then launch k (0 <= k <= K) = k_step(run k's evaluation
+//   (k < K), run k - 1's closing (k >= 1)), the next runs' paths launched before the first launch that
+//   needs them.  Run j's tables sit in ring slot j % (LQ_WIDE_RUNS + 1) (a slot is rewritten only after
+//   its run has closed), records j % 2.  K + 1 evaluation / closing launches + ceil(K / LQ_WIDE_RUNS)
+//   path launches.
+// * stepped (warm-started plans: run j + 1's path starts from run j's working sets): launch 0 = run
+//   0's path; launch k (1 <= k <= K) = k_step(run k's path (k < K), run k - 1's evaluation, run k - 2's
+//   closing (k >= 2)); launch K + 1 = run K - 1's closing.  Run j uses path table j % 2, records j % 2
+//   and cell-start working sets j % 3.
+// Per-EV outputs: run k writes w + k ev_stride N (cost, w0, status + k ev_stride); with ev_stride = 0
+// every run writes the same rows and only the LAST run's closing writes per-EV outputs (every earlier
+// closing shares its launch with a later run's evaluation, whose rows must win).  Set outputs of run
+// k at the per-run strides.  With a communicator, run j's closing fills send slot j % 2 and its
+// all-gather + combine follow the launch that carried it, on the same stream (one collective per run).
 // split (LOMPC_STEPS_PER_KERNEL): every launch above issued as one launch per part (path / evaluation
 // / closing), in that order — the same kernels on the same arguments without the overlap, so the same
-// bits (what the bench's verification compares).  span: one event pair from the start of launch 1's
-// dispatch to the end of launch K - 1's (hipExtLaunchKernel events), read as K - 1 launches.
+// bits (what the bench's verification compares).  span: one event pair from the start of the first
+// steady launch's dispatch (the first that carries an evaluation and a closing) to the end of the last
+// steady one of the first path group (hipExtLaunchKernel events), read as that many launches.
 int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride, const double* lmbd_r,
                          int64_t lmbd_r_stride, int n_runs, int profile_every, bool span_events, double* w, double* cost,
                          double* w0, int8_t* status, int64_t ev_stride, double* set_sum_w, int64_t sw_stride,
                          double* set_stats, int64_t st_stride, bool split, hipStream_t st) {
   auto& z = p->stp;
   int rc;
-  if (!z.ok && (rc = stepped_setup(p, st))) return rc;
+  const bool wide = (p->flags & LOMPC_PLAN_WARM_START) == 0;
+  if ((!z.ok || z.wide != wide) && (rc = stepped_setup(p, st, wide))) return rc;
   const int N = p->N;
   const int64_t ncell = p->S * p->G, L = p->S * (N + LOMPC_SET_STATS);
   const bool xr = p->comm != nullptr;
   if (xr && (rc = lq_xbufs(p, 2))) return rc;
   const int K = n_runs;
+  const int Kc = std::min(K, LQ_WIDE_RUNS), slots = LQ_WIDE_RUNS + 1;
+  if (wide && (int64_t)slots * ncell > z.cap_wt) {
+    auto& t = z.wt;
+    const int64_t c = (int64_t)slots * ncell;
+    if ((rc = grow(p, &t.cnt, c)) || (rc = grow(p, &t.lo, c)) || (rc = grow(p, &t.ge, c * LQ_PPL)) ||
+        (rc = grow(p, &t.cf, c * LQ_PPL * 8)) || (rc = grow(p, &t.ab, c * LQ_PPL * N)) || (rc = grow(p, &t.sl, c * 64)))
+      return rc;
+    z.cap_wt = c;
+  }
   auto tab = [&](int j) {
+    if (wide) {  // ring slot j % slots
+      const int64_t o = (int64_t)(j % slots) * ncell;
+      PathTab t;
+      t.cnt = z.wt.cnt + o;
+      t.lo = z.wt.lo + o;
+      t.ge = z.wt.ge + o * LQ_PPL;
+      t.cf = z.wt.cf + o * LQ_PPL * 8;
+      t.ab = z.wt.ab + o * LQ_PPL * N;
+      t.sl = z.wt.sl + o * 64;
+      return t;
+    }
     PathTab t = z.tab[j & 1];
     t.sl = z.sl3 + (size_t)(j % 3) * ncell * 64;
     return t;
@@ -2377,8 +2444,12 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   const int cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
   const size_t lds = eval_lds(N, p->G, cap);
   const StepKernel kern = step_kernel(N);
+  // the steady launches: stepped 1 .. K - 1 (path + evaluation + closing); wide 1 .. Kc - 1
+  // (evaluation + closing, no path launch between them)
+  const int s_first = 1, s_last = wide ? Kc - 1 : K - 1;
   hipEvent_t span0 = nullptr, span1 = nullptr;
-  if (span_events && K >= 2 && plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &span0, &span1)) return fail_arg(p, "profiling events");
+  if (span_events && s_last >= s_first && plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &span0, &span1))
+    return fail_arg(p, "profiling events");
   // one k_step launch of (npw path, ne evaluation, nf closing workgroups); prof: its own event pair
   auto launch = [&](const PathArgs& pa, const EvalArgs& ea, const FinalArgs& ff, int npw, int ne, int nf, bool prof,
                     hipEvent_t s0, hipEvent_t s1) -> int {
@@ -2391,19 +2462,47 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     if (prof) plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1);
     return LOMPC_OK;
   };
-  for (int k = 0; k <= K + 1; ++k) {
-    const PathArgs pa = k < K ? path_args(p, lm(k), lr(k), tab(k)) : PathArgs{};
-    const int npw = k < K ? z.np_wg : 0;
+  int paths_to = 0;  // wide: runs whose paths are launched
+  const int last = wide ? K : K + 1;
+  for (int k = 0; k <= last; ++k) {
+    PathArgs pa{};
+    int npw = 0;
     EvalArgs ea{}, unused_e;
     FinalArgs ff{}, unused_f;
     int ne = 0, nf = 0;
-    if (k >= 1 && k - 1 < K) {
-      args(k - 1, ea, unused_f);
-      ne = z.nblk;
-    }
-    if (k >= 2) {
-      args(k - 2, unused_e, ff);
-      nf = (int)p->S;
+    if (wide) {
+      if (k < K && k >= paths_to) {  // the next group's paths, one launch
+        const int n = std::min(LQ_WIDE_RUNS, K - k);
+        PathArgs pw = path_args(p, lmbd, lmbd_r, z.wt);
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
+        hipExtLaunchKernelGGL(paths_kernel(N), dim3((unsigned)(n * ncell)), dim3(64), 0, st, e0, e1, 0, pw, lmbd_stride,
+                              lmbd_r_stride, k, slots);
+        HIPCHK(p, hipGetLastError());
+        plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
+        paths_to = k + n;
+      }
+      if (k < K) {
+        args(k, ea, unused_f);
+        ne = z.nblk;
+      }
+      if (k >= 1) {
+        args(k - 1, unused_e, ff);
+        nf = (int)p->S;
+      }
+    } else {
+      if (k < K) {
+        pa = path_args(p, lm(k), lr(k), tab(k));
+        npw = z.np_wg;
+      }
+      if (k >= 1 && k - 1 < K) {
+        args(k - 1, ea, unused_f);
+        ne = z.nblk;
+      }
+      if (k >= 2) {
+        args(k - 2, unused_e, ff);
+        nf = (int)p->S;
+      }
     }
     int npw_l = npw;
 #ifdef LQ_STEP_DIAG
@@ -2414,10 +2513,10 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
       if (LQ_STEP_DIAG == 2) ne = nf = 0;
     }
 #endif
-    // the full k_step launches (1 .. K - 1) carry the events: sampled, or one pair around all of them
-    const bool steady = k >= 1 && k < K;
+    // the steady launches carry the events: sampled, or one pair around all of them
+    const bool steady = k >= s_first && k <= s_last;
     const bool prof = !span_events && steady && (profile_every <= 0 || (k - 1) % profile_every == 0);
-    const hipEvent_t s0 = (span0 && k == 1) ? span0 : nullptr, s1 = (span0 && k == K - 1) ? span1 : nullptr;
+    const hipEvent_t s0 = (span0 && k == s_first) ? span0 : nullptr, s1 = (span0 && k == s_last) ? span1 : nullptr;
     if (split) {  // the same parts, one launch each (no overlap)
       if ((rc = launch(pa, ea, ff, npw_l, 0, 0, false, nullptr, nullptr)) ||
           (rc = launch(pa, ea, ff, 0, ne, 0, prof, s0, s1)) || (rc = launch(pa, ea, ff, 0, 0, nf, false, nullptr, nullptr)))
@@ -2425,8 +2524,9 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     } else if ((rc = launch(pa, ea, ff, npw_l, ne, nf, prof, s0, s1))) {
       return rc;
     }
-    if (s1) plan_prof_end(p, LOMPC_PLAN_K_EVAL, span0, span1, K - 1);
-    if (xr && nf && (rc = lq_exchange(p, xsend(k - 2), sw_of(k - 2), st_of(k - 2), st))) return rc;
+    if (s1) plan_prof_end(p, LOMPC_PLAN_K_EVAL, span0, span1, s_last - s_first + 1);
+    const int closed = wide ? k - 1 : k - 2;  // the run closed by this launch
+    if (xr && nf && (rc = lq_exchange(p, xsend(closed), sw_of(closed), st_of(closed), st))) return rc;
   }
   return LOMPC_OK;
 }

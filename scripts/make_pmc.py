@@ -20,7 +20,7 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc.json"
 qp = float(sys.argv[3]) if len(sys.argv) > 3 else 262144.0
 N = int(sys.argv[4]) if len(sys.argv) > 4 else 24
-KERNELS = ("k_step", "k_path", "k_eval", "k_finalize")
+KERNELS = ("k_step", "k_paths", "k_path", "k_eval", "k_finalize")
 vals = {k: collections.defaultdict(list) for k in KERNELS}
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):

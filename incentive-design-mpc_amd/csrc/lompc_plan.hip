@@ -2355,7 +2355,8 @@ int stepped_setup(lompc_plan* p, hipStream_t st, bool wide) {
   return LOMPC_OK;
 }
 
-#define LQ_WIDE_RUNS 32  // wide form: runs per path launch (its table ring holds one more)
+#define LQ_WIDE_RUNS 32                 // wide form: runs per path launch (its table ring holds one more)
+#define LQ_WIDE_BYTES (1ll << 30)        // wide form: the table ring's memory at most
 
 // K >= 1 independent runs.  Two schedules, one per plan kind:
 // * wide (no warm start — every run's path depends on its own prices only): the paths of up to
@@ -2384,17 +2385,25 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
                          double* set_stats, int64_t st_stride, bool split, hipStream_t st) {
   auto& z = p->stp;
   int rc;
-  const bool wide = (p->flags & LOMPC_PLAN_WARM_START) == 0;
-  if ((!z.ok || z.wide != wide) && (rc = stepped_setup(p, st, wide))) return rc;
   const int N = p->N;
   const int64_t ncell = p->S * p->G, L = p->S * (N + LOMPC_SET_STATS);
+  const int K = n_runs;
+  // wide: runs per path launch, bounded by the table ring's memory (LQ_WIDE_BYTES) and the grid; a
+  // plan too big for two table slots takes the stepped form
+  const int64_t cell_bytes = LQ_PPL * (16 * (int64_t)N + 8 * 8 + 8) + 4 + 8 + 64;
+  const int64_t fit = std::min<int64_t>(LQ_WIDE_BYTES / (ncell * cell_bytes), INT32_MAX / 64 / ncell) - 1;
+  const int Kc = (int)std::min<int64_t>({(int64_t)K, LQ_WIDE_RUNS, fit});
+  const bool wide = (p->flags & LOMPC_PLAN_WARM_START) == 0 && Kc >= 1;
+  const int slots = Kc + 1;
+  if ((!z.ok || z.wide != wide) && (rc = stepped_setup(p, st, wide))) return rc;
   const bool xr = p->comm != nullptr;
   if (xr && (rc = lq_xbufs(p, 2))) return rc;
-  const int K = n_runs;
-  const int Kc = std::min(K, LQ_WIDE_RUNS), slots = LQ_WIDE_RUNS + 1;
-  if (wide && (int64_t)slots * ncell > z.cap_wt) {
+  // (the ring sized for the largest group the plan allows, whatever this call's K: a later call with
+  // more runs must not reallocate — hipMalloc / hipFree synchronise the device)
+  const int64_t ring = (std::min<int64_t>(LQ_WIDE_RUNS, fit) + 1) * ncell;
+  if (wide && ring > z.cap_wt) {
     auto& t = z.wt;
-    const int64_t c = (int64_t)slots * ncell;
+    const int64_t c = ring;
     if ((rc = grow(p, &t.cnt, c)) || (rc = grow(p, &t.lo, c)) || (rc = grow(p, &t.ge, c * LQ_PPL)) ||
         (rc = grow(p, &t.cf, c * LQ_PPL * 8)) || (rc = grow(p, &t.ab, c * LQ_PPL * N)) || (rc = grow(p, &t.sl, c * 64)))
       return rc;
@@ -2444,8 +2453,8 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   const int cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
   const size_t lds = eval_lds(N, p->G, cap);
   const StepKernel kern = step_kernel(N);
-  // the steady launches: stepped 1 .. K - 1 (path + evaluation + closing); wide 1 .. Kc - 1
-  // (evaluation + closing, no path launch between them)
+  // the steady launches 1 .. K - 1 (stepped: path + evaluation + closing; wide: evaluation +
+  // closing); the span events cover 1 .. s_last, wide: the first path group's (no path launch inside)
   const int s_first = 1, s_last = wide ? Kc - 1 : K - 1;
   hipEvent_t span0 = nullptr, span1 = nullptr;
   if (span_events && s_last >= s_first && plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &span0, &span1))
@@ -2472,7 +2481,7 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     int ne = 0, nf = 0;
     if (wide) {
       if (k < K && k >= paths_to) {  // the next group's paths, one launch
-        const int n = std::min(LQ_WIDE_RUNS, K - k);
+        const int n = std::min(Kc, K - k);
         PathArgs pw = path_args(p, lmbd, lmbd_r, z.wt);
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
@@ -2514,7 +2523,7 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     }
 #endif
     // the steady launches carry the events: sampled, or one pair around all of them
-    const bool steady = k >= s_first && k <= s_last;
+    const bool steady = k >= 1 && k <= K - 1;
     const bool prof = !span_events && steady && (profile_every <= 0 || (k - 1) % profile_every == 0);
     const hipEvent_t s0 = (span0 && k == s_first) ? span0 : nullptr, s1 = (span0 && k == s_last) ? span1 : nullptr;
     if (split) {  // the same parts, one launch each (no overlap)

@@ -845,9 +845,18 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
   std::vector<double> dz_a(n), dsg_a(mg), dlg_a(mg), dllo_a(n), dlhi_a(n);
   std::vector<double> rclo(n), rchi(n), rcg(mg);
   int it = 0, status = LOMPC_ERR_NOT_CONVERGED;
-  const bool trace = getenv("LOMPC_BIMPC_TRACE") != nullptr;
-  // LOMPC_BIMPC_PROF: wall time of the phases on stderr (diagnostics)
-  const bool tprof = getenv("LOMPC_BIMPC_PROF") != nullptr;
+  // diagnostic builds only (-DLQ_BIMPC_TRACE / -DLQ_BIMPC_PROF): the iterations / the phases' wall
+  // times on stderr
+#ifdef LQ_BIMPC_TRACE
+  constexpr bool trace = true;
+#else
+  constexpr bool trace = false;
+#endif
+#ifdef LQ_BIMPC_PROF
+  constexpr bool tprof = true;
+#else
+  constexpr bool tprof = false;
+#endif
   auto now = []() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   double t_fac = 0.0, t_dir = 0.0, t_pol = 0.0, t_res = 0.0;
   const double t_all = tprof ? now() : 0.0;

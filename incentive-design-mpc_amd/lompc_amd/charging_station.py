@@ -25,7 +25,6 @@ redundantly on identical inputs; the re-draw replays the global random stream.
 from __future__ import annotations
 
 import concurrent.futures
-import os
 import time
 
 from dataclasses import dataclass
@@ -150,6 +149,9 @@ class ChargingStation:
         self._pool = None  # one worker thread: the large-EV price chain beside the small one
         self._stage_pool = None  # two worker threads: the partition plans staged beside the BiMPC solve
         self.profile_phases = False  # accumulate per-phase wall times of _step in phase_ms (synchronising)
+        # every partition's loop plan of a step prepared beside the BiMPC solve (False: each partition's
+        # plan prepared when its loop starts — for A/B timing)
+        self.stage_partitions = True
         self.phase_ms = {}
         self.device = torch.cuda.current_device() if device is None else int(device)
         self._dev = f"cuda:{self.device}"
@@ -329,7 +331,7 @@ class ChargingStation:
                 assert st_l[p, 2] >= 0 and st_l[p, 1] <= self.consts_l.y_max
                 beta_l[p], gamma_lm[p] = self._robustness(self.price_solver_l, st_l[p], lmbd_r)
         self._pstats = (st_s, st_l)
-        self._staged = os.environ.get("LOMPC_STAGE_PARTITIONS", "1") != "0"  # (0: diagnostics / A-B)
+        self._staged = self.stage_partitions
         staging = self._stage_partitions() if self._staged else []
         Mp_s_ = Mp_s / self.B
         Mp_l_ = Mp_l / self.B

@@ -30,7 +30,6 @@ from __future__ import annotations
 
 import ctypes
 import functools
-import os
 import time
 
 import numpy as np
@@ -111,8 +110,8 @@ class PriceSolver:
         self.native_loop = True  # the price loop in C++ (lompc_price_loop) whenever the plan allows it
         self.profile_loops = False  # accumulate the native loop's per-part times in loop_prof
         # the convergence test and the price QP on the GPU after every engine call, no host round trip
-        # per iteration (lompc_loop.hip); LOMPC_HOST_LOOP=1: the host form (one copy + sync per iteration)
-        self.device_loop = os.environ.get("LOMPC_HOST_LOOP", "0") != "1"
+        # per iteration (lompc_loop.hip); False: the host form (one copy + sync per iteration)
+        self.device_loop = True
         if self.group is not None:
             import torch.distributed as dist
 

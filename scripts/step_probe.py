@@ -74,6 +74,15 @@ for libname in args.libs:
         plan.check()
         alone = {k: plan.profile(read=True, kernel=k) for k in ("k_path", "k_eval", "k_finalize")}
         plan.profile(enable=False)
+        # host cost of the call itself (Python wrapper + C-ABI entry, no launch: n_runs = 0) — GPU idle
+        # time at the start of a timed call
+        outs = {k: torch.empty((0,) + tuple(plan.out[k].shape), dtype=torch.float64, device="cuda")
+                for k in ("set_sum_w", "set_stats")}
+        t0 = time.perf_counter()
+        for _ in range(200):
+            plan.run_steps(lm, lr, 0, lm[0].numel(), lr[0].numel(), out=outs)
+        wrap_us = (time.perf_counter() - t0) / 200 * 1e6
+        print(f"   run_steps call overhead (n_runs = 0, out given): {wrap_us:6.1f} us", flush=True)
         print(f"{libname} cells {plan.cells} {args.outputs}: per step {np.median(walls):6.2f} us (min {min(walls):6.2f})"
               f"  k_step {np.median(ks):6.2f} us  alone: " +
               "  ".join(f"{k} {ms / max(n, 1) * 1e3:6.2f}" for k, (ms, n) in alone.items()), flush=True)

@@ -1333,8 +1333,12 @@ StepKernel step_kernel(int N) {
 // run0 + nruns - 1 in ONE launch, one wave per (run, set, cell) — thousands of independent
 // latency-bound chains at once instead of one run's 384 beside an evaluation; run j's prices at
 // lmbd + j lm_stride, its tables in ring slot j % slots
+#ifndef LQ_PATHS_WAVES
+#define LQ_PATHS_WAVES 1  // k_paths: min waves per SIMD the compiler must fit (registers)
+#endif
 template <int NT>
-__global__ __launch_bounds__(64) void k_paths(PathArgs a, int64_t lm_stride, int64_t lr_stride, int run0, int slots) {
+__global__ __launch_bounds__(64, LQ_PATHS_WAVES) void k_paths(PathArgs a, int64_t lm_stride, int64_t lr_stride, int run0,
+                                                               int slots) {
   const int SG = a.S * a.G;
   const int r = (int)blockIdx.x / SG, cell = (int)blockIdx.x - r * SG;
   const int j = run0 + r;

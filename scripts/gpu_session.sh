@@ -2,7 +2,7 @@
 # One GPU-box session: smoke -> gpu tests -> bench -> rocprofv3 kernel trace.
 # Stops at the first step that faults / aborts / times out (rc not in {0,1}).
 # usage: bash scripts/gpu_session.sh [steps...]   (default: smoke tests bench prof)
-# (no LOMPC_* run-time knobs exist in the product library: variants are -D builds, scripts/variants.sh)
+# (no LOMPC_* run-time knobs exist in the product library: variants are -D builds, scripts/build_variant.py)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out

@@ -465,16 +465,19 @@ class ChargingStation:
         creates its plans' device communicators in the same order)."""
         torch = _torch()
         st_s, st_l = self._pstats
+        main = torch.cuda.current_stream(self.device)
         jobs = []
         for kind, solver, y, idx, st in (("Small", self.price_solver_s, self.y_s, self.idx_s, st_s),
                                          ("Large", self.price_solver_l, self.y_l, self.idx_l, st_l)):
-            ys, off = self._partition_layout(kind, y, idx)  # (host sync: on this thread)
-            solver._stream.wait_stream(torch.cuda.current_stream(self.device))
-            jobs.append((solver, ys, off, st))
+            solver._stream.wait_stream(main)  # (the state the layout sorts is the main stream's)
+            jobs.append((kind, solver, y, idx, st))
 
         def stage(job):
-            solver, ys, off, st = job
+            kind, solver, y, idx, st = job
             with torch.cuda.device(self.device), torch.cuda.stream(solver._stream):
+                # the type's partition layout too (its sorts and one host sync: on this thread, beside
+                # the interior point, not before it); its tensors are read on the main stream later
+                ys, off = self._partition_layout(kind, y, idx, main)
                 for p in range(self.P):
                     if st[p, 0] > 0:
                         solver.stage_partition(p, ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3],
@@ -488,7 +491,7 @@ class ChargingStation:
             self._stage_pool = concurrent.futures.ThreadPoolExecutor(max_workers=2)
         return [self._stage_pool.submit(stage, job) for job in jobs]
 
-    def _partition_layout(self, kind, y, idx):
+    def _partition_layout(self, kind, y, idx, reader=None):
         """This rank's EVs of one type grouped by partition, each partition in descending charge
         level (ascending gamma = y_max - y: the price loops' plans aggregate per certified piece,
         LOMPC_PLAN_SORTED_GAMMA), once per step: (charge levels in that order, host offsets
@@ -502,7 +505,11 @@ class ChargingStation:
             perm = by_y[torch.argsort(idx[by_y], stable=True)]
             counts = torch.bincount(idx, minlength=self.P)[: self.P].cpu().numpy()
             off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
-            self._layout[kind] = (perm, off, y[perm])
+            ys = y[perm]
+            if reader is not None:  # (made on another stream: the allocator keeps them until `reader` is done)
+                perm.record_stream(reader)
+                ys.record_stream(reader)
+            self._layout[kind] = (perm, off, ys)
         perm, off, ys = self._layout[kind]
         return ys, off
 

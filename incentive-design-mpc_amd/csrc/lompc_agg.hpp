@@ -102,33 +102,56 @@ __global__ __launch_bounds__(256) void k_sorted_sum(SortArgs a) {
 }
 
 // (2) per set (one workgroup): exclusive scan of the block totals (written back in place as
-// offsets), the set's valid count and order flag; an empty index for a set without valid EVs
+// offsets), the set's valid count and order flag; an empty index for a set without valid EVs.
+// 256 blocks per pass, a workgroup-wide scan each (integer sums: exact, so the same values as a
+// sequential scan in any order)
 __global__ __launch_bounds__(256) void k_sorted_scan(SortArgs a) {
-  __shared__ int s_nv;
-  const int s = blockIdx.x;
+  __shared__ unsigned long long sh[4][256];
+  __shared__ unsigned long long carry[4];  // sum x, sum hi(x^2), sum lo(x^2), valid count so far
+  __shared__ int s_bad, s_nv;
+  const int s = blockIdx.x, t = threadIdx.x;
   const int b0 = a.sblk_prefix[s], b1 = a.sblk_prefix[s + 1];
-  if (threadIdx.x == 0) {  // (a few thousand blocks at most: one thread, in order)
-    unsigned long long c[3] = {0, 0, 0}, nv = 0, bad = 0;
-    for (int b = b0; b < b1; ++b) {
-      unsigned long long* r = a.bsum + (size_t)b * 4;
-      const unsigned long long v[4] = {r[0], r[1], r[2], r[3]};
-      r[0] = c[0];
-      r[1] = c[1];
-      r[2] = c[2];
-      r[3] = nv;
-      c[0] += v[0];
-      c[1] += v[1];
-      c[2] += v[2];
-      nv += v[3] & 0xffffffffull;
-      bad |= v[3] >> 32;
+  if (t < 4) carry[t] = 0;
+  if (t == 0) s_bad = 0;
+  __syncthreads();
+  for (int base = b0; base < b1; base += 256) {
+    const int b = base + t;
+    unsigned long long* r = a.bsum + (size_t)b * 4;
+    unsigned long long x[4] = {0, 0, 0, 0};
+    if (b < b1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[k] = r[k];
+      if (x[3] >> 32) s_bad = 1;  // (every writer stores the same value)
+      x[3] &= 0xffffffffull;
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sh[k][t] = x[k];
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // inclusive scan, Hillis-Steele
+      unsigned long long y[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) y[k] = t >= o ? sh[k][t - o] : 0ull;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sh[k][t] += y[k];
+      __syncthreads();
+    }
+    if (b < b1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = carry[k] + sh[k][t] - x[k];  // exclusive offsets
+    }
+    __syncthreads();
+    if (t < 4) carry[t] += sh[t][255];
+    __syncthreads();
+  }
+  if (t == 0) {
     // the set's totals at position n (valid EVs are the first nv positions)
     const size_t e = (size_t)(a.set_off[s + 1] + s);
-    a.P[e] = c[0];
-    a.P[a.PB + e] = c[1];
-    a.P[2 * a.PB + e] = c[2];
-    a.sinfo[s] = make_int4((int)nv, bad ? 0 : 1, 0, 0);
-    s_nv = (int)nv;
+    a.P[e] = carry[0];
+    a.P[a.PB + e] = carry[1];
+    a.P[2 * a.PB + e] = carry[2];
+    a.sinfo[s] = make_int4((int)carry[3], s_bad ? 0 : 1, 0, 0);
+    s_nv = (int)carry[3];
   }
   __syncthreads();
   if (s_nv == 0) {

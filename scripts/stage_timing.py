@@ -1,0 +1,72 @@
+"""Diagnostic: host time of one partition's plan staging (PriceSolver.stage_partition) at config 5.
+
+    python scripts/stage_timing.py     # on the GPU box
+
+Builds the config-5 station (bench.py's station leg), runs two closed-loop steps, then stages every
+partition of the large type again on the main thread, timing each call and its parts (levels,
+gamma copy, plan update) with the stream synchronised around each part.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "incentive-design-mpc_amd"))
+import torch  # noqa: E402
+
+from lompc_amd import settings  # noqa: E402
+from lompc_amd.charging_station import ChargingStation  # noqa: E402
+from lompc_amd.example import DEMAND_SCALE, NUM_EVS_PER_EV_TYPE, station_consts  # noqa: E402
+
+settings.PRINT_LEVEL = 0
+M_2, N, P = 1048576, 48, 12
+consts = station_consts(8, M_2, n_lo=N, n_bi=N, partitions=P, price_type="linear-convex",
+                        demand_scale=DEMAND_SCALE * M_2 / NUM_EVS_PER_EV_TYPE, u_b_max=0.5, x_max=0.5)
+np.random.seed(0)
+st = ChargingStation(consts, device=0)
+for _ in range(2):
+    st._step()
+torch.cuda.synchronize()
+sol = st.price_solver_l
+ys, off = st._partition_layout("Large", st.y_l, st.idx_l)
+stl = st._pstats[1]
+t_tot = []
+for rep in range(3):
+    for p in range(P):
+        if stl[p, 0] <= 0:
+            continue
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(sol._stream):
+            sol.stage_partition(p, ys[off[p]:off[p + 1]], stl[p, 0], stl[p, 1], stl[p, 2], stl[p, 3], descending=True)
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        t_tot.append(((t1 - t0) * 1e6, (t2 - t0) * 1e6))
+a = np.array(t_tot)
+print(f"stage_partition: host {a[:, 0].mean():7.1f} us (median {np.median(a[:, 0]):7.1f}), "
+      f"with the GPU work {a[:, 1].mean():7.1f} us, over {len(a)} calls")
+# the parts of one call, host time each (no sync between them)
+p = int(np.argmax(stl[:, 0]))
+y0 = ys[off[p]:off[p + 1]]
+parts = {}
+for rep in range(20):
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sol._stream):
+        t0 = time.perf_counter()
+        g = sol.consts.y_max - y0
+        t1 = time.perf_counter()
+        B = int(g.numel())
+        gam = torch.empty(B + 1, dtype=torch.float64, device=g.device)
+        gam[:B] = g
+        gam[B] = 0.5
+        t2 = time.perf_counter()
+        sol.use_partition(p)
+        sol._plan.update(sol._gam, np.array([0, B, B + 1], dtype=np.int64), w_ref=sol._wr2, validate=False)
+        t3 = time.perf_counter()
+    for k, v in (("y_max - y0", t1 - t0), ("gamma buffer", t2 - t1), ("plan.update", t3 - t2)):
+        parts.setdefault(k, []).append(v * 1e6)
+torch.cuda.synchronize()
+print("   parts (host us, median): " + ", ".join(f"{k} {np.median(v):.1f}" for k, v in parts.items()))

@@ -515,7 +515,8 @@ class ChargingStation:
 
     def _w0_batched(self, kind, solver: PriceSolver, y, idx, prices, lmbd_r):
         """All partitions of one EV type in ONE engine call (price_solver.py:272-285 per partition).
-        Returns (w0 in EV order, per-partition (sum w0, sum price0, count) combined over ranks)."""
+        Returns (w0 in EV order, the device rows per partition (sum w0, sum price0, count, failed,
+        invalid) combined over ranks — `_w0_checked` reads and checks them)."""
         torch = _torch()
         N, P = self.N_lo, self.P
         ys, off = self._partition_layout(kind, y, idx)
@@ -536,17 +537,22 @@ class ChargingStation:
             dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
         w0 = torch.empty_like(y)
         w0[perm] = res["w0"]
+        return w0, red  # (red on the device: both types' engine calls are issued before one host sync)
+
+    @staticmethod
+    def _w0_checked(red) -> np.ndarray:
         red = red.cpu().numpy()
         if np.any(red[:, 4] > 0):
             raise AssertionError("gamma outside [0, y_max]")
         if np.any(red[:, 3] > 0):
             raise SolverError("LoMPC QPs without a certified optimum")
-        return w0, red[:, :3]
+        return red[:, :3]
 
     def _get_w0_price0(self, prices_s, prices_l, lmbd_r: float):
         # charging_station.py:310-329
         w0_s, red_s = self._w0_batched("Small", self.price_solver_s, self.y_s, self.idx_s, prices_s, lmbd_r)
         w0_l, red_l = self._w0_batched("Large", self.price_solver_l, self.y_l, self.idx_l, prices_l, lmbd_r)
+        red_s, red_l = self._w0_checked(red_s), self._w0_checked(red_l)
         price0_s, price0_l = np.zeros((self.P,)), np.zeros((self.P,))
         for p in range(self.P):
             if red_s[p, 2] > 0:

@@ -566,16 +566,33 @@ class ChargingStation:
         # charging_station.py:331-370
         torch = _torch()
         residual_charge = 0
-        self.y_s += w0_s
         thr_s = MIN_FULL_CHARGE_FRACTION * self.consts_s.y_max
-        mask_s = self.y_s > thr_s
-        residual_charge += self.consts_s.theta * self._global_sum(torch.where(mask_s, self.y_s - thr_s, 0.0))
-        self.ncharged_s += redraw_full(self.y_s, mask_s, self.y0_min, self.y0_max, np.random.random, self.group)
-        self.y_l += w0_l
         thr_l = MIN_FULL_CHARGE_FRACTION * self.consts_l.y_max
-        mask_l = self.y_l > thr_l
-        residual_charge += self.consts_l.theta * self._global_sum(torch.where(mask_l, self.y_l - thr_l, 0.0))
-        self.ncharged_l += redraw_full(self.y_l, mask_l, self.y0_min, self.y0_max, np.random.random, self.group)
+        if self.group is None:
+            # both types' residual sums and full counts in ONE host sync; the redraws then fill the
+            # full EVs in index order (masked_scatter_: no further sync), small type's draws first
+            self.y_s += w0_s
+            self.y_l += w0_l
+            mask_s, mask_l = self.y_s > thr_s, self.y_l > thr_l
+            h = torch.stack([torch.where(mask_s, self.y_s - thr_s, 0.0).sum(), torch.where(mask_l, self.y_l - thr_l, 0.0).sum(),
+                             mask_s.sum().to(torch.float64), mask_l.sum().to(torch.float64)]).cpu().numpy()
+            residual_charge += self.consts_s.theta * float(h[0])
+            for y, mask, n in ((self.y_s, mask_s, int(h[2])), (self.y_l, mask_l, int(h[3]))):
+                if n:
+                    draws = self.y0_min + (self.y0_max - self.y0_min) * np.random.random((n,))
+                    y.masked_scatter_(mask, torch.as_tensor(draws, dtype=torch.float64, device=y.device))
+            self.ncharged_s += int(h[2])
+            self.ncharged_l += int(h[3])
+            residual_charge += self.consts_l.theta * float(h[1])
+        else:
+            self.y_s += w0_s
+            mask_s = self.y_s > thr_s
+            residual_charge += self.consts_s.theta * self._global_sum(torch.where(mask_s, self.y_s - thr_s, 0.0))
+            self.ncharged_s += redraw_full(self.y_s, mask_s, self.y0_min, self.y0_max, np.random.random, self.group)
+            self.y_l += w0_l
+            mask_l = self.y_l > thr_l
+            residual_charge += self.consts_l.theta * self._global_sum(torch.where(mask_l, self.y_l - thr_l, 0.0))
+            self.ncharged_l += redraw_full(self.y_l, mask_l, self.y0_min, self.y0_max, np.random.random, self.group)
         self._update_indices()
         if not ADD_RESIDUAL_CHARGE_TO_BATTERY:
             residual_charge = 0

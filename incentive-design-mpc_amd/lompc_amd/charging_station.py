@@ -214,15 +214,23 @@ class ChargingStation:
         self.ncharged_s = 0
         self.ncharged_l = 0
         n = self._hi - self._lo
+        self._bounds = {}
         self.idx_s = torch.zeros((n,), dtype=torch.int64, device=self._dev)
         self.idx_l = torch.zeros((n,), dtype=torch.int64, device=self._dev)
         self._update_indices()
 
     def _update_indices(self) -> None:
-        # charging_station.py:111-116 (later partitions win on shared edges, as there)
-        for p in range(self.P):  # masked_fill_: no host sync (boolean-index assignment would)
-            self.idx_s.masked_fill_((self.y_s >= self.y0_s_rng[p]) & (self.y_s <= self.y0_s_rng[p + 1]), p)
-            self.idx_l.masked_fill_((self.y_l >= self.y0_l_rng[p]) & (self.y_l <= self.y0_l_rng[p + 1]), p)
+        # charging_station.py:111-116: partition p takes the EVs with rng[p] <= y <= rng[p+1], later
+        # partitions winning on shared edges, EVs outside [rng[0], rng[P]] keeping their index.  The
+        # boundaries increase, so that is the last boundary <= y (one searchsorted, clamped for
+        # y == rng[P]); no host sync, a fixed handful of launches instead of four per partition
+        torch = _torch()
+        for idx, y, rng in ((self.idx_s, self.y_s, self.y0_s_rng), (self.idx_l, self.y_l, self.y0_l_rng)):
+            b = self._bounds.get(id(rng))
+            if b is None:  # the boundaries on the device once (a per-call copy would sync)
+                b = self._bounds[id(rng)] = torch.as_tensor(rng, dtype=y.dtype, device=y.device)
+            p = (torch.searchsorted(b, y, right=True) - 1).clamp_(0, self.P - 1)
+            idx.copy_(torch.where((y >= b[0]) & (y <= b[-1]), p, idx))
         self._layout = {}
 
     def _init_logs(self, consts: ChargingStationConstants) -> None:

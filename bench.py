@@ -390,6 +390,8 @@ def main():
         "verified_steps": verified["steps"] if verified else 0,
         "verification": verified or "per-step issue: no per-step records kept",
     }
+    if sharded:
+        line["collective"] = collective_cost(runs, args, world, dev, torch, dist, comm, batched, dt)
     pmc = load_pmc(args, N, qp_per_launch)
     pk = "k_step" if stepped else "k_eval"
     if pmc and pk in pmc and "hbm_bytes_per_launch" in pmc[pk]:
@@ -406,6 +408,8 @@ def main():
                 line["kernels"]["k_step"]["pmc"] = {x: pmc["k_step"][x] for x in pmc["k_step"] if x != "hbm_bytes_per_launch"}
     if path and world == 1 and not multi and not args.no_contracts:
         line["contracts"] = contract_legs(eng, runs[0], N, P, args, nsteps, dev, torch, comm, pmc)
+        if batched and comm is None:
+            line["contracts"]["sequential"] = sequential_leg(runs[0], eng, N, P, args, torch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(eng, N, args.cpu_seconds, args.seed)
         if path:
@@ -445,6 +449,73 @@ def verify_steps(run, args, outs_t, outs_v, torch):
     return {"steps": sum(ok), "how": "every timed step's set reductions and the last step's w / cost re-run through "
                                      "lompc_plan_run_steps(LOMPC_STEPS_PER_KERNEL) after the timed region: bitwise equal",
             "counts_ok": bool((st[:, :, 0].sum(dim=1) == plan.B).all()) if st is not None else None}
+
+
+def collective_cost(runs, args, world, dev, torch, dist, comm, batched, dt):
+    """The per-step cost of the cross-rank exchange, so a scaling run is attributable: the same K
+    timed steps again WITHOUT the exchange (RCCL: the plan's communicator detached, so no all-gather /
+    combine kernel; gloo: no torch.distributed combine), max over ranks; collective_us_per_step =
+    timed step - that step.  Also the exchange alone (RCCL: K all-gathers of the packed set records
+    through torch.distributed on the same communicator size; gloo: K combine_set_results calls)."""
+    from lompc_amd.dist import combine_set_results
+
+    K = args.steps
+    r = runs[0]
+
+    def timed(fn):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t = time.perf_counter() - t0
+        if world > 1:
+            x = torch.tensor([t], dtype=torch.float64, device=dev)
+            dist.all_reduce(x, op=dist.ReduceOp.MAX)
+            t = float(x.item())
+        return t
+
+    if comm is not None and batched:
+        plan = r["plan"]
+        plan.set_comm(None)
+        try:
+            plan.run_steps(r["lm_ptr"][args.warmup], r["lr_ptr"], K, r["lm_stride"], 0)
+            t_no = timed(lambda: plan.run_steps(r["lm_ptr"][args.warmup], r["lr_ptr"], K, r["lm_stride"], 0))
+        finally:
+            plan.set_comm(comm)
+        S, N = plan.S, plan.N
+        rec = torch.zeros(S * (N + 8), dtype=torch.float64, device=dev)
+        recv = torch.empty(world * rec.numel(), dtype=torch.float64, device=dev)
+
+        def gathers():
+            for _ in range(K):
+                dist.all_gather_into_tensor(recv, rec)
+
+        gathers()
+        t_ag = timed(gathers)
+        how = "RCCL all-gather of the packed set records + the k_combine kernel, inside each step's run"
+    else:
+        outs = [(x["plan"].out["set_sum_w"], x["plan"].out["set_stats"]) for x in runs]
+
+        def without():
+            for k in range(args.warmup, args.warmup + K):
+                for x in runs:
+                    x["plan"].run(x["lm_ptr"][k], x["lr_ptr"])
+
+        def combines():
+            for _ in range(K):
+                combine_set_results(outs)
+
+        without()
+        t_no = timed(without)
+        t_ag = timed(combines)
+        how = f"torch.distributed ({args.dist_backend}) all-gather + host-ordered combine after each step's run"
+    return {"how": how, "steps": K, "ms_per_step_with": dt / K * 1e3, "ms_per_step_without": t_no / K * 1e3,
+            "collective_us_per_step": (dt - t_no) / K * 1e6, "exchange_alone_us_per_step": t_ag / K * 1e6,
+            "ranks": world}
 
 
 def load_pmc(args, N, qp_per_launch):
@@ -581,10 +652,83 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
                      "repaired_qps": rep, "k_step_avg_us": ev_us, "k_step_launches_timed": n_e,
                      "roofline": {"bound": "hbm", "kernel": "k_step", "bytes_per_qp": bpq,
                                   "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-                                  "note": "latency-bound: the path chain of the launch, not bytes, sets its time"}}
+                                  "note": ("the evaluation + closing launch of the wide form (the K paths run in "
+                                           "one k_paths launch before, not in this duration): latency-bound, its "
+                                           "staging and lookup rounds, not 8-16 B per QP, set its time")}}
         plan.profile(enable=False)
         del plan
     return out
+
+
+def sequential_leg(run, eng, N, P, args, torch):
+    """The reference's call pattern at config 3: K DEPENDENT steps, step k+1's prices computed on the
+    device from step k's set reductions (lompc_plan_run_chain: a projected dual-gradient step
+    max(0, lmbd + step (phi(mean w) - phi(w_ref))) per set, as each price iteration of
+    price_solver.py:111-140 depends on the previous one's reductions), so no two steps overlap: every
+    step is its own path -> evaluation -> closing chain (+ the price update launch).  Same plan, batch,
+    outputs (w, cost, set reductions) and roofline bytes as the headline; ms_per_step from the timed
+    call, per-kernel durations from a second call with HIP events on every launch; every step's
+    reductions re-computed afterwards by an independent wide run_steps over the recorded prices
+    (bitwise equal -> verified_steps)."""
+    plan = run["plan"]
+    K = args.steps
+    S = plan.S
+    lm0 = torch.as_tensor(np.concatenate([e["lm"][args.warmup].cpu().numpy() for e in eng]), device=plan.gamma.device)
+    lr = torch.zeros(S, dtype=torch.float64, device=plan.gamma.device)
+    wt = plan.w_ref
+    step = 0.5
+    out = {k: torch.empty(s, dtype=torch.float64, device=lm0.device) for k, s in
+           (("lmbd", (K, S, 3 * N)), ("set_sum_w", (K, S, N)), ("set_stats", (K, S, 8)))}
+    plan.profile(enable=False)
+    kw = max(1, min(args.warmup, K))  # (untimed: the chain's first launches, same form)
+    plan.run_chain(lm0, lr, wt, step, kw, out={k: v[:kw] for k, v in out.items()})
+    assert plan.check()[1:] == (0, 0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    plan.run_chain(lm0, lr, wt, step, K, out=out)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    rep, fail, inv = plan.check()
+    assert fail == 0 and inv == 0, (fail, inv)
+    # per-kernel durations: the same chain again with a HIP-event pair on every launch
+    kernels = ("k_path", "k_eval", "k_finalize")
+    plan.profile(enable=kernels)
+    for k in kernels:
+        plan.profile(read=True, reset=True, kernel=k)
+    plan.run_chain(lm0, lr, wt, step, K)
+    assert plan.check()[1:] == (0, 0)
+    kus = {}
+    for k in kernels:
+        ms, n = plan.profile(read=True, kernel=k)
+        if n:
+            kus[k] = {"avg_us": ms / n * 1e3, "launches": n}
+    plan.profile(enable=False)
+    last = {k: plan.out[k].clone() for k in ("w", "cost") if plan.out.get(k) is not None}
+    # verification: an independent wide run_steps over the K recorded price vectors
+    vo = {k: torch.empty_like(out[k]) for k in ("set_sum_w", "set_stats")}
+    plan.run_steps(out["lmbd"], lr, K, S * 3 * N, 0, out=vo)
+    assert plan.check()[1:] == (0, 0)
+    ok = [all(bool(torch.equal(out[k][j], vo[k][j])) for k in vo) for j in range(K)]
+    rows = all(bool(torch.equal(v, plan.out[k])) for k, v in last.items())
+    if not (all(ok) and rows):
+        raise SystemExit(f"bench.py: sequential steps differ from their independent re-run: {ok}, rows {rows}")
+    moved = float((out["lmbd"][-1] - out["lmbd"][0]).abs().max())
+    B = plan.B
+    bpq = 8 * (N + 2)
+    ev_us = kus.get("k_eval", {}).get("avg_us", 0.0)
+    gbs = bpq * B / (ev_us * 1e-6) / 1e9 if ev_us else 0.0
+    return {"value": B * K / dt, "unit": "QP/s", "ms_per_step": dt / K * 1e3, "steps": K,
+            "issue": "one lompc_plan_run_chain call: per step the price update (k_chain_price) then k_path, k_eval, "
+                     "k_finalize of that step (4 launches; no overlap between steps is possible)",
+            "price_rule": f"lmbd_(k+1) = max(0, lmbd_k + {step} (phi(sum_w / count) - phi(w_ref))) per set, on the device",
+            "max_price_change": moved, "repaired_qps": rep, "kernels": kus,
+            "verified_steps": sum(ok),
+            "verification": "every step's set reductions (and the last step's w / cost) re-computed by an independent "
+                            "wide lompc_plan_run_steps over the recorded prices: bitwise equal",
+            "roofline": {"bound": "hbm", "kernel": "k_eval", "bytes_per_qp": bpq, "achieved": gbs,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                         "note": "k_eval's duration from the events pass; the step adds the path (latency-bound) and "
+                                 "the closing, which no other step can hide here"}}
 
 
 def station_leg(args, world, dev, sharded=False):
@@ -624,7 +768,7 @@ def station_leg(args, world, dev, sharded=False):
                       "bimpc_cost": "EXP_UNWEIGHTED, exp_rate 5", "demand_scale": f"DEMAND_SCALE * {M_2} / 500",
                       "storage": {"u_b_max": 0.5, "x_max": 0.5,
                                   "why": "the example lists x_max in {0.3, 0.5} and u_b_max in {0.15, 0.3} "
-                                         "(real_time_price_control.py:45-46); at horizon 48 the first BiMPC from an "
+                                         "(real_time_price_control.py:46-47); at horizon 48 the first BiMPC from an "
                                          "empty battery needs u_b_max >= 2 d_e ~ 0.37 (beta = 0.183), so 0.3 is "
                                          "infeasible and u_b_max = 0.5 is used"},
                       "sharded_code_path": bool(sharded)}}
@@ -679,7 +823,9 @@ def station_leg(args, world, dev, sharded=False):
                     "price_iterations_per_step": float(np.sum(it[it >= 0])) / steps,
                     "engine_calls_per_step": ncalls / steps,
                     "per_step": spread,
-                    "lompc_qps_per_sec_est": (ncalls + 2 * P * steps) * M_2 / P / dt,
+                    # (an equivalent, not a measurement: k_agg aggregates certified pieces from prefix sums
+                    # and solves no per-EV QP; it counts M_p QPs per engine call)
+                    "equivalent_qps_per_sec_k_agg_no_per_ev_solves": (ncalls + 2 * P * steps) * M_2 / P / dt,
                     "checks": {"storage_x_final": float(st.x), "x_max": float(consts.bimpc_consts.x_max),
                                "bimpc_iterations_last": info.get("iterations"),
                                "bimpc_primal_residual_last": info.get("primal_residual"),
@@ -762,7 +908,7 @@ def cpu_same_algorithm(eng, N, P, args, ref):
     (set, gamma cell) exact start solve + parametric active-set tracking with certified pieces, per-EV
     lookup and row write, per-set reductions — SURVEY.md §8(d)(1)) on the SAME workload as the GPU line:
     all 262 144 EVs of both types, 24 sets, full outputs (w, cost, set reductions), the timed steps'
-    fresh prices in turn; all host threads and one thread.  Its outputs for the first timed step are
+    fresh prices in turn; all host threads and one thread.  Its outputs for the last timed step are
     compared with the GPU's (``parity``): the two implementations of one algorithm, fp64 both."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_c  # baseline only

@@ -49,8 +49,8 @@
 #define __builtin_amdgcn_s_memtime __builtin_amdgcn_s_memrealtime
 #endif
 __device__ long long g_stamps[65536 * 8];
-__device__ long long g_wstart[32768 * 8];
-__device__ unsigned long long g_lstamps[64 * 16];  // k_loop_iter's phase sums (LQ_LSTAMP)  // k_eval: start of wave w of workgroup b at [b * 8 + w]
+__device__ long long g_wstart[32768 * 8];          // k_eval: start of wave w of workgroup b at [b * 8 + w]
+__device__ unsigned long long g_lstamps[64 * 16];  // k_loop_iter's phase sums (LQ_LSTAMP)
 #define LQ_WSTART()                                                                              \
   do {                                                                                           \
     const long long t__ = __builtin_amdgcn_s_memtime();                                          \
@@ -792,6 +792,35 @@ __global__ __launch_bounds__(256) void k_combine(const double* __restrict__ recv
     } else if (set_stats) {
       set_stats[c - SN] = v;
     }
+  }
+}
+
+// lompc_plan_run_chain: run k's prices from run k - 1's closed set reductions (the dependence of the
+// reference's price iterations, price_solver.py:111-140): one workgroup per set, lane = price
+// coordinate i = seg N + t,
+//   lmbd_k[i] = max(0, lmbd_{k-1}[i] + step (phi(wbar)[i] - phi(w_target)[i])),  wbar = sum_w / count
+// with phi = (theta w, theta (w_max - w), q_s w^2) (lompc.py:172-177) of the set's EV type.  A set
+// without EVs keeps its prices.
+__global__ __launch_bounds__(256) void k_chain_price(const QPConst* __restrict__ q, CtxEnds ce, int nctx, int N,
+                                                     const double* __restrict__ prev, const double* __restrict__ sum_w,
+                                                     const double* __restrict__ stats,
+                                                     const double* __restrict__ target, double step,
+                                                     double* __restrict__ next) {
+  const int s = blockIdx.x;
+  int k = 0;
+  while (k + 1 < nctx && s >= ce.end[k]) ++k;
+  const double th = q[k].theta, wm = q[k].w_max, qs = q[k].q_scale;
+  const double n = stats[(size_t)s * LOMPC_SET_STATS + LOMPC_STAT_COUNT];
+  for (int i = threadIdx.x; i < 3 * N; i += blockDim.x) {
+    const int seg = i / N, t = i - seg * N;
+    const double x = prev[(size_t)s * 3 * N + i];
+    double v = x;
+    if (n > 0) {
+      const double wb = sum_w[(size_t)s * N + t] / n, wr = target[(size_t)s * N + t];
+      const double g = seg == 0 ? th * (wb - wr) : (seg == 1 ? th * ((wm - wb) - (wm - wr)) : qs * (wb * wb - wr * wr));
+      v = fmax(0.0, x + step * g);
+    }
+    next[(size_t)s * 3 * N + i] = v;
   }
 }
 
@@ -2597,6 +2626,31 @@ int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     HIPCHK(p, hipGetLastError());
   }
   return rc;
+}
+
+int lompc_plan_run_chain(lompc_plan* p, const double* lmbd0, const double* lmbd_r, const double* w_target, double step,
+                         int n_runs, double* lmbd_out, double* w, double* cost, double* w0, int8_t* status,
+                         double* set_sum_w, double* set_stats, void* stream) {
+  if (!p || n_runs < 0 || !lmbd0 || !lmbd_r || !w_target || !lmbd_out || !set_sum_w || !set_stats ||
+      !(step >= 0.0) || !std::isfinite(step))
+    return LOMPC_ERR_INVALID_ARG;
+  HIPCHK(p, hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  const int N = p->N;
+  const size_t L = (size_t)p->S * 3 * N, SN = (size_t)p->S * N, SS = (size_t)p->S * LOMPC_SET_STATS;
+  for (int k = 0; k < n_runs; ++k) {
+    double* lm = lmbd_out + (size_t)k * L;
+    if (k == 0) {
+      if (lm != lmbd0) HIPCHK(p, hipMemcpyAsync(lm, lmbd0, L * sizeof(double), hipMemcpyDeviceToDevice, st));
+    } else {  // run k's prices from run k - 1's (combined) reductions
+      hipLaunchKernelGGL(k_chain_price, dim3((unsigned)p->S), dim3(64 * ((3 * N + 63) / 64)), 0, st, p->d_q, p->ce,
+                         p->nctx, N, lm - L, set_sum_w + (k - 1) * SN, set_stats + (k - 1) * SS, w_target, step, lm);
+      HIPCHK(p, hipGetLastError());
+    }
+    const int rc = lq_plan_launch(p, lm, lmbd_r, w, cost, w0, status, set_sum_w + k * SN, set_stats + k * SS, st, nullptr);
+    if (rc) return rc;
+  }
+  return LOMPC_OK;
 }
 
 int lompc_plan_status(lompc_plan* p, void* stream, int64_t* n_repaired, int64_t* n_failed, int64_t* n_invalid) {

@@ -91,6 +91,7 @@ SIGNATURES = [
     ("lompc_plan_create", _I, [_I, _P, _P, _L, _P, _P, _P, _I, _P, ctypes.POINTER(_P)]),
     ("lompc_plan_run", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_plan_run_steps", _I, [_P, _P, _L, _P, _L, _I, _I, _P, _P, _P, _P, _P, _P, _L, _L, _L, _I, _P]),
+    ("lompc_plan_run_chain", _I, [_P, _P, _P, _P, _D, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_plan_status", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_get_info", _I, [_P, _P, _P, _P, _P, _P]),
     ("lompc_plan_update", _I, [_P, _L, _P, _P, _P, _P]),
@@ -120,7 +121,7 @@ LOMPC_BIMPC_WEIGHTED = 0
 LOMPC_BIMPC_UNWEIGHTED = 1
 LOMPC_BIMPC_EXP_UNWEIGHTED = 2
 LOMPC_BIMPC_INFO = 5
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class PriceLoopArgs(ctypes.Structure):

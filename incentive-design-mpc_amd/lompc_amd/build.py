@@ -12,8 +12,10 @@ CSRC = os.path.join(ROOT, "csrc")
 OUT = os.path.join(PKG, "liblompc_amd.so")
 SOURCES = ["lompc_kernels.hip", "lompc_plan.hip", "lompc_price.cpp", "lompc_bimpc.cpp", "lompc_comm.cpp",
            "lompc_loop.hip"]
-DEPS = SOURCES + ["lompc_qp.hpp", "lompc_wave.hpp", "lompc_pricewave.hpp", "lompc_agg.hpp", "lompc_dense.hpp", "lompc_ctx.hpp",
-                  os.path.join("..", "..", "include", "lompc_amd.h")]
+# every header under csrc/ (not a hand-kept list: an edit to any included header must rebuild the
+# pushed .so; tests/test_build_deps.py checks each `#include "…"` resolves to a DEPS entry)
+DEPS = SOURCES + sorted(f for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))) + \
+    [os.path.join("..", "..", "include", "lompc_amd.h")]
 ARCH = os.environ.get("LOMPC_OFFLOAD_ARCH", "gfx950")
 
 

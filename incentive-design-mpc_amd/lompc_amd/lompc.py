@@ -301,8 +301,8 @@ class LoMPC:
         self._check_rc(rc)
         if inv.value:
             raise AssertionError(f"{inv.value} EVs with gamma outside [0, y_max]")
-        if fail.value:  # (the plan's text names an unsorted set of a sorted_gamma plan)
-            why = self._lib.lompc_plan_last_error(self._plan).decode(errors="replace") or \
+        if fail.value:  # a context has no plan: its own error text, if it set one
+            why = self._lib.lompc_last_error(self._ctx).decode(errors="replace") or \
                 "LoMPC QPs without a certified optimum"
             raise SolverError(f"{fail.value} EVs failed: {why}")
         return rep.value, fail.value, inv.value
@@ -584,6 +584,41 @@ class BatchPlan:
                                             self._stream)
         if rc:
             self._check_rc(rc)
+        return res
+
+    def run_chain(self, lmbd0, lmbd_r, w_target, step: float, n_runs: int, out=None) -> dict:
+        """n_runs DEPENDENT runs in one C-ABI call (lompc_plan_run_chain): run 0 at lmbd0 (S, 3N), run
+        k >= 1 at prices computed on the device from run k-1's set reductions by a projected
+        dual-gradient step ``max(0, lmbd + step (phi(sum_w / count) - phi(w_target)))`` — the
+        dependence of the reference's price iterations (price_solver.py:111-140).  Returns the plan's
+        ``out`` with ``lmbd`` (n_runs, S, 3N), ``set_sum_w`` (n_runs, S, N) and ``set_stats``
+        (n_runs, S, 8) per run (``out``: preallocated tensors for any of those three); the per-EV
+        outputs are the plan's buffers, holding the last run's."""
+        if self.direct:
+            raise ValueError("run_chain: PATH-mode plans only")
+        if self.out["set_sum_w"] is None:
+            raise ValueError("run_chain: the plan needs its set outputs (want_set=True)")
+        self._usable()
+        torch = _torch()
+        K, S, N = int(n_runs), self.S, self.N
+        dev = self.out["set_sum_w"].device
+        shapes = {"lmbd": (K, S, 3 * N), "set_sum_w": (K, S, N), "set_stats": (K, S, _lib.LOMPC_SET_STATS)}
+        res = dict(self.out)
+        for k, shp in shapes.items():
+            t = (out or {}).get(k)
+            if t is None:
+                t = torch.empty(shp, dtype=torch.float64, device=dev)
+            elif tuple(t.shape) != shp or t.dtype != torch.float64 or not t.is_contiguous() or t.device != dev:
+                raise ValueError(f"run_chain: out[{k!r}] must be a contiguous float64 tensor {shp} on {dev}")
+            res[k] = t
+        lo = self.lompc
+        l0, lr, wt = lo._dev(lmbd0).reshape(S, 3 * N), lo._dev(lmbd_r).reshape(S), lo._dev(w_target).reshape(S, N)
+        rc = self._lib.lompc_plan_run_chain(self._plan, _ptr(l0), _ptr(lr), _ptr(wt), float(step), K, _ptr(res["lmbd"]),
+                                            *self._outs[:4], _ptr(res["set_sum_w"]), _ptr(res["set_stats"]),
+                                            self._stream)
+        if rc:
+            self._check_rc(rc)
+        res["_keep"] = (l0, lr, wt)  # (alive until the caller's stream has used them)
         return res
 
     def check(self) -> tuple[int, int, int]:

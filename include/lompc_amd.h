@@ -149,7 +149,7 @@ const char* lompc_status_string(int status);
 const char* lompc_last_error(const lompc_ctx* ctx);
 
 /* ABI version (bumped on any signature change). */
-#define LOMPC_ABI_VERSION 4
+#define LOMPC_ABI_VERSION 5
 int lompc_abi_version(void);
 
 /* ---------------------------------------------------------------------------
@@ -219,7 +219,7 @@ int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, d
                    double* cost, double* w0, int8_t* status, double* set_sum_w,
                    double* set_stats, void* stream);
 
-/* n_runs consecutive independent runs (as n_runs lompc_plan_run calls) at the prices
+/* n_runs consecutive independent runs (the same optima as n_runs lompc_plan_run calls) at the prices
  * lmbd + k lmbd_stride and lmbd_r + k lmbd_r_stride (k = 0 .. n_runs - 1, strides in doubles).
  * Run k's set reductions go to set_sum_w + k set_sum_w_stride and set_stats + k set_stats_stride,
  * its per-EV outputs to w + k ev_stride N, cost / w0 / status + k ev_stride (strides in elements;
@@ -228,7 +228,11 @@ int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, d
  * E-th launch carries the enabled profiling events.
  * One C-ABI call for a sequence of independent batches (a benchmark's timed steps).  Plans whose
  * cells fill whole path workgroups take the STEPPED form: one launch carries the
- * path of run k + 1, the evaluation of run k and the closing of run k - 1.  steps_flags:
+ * path of run k + 1, the evaluation of run k and the closing of run k - 1.  In that form every
+ * set is closed by summing its evaluated rows (k_finalize's order), also for runs without w
+ * output; lompc_plan_run on a plan without w output closes from the pieces' aggregates inside the
+ * evaluation instead: the two agree to the certification tolerance (~1e-12 relative), bit for bit
+ * only when the plan closes in k_finalize (tests/test_gpu_pipeline.py).  steps_flags:
  *   LOMPC_STEPS_PER_KERNEL  the same runs issued one part per launch (paths / evaluations /
  *                           closings), with the same evaluation block map, so bit for bit the same
  *                           outputs (verification / A-B)
@@ -242,6 +246,23 @@ int lompc_plan_run_steps(lompc_plan* plan, const double* lmbd, int64_t lmbd_stri
                          int profile_every, double* w, double* cost, double* w0, int8_t* status,
                          double* set_sum_w, double* set_stats, int64_t set_sum_w_stride,
                          int64_t set_stats_stride, int64_t ev_stride, int steps_flags, void* stream);
+
+/* n_runs DEPENDENT runs: the call pattern of the reference's price loop (price_solver.py:111-140,
+ * where iteration k + 1's prices are computed from iteration k's reductions), so no two runs can
+ * overlap.  Run 0 at lmbd0 (dev [S, 3N]); before run k >= 1 one device launch sets, per set s and
+ * price coordinate i = seg N + t,
+ *   lmbd_k[s][i] = max(0, lmbd_{k-1}[s][i] + step (phi(wbar)[i] - phi(w_target[s])[i])),
+ *   wbar = run k-1's set_sum_w[s] / count[s],  phi(w) = (theta w, theta (w_max - w), q_s w^2)
+ * (a projected dual-gradient step, phi of lompc.py:172-177; a set without EVs keeps its prices).
+ * Every run is one lompc_plan_run (three launches; with a communicator its all-gather + combine, so
+ * the next prices come from the combined reductions on every rank).  Outputs: lmbd_out dev
+ * [n_runs][S][3N] (every run's prices; lmbd_out == lmbd0 allowed), set_sum_w dev [n_runs][S][N],
+ * set_stats dev [n_runs][S][LOMPC_SET_STATS] (required); w / cost / w0 / status as lompc_plan_run
+ * (one buffer: the last run's remain).  lmbd_r dev [S], w_target dev [S][N]; step >= 0.
+ * No synchronisation. */
+int lompc_plan_run_chain(lompc_plan* plan, const double* lmbd0, const double* lmbd_r, const double* w_target,
+                         double step, int n_runs, double* lmbd_out, double* w, double* cost, double* w0,
+                         int8_t* status, double* set_sum_w, double* set_stats, void* stream);
 
 /* Synchronise ``stream``; EVs repaired / failed / invalid summed over EVERY run since the previous
  * lompc_plan_status call (sticky device tallies, zeroed here), so a failure in any of the runs of a

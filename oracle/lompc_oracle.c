@@ -138,7 +138,9 @@ static int chol_solve(int n, double* M, double* b) {
 }
 
 /* Dense primal active set (Nocedal & Wright Alg. 16.3), as oracle/lompc_oracle.py */
-static int solve_one(const ocfg* c, const double* H, const double* g, double* w, int* st, int* iters) {
+/* warm != 0: start from the working set already in st (a feasible point: fixed coordinates at
+ * their knot, free ones at their segment's midpoint) instead of w = 0 with every coordinate at 0 */
+static int solve_one(const ocfg* c, const double* H, const double* g, double* w, int* st, int* iters, int warm) {
   const int N = c->N;
   double wh[OMAXN], p[OMAXN], rhs[OMAXN], M[OMAXN * OMAXN];
   int F[OMAXN];
@@ -151,8 +153,8 @@ static int solve_one(const ocfg* c, const double* H, const double* g, double* w,
   double scale = 1.0 + gmax + hmax * c->w_max * N + fabs(c->slopes[c->m - 1]);
   const double tol = 1e-12 * scale;
   for (int j = 0; j < N; ++j) {
-    st[j] = 0;
-    w[j] = 0.0;
+    if (!warm) st[j] = 0;
+    w[j] = (st[j] & 1) ? 0.5 * (c->knots[(st[j] - 1) >> 1] + c->knots[(st[j] + 1) >> 1]) : c->knots[st[j] >> 1];
   }
   for (int it = 0; it < 100000; ++it) {
     int nf = 0;
@@ -224,7 +226,7 @@ int oracle_lompc_solve(int N, int ev_small, double delta, double theta, double y
   double g[OMAXN], c0;
   int st[OMAXN];
   build_qp(&c, lmbd, lmbd_r, gamma, H, g, &c0);
-  int rc = solve_one(&c, H, g, w, st, iters);
+  int rc = solve_one(&c, H, g, w, st, iters, 0);
   if (cost) *cost = objective(&c, w, lmbd, lmbd_r, gamma);
   free(H);
   return rc;
@@ -252,7 +254,46 @@ int64_t oracle_lompc_solve_batch(int N, int ev_small, double delta, double theta
 #endif
     for (int64_t i = 0; i < B; ++i) {
       build_qp(&c, lmbd, lmbd_r, gamma[i], H, g, &c0);
-      int rc = solve_one(&c, H, g, w + i * N, st, NULL);
+      int rc = solve_one(&c, H, g, w + i * N, st, NULL, 0);
+      if (rc) nfail += 1;
+      if (cost) cost[i] = objective(&c, w + i * N, lmbd, lmbd_r, gamma[i]);
+    }
+    free(H);
+  }
+  return nfail;
+}
+
+/* As oracle_lompc_solve_batch, but each thread walks a contiguous range of the batch and starts
+ * every solve from the working set its previous solve ended with (the same dense active set and
+ * the same final equality-constrained solve: only the start differs).  With gamma sorted, nearby
+ * EVs share most of their optimal working set, so a solve takes a few iterations instead of
+ * O(N): the test checker for config-5-sized partitions (tests/test_gpu_price_loop_c5.py). */
+int64_t oracle_lompc_solve_batch_warm(int N, int ev_small, double delta, double theta, double y_max, double w_max,
+                                      const double* lmbd, double lmbd_r, int64_t B, const double* gamma, double* w,
+                                      double* cost, int nthreads) {
+  if (N < 1 || N > OMAXN) return -1;
+  int64_t nfail = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel reduction(+ : nfail)
+#endif
+  {
+    ocfg c;
+    cfg_init(&c, N, ev_small, delta, theta, y_max, w_max);
+    double* H = (double*)malloc((size_t)N * N * sizeof(double));
+    double g[OMAXN], c0;
+    int st[OMAXN];
+    int warm = 0;
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+    for (int64_t i = 0; i < B; ++i) {
+      build_qp(&c, lmbd, lmbd_r, gamma[i], H, g, &c0);
+      int rc = solve_one(&c, H, g, w + i * N, st, NULL, warm);
+      if (rc) { /* a warm start that failed: once more from w = 0 */
+        rc = solve_one(&c, H, g, w + i * N, st, NULL, 0);
+      }
+      warm = rc == 0;
       if (rc) nfail += 1;
       if (cost) cost[i] = objective(&c, w + i * N, lmbd, lmbd_r, gamma[i]);
     }

@@ -39,20 +39,25 @@ def load():
         lib.oracle_lompc_solve.argtypes = [I, I, D, D, D, D, P, D, D, P, P, P]
         lib.oracle_lompc_solve_batch.restype = L
         lib.oracle_lompc_solve_batch.argtypes = [I, I, D, D, D, D, P, D, L, P, P, P, I]
+        lib.oracle_lompc_solve_batch_warm.restype = L
+        lib.oracle_lompc_solve_batch_warm.argtypes = [I, I, D, D, D, D, P, D, L, P, P, P, I]
         lib.oracle_max_threads.restype = I
         _lib = lib
     return _lib
 
 
-def solve_batch(N, consts, lmbd, lmbd_r, gamma, nthreads=0):
-    """(B,) gammas against one parameter set -> (w (B,N), cost (B,), nfail)."""
+def solve_batch(N, consts, lmbd, lmbd_r, gamma, nthreads=0, warm=False):
+    """(B,) gammas against one parameter set -> (w (B,N), cost (B,), nfail).  warm: each thread's
+    solves start from its previous solve's working set (oracle_lompc_solve_batch_warm; fast for
+    sorted gamma, same optimum)."""
     lib = load()
+    fn = lib.oracle_lompc_solve_batch_warm if warm else lib.oracle_lompc_solve_batch
     lm = np.ascontiguousarray(np.asarray(lmbd, dtype=np.float64))
     g = np.ascontiguousarray(np.asarray(gamma, dtype=np.float64))
     B = g.shape[0]
     w = np.empty((B, N))
     cost = np.empty(B)
-    nf = lib.oracle_lompc_solve_batch(int(N), int(consts.ev_type == "small"), consts.delta, consts.theta,
+    nf = fn(int(N), int(consts.ev_type == "small"), consts.delta, consts.theta,
                                       consts.y_max, consts.w_max, lm.ctypes.data, float(lmbd_r), B,
                                       g.ctypes.data, w.ctypes.data, cost.ctypes.data, int(nthreads))
     return w, cost, int(nf)

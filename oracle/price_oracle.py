@@ -122,6 +122,7 @@ class OraclePriceSolver:
         self.A = self.lompc.get_input_mat()
         self.m = self.lompc.get_sc_modulus()
         self.lp = lp  # optional LP solver override (A, b, c) -> x
+        self.warm = False  # oracle_c's warm-started batch (same optima; fast on sorted gamma)
 
     def set_charge_levels(self, y0):
         self.nEVs, self.y0_rng, self.gamma_sc, self.gamma_sm = O.set_charge_levels(y0, self.consts.y_max)
@@ -131,7 +132,7 @@ class OraclePriceSolver:
         import oracle_c
 
         g = self.consts.y_max - self.y0
-        w, _, nf = oracle_c.solve_batch(self.N, self.consts, lmbd, lmbd_r, g)
+        w, _, nf = oracle_c.solve_batch(self.N, self.consts, lmbd, lmbd_r, g, warm=self.warm)
         assert nf == 0
         return w
 
@@ -139,7 +140,7 @@ class OraclePriceSolver:
         """price_solver.py:196-214 (vectorised over the oracle batch)."""
         W = self._batch(lmbd, lmbd_r)
         dv = W - w_ref
-        w_err_max = float(np.max(np.sqrt(np.einsum("bi,ij,bj->b", dv, A_bar, dv))))
+        w_err_max = float(np.max(np.sqrt(np.einsum("bi,bi->b", dv @ A_bar, dv))))
         w_avg = W.sum(axis=0) / self.nEVs
         w_avg_err = np.sqrt((w_avg - w_ref) @ A_bar @ (w_avg - w_ref))
         return w_err_max, np.abs(w_avg[0] - w_ref[0]), w_avg_err
@@ -178,3 +179,16 @@ class OraclePriceSolver:
 
     def get_w0_price0(self, lmbd, lmbd_r):
         return O.get_w0_price0(self.lompc, self.y0, lmbd, self.r, lmbd_r)
+
+    def get_w0_price0_batch(self, lmbd, lmbd_r):
+        """get_w0_price0 (price_solver.py:272-285, lompc.py:164-170) over the C oracle batch: the same
+        per-EV optima and price0 formula as lompc_oracle.get_w0_price0, vectorised (large batches)."""
+        N, c = self.N, self.consts
+        lm = np.zeros(3 * N)
+        lm[: self.r] = lmbd
+        W = self._batch(lm, lmbd_r)
+        w0 = W[:, 0].copy()
+        q_scale = 3 * c.theta / (4 * c.w_max)
+        price0 = (c.theta * (w0 * lm[0] + (c.w_max - w0) * lm[N]) + q_scale * w0 ** 2 * lm[2 * N]
+                  + c.theta ** 2 * w0 ** 2 * lmbd_r)
+        return w0, float(price0.sum()) / len(w0)

@@ -133,3 +133,39 @@ def test_lompc_constructor_checks_match_reference():
         LoMPC(12, LoMPCConstants(0.05, 10, 0.9, 0.25, "medium"))
     with pytest.raises(ZeroDivisionError):  # q_scale = 3 theta / (4 w_max), lompc.py:67
         LoMPC(12, LoMPCConstants(0.05, 10, 0.9, 0, "small"))
+
+
+def test_check_last_raises_solver_error_without_plan():
+    """LoMPC.check_last on a failed batch raises SolverError with the context's text (a LoMPC has
+    no plan handle).  The C library is replaced by a stub reporting one failed QP."""
+    import ctypes
+
+    from lompc_amd.lompc import BatchPlan, LoMPC, SolverError
+
+    class FakeLib:
+        def lompc_last_status(self, ctx, stream, rep, fail, inv):
+            ctypes.cast(fail, ctypes.POINTER(ctypes.c_int64)).contents.value = 1
+            return _lib.LOMPC_OK
+
+        lompc_plan_status = None
+
+        def lompc_last_error(self, ctx):
+            return b"context text"
+
+    lm = object.__new__(LoMPC)
+    lm._lib, lm._ctx, lm.device = FakeLib(), None, 0
+    lm._stream = lambda: 0
+    with pytest.raises(SolverError, match="1 EVs failed: context text"):
+        lm.check_last()
+
+    class FakePlanLib(FakeLib):
+        def lompc_plan_status(self, plan, stream, rep, fail, inv):
+            return self.lompc_last_status(None, stream, rep, fail, inv)
+
+        def lompc_plan_last_error(self, plan):
+            return b""
+
+    bp = object.__new__(BatchPlan)
+    bp._lib, bp._plan, bp._stream, bp.direct = FakePlanLib(), None, 0, False
+    with pytest.raises(SolverError, match="without a certified optimum"):
+        bp.check()

@@ -112,3 +112,20 @@ def test_oracle_input_checks():
         o.solve_lompc(-np.ones(36), 0.0, 0.5)
     with pytest.raises(AssertionError):
         O.OracleLoMPC(12, O.OracleConstants(0.05, 10, 0.95, 0.25, "small"))
+
+
+def test_c_oracle_warm_batch_equals_cold_batch():
+    """oracle_c.solve_batch(warm=True) (each solve started from the previous solve's working set)
+    returns the same optima as the cold batch (the same final equality-constrained solve)."""
+    import oracle_c
+
+    rng = np.random.default_rng(4)
+    for c, N in ((O.small_consts(), 48), (O.large_consts(), 48), (O.large_consts(), 12)):
+        lm = c.theta * rng.random(3 * N)
+        g = np.sort(c.y_max - (0.3 + 0.2 * rng.random(3000)))
+        for gg in (g, rng.permutation(g)):
+            w, cost, nf = oracle_c.solve_batch(N, c, lm, 0.0, gg)
+            w2, cost2, nf2 = oracle_c.solve_batch(N, c, lm, 0.0, gg, warm=True)
+            assert nf == nf2 == 0
+            np.testing.assert_allclose(w2, w, rtol=0, atol=1e-12)
+            np.testing.assert_allclose(cost2, cost, rtol=1e-12, atol=1e-12)

@@ -84,3 +84,38 @@ def test_sharded_stats_and_redraw_world2():
         np.testing.assert_allclose(st[:, 3], ref_st[:, 3], rtol=1e-14)
         assert cnt == mask_all.sum()
     np.testing.assert_array_equal(y_got, y_ref)
+
+
+def _ref_indices(y, rng, idx0):
+    """charging_station.py:111-116 as written: the masked loop, later partitions winning."""
+    idx = idx0.copy()
+    for p in range(len(rng) - 1):
+        idx[(y >= rng[p]) & (y <= rng[p + 1])] = p
+    return idx
+
+
+def test_update_indices_matches_reference_loop_on_edges():
+    """The searchsorted form of _update_indices equals the reference's masked loop on every
+    boundary value, below rng[0], above rng[P], and with repeated boundaries."""
+    from lompc_amd.charging_station import ChargingStation
+
+    rs = np.random.default_rng(3)
+    cases = [np.linspace(0.2, 0.9, 13), np.array([0.0, 0.0, 0.5, 1.0]), np.array([0.0, 0.5, 1.0, 1.0]),
+             np.array([0.1, 0.4, 0.4, 0.4, 0.8]), np.array([0.3, 0.3])]
+    for rng in cases:
+        P = len(rng) - 1
+        eps = 1e-12
+        y = np.concatenate([rng, np.nextafter(rng, -np.inf), np.nextafter(rng, np.inf), [rng[0] - 0.1, rng[-1] + 0.1,
+                            rng[0] - eps, rng[-1] + eps], rng[0] + (rng[-1] - rng[0]) * rs.random(50)])
+        idx0 = rs.integers(0, P, len(y))
+        cs = object.__new__(ChargingStation)
+        cs.P = P
+        cs.y_s = torch.as_tensor(y)
+        cs.y_l = torch.as_tensor(y[::-1].copy())
+        cs.idx_s = torch.as_tensor(idx0.copy())
+        cs.idx_l = torch.as_tensor(idx0[::-1].copy())
+        cs.y0_s_rng, cs.y0_l_rng = rng, rng.copy()
+        cs._bounds = {}
+        ChargingStation._update_indices(cs)
+        assert np.array_equal(cs.idx_s.numpy(), _ref_indices(y, rng, idx0)), rng
+        assert np.array_equal(cs.idx_l.numpy(), _ref_indices(y[::-1], rng, idx0[::-1])), rng

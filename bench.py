@@ -323,9 +323,15 @@ def main():
     # the stepped form (lompc_plan_run_steps, full outputs, no communicator): the timed region's
     # events sit on its k_step launches
     stepped = batched and args.mode == "path" and runs[0]["plan"].info()["cells"] % 4 == 0
+    # wide form (no warm start): per group of <= 32 steps k_paths (the paths), k_evals (every step's
+    # evaluation, each workgroup through its block of every step) and k_closes (the closings); its events
+    # sit on k_evals and read as one launch per step
+    wide = stepped and not args.warm
     rkernel = (("k_step (step k+1's path + step k's evaluation + step k-1's closing)" if args.warm else
-                "k_step (step k's evaluation + step k-1's closing; the K steps' paths in one k_paths launch before)")
+                "k_evals (the K steps' evaluations in ONE launch, read per step: its duration / K; the K paths in "
+                "one k_paths launch before it, the K closings in one k_closes launch after it)")
                if stepped else ("k_eval" if args.mode == "path" else "k_direct"))
+    kname = rkernel.split()[0]
 
     total_qp = world * B * args.steps
     value = total_qp / dt
@@ -359,15 +365,18 @@ def main():
                                                       if sharded else "dp1")),
             "sharded_code_path": bool(sharded),
             "dist_backend": (args.dist_backend if sharded else None),
-            "launches_per_step": (("1 (k_step) + 2 for the K steps' pipeline fill and drain"
-                                   + ("; + per step the all-gather and the combine kernel" if comm is not None else ""))
+            "launches_per_step": (("3 per group of up to 32 steps (k_paths, k_evals, k_closes)" if wide else
+                                   "1 (k_step) + 2 for the K steps' pipeline fill and drain")
+                                  + ("; + per step the all-gather and the combine kernel" if comm is not None else "")
                                   if stepped else sum(r["plan"].launches_per_run() for r in runs)),
             "step_outputs": ("set reductions: every step's own [K][S][...]; w, cost: one buffer every step rewrites"
                              if batched else "shared buffers (the last step's remain)"),
             "kernel_events": ("none" if no_events else
-                              (f"{rkernel.split()[0]}: one pair spanning {k_n} steady-state launches" if args.kernel_events == "span"
-                               else f"{rkernel.split()[0]}, 1 in {ev_every} timed launches")),
-            "issue": ("one lompc_plan_run_steps call for the K timed steps" + (" (stepped form)" if stepped else ""))
+                              ((f"k_evals: one pair around its launch, read as its {k_n} steps" if wide else
+                                f"{kname}: one pair spanning {k_n} steady-state launches") if args.kernel_events == "span"
+                               else f"{kname}, 1 in {ev_every} timed launches")),
+            "issue": ("one lompc_plan_run_steps call for the K timed steps" +
+                      ((" (wide form)" if wide else " (stepped form)") if stepped else ""))
                      if batched else "per-step lompc_plan_run",
             "correctness_gate": "sticky device tallies: no failed / invalid QP in any warmup or timed step",
         },
@@ -393,19 +402,20 @@ def main():
     if sharded:
         line["collective"] = collective_cost(runs, args, world, dev, torch, dist, comm, batched, dt)
     pmc = load_pmc(args, N, qp_per_launch)
-    pk = "k_step" if stepped else "k_eval"
+    pk = kname if stepped else "k_eval"
     if pmc and pk in pmc and "hbm_bytes_per_launch" in pmc[pk]:
         line["roofline"]["traffic"] = pmc[pk]["hbm_bytes_per_launch"]
         line["roofline"]["traffic_source"] = pmc["source"]
     if path and world == 1 and len(runs) == 1:
         line["kernels"] = kernel_breakdown(runs[0], step, args, nsteps, pmc, torch)
         if stepped:
-            line["kernels"]["k_step"] = {"avg_us": avg_launch_s * 1e6, "launches_timed": k_n,
-                                         "note": "the timed region's launches (each as k_path + k_eval + k_finalize of "
-                                                 "three different steps); the entries above: each kernel as its own "
-                                                 "launch"}
-            if pmc and "k_step" in pmc:
-                line["kernels"]["k_step"]["pmc"] = {x: pmc["k_step"][x] for x in pmc["k_step"] if x != "hbm_bytes_per_launch"}
+            line["kernels"][kname] = {"avg_us": avg_launch_s * 1e6, "launches_timed": k_n,
+                                      "note": ("the timed region's evaluation launch, per step (its duration / K); the "
+                                               "entries above: each kernel of a single run as its own launch") if wide else
+                                              ("the timed region's launches (each as k_path + k_eval + k_finalize of "
+                                               "three different steps); the entries above: each kernel as its own launch")}
+            if pmc and kname in pmc:
+                line["kernels"][kname]["pmc"] = {x: pmc[kname][x] for x in pmc[kname] if x != "hbm_bytes_per_launch"}
     if path and world == 1 and not multi and not args.no_contracts:
         line["contracts"] = contract_legs(eng, runs[0], N, P, args, nsteps, dev, torch, comm, pmc)
         if batched and comm is None:

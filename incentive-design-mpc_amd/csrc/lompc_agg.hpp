@@ -193,19 +193,35 @@ __global__ __launch_bounds__(256) void k_sorted_fill(SortArgs a) {
     ch += h;
     cl += l;
   }
-  sh[0][t] = c1;
-  sh[1][t] = ch;
-  sh[2][t] = cl;
-  __syncthreads();
-  if (t < 3) {  // exclusive scan of the 256 thread totals (one thread per quantity)
-    unsigned long long acc = off[t];
-    for (int k = 0; k < 256; ++k) {
-      const unsigned long long v = sh[t][k];
-      sh[t][k] = acc;
-      acc += v;
+  // exclusive scan of the 256 thread totals: a wave-wide inclusive scan (shuffles), the four wave
+  // totals combined in LDS (integer sums: exact, so any order gives the sequential scan's values)
+  const int lane = t & 63, wv = t >> 6;
+  unsigned long long i1 = c1, ih = ch, il = cl;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y1 = __shfl_up(i1, o), yh = __shfl_up(ih, o), yl = __shfl_up(il, o);
+    if (lane >= o) {
+      i1 += y1;
+      ih += yh;
+      il += yl;
     }
   }
+  __shared__ unsigned long long wt[3][4];
+  if (lane == 63) {
+    wt[0][wv] = i1;
+    wt[1][wv] = ih;
+    wt[2][wv] = il;
+  }
   __syncthreads();
+  unsigned long long b1 = off[0], bh = off[1], bl = off[2];
+  for (int w = 0; w < wv; ++w) {
+    b1 += wt[0][w];
+    bh += wt[1][w];
+    bl += wt[2][w];
+  }
+  sh[0][t] = b1 + i1 - c1;
+  sh[1][t] = bh + ih - ch;
+  sh[2][t] = bl + il - cl;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int i = i0 + u;

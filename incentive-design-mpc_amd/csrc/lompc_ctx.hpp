@@ -151,6 +151,10 @@ struct lompc_plan {
     bool wide = false;            // the map is the wide form's (no path workgroups in its launches)
     PathTab wt{};                 // wide form: a ring of per-run path tables, slot-major
     int64_t cap_wt = 0;           // its capacity in cells (slots x S x G)
+    double* rpart = nullptr;      // wide form, batched evaluation (k_evals / k_closes): per-run record
+    int* rfcnt = nullptr;         // slots of a path group, [runs][nblk][...]
+    int* rfidx = nullptr;
+    int64_t cap_rrec = 0;         // their capacity in blocks (runs x nblk)
   } stp;
   int* d_errflag = nullptr;
   unsigned long long* d_tally = nullptr;  // [3] EVs repaired / failed / invalid over every run since

@@ -170,6 +170,19 @@ struct WindowArgs {
 // double, so min/max are exact and the result does not depend on the order); the set's last
 // block writes the window and zeroes the accumulators for the next launch.  One extra workgroup
 // (the last) writes the windows of the empty sets, which have no blocks.
+// the window from the set's smallest / largest valid gamma (any: there is one)
+__device__ __forceinline__ void window_store(double* window, int s, double ym, bool any, double lo, double hi) {
+  const double mg = 1e-7 * ym;
+  double wlo = 0.0, whi = ym;
+  if (any) {
+    wlo = fmin(fmax(lo - mg, 0.0), ym);
+    whi = fmin(fmax(hi + mg, wlo + mg), ym);
+    if (!(whi > wlo)) wlo = fmax(whi - 2.0 * mg, 0.0);
+  }
+  window[2 * s] = wlo;
+  window[2 * s + 1] = whi;
+}
+
 __global__ __launch_bounds__(256) void k_plan_window(WindowArgs a) {
   __shared__ double smin[4], smax[4];
   __shared__ int last;
@@ -222,15 +235,41 @@ __global__ __launch_bounds__(256) void k_plan_window(WindowArgs a) {
   __threadfence();
   const unsigned long long blo = atomicExch(&acc[0], 0ull), bhi = atomicExch(&acc[1], 0ull);
   atomicExch(&acc[2], 0ull);
-  const double mg = 1e-7 * ym;
-  double wlo = 0.0, whi = ym;
-  if (blo != 0) {  // some valid gamma
-    wlo = fmin(fmax(__longlong_as_double((long long)~blo) - mg, 0.0), ym);
-    whi = fmin(fmax(__longlong_as_double((long long)bhi) + mg, wlo + mg), ym);
-    if (!(whi > wlo)) wlo = fmax(whi - 2.0 * mg, 0.0);
+  window_store(a.window, s, ym, blo != 0, __longlong_as_double((long long)~blo), __longlong_as_double((long long)bhi));
+}
+
+// gamma-sorted plans (LOMPC_PLAN_SORTED_GAMMA): one wave per set.  An ascending set whose first and
+// last gamma are valid has its valid range at its ends — the same window as k_plan_window's in one
+// load round instead of a pass over the set and one atomic per block (a set whose ends are not both
+// valid is folded by the wave, as k_plan_window does; an unsorted set is reported failed by k_agg).
+__global__ __launch_bounds__(64) void k_plan_window_sorted(WindowArgs a, const int64_t* __restrict__ set_off) {
+  const int s = (int)blockIdx.x, lane = (int)threadIdx.x;
+  const double ym = set_consts(a.qd, a.ce, s).y_max;
+  const int64_t s0 = set_off[s], s1 = set_off[s + 1];
+  if (s1 == s0) {
+    if (lane == 0) window_store(a.window, s, ym, false, 0.0, 0.0);
+    return;
   }
-  a.window[2 * s] = wlo;
-  a.window[2 * s + 1] = whi;
+  const double g0 = a.gamma[s0], g1 = a.gamma[s1 - 1];
+  const bool v0 = g0 >= 0.0 && g0 <= ym, v1 = g1 >= 0.0 && g1 <= ym;
+  double lo = g0, hi = g1;
+  if (!(v0 && v1)) {
+    lo = INFINITY;
+    hi = -INFINITY;
+    for (int64_t i = s0 + lane; i < s1; i += 64) {
+      const double g = a.gamma[i];
+      if (g >= 0.0 && g <= ym) {
+        lo = fmin(lo, g);
+        hi = fmax(hi, g);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = fmin(lo, __shfl_xor(lo, o));
+      hi = fmax(hi, __shfl_xor(hi, o));
+    }
+  }
+  if (lane == 0) window_store(a.window, s, ym, lo <= hi, lo + 0.0, hi + 0.0);
 }
 
 // cell of a valid gamma in a set's window (k_eval), the same arithmetic as k_path's cell bounds
@@ -735,7 +774,7 @@ __device__ __forceinline__ void finalize_set(const FinalArgs& r, const int s, do
       default: v = red[0][N + PX_N_INVALID]; break;
     }
     if (r.set_stats) r.set_stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
-    r.stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
+    if (r.stats) r.stats[(size_t)s * LOMPC_SET_STATS + tid] = v;
   }
 }
 
@@ -834,8 +873,20 @@ __global__ __launch_bounds__(256) void k_chain_price(const QPConst* __restrict__
 // write all the rows; the set's last arriver closes it (finalize_set) after its rows.  Rows of
 // EVs left to the individual re-solve are not written here (key ZD), the closing workgroup writes
 // them, so no two writes of a row race.
+// k_evals: where one run's tables, records, per-EV outputs and prices sit (offsets from the
+// EvalArgs pointers, so a loop over runs keeps one base per array instead of one pointer per run)
+struct RunOff {
+  int64_t tab = 0;  // cells: the run's path-table ring slot
+  int rec = 0;      // blocks: the run's record slot
+  int64_t ev = 0;   // EVs: per-run per-EV outputs
+  const double* lmbd = nullptr;    // (null: a.lmbd / a.lmbd_r)
+  const double* lmbd_r = nullptr;
+  bool launder = false;
+};
+
 template <int NT = 0, bool CLOSE = false>
-__device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, const FinalArgs* fr = nullptr) {
+__device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, const FinalArgs* fr = nullptr,
+                                           const RunOff ro = RunOff{}) {
   // dynamic LDS: [cap + 2][NS] piece rows (rows cap, cap + 1: zero pieces) | [cap][8]
   // coefficients (cfx) | [LQ_PPL][Gs] piece ends | cells: coverage start | piece count | (CLOSE) per
   // piece: gamma sum, EV count.  Laid out for the banks (64 dwords for ds_read_b64 / b128): a
@@ -851,12 +902,23 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   __shared__ int s_fc[EVAL_WAVES];  // (CLOSE) re-solve list lengths
   __shared__ int s_last;            // (CLOSE) this workgroup closes the set
   __shared__ int s_mx;              // the set's largest piece count of a cell
-  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int tid_ = (int)threadIdx.x;
+  if (ro.launder) asm volatile("" : "+v"(tid_));  // (k_evals: lane-derived indices recomputed every run, not
+                                                  // hoisted out of its loop and spilled)
+  const int tid = tid_, lane = tid & 63, wv = tid >> 6;
   const int4 info = a.blk[blk];
+  const int rb = ro.rec + blk;  // this block's record (k_evals: in its run's record slot)
+  // per-EV outputs (k_evals with per-run outputs: at the run's offset)
+  double* const aw = a.w ? a.w + ro.ev * (NT ? NT : a.N) : nullptr;
+  double* const acost = a.cost ? a.cost + ro.ev : nullptr;
+  double* const aw0 = a.w0 ? a.w0 + ro.ev : nullptr;
+  int8_t* const astatus = a.status ? a.status + ro.ev : nullptr;
   const int s = info.x, start = info.y, end = info.z;  // thread: EVs start + tid + EVAL_EVS h
   LQ_STAMPW(6);  // (diagnostic build: the block map's load round)
-  const int N = NT ? NT : a.N, G = a.G;
-  const int cap = a.cap;
+  int G_ = a.G, cap_ = a.cap;
+  if (ro.launder) asm volatile("" : "+s"(G_), "+s"(cap_));  // (k_evals: the LDS layout per run, as tid)
+  const int N = NT ? NT : a.N, G = G_;
+  const int cap = cap_;
   const int ZK = cap;      // the zero piece (a = b = 0): rows of invalid (and, without CLOSE,
                            // re-solved) EVs, which then add exactly 0 to the row sums and need no
                            // branch in the row loop
@@ -879,7 +941,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   constexpr int CPW = (LQ_PIECE_CAP / LQ_PPL + EVAL_WAVES - 1) / EVAL_WAVES;
   constexpr int UA = ((NT ? NT : LOMPC_MAX_N) * LQ_PPL + 63) / 64;
   int wc = 0;  // lane j < CPW: piece count of cell wv + W j
-  if (lane < CPW && wv + EVAL_WAVES * lane < Gs) wc = ld_t<false>(a.t_cnt + (size_t)s * G + wv + EVAL_WAVES * lane);
+  if (lane < CPW && wv + EVAL_WAVES * lane < Gs) wc = ld_t<false>(a.t_cnt + ro.tab + (size_t)s * G + wv + EVAL_WAVES * lane);
   // this thread's EVs (caller order)
   double gh[EVAL_PASSES];
 #pragma unroll
@@ -889,16 +951,16 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   }
   const QPConst& q = set_consts(a.qd, a.ce, s);
   double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
-  const double* __restrict__ L = a.lmbd + (size_t)s * 3 * N;
+  const double* __restrict__ L = (ro.lmbd ? ro.lmbd : a.lmbd) + (size_t)s * 3 * N;
   double l0[3] = {L[0], L[N], L[2 * N]};  // price0 (lompc.py:164-170)
-  double lr = a.lmbd_r[s];
-  const int cb = s * G;
+  double lr = (ro.lmbd_r ? ro.lmbd_r : a.lmbd_r)[s];
+  const int64_t cb = ro.tab + (int64_t)s * G;  // the set's first cell in the table
   // the set's USED piece slots (a cell's first t_cnt of its LQ_PPL; cells past the first `cap`
   // slots are re-solved individually) and the cells' counts / coverage starts.  Two memory rounds,
   // both wave-local (no barrier): each wave reads the counts of the cells whose pieces it stages
   // (issued before the gamma loads, above), then only those cells' used rows, coefficient records
   // and piece ends — cells hold 1-2 pieces on average, so this moves a fraction of the 8 slots
-  const size_t sb = (size_t)s * G * LQ_PPL;
+  const size_t sb = (size_t)cb * LQ_PPL;
   {
     int vn = 0;
     double vl = 0.0;
@@ -1001,9 +1063,9 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     const bool cov = valid && ke > kb && ke <= np && g >= glo_c && g <= gend;
     if (act && !valid) {
       ++n_inv;
-      if (a.cost) st_wt8(a.cost + i, NAN);
-      if (a.w0) st_wt8(a.w0 + i, NAN);
-      if (a.status) a.status[i] = LOMPC_QP_INVALID;
+      if (acost) st_wt8(acost + i, NAN);
+      if (aw0) st_wt8(aw0 + i, NAN);
+      if (astatus) astatus[i] = LOMPC_QP_INVALID;
     } else if (cov) {
       const double2 q0 = *reinterpret_cast<const double2*>(s_cf + cfx(key, 0));
       const double2 q1 = *reinterpret_cast<const double2*>(s_cf + cfx(key, 2));
@@ -1020,9 +1082,9 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       acc_p0 += p0;
       acc_err = fmax(acc_err, er);
       ++n_ok;
-      if (a.cost) st_wt8(a.cost + i, cst);
-      if (a.w0) st_wt8(a.w0 + i, w0v);
-      if (a.status) a.status[i] = LOMPC_QP_OK;
+      if (acost) st_wt8(acost + i, cst);
+      if (aw0) st_wt8(aw0 + i, w0v);
+      if (astatus) astatus[i] = LOMPC_QP_OK;
       if (CLOSE) {
         atomicAdd(s_pn + key, 1);
         atomicAdd(s_pf + key, (unsigned long long)rint(fmax(g - wlo, 0.0) * fxs));
@@ -1033,7 +1095,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     inv_rows |= __ballot(act && !valid) != 0ull;
     const unsigned long long need = __ballot(valid && !cov);
     if (valid && !cov) {
-      st_wt4(a.fail_idx + (size_t)blk * EVAL_MAXB + 64 * EVAL_PASSES * wv + nlist +
+      st_wt4(a.fail_idx + (size_t)rb * EVAL_MAXB + 64 * EVAL_PASSES * wv + nlist +
                  __popcll(need & ((1ull << lane) - 1ull)), i);
       ++n_fail;
     }
@@ -1066,7 +1128,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   };
   // the workgroup record (fixed-order combination of the waves'), by the threads of `lanes`
   auto store_record = [&](int t, int nthreads) {
-    double* part = a.partial + (size_t)blk * (N + NPX);
+    double* part = a.partial + (size_t)rb * (N + NPX);
     for (int c = t; c < N + NPX; c += nthreads) {
       double v = 0.0;
       if (c < N) {
@@ -1115,7 +1177,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     for (int k = 0; k < EVAL_WAVES; ++k) any_inv |= s_red[k][PX_N_INVALID] > 0.0;
     if (wv == 0) {  // publish the record, then arrive (nothing but the lookup's stores in flight)
       store_record(lane, 64);
-      if (lane < EVAL_WAVES) st_wt4(a.fail_cnt + (size_t)blk * EVAL_WAVES + lane, s_fc[lane]);
+      if (lane < EVAL_WAVES) st_wt4(a.fail_cnt + (size_t)rb * EVAL_WAVES + lane, s_fc[lane]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) {
         const int nb = fr->blk_prefix[s + 1] - fr->blk_prefix[s];
@@ -1139,9 +1201,9 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   // no per-row branch: the stores of a full batch use one address register and immediate
   // offsets; lanes past the row width (rlane false) store out of the descriptor's range, which
   // drops them
-  const bool fast = a.w && a.w_rsrc_ok;
+  const bool fast = aw && a.w_rsrc_ok;
   const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(a.w, (short)0, a.w ? a.w_bytes : 0, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(aw, (short)0, aw ? a.w_bytes : 0, 0x00020000);
   auto row_segment = [&](const int r0b, const int nrows) {
     const int* sk = s_k + r0b;
     const double* sg = s_g + r0b;
@@ -1188,8 +1250,8 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
               const int off = vb + (r0 + j * R) * N * 8;
               if (V == 2) st_wt16(rs, off, x0, x1);
               else st_wt8b(rs, off, x0);
-            } else if (a.w) {
-              double* dst = a.w + (size_t)(rbase + r0 + j * R + rr) * N + t0;
+            } else if (aw) {
+              double* dst = aw + (size_t)(rbase + r0 + j * R + rr) * N + t0;
               st_wt8(dst, x0);
               if (V == 2) st_wt8(dst + 1, x1);
             }
@@ -1220,16 +1282,16 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     }
     // rows of invalid EVs (gamma outside [0, y_max] or NaN): NaN, written after the loop's
     // zeros of the same rows (rare; ordered by the wait)
-    if (any_inv && a.w) {
+    if (any_inv && aw) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       for (int r = 0; r < nrows; ++r) {
         const double g = sg[r];
-        if (!(g >= 0.0 && g <= ym) && lane < N) st_wt8(a.w + (size_t)(rbase + r) * N + lane, NAN);
+        if (!(g >= 0.0 && g <= ym) && lane < N) st_wt8(aw + (size_t)(rbase + r) * N + lane, NAN);
       }
     }
   };
   if constexpr (CLOSE) {  // waves 1.. split the block's rows evenly (wave 0 published the record)
-    if (wv > 0 && a.w) {  // (no w output: nothing to write, the sums are in the record)
+    if (wv > 0 && aw) {  // (no w output: nothing to write, the sums are in the record)
       const int tot = end - start;
       const int lo = (wv - 1) * tot / (EVAL_WAVES - 1), hi = wv * tot / (EVAL_WAVES - 1);
       if (hi > lo) row_segment(lo, hi - lo);
@@ -1246,7 +1308,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       const int nh = max(0, min(64, end - start - r0b));  // wave-uniform
       if (nh > 0) row_segment(r0b, nh);
     }
-    if (lane == 0) st_wt4(a.fail_cnt + (size_t)blk * EVAL_WAVES + wv, nlist);
+    if (lane == 0) st_wt4(a.fail_cnt + (size_t)rb * EVAL_WAVES + wv, nlist);
     wave_record();
   }
   LQ_STAMPE(4);
@@ -1393,6 +1455,104 @@ PathsKernel paths_kernel(int N) {
     case 48: return k_paths<48>;
     default: return k_paths<0>;
   }
+}
+
+// The wide form's evaluations (lompc_plan_run_steps without warm starts, one part per kind): the
+// evaluations of runs run0 .. run0 + nruns - 1 in ONE launch.  Workgroup b evaluates its block of
+// every run in turn (k_eval's block map and arithmetic: eval_block), run j from ring slot j % slots
+// of the path tables and into record slot j - run0, so the launch holds no kernel boundary between
+// runs: while one workgroup stages run j + 1's pieces (its own loads wait for its row stores to be
+// acknowledged: vmcnt counts both in order), the other workgroups of the CU keep their rows streaming,
+// and no workgroup tail idles the chip between two runs.  Per-EV outputs at j ev_stride (0: every
+// run rewrites the same rows, each row by the same wave and lane in every run, so in run order).
+struct EvalsArgs {
+  int run0, nruns, slots, nblk;
+  int64_t lm_stride, lr_stride, ev_stride, SG;
+};
+
+template <int NT>
+__global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_evals(EvalArgs a, EvalsArgs x) {
+  const int b = (int)blockIdx.x;
+  for (int r = 0; r < x.nruns; ++r) {
+    const int j = x.run0 + r;
+    RunOff ro;
+    ro.tab = (int64_t)(j % x.slots) * x.SG;
+    ro.rec = r * x.nblk;
+    ro.ev = (int64_t)j * x.ev_stride;
+    ro.lmbd = a.lmbd + (size_t)j * x.lm_stride;
+    ro.lmbd_r = a.lmbd_r + (size_t)j * x.lr_stride;
+    ro.launder = true;
+    // (the block index laundered per run: nothing derived from it — the block's EVs and gamma, the set's
+    // constants — is hoisted out of the loop and kept live across runs, which made the loop spill)
+    int bl = b;
+    asm volatile("" : "+s"(bl));
+#ifdef LOMPC_STAMPS
+    // diagnostic build (scripts/evals_stamps.py): per (workgroup, run < 32) the run's start, the end
+    // of its staging, the end of its rows and its end, at g_stamps[((b * 32 + r) * 4 + k]
+    const long long t0__ = __builtin_amdgcn_s_memtime();
+#endif
+    eval_block<NT, false>(a, bl, nullptr, ro);
+    __syncthreads();  // (the staged table and the record scratch are the next run's)
+#ifdef LOMPC_STAMPS
+    if (threadIdx.x == 0 && r < 32 && b < 512) {
+      long long* q = g_stamps + ((size_t)b * 32 + r) * 4;
+      q[0] = t0__;
+      q[1] = g_stamps[(32768 + b) * 8 + 1];
+      q[2] = g_stamps[(32768 + b) * 8 + 4];
+      q[3] = __builtin_amdgcn_s_memtime();
+    }
+#endif
+  }
+}
+
+typedef void (*EvalsKernel)(EvalArgs, EvalsArgs);
+EvalsKernel evals_kernel(int N) {
+  switch (N) {
+    case 12: return k_evals<12>;
+    case 16: return k_evals<16>;
+    case 24: return k_evals<24>;
+    case 48: return k_evals<48>;
+    default: return k_evals<0>;
+  }
+}
+
+// ... and their closings in ONE launch: workgroup (r, s) closes set s of run run0 + r (finalize_set: the
+// same summation order as every other closing form).  Set outputs at j sw_stride / st_stride; with
+// shared set outputs (stride 0) or shared per-EV outputs (ev_stride 0) only the call's last run writes
+// them (the closings of one launch are unordered); the plan's status rows likewise.
+struct ClosesArgs {
+  int run0, nruns, slots, nblk, S, last;
+  int rel;  // set outputs indexed by the run's place in the launch (a communicator's send slots), not j
+  int64_t lm_stride, lr_stride, ev_stride, sw_stride, st_stride, SG;
+};
+
+__global__ __launch_bounds__(256) void k_closes(FinalArgs f, ClosesArgs x) {
+  __shared__ double red[LQ_FIN_CLASSES][FIN_W];
+  __shared__ double rep[LQ_FIN_CLASSES][FIN_W];
+  const int r = (int)blockIdx.x / x.S, s = (int)blockIdx.x - r * x.S, j = x.run0 + r, N = f.N;
+  FinalArgs c = f;
+  c.lmbd = f.lmbd + (size_t)j * x.lm_stride;
+  c.lmbd_r = f.lmbd_r + (size_t)j * x.lr_stride;
+  c.t_sl = f.t_sl + (int64_t)(j % x.slots) * x.SG * 64;
+  c.partial = f.partial + (size_t)r * x.nblk * (N + NPX);
+  c.fail_cnt = f.fail_cnt + (size_t)r * x.nblk * EVAL_WAVES;
+  c.fail_idx = f.fail_idx + (size_t)r * x.nblk * EVAL_MAXB;
+  const bool last = j == x.last;
+  if (x.ev_stride) {
+    const size_t eo = (size_t)j * x.ev_stride;
+    if (f.w) c.w = f.w + eo * N;
+    if (f.cost) c.cost = f.cost + eo;
+    if (f.w0) c.w0 = f.w0 + eo;
+    if (f.status) c.status = f.status + eo;
+  } else if (!last) {
+    c.w = c.cost = c.w0 = nullptr;
+    c.status = nullptr;
+  }
+  const int js = x.rel ? r : j;
+  if (f.set_sum_w) c.set_sum_w = (x.sw_stride || last) ? f.set_sum_w + (size_t)js * x.sw_stride : nullptr;
+  if (f.set_stats) c.set_stats = (x.st_stride || last) ? f.set_stats + (size_t)js * x.st_stride : nullptr;
+  if (!last) c.stats = nullptr;
+  finalize_set<4, false>(c, s, red, rep);
 }
 
 #include "lompc_agg.hpp"
@@ -1799,7 +1959,8 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   HIPCHK(p, hipMemcpyAsync(p->d_meta, p->h_buf, need_h, hipMemcpyHostToDevice, st));
   HIPCHK(p, hipEventRecord(p->ev_stage, st));
   WindowArgs wa{p->d_q, p->ce, p->d_blk, p->d_blk_prefix, gamma, p->d_wacc, p->d_window, (int)S, (int)nblk};
-  hipLaunchKernelGGL(k_plan_window, dim3((unsigned)nblk + 1), dim3(256), 0, st, wa);
+  if (sorted) hipLaunchKernelGGL(k_plan_window_sorted, dim3((unsigned)S), dim3(64), 0, st, wa, p->d_set_off);
+  else hipLaunchKernelGGL(k_plan_window, dim3((unsigned)nblk + 1), dim3(256), 0, st, wa);
   HIPCHK(p, hipGetLastError());
   if (sorted) {  // order check, prefix sums and fine index of the sorted sets (lompc_agg.hpp)
     SortArgs sa{p->d_q, p->ce, p->d_sblk, p->d_sblk_prefix, p->d_set_off, gamma, p->d_window, p->d_bsum, p->d_P,
@@ -2097,7 +2258,7 @@ void lq_plan_free(lompc_plan* p) {
         if (x) (void)hipFree(x);
     }
     for (void* x : {(void*)z.d_map, (void*)z.sl3, (void*)z.wt.cnt, (void*)z.wt.lo, (void*)z.wt.ge, (void*)z.wt.cf,
-                    (void*)z.wt.ab, (void*)z.wt.sl})
+                    (void*)z.wt.ab, (void*)z.wt.sl, (void*)z.rpart, (void*)z.rfcnt, (void*)z.rfidx})
       if (x) (void)hipFree(x);
     if (z.h_map) (void)hipHostFree(z.h_map);
   }
@@ -2486,6 +2647,67 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   const int cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
   const size_t lds = eval_lds(N, p->G, cap);
   const StepKernel kern = step_kernel(N);
+  if (wide && !split) {
+    // batched: per path group of n <= Kc runs THREE launches — k_paths (the n paths), k_evals (the n
+    // evaluations, each workgroup through its block of every run) and k_closes (the n x S closings);
+    // the same kernels' arithmetic as the split form below, so the same bits
+    const int64_t need = std::min<int64_t>(LQ_WIDE_RUNS, fit) * z.nblk;  // record slots x blocks
+    if (need > z.cap_rrec) {
+      if ((rc = grow(p, &z.rpart, need * (N + NPX))) || (rc = grow(p, &z.rfcnt, need * EVAL_WAVES)) ||
+          (rc = grow(p, &z.rfidx, need * EVAL_MAXB)))
+        return rc;
+      z.cap_rrec = need;
+    }
+    if (xr && (rc = lq_xbufs(p, Kc))) return rc;
+    EvalArgs ea;
+    FinalArgs ff;
+    eval_args(p, lmbd, lmbd_r, w, cost, w0, status, tab(0), ea, ff);
+    ea.blk = reinterpret_cast<const int4*>(z.d_map);
+    ea.nblk = z.nblk;
+    ea.partial = z.rpart;
+    ff.partial = z.rpart;
+    ea.fail_cnt = z.rfcnt;
+    ff.fail_cnt = z.rfcnt;
+    ea.fail_idx = z.rfidx;
+    ff.fail_idx = z.rfidx;
+    ff.blk_prefix = reinterpret_cast<const int*>(z.d_map + (((size_t)z.nblk * sizeof(int4) + 15) & ~(size_t)15));
+    ff.set_sum_w = xr ? p->d_xsend : set_sum_w;
+    ff.set_stats = xr ? p->d_xsend + p->S * N : set_stats;
+    for (int g0 = 0; g0 < K; g0 += Kc) {
+      const int n = std::min(Kc, K - g0);
+      {
+        PathArgs pw = path_args(p, lmbd, lmbd_r, z.wt);
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
+        hipExtLaunchKernelGGL(paths_kernel(N), dim3((unsigned)(n * ncell)), dim3(64), 0, st, e0, e1, 0, pw, lmbd_stride,
+                              lmbd_r_stride, g0, slots);
+        HIPCHK(p, hipGetLastError());
+        plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
+      }
+      {  // the evaluation launch carries the K_EVAL timing (span: the first group's only), as n runs
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        const bool ev = !span_events || g0 == 0;
+        if (ev && plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1)) return fail_arg(p, "profiling events");
+        const EvalsArgs x{g0, n, slots, z.nblk, lmbd_stride, lmbd_r_stride, ev_stride, ncell};
+        hipExtLaunchKernelGGL(evals_kernel(N), dim3((unsigned)z.nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, ea, x);
+        HIPCHK(p, hipGetLastError());
+        if (ev) plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1, n);
+      }
+      {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (plan_prof_begin(p, LOMPC_PLAN_K_FINAL, &e0, &e1)) return fail_arg(p, "profiling events");
+        const ClosesArgs c{g0, n, slots, z.nblk, (int)p->S, K - 1, xr ? 1 : 0, lmbd_stride, lmbd_r_stride, ev_stride,
+                           xr ? L : sw_stride, xr ? L : st_stride, ncell};
+        hipExtLaunchKernelGGL(k_closes, dim3((unsigned)(n * p->S)), dim3(256), 0, st, e0, e1, 0, ff, c);
+        HIPCHK(p, hipGetLastError());
+        plan_prof_end(p, LOMPC_PLAN_K_FINAL, e0, e1, n);
+      }
+      if (xr)  // one collective per run, in run order (each into that run's set outputs)
+        for (int r = 0; r < n; ++r)
+          if ((rc = lq_exchange(p, p->d_xsend + (size_t)r * L, sw_of(g0 + r), st_of(g0 + r), st))) return rc;
+    }
+    return LOMPC_OK;
+  }
   // the steady launches 1 .. K - 1 (stepped: path + evaluation + closing; wide: evaluation +
   // closing); the span events cover 1 .. s_last, wide: the first path group's (no path launch inside)
   const int s_first = 1, s_last = wide ? Kc - 1 : K - 1;

@@ -327,8 +327,11 @@ class ChargingStation:
         Mp_s, Mp_l = np.zeros((self.P,), dtype=int), np.zeros((self.P,), dtype=int)
         beta_s, beta_l = np.zeros((self.P,)), np.zeros((self.P,))
         gamma_sm, gamma_lm = np.zeros((self.P,)), np.zeros((self.P,))
-        st_s = partition_stats(self.y_s, self.idx_s, self.P, self.group)
-        st_l = partition_stats(self.y_l, self.idx_l, self.P, self.group)
+        # one rank: each type's EVs sorted once by charge level, the partitions' statistics from that
+        # order (both types in one host sync); the layout the price loops need comes with it
+        sl = self._sorted_layouts() if self.group is None else None
+        st_s = sl["Small"] if sl and "Small" in sl else partition_stats(self.y_s, self.idx_s, self.P, self.group)
+        st_l = sl["Large"] if sl and "Large" in sl else partition_stats(self.y_l, self.idx_l, self.P, self.group)
         for p in range(self.P):
             Mp_s[p] = int(st_s[p, 0])
             if Mp_s[p] > 0:
@@ -399,9 +402,8 @@ class ChargingStation:
                 if self._staged:
                     solver.use_partition(p)  # (staged before the BiMPC solve, _stage_partitions)
                 else:
-                    ys, off = self._partition_layout(kind, y, idx)
-                    solver.set_charge_levels_stats(ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3],
-                                                   descending=True)
+                    ys, (a, b) = self._part_slice(kind, y, idx, p)
+                    solver.set_charge_levels_stats(ys[a:b], st[p, 0], st[p, 1], st[p, 2], st[p, 3], descending=True)
                 if PRINT_LEVEL >= 1 and self._rank0():
                     print(f"{kind} EVs, partition {p:2d}: ", end="")
                     if PRINT_LEVEL >= 2:
@@ -485,11 +487,11 @@ class ChargingStation:
             with torch.cuda.device(self.device), torch.cuda.stream(solver._stream):
                 # the type's partition layout too (its sorts and one host sync: on this thread, beside
                 # the interior point, not before it); its tensors are read on the main stream later
-                ys, off = self._partition_layout(kind, y, idx, main)
+                self._partition_layout(kind, y, idx, main)
                 for p in range(self.P):
                     if st[p, 0] > 0:
-                        solver.stage_partition(p, ys[off[p]:off[p + 1]], st[p, 0], st[p, 1], st[p, 2], st[p, 3],
-                                               descending=True)
+                        ys, (a, b) = self._part_slice(kind, y, idx, p)
+                        solver.stage_partition(p, ys[a:b], st[p, 0], st[p, 1], st[p, 2], st[p, 3], descending=True)
 
         if self.group is not None:
             for job in jobs:
@@ -499,12 +501,65 @@ class ChargingStation:
             self._stage_pool = concurrent.futures.ThreadPoolExecutor(max_workers=2)
         return [self._stage_pool.submit(stage, job) for job in jobs]
 
+    def _sorted_layouts(self):
+        """Both EV types' partition layouts and statistics from ONE sort per type (one rank): y sorted
+        descending, so partition p (charge levels in [rng[p], rng[p+1]], later partitions winning on
+        shared edges, charging_station.py:111-116) is one contiguous run — partition P-1 first — in
+        descending charge level (ascending gamma, as the loop plans want); the runs' bounds come from a
+        searchsorted of the boundaries, max / min from the runs' ends and the sums by a segment
+        reduction.  One host sync for both types.  A type with a charge level outside [rng[0], rng[P]]
+        (whose EVs keep their previous partition index, :111-116, so the runs would not be the
+        partitions) is left out of the result: the caller takes the index-based path for it.
+        Returns {kind: (P, 4) host statistics (count, max, min, sum)}; the layouts go to self._layout."""
+        torch = _torch()
+        P = self.P
+        parts, recs = [], []
+        for kind, y, rng in (("Small", self.y_s, self.y0_s_rng), ("Large", self.y_l, self.y0_l_rng)):
+            n = int(y.numel())
+            if n == 0:
+                return None
+            b = self._bounds.get(id(rng))
+            if b is None:
+                b = self._bounds[id(rng)] = torch.as_tensor(rng, dtype=y.dtype, device=y.device)
+            ys, perm = torch.sort(y, descending=True)
+            # c[p] = #{y >= rng[p]}, p = 1 .. P-1 (searchsorted over -ys, ascending); c[0] = n, c[P] = 0
+            c = torch.searchsorted(-ys, -b[1:P], right=True) if P > 1 else torch.zeros(0, dtype=torch.int64,
+                                                                                       device=y.device)
+            z = torch.zeros(1, dtype=torch.int64, device=y.device)
+            cge = torch.cat([torch.full((1,), n, dtype=torch.int64, device=y.device), c, z])  # [P + 1]
+            start, end = cge[1:], cge[:-1]  # partition p: [c[p+1], c[p])
+            cnt = end - start
+            first = start.clamp(max=n - 1)
+            last = (end - 1).clamp(min=0)
+            # segment sums in storage order (partition P-1 first)
+            sums = torch.segment_reduce(ys, "sum", lengths=cnt.flip(0)).flip(0)
+            recs.append(torch.stack([cnt.to(torch.float64), ys[first], ys[last], sums]))
+            recs.append(torch.stack([ys[0], ys[n - 1], b[0], b[P]]).reshape(4, 1).expand(4, P))
+            parts.append((kind, ys, perm, n))
+        h = torch.cat(recs, dim=1).cpu().numpy()  # the one host sync
+        out = {}
+        for j, (kind, ys, perm, n) in enumerate(parts):
+            st = h[:, 2 * j * P: (2 * j + 1) * P].T.copy()  # (P, 4): count, max, min, sum
+            ymax, ymin, lo, hi = h[:, (2 * j + 1) * P]
+            if not (ymin >= lo and ymax <= hi):  # (NaN fails too)
+                continue
+            cnt = st[:, 0].astype(np.int64)
+            st[cnt == 0, 1:] = (-np.inf, np.inf, 0.0)
+            ends = np.cumsum(cnt[::-1])  # storage offsets, partition P-1 first
+            seg = {}
+            for k, p in enumerate(range(P - 1, -1, -1)):
+                seg[p] = (int(ends[k] - cnt[p]), int(ends[k]))
+            self._layout[kind] = (perm, ys, seg)
+            out[kind] = st
+        return out
+
     def _partition_layout(self, kind, y, idx, reader=None):
         """This rank's EVs of one type grouped by partition, each partition in descending charge
         level (ascending gamma = y_max - y: the price loops' plans aggregate per certified piece,
-        LOMPC_PLAN_SORTED_GAMMA), once per step: (charge levels in that order, host offsets
-        [P+1]) — per-partition slices without boolean indexing (one host sync per type and step
-        instead of one per partition)."""
+        LOMPC_PLAN_SORTED_GAMMA), once per step: (permutation, charge levels in that order, host
+        {partition: (start, end)}) — per-partition slices without boolean indexing (one host sync per
+        type and step instead of one per partition).  Made by _sorted_layouts on one rank; otherwise
+        here from the partition indices."""
         torch = _torch()
         if kind not in self._layout:
             # (partition, -y) order exactly: a stable sort by descending y, then a stable sort by
@@ -517,9 +572,13 @@ class ChargingStation:
             if reader is not None:  # (made on another stream: the allocator keeps them until `reader` is done)
                 perm.record_stream(reader)
                 ys.record_stream(reader)
-            self._layout[kind] = (perm, off, ys)
-        perm, off, ys = self._layout[kind]
-        return ys, off
+            self._layout[kind] = (perm, ys, {p: (int(off[p]), int(off[p + 1])) for p in range(self.P)})
+        return self._layout[kind]
+
+    def _part_slice(self, kind, y, idx, p):
+        """(charge levels in layout order, (start, end) of partition p in it)."""
+        perm, ys, seg = self._partition_layout(kind, y, idx)
+        return ys, seg[p]
 
     def _w0_batched(self, kind, solver: PriceSolver, y, idx, prices, lmbd_r):
         """All partitions of one EV type in ONE engine call (price_solver.py:272-285 per partition).
@@ -527,18 +586,22 @@ class ChargingStation:
         invalid) combined over ranks — `_w0_checked` reads and checks them)."""
         torch = _torch()
         N, P = self.N_lo, self.P
-        ys, off = self._partition_layout(kind, y, idx)
-        perm = self._layout[kind][0]
+        perm, ys, seg = self._partition_layout(kind, y, idx)
+        # the sets in layout order (each partition's run of EVs; _sorted_layouts stores partition P-1
+        # first): set k = partition order[k]
+        order = sorted(range(P), key=lambda p: seg[p])
+        off = np.array([seg[order[0]][0]] + [seg[p][1] for p in order], dtype=np.int64)
         gamma = (solver.consts.y_max - ys).contiguous()
         lm = np.zeros((P, 3 * N))
-        lm[:, : self.r] = prices
+        lm[:, : self.r] = prices[order]
         lompc = solver.lompc
         lompc.set_params(lm, np.full(P, float(lmbd_r)))
         res = lompc.solve_batch(gamma, off, want_w=False, want_cost=False, want_w0=True, want_set=True, check=False)
         st = res["set_stats"]
+        back = torch.as_tensor(np.argsort(order), device=st.device)  # partition p's row: set back[p]
         red = torch.stack([st[:, _lib.LOMPC_STAT_SUM_W0], st[:, _lib.LOMPC_STAT_SUM_PRICE0],
                            st[:, _lib.LOMPC_STAT_COUNT], st[:, _lib.LOMPC_STAT_N_FAILED],
-                           st[:, _lib.LOMPC_STAT_N_INVALID]], dim=1).contiguous()
+                           st[:, _lib.LOMPC_STAT_N_INVALID]], dim=1)[back].contiguous()
         if self.group is not None:
             import torch.distributed as dist
 

@@ -8,7 +8,11 @@ counter group over `bench.py --steps 3 --warmup 2`), per plan kernel, per dispat
   fraction of a wave's lifetime = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES, the stall split
   WAIT_ANY (parked on s_waitcnt / barriers) and WAIT_INST_ANY (issue stalls).
 
-usage: python scripts/make_pmc.py [pmc_dir] [out] [evs] [horizon]
+* k_evals (the wide run_steps' batched evaluation: one dispatch carries R runs): traffic per RUN =
+  per dispatch / R (the session runs bench.py with --warmup R --steps R, so every k_evals dispatch
+  carries R runs).
+
+usage: python scripts/make_pmc.py [pmc_dir] [out] [evs] [horizon] [runs per k_evals dispatch]
 """
 import collections
 import csv
@@ -20,7 +24,8 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc.json"
 qp = float(sys.argv[3]) if len(sys.argv) > 3 else 262144.0
 N = int(sys.argv[4]) if len(sys.argv) > 4 else 24
-KERNELS = ("k_step", "k_paths", "k_path", "k_eval", "k_finalize")
+R = int(sys.argv[5]) if len(sys.argv) > 5 else 3
+KERNELS = ("k_evals", "k_closes", "k_step", "k_paths", "k_path", "k_eval", "k_finalize")
 vals = {k: collections.defaultdict(list) for k in KERNELS}
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
@@ -49,7 +54,7 @@ def mean(k, c):
 
 rec = {"mode": "path", "horizon": N, "qp_per_launch": qp,
        "source": "rocprofv3 --kernel-trace --pmc, one pass per counter group (scripts/pmc_session.sh), "
-                 "bench.py --steps 3 --warmup 2; FETCH_SIZE doubled per MI355X_MICROARCH.md; KiB -> bytes"}
+                 "bench.py --steps 3 --warmup 3; FETCH_SIZE doubled per MI355X_MICROARCH.md; KiB -> bytes"}
 for k in KERNELS:
     d = {}
     waves, cyc = mean(k, "SQ_WAVES"), mean(k, "SQ_WAVE_CYCLES")
@@ -69,10 +74,13 @@ for k in KERNELS:
         d["lds_bank_conflict_frac"] = bc / ia  # conflict cycles / all LDS-array cycles
     fs, ws = mean(k, "FETCH_SIZE"), mean(k, "WRITE_SIZE")
     if fs is not None and ws is not None:
-        d["fetch_bytes_per_launch"] = 2.0 * fs * 1024.0
-        d["write_bytes_per_launch"] = ws * 1024.0
+        per = R if k == "k_evals" else 1  # (k_evals: per run)
+        d["fetch_bytes_per_launch"] = 2.0 * fs * 1024.0 / per
+        d["write_bytes_per_launch"] = ws * 1024.0 / per
+        if per > 1:
+            d["runs_per_dispatch"] = per
         d["hbm_bytes_per_launch"] = d["fetch_bytes_per_launch"] + d["write_bytes_per_launch"]
-        if k in ("k_eval", "k_step"):
+        if k in ("k_eval", "k_step", "k_evals"):
             d["algorithmic_bytes_per_launch"] = 8.0 * (N + 2) * qp
     d["dispatches"] = max((len(v) for v in vals[k].values()), default=0)
     if d["dispatches"]:

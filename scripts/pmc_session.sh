@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
-ARGS=${BENCH_ARGS:-"--steps 3 --warmup 2 --no-cpu-baseline --no-station --no-direct --no-contracts"}
+ARGS=${BENCH_ARGS:-"--steps 3 --warmup 3 --no-cpu-baseline --no-station --no-direct --no-contracts"}
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue

@@ -30,7 +30,7 @@ for _ in range(2):
     st._step()
 torch.cuda.synchronize()
 sol = st.price_solver_l
-ys, off = st._partition_layout("Large", st.y_l, st.idx_l)
+_, ys, seg = st._partition_layout("Large", st.y_l, st.idx_l)
 stl = st._pstats[1]
 t_tot = []
 for rep in range(3):
@@ -40,7 +40,7 @@ for rep in range(3):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         with torch.cuda.stream(sol._stream):
-            sol.stage_partition(p, ys[off[p]:off[p + 1]], stl[p, 0], stl[p, 1], stl[p, 2], stl[p, 3], descending=True)
+            sol.stage_partition(p, ys[seg[p][0]:seg[p][1]], stl[p, 0], stl[p, 1], stl[p, 2], stl[p, 3], descending=True)
         t1 = time.perf_counter()
         torch.cuda.synchronize()
         t2 = time.perf_counter()

@@ -25,13 +25,14 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--outputs", default="full")
 ap.add_argument("--horizon", type=int, default=24)
+ap.add_argument("--evs", type=int, default=262144)
 args = ap.parse_args()
 
 import torch  # noqa: E402
 
 from lompc_amd import _lib  # noqa: E402
 
-N, P, B = args.horizon, 12, 262144
+N, P, B = args.horizon, 12, args.evs
 for libname in args.libs:
     lib = _lib.load(os.path.join(ROOT, "incentive-design-mpc_amd", "lompc_amd", libname))
     _lib._lib = lib

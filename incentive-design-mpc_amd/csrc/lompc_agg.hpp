@@ -230,16 +230,35 @@ __global__ __launch_bounds__(256) void k_sorted_fill(SortArgs a) {
       a.P[e] = sh[0][t] + x1[u];
       a.P[a.PB + e] = sh[1][t] + xh[u];
       a.P[2 * a.PB + e] = sh[2][t] + xl[u];
-      // fine bucket boundaries: bucket b starts at the first valid position whose bucket is >= b
-      const int j = (int)(i - s0);
-      if (j < nv) {
-        const int fb = agg_fine(a.gamma[i], lo, fs, a.F);
-        const int fp = j == 0 ? -1 : agg_fine(a.gamma[i - 1], lo, fs, a.F);
-        int* ps = a.pos + (size_t)s * (a.F + 1);
-        for (int b = fp + 1; b <= fb; ++b) ps[b] = j;
-        if (j == nv - 1)
-          for (int b = fb + 1; b <= a.F; ++b) ps[b] = nv;
+    }
+  }
+  // fine bucket index: bucket b starts at the first valid position whose bucket is >= b (buckets past
+  // the last valid position's: nv).  The block owns the buckets from its first valid position's
+  // predecessor's bucket + 1 to its last valid position's (to F when that is the set's last valid
+  // position); they are written cooperatively, each by a binary search over the block's buckets in
+  // LDS — a set with few EVs has thousands of buckets per EV, which one lane writing its own range
+  // serially took tens of microseconds for
+  __shared__ int s_fb[LQ_AGG_SB];
+  const int jb0 = (int)(bk.y - s0), jb1 = min((int)(bk.z - s0), nv);  // the block's valid positions
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = i0 + u, k = i - bk.y;
+    if (i < bk.z && (int)(i - s0) < nv) s_fb[k] = agg_fine(a.gamma[i], lo, fs, a.F);
+  }
+  __syncthreads();
+  if (jb0 < jb1) {
+    const int m = jb1 - jb0;
+    const int b_lo = jb0 == 0 ? 0 : agg_fine(a.gamma[s0 + jb0 - 1], lo, fs, a.F) + 1;
+    const int b_hi = jb1 == nv ? a.F : s_fb[m - 1];
+    int* ps = a.pos + (size_t)s * (a.F + 1);
+    for (int b = b_lo + t; b <= b_hi; b += 256) {
+      int l = 0, h = m;  // first block position with bucket >= b
+      while (l < h) {
+        const int mid = (l + h) >> 1;
+        if (s_fb[mid] < b) l = mid + 1;
+        else h = mid;
       }
+      ps[b] = l < m ? jb0 + l : nv;
     }
   }
 }

@@ -1,0 +1,125 @@
+// lompc_levels.hip — the charging station's per-step partition layout on the device.
+//
+// Reference: ChargingStation._update_indices (chargingstation/charging_station.py:111-116) puts EV i
+// in partition p when rng[p] <= y_i <= rng[p+1] (later partitions winning on shared edges), and
+// every step each (type, partition) price loop needs its EVs' count / max / min / mean charge level
+// (PriceSolver.set_charge_levels, price_solver.py:66-77, via charging_station.py:187-266) and — for
+// the batched engine's gamma-sorted loop plans — its EVs in descending charge level.  With every
+// level inside [rng[0], rng[P]] (the station's dynamics keep them there: levels only grow, and full
+// EVs are redrawn inside the range) partition p is one contiguous run of the levels sorted in
+// descending order, so ONE sort gives the layout and the statistics:
+//   (1) rocprim's radix sort of (y, index) pairs, descending (stable: ties keep index order);
+//   (2) k_lv_bounds: the runs' ends by a 64-way search per boundary (three load rounds for 2^18 EVs);
+//   (3) k_lv_partials: per (partition, chunk) partial sums, in a fixed order;
+//   (4) k_lv_stats: per partition count / max / min / sum (partials summed in chunk order) and the
+//       levels' overall max / min beside rng[0] / rng[P] (the caller's range check: outside it, EVs
+//       keep their previous partition and the runs are not the partitions — the caller then takes
+//       the index-based path).
+// Deterministic: the same levels give the same bits.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
+#include "../../include/lompc_amd.h"
+
+namespace {
+
+constexpr int LV_CHUNKS = 32;  // partial-sum chunks per partition
+constexpr int LV_MAXP = 256;   // partitions at most
+
+// c[p] = #{i : ys[i] >= bounds[p]} for p = 1 .. P-1 in the descending levels (one wave per boundary):
+// each round the wave samples 64 evenly spaced positions of the remaining interval and keeps the one
+// sub-interval where the predicate flips
+__global__ __launch_bounds__(64) void k_lv_bounds(const double* __restrict__ ys, int64_t n,
+                                                  const double* __restrict__ bounds, int64_t* __restrict__ cge) {
+  const int p = (int)blockIdx.x + 1, lane = (int)threadIdx.x;
+  const double v = bounds[p];
+  int64_t lo = 0, hi = n;  // answer in [lo, hi]: ys[lo - 1] >= v (or lo = 0), ys[hi] < v (or hi = n)
+  while (hi - lo > 64) {
+    const int64_t step = (hi - lo + 63) / 64;
+    const int64_t i = lo + (int64_t)lane * step;
+    const bool ge = i < hi && ys[i] >= v;
+    const unsigned long long m = __ballot(ge);
+    const int k = __popcll(m);  // samples 0 .. k-1 are >= v (descending)
+    const int64_t nlo = k == 0 ? lo : lo + (int64_t)(k - 1) * step + 1;
+    const int64_t nhi = lo + (int64_t)k * step < hi ? lo + (int64_t)k * step : hi;
+    lo = nlo;
+    hi = nhi;
+  }
+  const int64_t i = lo + lane;
+  const bool ge = i < hi && ys[i] >= v;
+  const int64_t r = lo + __popcll(__ballot(ge));
+  if (lane == 0) cge[p] = r;
+}
+
+// partition p = [c[p+1], c[p]) with c[0] = n, c[P] = 0; block (chunk, p) sums its chunk
+__global__ __launch_bounds__(256) void k_lv_partials(const double* __restrict__ ys, int64_t n, int P,
+                                                     const int64_t* __restrict__ cge, double* __restrict__ part) {
+  const int c = (int)blockIdx.x, p = (int)blockIdx.y, t = (int)threadIdx.x;
+  const int64_t a = p + 1 < P ? cge[p + 1] : 0, b = p > 0 ? cge[p] : n;
+  const int64_t len = b > a ? b - a : 0;
+  const int64_t c0 = a + len * c / LV_CHUNKS, c1 = a + len * (c + 1) / LV_CHUNKS;
+  double s = 0.0;
+  for (int64_t i = c0 + t; i < c1; i += 256) s += ys[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  __shared__ double w[4];
+  if ((t & 63) == 0) w[t >> 6] = s;
+  __syncthreads();
+  if (t == 0) part[(size_t)p * LV_CHUNKS + c] = ((w[0] + w[1]) + w[2]) + w[3];
+}
+
+// stats [P][4] = (count, max, min, sum) (an empty partition: 0, -inf, +inf, 0), then
+// [4] = (ys[0], ys[n-1], bounds[0], bounds[P])
+__global__ __launch_bounds__(256) void k_lv_stats(const double* __restrict__ ys, int64_t n, int P,
+                                                  const double* __restrict__ bounds, const int64_t* __restrict__ cge,
+                                                  const double* __restrict__ part, double* __restrict__ stats) {
+  for (int p = (int)threadIdx.x; p < P; p += 256) {
+    const int64_t a = p + 1 < P ? cge[p + 1] : 0, b = p > 0 ? cge[p] : n;
+    double s = 0.0;
+    for (int c = 0; c < LV_CHUNKS; ++c) s += part[(size_t)p * LV_CHUNKS + c];
+    const bool any = b > a;
+    stats[4 * p + 0] = any ? (double)(b - a) : 0.0;
+    stats[4 * p + 1] = any ? ys[a] : -INFINITY;
+    stats[4 * p + 2] = any ? ys[b - 1] : INFINITY;
+    stats[4 * p + 3] = any ? s : 0.0;
+  }
+  if (threadIdx.x == 0) {
+    stats[4 * P + 0] = ys[0];
+    stats[4 * P + 1] = ys[n - 1];
+    stats[4 * P + 2] = bounds[0];
+    stats[4 * P + 3] = bounds[P];
+  }
+}
+
+size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" int lompc_levels_layout(const double* y, int64_t n, const double* bounds, int P, double* ys, int64_t* perm,
+                                   double* stats, void* work, size_t* work_bytes, void* stream) {
+  if (!work_bytes || n < 1 || n >= (1ll << 31) || P < 1 || P > LV_MAXP) return LOMPC_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  size_t sort_bytes = 0;
+  rocprim::counting_iterator<int64_t> iota(0);
+  if (rocprim::radix_sort_pairs_desc(nullptr, sort_bytes, y, ys, iota, perm, (unsigned)n, 0, 64, st) != hipSuccess)
+    return LOMPC_ERR_HIP;
+  const size_t o_cge = up256(sort_bytes), o_part = o_cge + up256((size_t)(P + 1) * sizeof(int64_t));
+  const size_t need = o_part + (size_t)P * LV_CHUNKS * sizeof(double);
+  if (!work) {
+    *work_bytes = need;
+    return LOMPC_OK;
+  }
+  if (*work_bytes < need || !y || !bounds || !ys || !perm || !stats) return LOMPC_ERR_INVALID_ARG;
+  char* wk = static_cast<char*>(work);
+  if (rocprim::radix_sort_pairs_desc(wk, sort_bytes, y, ys, iota, perm, (unsigned)n, 0, 64, st) != hipSuccess)
+    return LOMPC_ERR_HIP;
+  int64_t* cge = reinterpret_cast<int64_t*>(wk + o_cge);
+  double* part = reinterpret_cast<double*>(wk + o_part);
+  if (P > 1) hipLaunchKernelGGL(k_lv_bounds, dim3((unsigned)(P - 1)), dim3(64), 0, st, ys, n, bounds, cge);
+  hipLaunchKernelGGL(k_lv_partials, dim3(LV_CHUNKS, (unsigned)P), dim3(256), 0, st, ys, n, P, cge, part);
+  hipLaunchKernelGGL(k_lv_stats, dim3(1), dim3(256), 0, st, ys, n, P, bounds, cge, part, stats);
+  return hipGetLastError() == hipSuccess ? LOMPC_OK : LOMPC_ERR_HIP;
+}

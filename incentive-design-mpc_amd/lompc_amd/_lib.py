@@ -92,10 +92,12 @@ SIGNATURES = [
     ("lompc_plan_run", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_plan_run_steps", _I, [_P, _P, _L, _P, _L, _I, _I, _P, _P, _P, _P, _P, _P, _L, _L, _L, _I, _P]),
     ("lompc_plan_run_chain", _I, [_P, _P, _P, _P, _D, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    ("lompc_levels_layout", _I, [_P, _L, _P, _I, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lompc_plan_status", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_get_info", _I, [_P, _P, _P, _P, _P, _P]),
     ("lompc_plan_update", _I, [_P, _L, _P, _P, _P, _P]),
     ("lompc_price_loop", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    ("lompc_price_chain", _I, [_I, _P, _P, _P, _P]),
     ("lompc_plan_profile_enable", _I, [_P, _I]),
     ("lompc_plan_profile_read", _I, [_P, _I, _P, _P, _I]),
     ("lompc_plan_last_error", ctypes.c_char_p, [_P]),
@@ -134,6 +136,16 @@ class PriceLoopArgs(ctypes.Structure):
                 ("host_in", ctypes.c_void_p), ("dev_sw", ctypes.c_void_p), ("dev_st", ctypes.c_void_p),
                 ("host_sw", ctypes.c_void_p), ("host_st", ctypes.c_void_p), ("prof", ctypes.c_void_p),
                 ("device_loop", ctypes.c_int)]
+
+class PriceChainPart(ctypes.Structure):
+    """include/lompc_amd.h lompc_price_chain_part."""
+    _fields_ = [("plan", ctypes.c_void_p), ("n_evs", ctypes.c_double), ("tol", ctypes.c_double),
+                ("w_ref", ctypes.c_void_p), ("dev_sw", ctypes.c_void_p), ("dev_st", ctypes.c_void_p),
+                ("lmbd", ctypes.c_void_p), ("w_k", ctypes.c_void_p), ("dec_actual", ctypes.c_void_p),
+                ("dec_pred", ctypes.c_void_p), ("iterations", ctypes.c_int), ("calls", ctypes.c_int),
+                ("rc", ctypes.c_int), ("pad", ctypes.c_int), ("price_before_reg", ctypes.c_double),
+                ("price_after_reg", ctypes.c_double)]
+
 
 _lock = threading.Lock()
 _lib = None

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(ROOT, "csrc")
 OUT = os.path.join(PKG, "liblompc_amd.so")
 SOURCES = ["lompc_kernels.hip", "lompc_plan.hip", "lompc_price.cpp", "lompc_bimpc.cpp", "lompc_comm.cpp",
-           "lompc_loop.hip"]
+           "lompc_loop.hip", "lompc_levels.hip"]
 # every header under csrc/ (not a hand-kept list: an edit to any included header must rebuild the
 # pushed .so; tests/test_build_deps.py checks each `#include "…"` resolves to a DEPS entry)
 DEPS = SOURCES + sorted(f for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))) + \

@@ -25,6 +25,7 @@ redundantly on identical inputs; the re-draw replays the global random stream.
 from __future__ import annotations
 
 import concurrent.futures
+import ctypes
 import time
 
 from dataclasses import dataclass
@@ -215,6 +216,7 @@ class ChargingStation:
         self.ncharged_l = 0
         n = self._hi - self._lo
         self._bounds = {}
+        self._lv = {}  # lompc_levels_layout's buffers per EV type
         self.idx_s = torch.zeros((n,), dtype=torch.int64, device=self._dev)
         self.idx_l = torch.zeros((n,), dtype=torch.int64, device=self._dev)
         self._update_indices()
@@ -427,9 +429,25 @@ class ChargingStation:
             main = torch.cuda.current_stream(self.device)
 
             def run_chain(chain):
-                solver = chain[1]
+                kind, solver, _, _, st, w_hat, prices, stats = chain
                 # the chain's thread works on its solver's stream (no waits through a shared one)
                 with torch.cuda.device(self.device), torch.cuda.stream(solver._stream):
+                    parts = [p for p in range(self.P) if st[p, 0] > 0]
+                    if self._staged and solver.chain_ok(parts):
+                        # every partition's loop and regularisation in ONE native call (no Python
+                        # between the partitions: the other type's chain runs beside it)
+                        t0 = time.perf_counter() if prof else 0.0
+                        res = dict(zip(parts, solver.compute_optimal_prices_chain(parts, w_hat[parts, :], lmbd_r)))
+                        if prof:
+                            key = f"prices/{kind}/optimal_prices"
+                            self.phase_ms[key] = self.phase_ms.get(key, 0.0) + (time.perf_counter() - t0) * 1e3
+                        for p in range(self.P):
+                            if p in res:
+                                prices[p, :] = res[p][0][: self.r]
+                                stats.append(res[p][1])
+                            else:
+                                stats.append({})
+                        return
                     for p in range(self.P):
                         one(chain, p)
 
@@ -502,17 +520,19 @@ class ChargingStation:
         return [self._stage_pool.submit(stage, job) for job in jobs]
 
     def _sorted_layouts(self):
-        """Both EV types' partition layouts and statistics from ONE sort per type (one rank): y sorted
-        descending, so partition p (charge levels in [rng[p], rng[p+1]], later partitions winning on
-        shared edges, charging_station.py:111-116) is one contiguous run — partition P-1 first — in
-        descending charge level (ascending gamma, as the loop plans want); the runs' bounds come from a
-        searchsorted of the boundaries, max / min from the runs' ends and the sums by a segment
-        reduction.  One host sync for both types.  A type with a charge level outside [rng[0], rng[P]]
+        """Both EV types' partition layouts and statistics from ONE sort per type (one rank), by the
+        extension's lompc_levels_layout: y sorted descending, so partition p (charge levels in
+        [rng[p], rng[p+1]], later partitions winning on shared edges, charging_station.py:111-116) is
+        one contiguous run — partition P-1 first — in descending charge level (ascending gamma, as the
+        loop plans want), with its count / max / min / sum (price_solver.py:66-77) computed on the
+        device.  One host sync for both types.  A type with a charge level outside [rng[0], rng[P]]
         (whose EVs keep their previous partition index, :111-116, so the runs would not be the
         partitions) is left out of the result: the caller takes the index-based path for it.
         Returns {kind: (P, 4) host statistics (count, max, min, sum)}; the layouts go to self._layout."""
         torch = _torch()
         P = self.P
+        lib = _lib.load()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
         parts, recs = [], []
         for kind, y, rng in (("Small", self.y_s, self.y0_s_rng), ("Large", self.y_l, self.y0_l_rng)):
             n = int(y.numel())
@@ -521,35 +541,35 @@ class ChargingStation:
             b = self._bounds.get(id(rng))
             if b is None:
                 b = self._bounds[id(rng)] = torch.as_tensor(rng, dtype=y.dtype, device=y.device)
-            ys, perm = torch.sort(y, descending=True)
-            # c[p] = #{y >= rng[p]}, p = 1 .. P-1 (searchsorted over -ys, ascending); c[0] = n, c[P] = 0
-            c = torch.searchsorted(-ys, -b[1:P], right=True) if P > 1 else torch.zeros(0, dtype=torch.int64,
-                                                                                       device=y.device)
-            z = torch.zeros(1, dtype=torch.int64, device=y.device)
-            cge = torch.cat([torch.full((1,), n, dtype=torch.int64, device=y.device), c, z])  # [P + 1]
-            start, end = cge[1:], cge[:-1]  # partition p: [c[p+1], c[p])
-            cnt = end - start
-            first = start.clamp(max=n - 1)
-            last = (end - 1).clamp(min=0)
-            # segment sums in storage order (partition P-1 first)
-            sums = torch.segment_reduce(ys, "sum", lengths=cnt.flip(0)).flip(0)
-            recs.append(torch.stack([cnt.to(torch.float64), ys[first], ys[last], sums]))
-            recs.append(torch.stack([ys[0], ys[n - 1], b[0], b[P]]).reshape(4, 1).expand(4, P))
-            parts.append((kind, ys, perm, n))
-        h = torch.cat(recs, dim=1).cpu().numpy()  # the one host sync
+            lv = self._lv.get(kind)
+            if lv is None or lv["n"] != n:  # (buffers per type, reused from step to step)
+                wb = ctypes.c_size_t(0)
+                rc = lib.lompc_levels_layout(None, n, None, P, None, None, None, None, ctypes.byref(wb), None)
+                if rc != _lib.LOMPC_OK:
+                    raise ValueError(_lib.status_text(lib, None, rc))
+                e = lambda m, dt: torch.empty(m, dtype=dt, device=y.device)
+                lv = self._lv[kind] = {"n": n, "ys": e(n, torch.float64), "perm": e(n, torch.int64),
+                                       "stats": e(4 * P + 4, torch.float64), "work": e(wb.value, torch.uint8),
+                                       "wb": wb.value}
+            wb = ctypes.c_size_t(lv["wb"])
+            rc = lib.lompc_levels_layout(y.data_ptr(), n, b.data_ptr(), P, lv["ys"].data_ptr(), lv["perm"].data_ptr(),
+                                         lv["stats"].data_ptr(), lv["work"].data_ptr(), ctypes.byref(wb), stream)
+            if rc != _lib.LOMPC_OK:
+                raise RuntimeError(_lib.status_text(lib, None, rc))
+            recs.append(lv["stats"])
+            parts.append((kind, lv["ys"], lv["perm"]))
+        h = torch.cat(recs).cpu().numpy()  # the one host sync
         out = {}
-        for j, (kind, ys, perm, n) in enumerate(parts):
-            st = h[:, 2 * j * P: (2 * j + 1) * P].T.copy()  # (P, 4): count, max, min, sum
-            ymax, ymin, lo, hi = h[:, (2 * j + 1) * P]
+        for j, (kind, ys, perm) in enumerate(parts):
+            rec = h[j * (4 * P + 4): (j + 1) * (4 * P + 4)]
+            st = rec[: 4 * P].reshape(P, 4).copy()  # count, max, min, sum
+            ymax, ymin, lo, hi = rec[4 * P:]
             if not (ymin >= lo and ymax <= hi):  # (NaN fails too)
                 continue
             cnt = st[:, 0].astype(np.int64)
-            st[cnt == 0, 1:] = (-np.inf, np.inf, 0.0)
-            ends = np.cumsum(cnt[::-1])  # storage offsets, partition P-1 first
-            seg = {}
-            for k, p in enumerate(range(P - 1, -1, -1)):
-                seg[p] = (int(ends[k] - cnt[p]), int(ends[k]))
-            self._layout[kind] = (perm, ys, seg)
+            ends = np.cumsum(cnt[::-1])  # runs in storage order, partition P-1 first
+            self._layout[kind] = (perm, ys, {p: (int(ends[k] - cnt[p]), int(ends[k]))
+                                             for k, p in enumerate(range(P - 1, -1, -1))})
             out[kind] = st
         return out
 

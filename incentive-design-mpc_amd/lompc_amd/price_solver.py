@@ -366,6 +366,76 @@ class PriceSolver:
         return self._finish_prices(lmbd_k, w_k, iter, dual_cost_decrease_ac, dual_cost_decrease_pred, lmbd_r, w_ref,
                                    A_bar, tol, w0_err_bound)
 
+    def chain_ok(self, parts) -> bool:
+        """compute_optimal_prices_chain applies: PRINT_LEVEL 0 (nothing printed per partition), one
+        rank, the native loop on (not profiling it), every staged partition's plan a PATH plan."""
+        if _settings.PRINT_LEVEL >= 1 or not self.native_loop or self.group is not None:
+            return False
+        return all(p in self._staged and self._staged[p]["_plan"] is not None and not self._staged[p]["_plan"].direct
+                   for p in parts)
+
+    def compute_optimal_prices_chain(self, parts, w_refs, lmbd_r: float):
+        """compute_optimal_prices for the staged partitions ``parts`` in order, each starting from
+        the previous one's prices (charging_station.py:275-307 with price_solver.py:79-174), in ONE
+        native call (lompc_price_chain): no Python between the partitions' loops.  w_refs: (len(parts),
+        N).  Returns [(lmbd (3N,), solver_stats)] per part, as compute_optimal_prices would; the
+        solver's prev_prices end as the last part's."""
+        MAX = _settings.MAX_PRICE_SOLVER_ITERATIONS
+        N, r = self.N, self.r
+        n = len(parts)
+        if n == 0:
+            return []
+        A_bar, A_bar_inv = self._get_w_inner_product_metric(lmbd_r)
+        A_bar = np.ascontiguousarray(A_bar, dtype=np.float64)
+        w_refs = np.ascontiguousarray(np.asarray(w_refs, dtype=np.float64).reshape(n, N))
+        lm = np.zeros((n, 3 * N))
+        wk = np.zeros((n, N))
+        dec = np.zeros((n, 2, MAX))
+        arr = (_lib.PriceChainPart * n)()
+        for k, p in enumerate(parts):
+            st = self._staged[p]
+            plan = st["_plan"]
+            plan._usable()
+            tol = np.sqrt(self.N) * st["y0_rng"] + self.eps_tol  # get_robustness_bounds (price_solver.py:182-186)
+            q = arr[k]
+            q.plan = plan._plan.value
+            q.n_evs, q.tol = float(st["nEVs"]), float(tol)
+            q.w_ref = w_refs[k].ctypes.data
+            q.dev_sw, q.dev_st = plan.out["set_sum_w"].data_ptr(), plan.out["set_stats"].data_ptr()
+            q.lmbd, q.w_k = lm[k].ctypes.data, wk[k].ctypes.data
+            q.dec_actual, q.dec_pred = dec[k, 0].ctypes.data, dec[k, 1].ctypes.data
+        args = _lib.PriceLoopArgs(
+            N, r, MAX, 1 if _settings.PRICE_SOLVER_TOL_TYPE != "max" else 0, float(self.consts.theta),
+            float(self.consts.w_max), float(self.m), float(self._kappa_of(A_bar_inv)), float(self.eps_reg), 0.0, 0.0,
+            float(lmbd_r), A_bar.ctypes.data, None, self._in.data_ptr(), self._h_in.data_ptr(), None, None,
+            self._h_sw.data_ptr(), self._h_st.data_ptr(), self.loop_prof.ctypes.data if self.profile_loops else None,
+            1 if self.device_loop else 0)
+        prev = np.ascontiguousarray(self.prev_prices, dtype=np.float64).copy()
+        t0 = time.perf_counter()
+        rc = self._lib.lompc_price_chain(n, ctypes.cast(arr, ctypes.c_void_p), ctypes.byref(args), prev.ctypes.data,
+                                         self._stream.cuda_stream)
+        if self.profile_loops:
+            self.loop_host_ms["native_loop"] += (time.perf_counter() - t0) * 1e3
+        self.n_batched_calls += sum(int(arr[k].calls) for k in range(n))
+        if rc != _lib.LOMPC_OK:
+            k = next((k for k in range(n) if arr[k].rc), n - 1)
+            text = self._lib.lompc_plan_last_error(arr[k].plan).decode(errors="replace")
+            if rc == _lib.LOMPC_ERR_NOT_CONVERGED:
+                raise SolverError(text)
+            if "gamma" in text:
+                raise AssertionError(text)
+            raise ValueError(text or _lib.status_text(self._lib, None, rc))
+        self.prev_prices = prev
+        out = []
+        for k in range(n):
+            q = arr[k]
+            m = q.calls - 1  # (decreases recorded: one per step taken)
+            out.append((lm[k], {"iter": int(q.iterations), "price_before_reg": float(q.price_before_reg),
+                                "price_after_reg": float(q.price_after_reg),
+                                "dual_cost_decrease_actual": dec[k, 0, :m].copy(),
+                                "dual_cost_decrease_predicted": dec[k, 1, :m].copy()}))
+        return out
+
     def _native_loop(self, lmbd_k, lmbd_r, w_ref, A_bar, tol):
         """price_solver.py:106-140 in ONE call (lompc_price_loop): plan runs, copies, syncs and
         price steps stay in C++ until convergence."""

@@ -264,6 +264,21 @@ int lompc_plan_run_chain(lompc_plan* plan, const double* lmbd0, const double* lm
                          double step, int n_runs, double* lmbd_out, double* w, double* cost, double* w0,
                          int8_t* status, double* set_sum_w, double* set_stats, void* stream);
 
+/* The charging station's partition layout of one EV type's charge levels (replaces
+ * ChargingStation._update_indices' masks, charging_station.py:111-116, and the per-partition
+ * statistics of PriceSolver.set_charge_levels, price_solver.py:66-77, taken at
+ * charging_station.py:196-210).  y dev [n] levels, bounds dev [P+1] the partition boundaries
+ * (rng, increasing).  Sorts the levels in descending order (ys dev [n], perm dev [n] int64: ys[k] =
+ * y[perm[k]]; stable: ties keep index order), so partition p — levels in [rng[p], rng[p+1]], later
+ * partitions winning on shared edges — is the run [c[p+1], c[p]) with c[p] = #{y >= rng[p]}, c[0] = n,
+ * c[P] = 0 (partition P-1 first); stats dev [4P + 4] = per partition (count, max, min, sum) (empty:
+ * 0, -inf, +inf, 0), then (max y, min y, rng[0], rng[P]): the runs are the reference's partitions only
+ * when min y >= rng[0] and max y <= rng[P] (outside it an EV keeps its previous index) — the caller
+ * checks.  work: dev scratch of *work_bytes; work == NULL: *work_bytes = the size needed, nothing runs.
+ * n < 2^31, 1 <= P <= 256.  Asynchronous on ``stream``. */
+int lompc_levels_layout(const double* y, int64_t n, const double* bounds, int P, double* ys, int64_t* perm,
+                        double* stats, void* work, size_t* work_bytes, void* stream);
+
 /* Synchronise ``stream``; EVs repaired / failed / invalid summed over EVERY run since the previous
  * lompc_plan_status call (sticky device tallies, zeroed here), so a failure in any of the runs of a
  * lompc_plan_run_steps call or of a price loop is seen.  These count this rank's EVs only; with a
@@ -372,6 +387,27 @@ typedef struct lompc_price_loop_args {
 int lompc_price_loop(lompc_plan* plan, const lompc_price_loop_args* args, double* lmbd, double* w_k,
                      double* dual_cost, double* dec_actual, double* dec_pred, int* iterations,
                      double* errs, void* stream);
+
+/* One EV type's partitions in order, ONE call (charging_station.py:275-307, whose loop over the
+ * partitions chains them through prev_prices): for every part with a plan, lompc_price_loop from
+ * the previous part's regularised prices (common args with the part's n_evs, tol, w_ref and set
+ * outputs), then the regularisation of price_solver.py:142-147 / 248-255 (lompc_lp_separable on
+ * A = Dphi(w)', b = A lmbd, c = phi(w)); a part without a plan (no EVs) is skipped.  prev_prices
+ * host [r] in / out.  Per part: lmbd host [3N] (its final prices), w_k host [N], dec_actual /
+ * dec_pred host [max_iter] (may be NULL), and on return iterations (the reference's `iter`),
+ * calls (engine calls made), price_before_reg / price_after_reg (phi(w)'lmbd before / after), rc.
+ * Stops at the first failing part (its rc, also returned; lompc_plan_last_error of its plan). */
+typedef struct lompc_price_chain_part {
+  lompc_plan* plan;
+  double n_evs, tol;
+  const double* w_ref;
+  const double* dev_sw; const double* dev_st;
+  double* lmbd; double* w_k; double* dec_actual; double* dec_pred;
+  int iterations, calls, rc, pad;
+  double price_before_reg, price_after_reg;
+} lompc_price_chain_part;
+int lompc_price_chain(int n_parts, lompc_price_chain_part* parts, const lompc_price_loop_args* common,
+                      double* prev_prices, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Host-side solvers of the price iteration (no device, no context).  They run

@@ -48,7 +48,8 @@ for s in $STEPS; do
     stampsrt) run stampsrt 300 env KS_RT=1 KS_VARIANT=rt python scripts/kstamps.py 24 ;;
     # the driver's exact command under the kernel trace: where the wall time per step goes
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-station --no-direct ;;
-    r5new) run r5new 600 $PYT tests/test_gpu_chain.py tests/test_gpu_price_loop_c5.py -m gpu ;;
+    r5new) run r5new 600 $PYT tests/test_gpu_chain.py tests/test_gpu_price_loop_c5.py tests/test_gpu_levels.py -m gpu ;;
+    stationt) run stationt 600 $PYT tests/test_gpu_station.py tests/test_gpu_example.py -m gpu ;;
     benchq) run benchq 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-station --no-direct ;;
     *) echo "unknown step $s" ;;
   esac

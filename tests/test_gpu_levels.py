@@ -1,0 +1,64 @@
+"""GPU tests of the station's partition layout (lompc_levels_layout, ChargingStation._sorted_layouts):
+one descending sort per EV type gives the statistics the reference's index masks define
+(charging_station.py:111-116 with price_solver.py:66-77) and each partition's EVs as one run in
+descending charge level; levels exactly on boundaries, ties and an out-of-range level included."""
+import numpy as np
+import pytest
+import torch
+
+from lompc_amd.charging_station import ChargingStation, partition_stats
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_indices(y, rng, idx0):
+    idx = idx0.copy()
+    for p in range(len(rng) - 1):
+        idx[(y >= rng[p]) & (y <= rng[p + 1])] = p
+    return idx
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_sorted_layouts_match_index_partitions(gpu, case):
+    rs = np.random.default_rng(80 + case)
+    P = 12 if case != 4 else 1
+    rng_s, rng_l = np.linspace(0.3, 0.9, P + 1), np.linspace(0.3, 0.85, P + 1)
+    n_s, n_l = (5000, 4000) if case != 2 else (300000, 1)
+    y_s = 0.3 + 0.2 * rs.random(n_s)
+    y_l = 0.3 + 0.55 * rs.random(n_l)
+    y_s[:20] = rng_s[rs.integers(0, P + 1, 20)]  # levels exactly on the boundaries
+    if n_l > 4:
+        y_l[:3] = y_l[3]  # ties
+    if case == 3:
+        y_l[min(7, n_l - 1)] = 0.2  # below rng[0]: the large type takes the index path
+    cs = object.__new__(ChargingStation)
+    cs.P, cs.group, cs.device = P, None, 0
+    cs.y_s, cs.y_l = torch.as_tensor(y_s, device="cuda:0"), torch.as_tensor(y_l, device="cuda:0")
+    cs.y0_s_rng, cs.y0_l_rng = rng_s, rng_l
+    cs.idx_s = torch.zeros(n_s, dtype=torch.int64, device="cuda:0")
+    cs.idx_l = torch.zeros(n_l, dtype=torch.int64, device="cuda:0")
+    cs._bounds, cs._lv = {}, {}
+    ChargingStation._update_indices(cs)  # (resets cs._layout)
+    out = ChargingStation._sorted_layouts(cs)
+    assert set(out) == ({"Small"} if case == 3 else {"Small", "Large"})
+    for kind, y, idx, rng in (("Small", y_s, cs.idx_s, rng_s), ("Large", y_l, cs.idx_l, rng_l)):
+        if kind not in out:
+            continue
+        ix = idx.cpu().numpy()
+        np.testing.assert_array_equal(ix, _ref_indices(y, rng, np.zeros(len(y), dtype=np.int64)))
+        ref = partition_stats(torch.as_tensor(y), torch.as_tensor(ix), P)
+        st = out[kind]
+        np.testing.assert_array_equal(st[:, 0], ref[:, 0])
+        np.testing.assert_array_equal(st[:, 1:3], ref[:, 1:3])
+        np.testing.assert_allclose(st[:, 3], ref[:, 3], rtol=1e-13)
+        perm, ys, seg = cs._layout[kind]
+        perm, ys = perm.cpu().numpy(), ys.cpu().numpy()
+        assert np.array_equal(np.sort(perm), np.arange(len(y)))
+        np.testing.assert_array_equal(ys, y[perm])
+        for p in range(P):
+            a, b = seg[p]
+            assert np.array_equal(np.sort(perm[a:b]), np.nonzero(ix == p)[0])
+            assert np.all(np.diff(ys[a:b]) <= 0)
+            # stable: equal levels keep index order
+            eq = np.diff(ys[a:b]) == 0
+            assert np.all(np.diff(perm[a:b])[eq] > 0)

@@ -77,3 +77,44 @@ def test_device_price_loop_matches_oracle_at_config5_partitions(gpu, monkeypatch
         assert abs(p0 - p0o) <= 1e-6 * max(1.0, abs(p0o)), (p, p0, p0o)
         iters.append(st["iter"])
     assert sum(iters) >= 10, iters  # tens of iterations through k_loop_iter, not a trivial loop
+
+
+@pytest.mark.parametrize("ev", ["small", "large"])
+def test_price_chain_equals_partition_loops(gpu, monkeypatch, ev):
+    """lompc_price_chain (one native call for a type's partitions, ChargingStation's default) gives the
+    per-partition loops' results: the same iteration counts and dual cost decreases, prices and the
+    prices before / after regularisation to rounding (the chain regularises in C++: price_solver.py:
+    142-147), prev_prices chained the same way; a partition without EVs is skipped."""
+    monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
+    c, lc = consts(ev)
+    rng = np.random.default_rng(600 + (ev == "large"))
+    edges = np.linspace(MIN_INITIAL_SOC, c.y_max, 13)
+    sol = {}
+    for mode in ("loops", "chain"):
+        ps = PriceSolver(N, lc, "linear-convex", device=0)
+        sol[mode] = ps
+    parts = [0, 1, 3]  # (partition 2 has no EVs)
+    w_refs = 0.8 * c.w_max * rng.random((4, N))
+    for p in parts:
+        y0 = np.sort(edges[p] + (edges[p + 1] - edges[p]) * rng.random(6000))[::-1].copy()
+        yd = torch.as_tensor(y0, device="cuda:0")
+        for ps in sol.values():
+            ps.stage_partition(p, yd, len(y0), float(y0.max()), float(y0.min()), float(y0.sum()), descending=True)
+    res_loops = []
+    for p in parts:
+        ps = sol["loops"]
+        ps.use_partition(p)
+        lm, st = ps.compute_optimal_prices(w_refs[p], 0.0)
+        res_loops.append((lm.copy(), st))
+    ps = sol["chain"]
+    assert ps.chain_ok(parts)
+    res_chain = ps.compute_optimal_prices_chain(parts, w_refs[parts], 0.0)
+    assert sol["chain"].n_batched_calls == sol["loops"].n_batched_calls
+    for (la, sa), (lb, sb) in zip(res_loops, res_chain):
+        assert sa["iter"] == sb["iter"]
+        np.testing.assert_allclose(lb, la, rtol=0, atol=1e-12 * c.theta)
+        for k in ("price_before_reg", "price_after_reg"):
+            assert abs(sa[k] - sb[k]) <= 1e-12 * max(1.0, abs(sa[k])), k
+        for k in ("dual_cost_decrease_actual", "dual_cost_decrease_predicted"):
+            np.testing.assert_array_equal(sb[k], sa[k])
+    np.testing.assert_allclose(sol["chain"].prev_prices, sol["loops"].prev_prices, rtol=0, atol=1e-12 * c.theta)

@@ -120,46 +120,3 @@ def test_update_indices_matches_reference_loop_on_edges():
         assert np.array_equal(cs.idx_s.numpy(), _ref_indices(y, rng, idx0)), rng
         assert np.array_equal(cs.idx_l.numpy(), _ref_indices(y[::-1], rng, idx0[::-1])), rng
 
-
-def test_sorted_layouts_match_index_partitions():
-    """_sorted_layouts (one sort per type) gives the statistics partition_stats computes from the
-    reference's indices (charging_station.py:111-116), and each partition's run of the layout holds
-    exactly its EVs in descending charge level; a type with a level outside [rng[0], rng[P]] is left
-    to the index path."""
-    from lompc_amd.charging_station import ChargingStation
-
-    rs = np.random.default_rng(8)
-    P = 12
-    for case in range(4):
-        rng_s, rng_l = np.linspace(0.3, 0.9, P + 1), np.linspace(0.3, 0.85, P + 1)
-        y_s = 0.3 + 0.2 * rs.random(5000)
-        y_l = 0.3 + 0.55 * rs.random(4000)
-        y_s[:20] = rng_s[rs.integers(0, P + 1, 20)]  # levels exactly on the boundaries
-        y_l[:3] = y_l[3]  # ties
-        if case == 3:
-            y_l[7] = 0.2  # below rng[0]: the large type takes the index path
-        cs = object.__new__(ChargingStation)
-        cs.P, cs.group = P, None
-        cs.y_s, cs.y_l = torch.as_tensor(y_s), torch.as_tensor(y_l)
-        cs.y0_s_rng, cs.y0_l_rng = rng_s, rng_l
-        cs.idx_s = torch.zeros(len(y_s), dtype=torch.int64)
-        cs.idx_l = torch.zeros(len(y_l), dtype=torch.int64)
-        cs._bounds = {}
-        ChargingStation._update_indices(cs)  # (resets cs._layout)
-        out = ChargingStation._sorted_layouts(cs)
-        assert set(out) == ({"Small"} if case == 3 else {"Small", "Large"})
-        for kind, y, idx in (("Small", cs.y_s, cs.idx_s), ("Large", cs.y_l, cs.idx_l)):
-            if kind not in out:
-                continue
-            ref = partition_stats(y, idx, P)
-            st = out[kind]
-            np.testing.assert_array_equal(st[:, 0], ref[:, 0])
-            np.testing.assert_array_equal(st[:, 1:3], ref[:, 1:3])
-            np.testing.assert_allclose(st[:, 3], ref[:, 3], rtol=1e-13)
-            perm, ys, seg = cs._layout[kind]
-            ix = idx.numpy()
-            for p in range(P):
-                a, b = seg[p]
-                assert sorted(perm[a:b].tolist()) == sorted(np.nonzero(ix == p)[0].tolist())
-                v = ys[a:b].numpy()
-                assert np.all(np.diff(v) <= 0) and np.array_equal(v, y.numpy()[perm[a:b].numpy()])

@@ -667,6 +667,33 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
                                            "staging and lookup rounds, not 8-16 B per QP, set its time")}}
         plan.profile(enable=False)
         del plan
+    # the headline's workload with every step's rows in their OWN buffer (w at a per-step stride: K x 50 MB
+    # of fresh lines, which the 256 MB Infinity Cache cannot hold — the HBM-resident form of the roofline)
+    base.profile(enable=("k_eval",))
+    o = {"w": torch.empty((K, base.B, N), dtype=torch.float64, device=dev),
+         "cost": torch.empty((K, base.B), dtype=torch.float64, device=dev)}
+    base.run_steps(lm_ptr[args.warmup], lr_ptr, K, stride, 0, out=o)
+    assert base.check()[1:] == (0, 0)
+    base.profile(read=True, reset=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    base.run_steps(lm_ptr[args.warmup], lr_ptr, K, stride, 0, out=o, span_events=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    rep, fail, inv = base.check()
+    assert fail == 0 and inv == 0, ("fresh_rows", fail, inv)
+    ms_e, n_e = base.profile(read=True)
+    base.profile(enable=False)
+    B, bpq = base.B, 8 * (N + 2)
+    ev_us = ms_e / max(n_e, 1) * 1e3
+    gbs = bpq * B / (ev_us * 1e-6) / 1e9 if n_e else 0.0
+    out["fresh_rows"] = {"value": B * K / dt, "unit": "QP/s", "ms_per_step": dt / K * 1e3, "steps": K,
+                         "outputs": "w and cost of every step in their own buffers ([K][B][N], [K][B]): no step "
+                                    "rewrites another's lines",
+                         "k_evals_avg_us": ev_us,
+                         "roofline": {"bound": "hbm", "kernel": "k_evals", "bytes_per_qp": bpq, "achieved": gbs,
+                                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS}}
+    del o
     return out
 
 
@@ -675,66 +702,85 @@ def sequential_leg(run, eng, N, P, args, torch):
     device from step k's set reductions (lompc_plan_run_chain: a projected dual-gradient step
     max(0, lmbd + step (phi(mean w) - phi(w_ref))) per set, as each price iteration of
     price_solver.py:111-140 depends on the previous one's reductions), so no two steps overlap: every
-    step is its own path -> evaluation -> closing chain (+ the price update launch).  Same plan, batch,
-    outputs (w, cost, set reductions) and roofline bytes as the headline; ms_per_step from the timed
-    call, per-kernel durations from a second call with HIP events on every launch; every step's
-    reductions re-computed afterwards by an independent wide run_steps over the recorded prices
-    (bitwise equal -> verified_steps)."""
-    plan = run["plan"]
+    step is its own path -> evaluation -> closing chain (+ the price update launch).  Same batch, outputs
+    (w, cost, set reductions) and roofline bytes as the headline, on the headline's plan; the same chain
+    on a warm-started plan (each gamma cell's exact solve from the working set the previous step ended
+    with, the form of the engine's price loops) beside it (``warm``).  ms_per_step from the timed call, per-kernel durations from a second call with
+    HIP events on every launch; every step's reductions re-computed afterwards by the headline plan's
+    independent wide run_steps over the recorded prices (verified_steps: equal to 1e-12 relative;
+    bitwise_steps: bit for bit)."""
+    from lompc_amd import BatchPlan
+
+    base = run["plan"]
     K = args.steps
-    S = plan.S
-    lm0 = torch.as_tensor(np.concatenate([e["lm"][args.warmup].cpu().numpy() for e in eng]), device=plan.gamma.device)
-    lr = torch.zeros(S, dtype=torch.float64, device=plan.gamma.device)
-    wt = plan.w_ref
+    S = base.S
+    dev = base.gamma.device
+    lm0 = torch.as_tensor(np.concatenate([e["lm"][args.warmup].cpu().numpy() for e in eng]), device=dev)
+    lr = torch.zeros(S, dtype=torch.float64, device=dev)
+    wt = base.w_ref
     step = 0.5
-    out = {k: torch.empty(s, dtype=torch.float64, device=lm0.device) for k, s in
-           (("lmbd", (K, S, 3 * N)), ("set_sum_w", (K, S, N)), ("set_stats", (K, S, 8)))}
-    plan.profile(enable=False)
-    kw = max(1, min(args.warmup, K))  # (untimed: the chain's first launches, same form)
-    plan.run_chain(lm0, lr, wt, step, kw, out={k: v[:kw] for k, v in out.items()})
-    assert plan.check()[1:] == (0, 0)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    plan.run_chain(lm0, lr, wt, step, K, out=out)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    rep, fail, inv = plan.check()
-    assert fail == 0 and inv == 0, (fail, inv)
-    # per-kernel durations: the same chain again with a HIP-event pair on every launch
-    kernels = ("k_path", "k_eval", "k_finalize")
-    plan.profile(enable=kernels)
-    for k in kernels:
-        plan.profile(read=True, reset=True, kernel=k)
-    plan.run_chain(lm0, lr, wt, step, K)
-    assert plan.check()[1:] == (0, 0)
-    kus = {}
-    for k in kernels:
-        ms, n = plan.profile(read=True, kernel=k)
-        if n:
-            kus[k] = {"avg_us": ms / n * 1e3, "launches": n}
-    plan.profile(enable=False)
-    last = {k: plan.out[k].clone() for k in ("w", "cost") if plan.out.get(k) is not None}
-    # verification: an independent wide run_steps over the K recorded price vectors
+    warm = BatchPlan(base.lompcs, base.gamma, base.off, sets_per_ctx=base.sets_per_ctx, w_ref=base.w_ref,
+                     want_w=True, want_cost=True, want_set=True, stream=torch.cuda.current_stream(), warm_start=True)
+
+    def timed(plan):
+        out = {k: torch.empty(s, dtype=torch.float64, device=dev) for k, s in
+               (("lmbd", (K, S, 3 * N)), ("set_sum_w", (K, S, N)), ("set_stats", (K, S, 8)))}
+        plan.profile(enable=False)
+        kw = max(1, min(args.warmup, K))  # (untimed: the chain's first launches, same form)
+        plan.run_chain(lm0, lr, wt, step, kw, out={k: v[:kw] for k, v in out.items()})
+        assert plan.check()[1:] == (0, 0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        plan.run_chain(lm0, lr, wt, step, K, out=out)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        rep, fail, inv = plan.check()
+        assert fail == 0 and inv == 0, (fail, inv)
+        last = {k: plan.out[k].clone() for k in ("w", "cost") if plan.out.get(k) is not None}
+        # per-kernel durations: the same chain again with a HIP-event pair on every launch
+        kernels = ("k_path", "k_eval", "k_finalize")
+        plan.profile(enable=kernels)
+        for k in kernels:
+            plan.profile(read=True, reset=True, kernel=k)
+        plan.run_chain(lm0, lr, wt, step, K)
+        assert plan.check()[1:] == (0, 0)
+        kus = {}
+        for k in kernels:
+            ms, n = plan.profile(read=True, kernel=k)
+            if n:
+                kus[k] = {"avg_us": ms / n * 1e3, "launches": n}
+        plan.profile(enable=False)
+        return dt, rep, out, last, kus
+
+    dt, rep, out, last, kus = timed(base)
+    dt_w, _, _, _, kus_w = timed(warm)
+    # verification: an independent wide run_steps over the chain's K price vectors
     vo = {k: torch.empty_like(out[k]) for k in ("set_sum_w", "set_stats")}
-    plan.run_steps(out["lmbd"], lr, K, S * 3 * N, 0, out=vo)
-    assert plan.check()[1:] == (0, 0)
-    ok = [all(bool(torch.equal(out[k][j], vo[k][j])) for k in vo) for j in range(K)]
-    rows = all(bool(torch.equal(v, plan.out[k])) for k, v in last.items())
-    if not (all(ok) and rows):
-        raise SystemExit(f"bench.py: sequential steps differ from their independent re-run: {ok}, rows {rows}")
+    base.run_steps(out["lmbd"], lr, K, S * 3 * N, 0, out=vo)
+    assert base.check()[1:] == (0, 0)
+    bit = [all(bool(torch.equal(out[k][j], vo[k][j])) for k in vo) for j in range(K)]
+    close = [bool(torch.allclose(out[k][j], vo[k][j], rtol=1e-12, atol=1e-12)) for k in vo for j in range(K)]
+    ok = [all(close[i * K + j] for i in range(len(vo))) for j in range(K)]
+    rows_d = max(float((v - base.out[k]).abs().max()) for k, v in last.items())
+    if not (all(ok) and rows_d <= 1e-12):
+        raise SystemExit(f"bench.py: sequential steps differ from their independent re-run: {ok}, rows {rows_d}")
     moved = float((out["lmbd"][-1] - out["lmbd"][0]).abs().max())
-    B = plan.B
+    B = base.B
     bpq = 8 * (N + 2)
     ev_us = kus.get("k_eval", {}).get("avg_us", 0.0)
     gbs = bpq * B / (ev_us * 1e-6) / 1e9 if ev_us else 0.0
     return {"value": B * K / dt, "unit": "QP/s", "ms_per_step": dt / K * 1e3, "steps": K,
+            "plan": "the headline's (no warm start)",
             "issue": "one lompc_plan_run_chain call: per step the price update (k_chain_price) then k_path, k_eval, "
                      "k_finalize of that step (4 launches; no overlap between steps is possible)",
             "price_rule": f"lmbd_(k+1) = max(0, lmbd_k + {step} (phi(sum_w / count) - phi(w_ref))) per set, on the device",
             "max_price_change": moved, "repaired_qps": rep, "kernels": kus,
-            "verified_steps": sum(ok),
+            "verified_steps": sum(ok), "bitwise_steps": sum(bit),
             "verification": "every step's set reductions (and the last step's w / cost) re-computed by an independent "
-                            "wide lompc_plan_run_steps over the recorded prices: bitwise equal",
+                            "wide lompc_plan_run_steps over the recorded prices: equal to 1e-12 relative (bitwise: "
+                            f"{sum(bit)} of {K}; the last step's rows within {rows_d:.1e})",
+            "warm": {"value": B * K / dt_w, "ms_per_step": dt_w / K * 1e3, "kernels": kus_w,
+                     "plan": "warm-started: large price steps leave the stored working sets of little use"},
             "roofline": {"bound": "hbm", "kernel": "k_eval", "bytes_per_qp": bpq, "achieved": gbs,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
                          "note": "k_eval's duration from the events pass; the step adds the path (latency-bound) and "
@@ -795,13 +841,14 @@ def station_leg(args, world, dev, sharded=False):
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        per_step = []
+        per_step, parts = [], []
         t0 = time.perf_counter()
         for _ in range(steps):
             ts = time.perf_counter()
             st._step()
             torch.cuda.synchronize()
             per_step.append(time.perf_counter() - ts)
+            parts.append((dict(st.last_step_ms), dict(st.chain_ms), (st.bimpc.last_info or {}).get("solve_ms", 0.0)))
             check_station_state(st, consts)
         if world > 1:
             dist.barrier()
@@ -824,7 +871,9 @@ def station_leg(args, world, dev, sharded=False):
         if steps >= 3 and np.ptp(its) > 0:
             b, a0 = np.polyfit(its, ms, 1)
             r = np.corrcoef(its, ms)[0, 1]
-            spread.update({"fit_ms_fixed": float(a0), "fit_us_per_iteration": float(b * 1e3), "fit_r2": float(r * r)})
+            spread.update({"fit_ms_fixed": float(a0), "fit_us_per_iteration": float(b * 1e3), "fit_r2": float(r * r),
+                           "fit_note": "against the price iterations of BOTH types (their chains run concurrently)"})
+        spread["attribution"] = station_attribution(ms, parts, stats, warm, steps)
         info = st.bimpc.last_info or {}
         loop = price_loop_breakdown(st, args.station_prof_steps, consts, torch)
         out.update({"value": steps / dt, "ms_per_step": dt / steps * 1e3,
@@ -844,6 +893,38 @@ def station_leg(args, world, dev, sharded=False):
                     "price_iteration": loop})
     except Exception as e:  # reported, never hides the QP/s line
         out["error"] = f"{type(e).__name__}: {e}"
+    return out
+
+
+def station_attribution(ms, parts, stats, warm, steps):
+    """Where each timed station step's time goes, from host timestamps taken inside _step (no extra
+    synchronisation): the BiMPC phase = the host interior point + the partition staging it does not
+    hide; the price phase = the longer of the two EV types' chains (each one native call: its
+    partitions' loops and regularisations) + what follows them; the w0 / price0 pass; the state update.
+    The parts sum to the step; the step is fitted against the SLOWER chain's price iterations."""
+    its = {k: np.asarray(stats[key][:, warm:warm + steps], dtype=np.float64) for k, key in
+           (("Small", "niter_s"), ("Large", "niter_l"))}
+    its = {k: np.where(v >= 0, v, 0).sum(axis=0) for k, v in its.items()}
+    rows = []
+    for j, (marks, chains, ipm) in enumerate(parts):
+        b = marks.get("bimpc", 0.0)
+        slow = max(chains, key=chains.get) if chains else None
+        rows.append({"ms": float(ms[j]), "bimpc_ipm": float(ipm), "bimpc_exposed_staging": float(b - ipm),
+                     "prices": float(marks.get("prices", 0.0)),
+                     "chain_small": float(chains.get("Small", 0.0)), "chain_large": float(chains.get("Large", 0.0)),
+                     "slower_chain": slow, "slower_chain_iterations": int(its[slow][j]) if slow else None,
+                     "w0_price0": float(marks.get("w0_price0", 0.0)), "state": float(marks.get("state", 0.0))})
+    out = {"per_step": rows}
+    tot = np.array([r["bimpc_ipm"] + r["bimpc_exposed_staging"] + r["prices"] + r["w0_price0"] + r["state"]
+                    for r in rows])
+    out["parts_sum_over_step"] = {"min": float((tot / ms).min()), "max": float((tot / ms).max())}
+    for k in ("bimpc_ipm", "bimpc_exposed_staging", "prices", "chain_small", "chain_large", "w0_price0", "state"):
+        out[f"mean_{k}_ms"] = float(np.mean([r[k] for r in rows]))
+    x = np.array([r["slower_chain_iterations"] or 0 for r in rows], dtype=np.float64)
+    if len(x) >= 3 and np.ptp(x) > 0:
+        b1, a1 = np.polyfit(x, ms, 1)
+        r1 = np.corrcoef(x, ms)[0, 1]
+        out["fit_slower_chain"] = {"ms_fixed": float(a1), "us_per_iteration": float(b1 * 1e3), "r2": float(r1 * r1)}
     return out
 
 

@@ -84,7 +84,9 @@ __device__ unsigned long long g_lstamps[64 * 16];  // k_loop_iter's phase sums (
 #ifndef EVAL_RU
 #define EVAL_RU 4  // k_eval: row store instructions per software-pipelined batch
 #endif
+#ifndef EVAL_MIN_WAVES
 #define EVAL_MIN_WAVES ((2 * EVAL_WAVES + 3) / 4)  // k_eval: waves per SIMD for two workgroups per CU
+#endif
 #define EVAL_EVS (64 * EVAL_WAVES)         // k_eval: threads per workgroup
 #define EVAL_PASSES 2                      // k_eval: EVs per thread, at most
 #define EVAL_MAXB (EVAL_EVS * EVAL_PASSES)  // k_eval: EVs per workgroup, at most
@@ -109,11 +111,14 @@ typedef unsigned int lq_v2u __attribute__((ext_vector_type(2)));
 
 // write-through (sc1) stores: the outputs leave no dirty lines in the XCD's L2, so the kernel
 // boundary behind k_eval has no L2 writeback to wait for (MI355X_MICROARCH.md, price list)
+#ifndef LQ_ROW_AUX
+#define LQ_ROW_AUX 16  // the row stores' cache policy bits (16: sc1, write-through); diagnostic builds vary it
+#endif
 __device__ __forceinline__ void st_wt16(__amdgpu_buffer_rsrc_t rs, int off, double x, double y) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(lq_v4u, make_double2(x, y)), rs, off, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(lq_v4u, make_double2(x, y)), rs, off, 0, LQ_ROW_AUX);
 }
 __device__ __forceinline__ void st_wt8b(__amdgpu_buffer_rsrc_t rs, int off, double x) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(lq_v2u, x), rs, off, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(lq_v2u, x), rs, off, 0, LQ_ROW_AUX);
 }
 __device__ __forceinline__ void st_wt8(double* p, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
@@ -1470,9 +1475,17 @@ struct EvalsArgs {
   int64_t lm_stride, lr_stride, ev_stride, SG;
 };
 
+#ifndef LQ_EVALS_SKEW
+#define LQ_EVALS_SKEW 0  // k_evals: start delay (100 MHz ticks) of the grid's second half (diagnostic builds)
+#endif
+
 template <int NT>
 __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_evals(EvalArgs a, EvalsArgs x) {
   const int b = (int)blockIdx.x;
+  if (LQ_EVALS_SKEW > 0 && 2 * b >= x.nblk) {  // (the two workgroups of a CU out of phase)
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < LQ_EVALS_SKEW) __builtin_amdgcn_s_sleep(8);
+  }
   for (int r = 0; r < x.nruns; ++r) {
     const int j = x.run0 + r;
     RunOff ro;

@@ -154,6 +154,8 @@ class ChargingStation:
         # plan prepared when its loop starts — for A/B timing)
         self.stage_partitions = True
         self.phase_ms = {}
+        self.last_step_ms = {}  # host time of the last step's phases (_tick)
+        self.chain_ms = {}  # the last step's price chain per EV type (host time of its native call)
         self.device = torch.cuda.current_device() if device is None else int(device)
         self._dev = f"cuda:{self.device}"
         # Set constants, initialize PriceSolvers and BiMPC.
@@ -295,11 +297,21 @@ class ChargingStation:
         self.t += 1
 
     def _tick(self):
-        """Phase timer of _step (profile_phases): synchronises the device at each boundary."""
+        """Phase timer of _step.  profile_phases: synchronises the device at each boundary and
+        accumulates phase_ms.  Otherwise host timestamps only (no synchronisation; every phase but
+        the BiMPC's ends in a host sync or a native call that waits for its loops, so the host time
+        covers its device work): last_step_ms, per step."""
         if not self.profile_phases:
-            return lambda name: None
-        import time
+            marks = {}
+            last = [time.perf_counter()]
 
+            def mark(name):
+                t = time.perf_counter()
+                marks[name] = (t - last[0]) * 1e3
+                last[0] = t
+
+            self.last_step_ms = marks
+            return mark
         torch = _torch()
         torch.cuda.synchronize(self.device)
         last = [time.perf_counter()]
@@ -386,6 +398,7 @@ class ChargingStation:
         # one host thread each (the price loops spend their time in C-ABI calls, outside the
         # GIL) on each solver's own stream.
         PRINT_LEVEL = _settings.PRINT_LEVEL
+        self.chain_ms = {}
         w_hat_s_opt, w_hat_l_opt = w_hat_s[:, : self.N_lo], w_hat_l[:, : self.N_lo]
         prices_s, prices_l = np.zeros((self.P, self.r)), np.zeros((self.P, self.r))
         stats_s, stats_l = [], []
@@ -436,8 +449,9 @@ class ChargingStation:
                     if self._staged and solver.chain_ok(parts):
                         # every partition's loop and regularisation in ONE native call (no Python
                         # between the partitions: the other type's chain runs beside it)
-                        t0 = time.perf_counter() if prof else 0.0
+                        t0 = time.perf_counter()
                         res = dict(zip(parts, solver.compute_optimal_prices_chain(parts, w_hat[parts, :], lmbd_r)))
+                        self.chain_ms[kind] = (time.perf_counter() - t0) * 1e3
                         if prof:
                             key = f"prices/{kind}/optimal_prices"
                             self.phase_ms[key] = self.phase_ms.get(key, 0.0) + (time.perf_counter() - t0) * 1e3

@@ -187,18 +187,52 @@ int lompc_price_loop(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd
   return lq_price_loop_host(p, a, lmbd, w_k, dual_cost, dec_actual, dec_pred, iterations, errs, st);
 }
 
+// The regularisation of price_solver.py:142-147 / 248-255 at the loop's final iterate w: the
+// column-separable LP of lompc_lp_separable with A = Dphi(w)'[:, :r], b = Dphi(w)' lmbd, c = phi(w)
+// (phi / Dphi of lompc.py:172-187), lmbd[:r] replaced by its solution; *pre / *post = phi(w)' lmbd
+// before / after.  One routine for the chain and PriceSolver's per-partition loops, so the two give
+// the same bits.
+int lompc_price_regularize(int N, int r, double theta, double w_max, const double* w, double* lmbd, double* pre,
+                           double* post) {
+  if (N < 1 || N > LOMPC_MAX_N || (r != 2 * N && r != 3 * N) || !w || !lmbd || !pre || !post)
+    return LOMPC_ERR_INVALID_ARG;
+  const int N3 = 3 * N;
+  const double th = theta, wm = w_max, qs = 3.0 * th / (4.0 * wm);
+  std::vector<double> A((size_t)N * r, 0.0), b(N), phi(N3), x(r);
+  for (int t = 0; t < N; ++t) {
+    phi[t] = th * w[t];
+    phi[N + t] = th * (wm - w[t]);
+    phi[2 * N + t] = qs * (w[t] * w[t]);
+  }
+  double s = 0.0;
+  for (int i = 0; i < N3; ++i) s += phi[i] * lmbd[i];
+  *pre = s;
+  for (int t = 0; t < N; ++t) {  // Dphi(w)'[:r]: row t holds theta (col t), -theta (col N + t), 2 q_s w_t
+    A[(size_t)t * r + t] = th;
+    A[(size_t)t * r + N + t] = -th;
+    if (r == 3 * N) A[(size_t)t * r + 2 * N + t] = 2.0 * qs * w[t];
+    double acc = 0.0;
+    for (int i = 0; i < r; ++i) acc += A[(size_t)t * r + i] * lmbd[i];
+    b[t] = acc;
+  }
+  const int rc = lompc_lp_separable(N, r, A.data(), b.data(), phi.data(), x.data());
+  if (rc) return rc;
+  for (int i = 0; i < r; ++i) lmbd[i] = x[i];
+  s = 0.0;
+  for (int i = 0; i < N3; ++i) s += phi[i] * lmbd[i];
+  *post = s;
+  return LOMPC_OK;
+}
+
 // One EV type's price loops over its partitions in order (charging_station.py:275-307): each
 // partition's loop (lompc_price_loop) starts from the previous partition's regularised prices, then
-// its prices are regularised (price_solver.py:142-147, 248-255: the column-separable LP of
-// lompc_lp_separable with A = Dphi(w)', b = Dphi(w)' lmbd, c = phi(w), phi of lompc.py:172-187).
+// its prices are regularised (lompc_price_regularize).
 int lompc_price_chain(int n_parts, lompc_price_chain_part* parts, const lompc_price_loop_args* common,
                       double* prev_prices, void* stream) {
   if (n_parts < 0 || (n_parts > 0 && (!parts || !common || !prev_prices))) return LOMPC_ERR_INVALID_ARG;
   if (n_parts == 0) return LOMPC_OK;
   const int N = common->N, r = common->r, N3 = 3 * N;
   if (N < 1 || N > LOMPC_MAX_N || (r != 2 * N && r != 3 * N)) return LOMPC_ERR_INVALID_ARG;
-  const double th = common->theta, wm = common->w_max, qs = 3.0 * th / (4.0 * wm);
-  std::vector<double> A((size_t)N * r), b(N), phi(N3), x(r);
   for (int k = 0; k < n_parts; ++k) {
     lompc_price_chain_part& q = parts[k];
     q.rc = LOMPC_OK;
@@ -217,31 +251,10 @@ int lompc_price_chain(int n_parts, lompc_price_chain_part* parts, const lompc_pr
     if (q.rc) return q.rc;
     q.calls = it + 1;
     q.iterations = std::min(it, a.max_iter - 1);  // (the reference's loop variable at its end)
-    const double* w = q.w_k;
-    for (int t = 0; t < N; ++t) {
-      phi[t] = th * w[t];
-      phi[N + t] = th * (wm - w[t]);
-      phi[2 * N + t] = qs * (w[t] * w[t]);
-    }
-    double pre = 0.0;
-    for (int i = 0; i < N3; ++i) pre += phi[i] * lm[i];
-    std::fill(A.begin(), A.end(), 0.0);
-    for (int t = 0; t < N; ++t) {  // Dphi(w)'[:r]: row t holds theta (col t), -theta (col N + t), 2 q_s w_t
-      A[(size_t)t * r + t] = th;
-      A[(size_t)t * r + N + t] = -th;
-      if (r == 3 * N) A[(size_t)t * r + 2 * N + t] = 2.0 * qs * w[t];
-      double acc = 0.0;
-      for (int i = 0; i < r; ++i) acc += A[(size_t)t * r + i] * lm[i];
-      b[t] = acc;
-    }
-    q.rc = lompc_lp_separable(N, r, A.data(), b.data(), phi.data(), x.data());
+    q.rc = lompc_price_regularize(N, r, common->theta, common->w_max, q.w_k, lm, &q.price_before_reg,
+                                  &q.price_after_reg);
     if (q.rc) return q.rc;
-    for (int i = 0; i < r; ++i) lm[i] = x[i];
-    double post = 0.0;
-    for (int i = 0; i < N3; ++i) post += phi[i] * lm[i];
-    q.price_before_reg = pre;
-    q.price_after_reg = post;
-    for (int i = 0; i < r; ++i) prev_prices[i] = x[i];
+    for (int i = 0; i < r; ++i) prev_prices[i] = lm[i];
   }
   return LOMPC_OK;
 }

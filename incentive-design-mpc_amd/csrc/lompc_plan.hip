@@ -125,6 +125,16 @@ __device__ __forceinline__ void st_wt8(double* p, double v) {
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// per-EV scalar outputs (cost, w0): 8-B write-through stores are one fabric write each (2.7x the
+// per-byte time of 16-B ones, MI355X_MICROARCH.md); EV_PLAIN (diagnostic builds) stores them plain
+#ifndef LQ_EV_PLAIN
+#define LQ_EV_PLAIN 0
+#endif
+__device__ __forceinline__ void st_ev8(double* p, double v) {
+  if (LQ_EV_PLAIN) *p = v;
+  else st_wt8(p, v);
+}
+
 __device__ __forceinline__ void st_wt4(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -839,6 +849,35 @@ __global__ __launch_bounds__(256) void k_combine(const double* __restrict__ recv
   }
 }
 
+// The wide form's exchange for a group of n runs (one all-gather of the n runs' packed records):
+// recv[rank][n][S (N + 8)]; run r's records combined in rank order as k_combine does, into the run's
+// set outputs at (run0 + r) * stride (stride 0: shared outputs, only run `last` writes them)
+struct CombineRunsArgs {
+  const double* recv;
+  int nranks, n, S, N, run0, last;
+  double* set_sum_w;
+  double* set_stats;
+  int64_t sw_stride, st_stride;
+};
+__global__ __launch_bounds__(256) void k_combine_runs(CombineRunsArgs a) {
+  const int SN = a.S * a.N, L = a.S * (a.N + LOMPC_SET_STATS);
+  const int64_t tot = (int64_t)a.n * L;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < tot; e += (int64_t)gridDim.x * 256) {
+    const int r = (int)(e / L), c = (int)(e - (int64_t)r * L), j = a.run0 + r;
+    const bool is_max = c >= SN && (c - SN) % LOMPC_SET_STATS == LOMPC_STAT_MAX_ERR;
+    double v = a.recv[(size_t)r * L + c];
+    for (int k = 1; k < a.nranks; ++k) {
+      const double x = a.recv[((size_t)k * a.n + r) * L + c];
+      v = is_max ? fmax(v, x) : v + x;
+    }
+    if (c < SN) {
+      if (a.set_sum_w && (a.sw_stride || j == a.last)) a.set_sum_w[(size_t)j * a.sw_stride + c] = v;
+    } else if (a.set_stats && (a.st_stride || j == a.last)) {
+      a.set_stats[(size_t)j * a.st_stride + c - SN] = v;
+    }
+  }
+}
+
 // lompc_plan_run_chain: run k's prices from run k - 1's closed set reductions (the dependence of the
 // reference's price iterations, price_solver.py:111-140): one workgroup per set, lane = price
 // coordinate i = seg N + t,
@@ -887,6 +926,7 @@ struct RunOff {
   const double* lmbd = nullptr;    // (null: a.lmbd / a.lmbd_r)
   const double* lmbd_r = nullptr;
   bool launder = false;
+  bool nostage = false;  // (diagnostic builds, LQ_EVALS_NOSTAGE: keep the previous run's staged table)
 };
 
 template <int NT = 0, bool CLOSE = false>
@@ -966,7 +1006,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   // (issued before the gamma loads, above), then only those cells' used rows, coefficient records
   // and piece ends — cells hold 1-2 pieces on average, so this moves a fraction of the 8 slots
   const size_t sb = (size_t)cb * LQ_PPL;
-  {
+  if (!ro.nostage) {
     int vn = 0;
     double vl = 0.0;
     if (tid < G) {
@@ -1068,8 +1108,8 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     const bool cov = valid && ke > kb && ke <= np && g >= glo_c && g <= gend;
     if (act && !valid) {
       ++n_inv;
-      if (acost) st_wt8(acost + i, NAN);
-      if (aw0) st_wt8(aw0 + i, NAN);
+      if (acost) st_ev8(acost + i, NAN);
+      if (aw0) st_ev8(aw0 + i, NAN);
       if (astatus) astatus[i] = LOMPC_QP_INVALID;
     } else if (cov) {
       const double2 q0 = *reinterpret_cast<const double2*>(s_cf + cfx(key, 0));
@@ -1087,8 +1127,8 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       acc_p0 += p0;
       acc_err = fmax(acc_err, er);
       ++n_ok;
-      if (acost) st_wt8(acost + i, cst);
-      if (aw0) st_wt8(aw0 + i, w0v);
+      if (acost) st_ev8(acost + i, cst);
+      if (aw0) st_ev8(aw0 + i, w0v);
       if (astatus) astatus[i] = LOMPC_QP_OK;
       if (CLOSE) {
         atomicAdd(s_pn + key, 1);
@@ -1495,6 +1535,9 @@ __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_evals(EvalArgs a, 
     ro.lmbd = a.lmbd + (size_t)j * x.lm_stride;
     ro.lmbd_r = a.lmbd_r + (size_t)j * x.lr_stride;
     ro.launder = true;
+#ifdef LQ_EVALS_NOSTAGE
+    ro.nostage = r > 0;  // (timing only: every run after the first evaluates run 0's table)
+#endif
     // (the block index laundered per run: nothing derived from it — the block's EVs and gamma, the set's
     // constants — is hoisted out of the loop and kept live across runs, which made the loop spill)
     int bl = b;
@@ -2112,16 +2155,16 @@ void eval_args(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* 
 
 // with a communicator: `slots` packed send records [S][N] sums | [S][8] stats and the all-gather's
 // receive buffer [nranks][S (N + 8)] (grown when the plan or the communicator outgrows them)
-int lq_xbufs(lompc_plan* p, int slots) {
+int lq_xbufs(lompc_plan* p, int slots, int recv_runs = 1) {
   const int64_t L = p->S * (p->N + LOMPC_SET_STATS);
   int rc;
   if (L * slots > p->cap_xsend) {
     if ((rc = grow(p, &p->d_xsend, L * slots))) return rc;
     p->cap_xsend = L * slots;
   }
-  if (L * p->comm->nranks > p->cap_xrecv) {
-    if ((rc = grow(p, &p->d_xrecv, L * p->comm->nranks))) return rc;
-    p->cap_xrecv = L * p->comm->nranks;
+  if (L * p->comm->nranks * recv_runs > p->cap_xrecv) {
+    if ((rc = grow(p, &p->d_xrecv, L * p->comm->nranks * recv_runs))) return rc;
+    p->cap_xrecv = L * p->comm->nranks * recv_runs;
   }
   return LOMPC_OK;
 }
@@ -2671,7 +2714,7 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
         return rc;
       z.cap_rrec = need;
     }
-    if (xr && (rc = lq_xbufs(p, Kc))) return rc;
+    if (xr && (rc = lq_xbufs(p, Kc, Kc))) return rc;
     EvalArgs ea;
     FinalArgs ff;
     eval_args(p, lmbd, lmbd_r, w, cost, w0, status, tab(0), ea, ff);
@@ -2715,9 +2758,20 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
         HIPCHK(p, hipGetLastError());
         plan_prof_end(p, LOMPC_PLAN_K_FINAL, e0, e1, n);
       }
-      if (xr)  // one collective per run, in run order (each into that run's set outputs)
-        for (int r = 0; r < n; ++r)
-          if ((rc = lq_exchange(p, p->d_xsend + (size_t)r * L, sw_of(g0 + r), st_of(g0 + r), st))) return rc;
+      if (xr) {  // ONE collective for the group's n runs (their send records are contiguous), one combine
+        if ((rc = lq_comm_allgather(p->comm, p->d_xsend, p->d_xrecv, (size_t)n * L, st))) {
+          p->err = p->comm->err;
+          return rc;
+        }
+        if (set_sum_w || set_stats) {
+          const CombineRunsArgs ca{p->d_xrecv, p->comm->nranks, n, (int)p->S, N, g0, K - 1, set_sum_w, set_stats,
+                                   sw_stride, st_stride};
+          const int64_t tot = (int64_t)n * L;
+          hipLaunchKernelGGL(k_combine_runs, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((tot + 255) / 256, 1024))),
+                             dim3(256), 0, st, ca);
+          HIPCHK(p, hipGetLastError());
+        }
+      }
     }
     return LOMPC_OK;
   }

@@ -85,6 +85,7 @@ SIGNATURES = [
     ("lompc_last_error", ctypes.c_char_p, [_P]),
     ("lompc_abi_version", _I, []),
     ("lompc_price_step", _I, [_I, _I, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P]),
+    ("lompc_price_regularize", _I, [_I, _I, _D, _D, _P, _P, _P, _P]),
     ("lompc_lp_separable", _I, [_I, _I, _P, _P, _P, _P]),
     ("lompc_lp_solve", _I, [_I, _I, _P, _P, _P, _P, _P]),
     ("lompc_bimpc_solve", _I, [_I, _I, _I] + [_D] * 10 + [_P] * 6 + [_D] + [_P] * 6),

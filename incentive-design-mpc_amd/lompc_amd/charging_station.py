@@ -343,7 +343,7 @@ class ChargingStation:
         gamma_sm, gamma_lm = np.zeros((self.P,)), np.zeros((self.P,))
         # one rank: each type's EVs sorted once by charge level, the partitions' statistics from that
         # order (both types in one host sync); the layout the price loops need comes with it
-        sl = self._sorted_layouts() if self.group is None else None
+        sl = self._sorted_layouts()
         st_s = sl["Small"] if sl and "Small" in sl else partition_stats(self.y_s, self.idx_s, self.P, self.group)
         st_l = sl["Large"] if sl and "Large" in sl else partition_stats(self.y_l, self.idx_l, self.P, self.group)
         for p in range(self.P):
@@ -534,15 +534,17 @@ class ChargingStation:
         return [self._stage_pool.submit(stage, job) for job in jobs]
 
     def _sorted_layouts(self):
-        """Both EV types' partition layouts and statistics from ONE sort per type (one rank), by the
-        extension's lompc_levels_layout: y sorted descending, so partition p (charge levels in
-        [rng[p], rng[p+1]], later partitions winning on shared edges, charging_station.py:111-116) is
-        one contiguous run — partition P-1 first — in descending charge level (ascending gamma, as the
-        loop plans want), with its count / max / min / sum (price_solver.py:66-77) computed on the
-        device.  One host sync for both types.  A type with a charge level outside [rng[0], rng[P]]
-        (whose EVs keep their previous partition index, :111-116, so the runs would not be the
-        partitions) is left out of the result: the caller takes the index-based path for it.
-        Returns {kind: (P, 4) host statistics (count, max, min, sum)}; the layouts go to self._layout."""
+        """Both EV types' partition layouts and statistics from ONE sort per type and rank, by the
+        extension's lompc_levels_layout: this rank's levels sorted descending, so partition p (charge
+        levels in [rng[p], rng[p+1]], later partitions winning on shared edges, charging_station.py:
+        111-116) is one contiguous run — partition P-1 first — in descending charge level (ascending
+        gamma, as the loop plans want), with its count / max / min / sum (price_solver.py:66-77)
+        computed on the device.  Sharded: the ranks' records all-gathered and combined in rank order
+        (counts and sums added rank 0 first, max / min), as partition_stats does; one host sync for
+        both types.  A type with a charge level outside [rng[0], rng[P]] on any rank (whose EVs keep
+        their previous partition index, :111-116, so the runs would not be the partitions) is left out
+        of the result: the caller takes the index-based path for it.  Returns {kind: (P, 4) host
+        statistics (count, max, min, sum)}; the layouts go to self._layout."""
         torch = _torch()
         P = self.P
         lib = _lib.load()
@@ -550,11 +552,14 @@ class ChargingStation:
         parts, recs = [], []
         for kind, y, rng in (("Small", self.y_s, self.y0_s_rng), ("Large", self.y_l, self.y0_l_rng)):
             n = int(y.numel())
-            if n == 0:
-                return None
             b = self._bounds.get(id(rng))
             if b is None:
                 b = self._bounds[id(rng)] = torch.as_tensor(rng, dtype=y.dtype, device=y.device)
+            if n == 0:  # (an empty shard: no levels, the empty record)
+                e = np.array([0.0, -np.inf, np.inf, 0.0] * P + [-np.inf, np.inf, rng[0], rng[P]])
+                recs.append(torch.as_tensor(e, device=y.device))
+                parts.append((kind, y.new_empty(0), torch.zeros(0, dtype=torch.int64, device=y.device)))
+                continue
             lv = self._lv.get(kind)
             if lv is None or lv["n"] != n:  # (buffers per type, reused from step to step)
                 wb = ctypes.c_size_t(0)
@@ -572,15 +577,33 @@ class ChargingStation:
                 raise RuntimeError(_lib.status_text(lib, None, rc))
             recs.append(lv["stats"])
             parts.append((kind, lv["ys"], lv["perm"]))
-        h = torch.cat(recs).cpu().numpy()  # the one host sync
+        rec = torch.stack(recs)  # (2, 4P + 4)
+        if self.group is None:
+            h = rec.cpu().numpy()[None]  # the one host sync
+        else:
+            import torch.distributed as dist
+
+            world = dist.get_world_size(self.group)
+            # (the concatenated output form: gloo rejects the stacked (world, ...) one)
+            allr = torch.empty((world * rec.shape[0], rec.shape[1]), dtype=rec.dtype, device=rec.device)
+            dist.all_gather_into_tensor(allr, rec.contiguous(), group=self.group)
+            h = allr.view(world, *rec.shape).cpu().numpy()  # the one host sync
         out = {}
         for j, (kind, ys, perm) in enumerate(parts):
-            rec = h[j * (4 * P + 4): (j + 1) * (4 * P + 4)]
-            st = rec[: 4 * P].reshape(P, 4).copy()  # count, max, min, sum
-            ymax, ymin, lo, hi = rec[4 * P:]
-            if not (ymin >= lo and ymax <= hi):  # (NaN fails too)
+            rows = h[:, j]  # (ranks, 4P + 4)
+            st = rows[0, : 4 * P].reshape(P, 4).copy()  # count, max, min, sum; the other ranks in rank order
+            for r in range(1, rows.shape[0]):
+                o = rows[r, : 4 * P].reshape(P, 4)
+                st[:, 0] += o[:, 0]
+                st[:, 3] += o[:, 3]
+                st[:, 1] = np.maximum(st[:, 1], o[:, 1])
+                st[:, 2] = np.minimum(st[:, 2], o[:, 2])
+            ymax, ymin = rows[:, 4 * P].max(), rows[:, 4 * P + 1].min()
+            lo, hi = rows[0, 4 * P + 2], rows[0, 4 * P + 3]
+            if not (ymin >= lo and ymax <= hi):  # (NaN fails too; every rank decides the same)
                 continue
-            cnt = st[:, 0].astype(np.int64)
+            mine = dist.get_rank(self.group) if self.group is not None else 0
+            cnt = rows[mine, : 4 * P].reshape(P, 4)[:, 0].astype(np.int64)  # this rank's runs
             ends = np.cumsum(cnt[::-1])  # runs in storage order, partition P-1 first
             self._layout[kind] = (perm, ys, {p: (int(ends[k] - cnt[p]), int(ends[k]))
                                              for k, p in enumerate(range(P - 1, -1, -1))})

@@ -37,7 +37,7 @@ import numpy as np
 from . import _lib
 from . import settings as _settings
 from .lompc import BatchPlan, LoMPC, LoMPCConstants, SolverError
-from .price_regularizer import PriceRegularizer
+from .price_regularizer import PriceRegularizer, PriceRegularizerError
 from .settings import PRICE_SOLVER_EPS_REG, PRICE_SOLVER_EPS_TOL
 
 
@@ -474,10 +474,17 @@ class PriceSolver:
     def _finish_prices(self, lmbd_k, w_k, iter, dual_cost_decrease_ac, dual_cost_decrease_pred, lmbd_r, w_ref,
                        A_bar, tol, w0_err_bound):
         PRINT_LEVEL = _settings.PRINT_LEVEL
-        # Regularize prices (price_solver.py:145-147).
-        price_pre = self.lompc.phi(w_k) @ lmbd_k
-        lmbd_k[: self.r] = self._regularize_prices(w_k, lmbd_k[: self.r])
-        price_new = self.lompc.phi(w_k) @ lmbd_k
+        # Regularize prices (price_solver.py:145-147): the native routine the chain uses too
+        # (lompc_price_regularize: the same LP as _regularize_prices, the same bits as the chain)
+        lmbd_k = np.ascontiguousarray(lmbd_k, dtype=np.float64)
+        w_k = np.ascontiguousarray(w_k, dtype=np.float64)
+        pre, post = ctypes.c_double(0.0), ctypes.c_double(0.0)
+        rc = self._lib.lompc_price_regularize(self.N, self.r, float(self.consts.theta), float(self.consts.w_max),
+                                              w_k.ctypes.data, lmbd_k.ctypes.data, ctypes.byref(pre),
+                                              ctypes.byref(post))
+        if rc != _lib.LOMPC_OK:
+            raise PriceRegularizerError("LP infeasible: " + _lib.status_text(self._lib, None, rc))
+        price_pre, price_new = pre.value, post.value
         if PRINT_LEVEL >= 1:
             (w_err_max, w0_err, w_avg_err), (w_k_, _) = self._iterate(lmbd_k, lmbd_r, w_ref, A_bar)
             if PRINT_LEVEL >= 2:

@@ -409,6 +409,14 @@ typedef struct lompc_price_chain_part {
 int lompc_price_chain(int n_parts, lompc_price_chain_part* parts, const lompc_price_loop_args* common,
                       double* prev_prices, void* stream);
 
+/* The regularisation step alone (price_solver.py:142-147 with :248-255; replaces the CVXPY call of
+ * price_regularizer.py:68-85 for the station's A = Dphi(w)', b = A lmbd, c = phi(w)): lmbd host [3N]
+ * in / out (lmbd[:r] replaced), w host [N] the loop's final iterate, *pre / *post = phi(w)'lmbd
+ * before / after.  lompc_price_chain regularises with it, and PriceSolver's per-partition loop too,
+ * so the two forms give identical prices. */
+int lompc_price_regularize(int N, int r, double theta, double w_max, const double* w, double* lmbd, double* pre,
+                           double* post);
+
 /* ---------------------------------------------------------------------------
  * Host-side solvers of the price iteration (no device, no context).  They run
  * once per price iteration / per partition next to the convergence test, like

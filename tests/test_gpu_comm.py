@@ -87,8 +87,9 @@ def test_plan_with_comm_equals_plain(nccl1, want_w):
     for key, v in plain.out.items():
         if v is not None:
             assert torch.equal(v, shard.out[key]), key
-    # the stepped run_steps with the communicator (one all-gather + combine per run, after the launch
-    # that closed it), every run's records kept: the plain plan's, both issue forms
+    # run_steps with the communicator (wide form: ONE all-gather of the group's runs' records after their
+    # closings and one combine kernel; the split form: one all-gather + combine per run), every run's
+    # records kept: the plain plan's, both issue forms
     for per_kernel in (False, True):
         for per_run in (False, True):  # (per_run: every output per run)
             o_s = shard.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, per_run=per_run,

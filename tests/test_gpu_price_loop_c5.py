@@ -82,9 +82,9 @@ def test_device_price_loop_matches_oracle_at_config5_partitions(gpu, monkeypatch
 @pytest.mark.parametrize("ev", ["small", "large"])
 def test_price_chain_equals_partition_loops(gpu, monkeypatch, ev):
     """lompc_price_chain (one native call for a type's partitions, ChargingStation's default) gives the
-    per-partition loops' results: the same iteration counts and dual cost decreases, prices and the
-    prices before / after regularisation to rounding (the chain regularises in C++: price_solver.py:
-    142-147), prev_prices chained the same way; a partition without EVs is skipped."""
+    per-partition loops' results bit for bit: iteration counts, dual cost decreases, prices and the
+    prices before / after regularisation (both regularise through lompc_price_regularize,
+    price_solver.py:142-147), prev_prices chained the same way; a partition without EVs is skipped."""
     monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
     c, lc = consts(ev)
     rng = np.random.default_rng(600 + (ev == "large"))
@@ -112,9 +112,9 @@ def test_price_chain_equals_partition_loops(gpu, monkeypatch, ev):
     assert sol["chain"].n_batched_calls == sol["loops"].n_batched_calls
     for (la, sa), (lb, sb) in zip(res_loops, res_chain):
         assert sa["iter"] == sb["iter"]
-        np.testing.assert_allclose(lb, la, rtol=0, atol=1e-12 * c.theta)
+        np.testing.assert_array_equal(lb, la)  # (both regularise with lompc_price_regularize)
         for k in ("price_before_reg", "price_after_reg"):
-            assert abs(sa[k] - sb[k]) <= 1e-12 * max(1.0, abs(sa[k])), k
+            assert sa[k] == sb[k], k
         for k in ("dual_cost_decrease_actual", "dual_cost_decrease_predicted"):
             np.testing.assert_array_equal(sb[k], sa[k])
-    np.testing.assert_allclose(sol["chain"].prev_prices, sol["loops"].prev_prices, rtol=0, atol=1e-12 * c.theta)
+    np.testing.assert_array_equal(sol["chain"].prev_prices, sol["loops"].prev_prices)

@@ -90,15 +90,23 @@ def _rank(rank, world, port, M_2, q):
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    settings.PRINT_LEVEL = 0
-    torch.cuda.set_device(0)
-    np.random.seed(5)
-    cs = ChargingStation(consts(M_2, Tf=2), device=0, group=dist.group.WORLD)
-    logs = cs.simulate()
-    q.put((rank, logs["inputs"], logs["prices"], logs["statistics"], logs["states"]["x"], cs.y_s.cpu().numpy()))
-    dist.barrier()
-    dist.destroy_process_group()
+    import faulthandler
+    import traceback
+
+    faulthandler.dump_traceback_later(100, exit=True)  # a hung rank names where it hangs
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        settings.PRINT_LEVEL = 0
+        torch.cuda.set_device(0)
+        np.random.seed(5)
+        cs = ChargingStation(consts(M_2, Tf=2), device=0, group=dist.group.WORLD)
+        logs = cs.simulate()
+        q.put((rank, logs["inputs"], logs["prices"], logs["statistics"], logs["states"]["x"], cs.y_s.cpu().numpy()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        q.put((rank, "error", traceback.format_exc()))
+        raise
 
 
 def test_sharded_loop_matches_single_process(gpu, monkeypatch):
@@ -117,7 +125,12 @@ def test_sharded_loop_matches_single_process(gpu, monkeypatch):
     procs = [ctx.Process(target=_rank, args=(r, 2, port, M_2, q)) for r in range(2)]
     for p in procs:
         p.start()
-    outs = sorted([q.get(timeout=300) for _ in range(2)], key=lambda o: o[0])
+    outs = []
+    for _ in range(2):  # (a rank's error is reported at once, not after the other rank's timeout)
+        o = q.get(timeout=120)
+        assert o[1] != "error", f"rank {o[0]}:\n{o[2]}"
+        outs.append(o)
+    outs.sort(key=lambda o: o[0])
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0

@@ -88,9 +88,13 @@ __device__ unsigned long long g_lstamps[64 * 16];  // k_loop_iter's phase sums (
 #define EVAL_MIN_WAVES ((2 * EVAL_WAVES + 3) / 4)  // k_eval: waves per SIMD for two workgroups per CU
 #endif
 #define EVAL_EVS (64 * EVAL_WAVES)         // k_eval: threads per workgroup
+#ifndef EVAL_PASSES
 #define EVAL_PASSES 2                      // k_eval: EVs per thread, at most
+#endif
 #define EVAL_MAXB (EVAL_EVS * EVAL_PASSES)  // k_eval: EVs per workgroup, at most
+#ifndef LQ_PIECE_CAP
 #define LQ_PIECE_CAP 128                   // k_eval: piece slots of one set staged in LDS (more: re-solved)
+#endif
 #define LQ_GMAX 1024                       // max cells per set
 #ifndef LQ_STEP_CELLS
 #define LQ_STEP_CELLS 4                    // k_step: path cells per workgroup, one per wave (<= EVAL_WAVES; 4: one per
@@ -926,6 +930,7 @@ struct RunOff {
   const double* lmbd = nullptr;    // (null: a.lmbd / a.lmbd_r)
   const double* lmbd_r = nullptr;
   bool launder = false;
+  bool gamma_lds = false;  // the block's gamma from the previous run's s_g (k_evals: the same EVs every run)
   bool nostage = false;  // (diagnostic builds, LQ_EVALS_NOSTAGE: keep the previous run's staged table)
 };
 
@@ -990,9 +995,9 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   // this thread's EVs (caller order)
   double gh[EVAL_PASSES];
 #pragma unroll
-  for (int h = 0; h < EVAL_PASSES; ++h) {
-    const int i = start + tid + EVAL_EVS * h;
-    gh[h] = i < end ? a.gamma[i] : 0.0;
+  for (int h = 0; h < EVAL_PASSES; ++h) {  // (k_evals after its first run: from LDS, no memory round
+    const int i = start + tid + EVAL_EVS * h;  //  queued behind the previous run's row stores)
+    gh[h] = ro.gamma_lds ? s_g[tid + EVAL_EVS * h] : i < end ? a.gamma[i] : 0.0;
   }
   const QPConst& q = set_consts(a.qd, a.ce, s);
   double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
@@ -1535,6 +1540,7 @@ __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_evals(EvalArgs a, 
     ro.lmbd = a.lmbd + (size_t)j * x.lm_stride;
     ro.lmbd_r = a.lmbd_r + (size_t)j * x.lr_stride;
     ro.launder = true;
+    ro.gamma_lds = r > 0;
 #ifdef LQ_EVALS_NOSTAGE
     ro.nostage = r > 0;  // (timing only: every run after the first evaluates run 0's table)
 #endif
@@ -1544,18 +1550,23 @@ __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_evals(EvalArgs a, 
     asm volatile("" : "+s"(bl));
 #ifdef LOMPC_STAMPS
     // diagnostic build (scripts/evals_stamps.py): per (workgroup, run < 32) the run's start, the end
-    // of its staging, the end of its rows and its end, at g_stamps[((b * 32 + r) * 4 + k]
+    // of its staging phases, the end of its rows and its end, at g_stamps[((b * 32 + r) * 8 + k]
     const long long t0__ = __builtin_amdgcn_s_memtime();
 #endif
     eval_block<NT, false>(a, bl, nullptr, ro);
     __syncthreads();  // (the staged table and the record scratch are the next run's)
 #ifdef LOMPC_STAMPS
-    if (threadIdx.x == 0 && r < 32 && b < 512) {
-      long long* q = g_stamps + ((size_t)b * 32 + r) * 4;
+    if (threadIdx.x == 0 && r < 32 && b < 512) {  // start, block map, scalars, counts, pieces, staged, rows, end
+      long long* q = g_stamps + ((size_t)b * 32 + r) * 8;
+      const long long* e = g_stamps + (32768 + b) * 8;
       q[0] = t0__;
-      q[1] = g_stamps[(32768 + b) * 8 + 1];
-      q[2] = g_stamps[(32768 + b) * 8 + 4];
-      q[3] = __builtin_amdgcn_s_memtime();
+      q[1] = e[6];
+      q[2] = e[0];
+      q[3] = e[2];
+      q[4] = e[3];
+      q[5] = e[1];
+      q[6] = e[4];
+      q[7] = __builtin_amdgcn_s_memtime();
     }
 #endif
   }

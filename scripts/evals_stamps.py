@@ -17,9 +17,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "incentive-design-mpc_amd"))
 from lompc_amd import _lib, build  # noqa: E402
 
-DBG = os.path.join(ROOT, "incentive-design-mpc_amd", "lompc_amd", "liblompc_amd_stamps_rt.so")
+NOSTAGE = "--nostage" in sys.argv  # (runs after the first keep run 0's staged table: LQ_EVALS_NOSTAGE)
+DBG = os.path.join(ROOT, "incentive-design-mpc_amd", "lompc_amd",
+                   os.environ.get("ES_LIB", "liblompc_amd_stamps_rt%s.so" % ("_nostage" if NOSTAGE else "")))
 if "--build" in sys.argv:
-    print(build.build(force=True, out=DBG, defines=("LOMPC_STAMPS", "LOMPC_STAMPS_RT")))
+    print(build.build(force=True, out=DBG, defines=("LOMPC_STAMPS", "LOMPC_STAMPS_RT") +
+                      (("LQ_EVALS_NOSTAGE",) if NOSTAGE else ())))
     sys.exit(0)
 
 import torch  # noqa: E402
@@ -48,16 +51,21 @@ for _ in range(3):
 plan.check()
 torch.cuda.synchronize()
 nb = plan.info()["workgroups"]
-buf = np.zeros(512 * 32 * 4, dtype=np.int64)
+buf = np.zeros(512 * 32 * 8, dtype=np.int64)
 assert lib.lompc_debug_stamps(buf.ctypes.data, buf.size) == 0
-st = buf.reshape(512, 32, 4)[:nb, :K].astype(np.float64) * 10e-3  # us
-t0 = st[:, 0, 0].min()
-st -= t0
+st8 = buf.reshape(512, 32, 8)[:nb, :K].astype(np.float64) * 10e-3  # us
+t0 = st8[:, 0, 0].min()
+st8 -= t0
+st = st8[:, :, [0, 5, 6, 7]]  # start, staged, rows done, end
 span = st[:, :, 3].max()
-print(f"workgroups {nb}, runs {K}: launch span (first start .. last end) {span:.2f} us = {span / K:.2f} us per run")
-ph = {"staging": st[:, :, 1] - st[:, :, 0], "rows": st[:, :, 2] - st[:, :, 1], "record": st[:, :, 3] - st[:, :, 2],
-      "run": st[:, :, 3] - st[:, :, 0]}
+print(f"workgroups {nb}, runs {K}{' (nostage)' if NOSTAGE else ''}: launch span (first start .. last end) "
+      f"{span:.2f} us = {span / K:.2f} us per run")
+ph = {"blockmap": st8[:, :, 1] - st8[:, :, 0], "scalars": st8[:, :, 2] - st8[:, :, 1],
+      "counts": st8[:, :, 3] - st8[:, :, 2], "pieces": st8[:, :, 4] - st8[:, :, 3],
+      "lds+bar": st8[:, :, 5] - st8[:, :, 4], "staging": st[:, :, 1] - st[:, :, 0],
+      "rows": st[:, :, 2] - st[:, :, 1], "record": st[:, :, 3] - st[:, :, 2], "run": st[:, :, 3] - st[:, :, 0]}
 for k, v in ph.items():
+    v = v[:, 1:]  # (runs after the first)
     print(f"  {k:8s} median {np.median(v):6.2f}  p10 {np.percentile(v, 10):6.2f}  p90 {np.percentile(v, 90):6.2f}  "
           f"max {v.max():6.2f} us")
 print("  per run (median over workgroups): start / staged / rows done / end")

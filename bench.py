@@ -778,7 +778,8 @@ def sequential_leg(run, eng, N, P, args, torch):
             "verified_steps": sum(ok), "bitwise_steps": sum(bit),
             "verification": "every step's set reductions (and the last step's w / cost) re-computed by an independent "
                             "wide lompc_plan_run_steps over the recorded prices: equal to 1e-12 relative (bitwise: "
-                            f"{sum(bit)} of {K}; the last step's rows within {rows_d:.1e})",
+                            f"{sum(bit)} of {K} — the wide form's staged evaluation sums a block's rows over seven "
+                            f"row waves, a single run's k_eval over eight; the last step's rows within {rows_d:.1e})",
             "warm": {"value": B * K / dt_w, "ms_per_step": dt_w / K * 1e3, "kernels": kus_w,
                      "plan": "warm-started: large price steps leave the stored working sets of little use"},
             "roofline": {"bound": "hbm", "kernel": "k_eval", "bytes_per_qp": bpq, "achieved": gbs,

@@ -147,8 +147,10 @@ struct lompc_plan {
     int* fcnt[2] = {nullptr, nullptr};
     int* fidx[2] = {nullptr, nullptr};
     int64_t cap_blk = 0;
-    int occ = 0, occ_N = -1;      // k_step workgroups per CU (occupancy query) and its horizon
+    int occ = 0;                  // evaluation workgroups per CU (occupancy query)
+    int64_t occ_key = -1;         // ... for this horizon, cell count and kernel
     bool wide = false;            // the map is the wide form's (no path workgroups in its launches)
+    bool stg = false;             // ... for k_evals_st (compact tables, blocks of <= LQ_EVALS_MAXB EVs)
     PathTab wt{};                 // wide form: a ring of per-run path tables, slot-major
     int64_t cap_wt = 0;           // its capacity in cells (slots x S x G)
     double* rpart = nullptr;      // wide form, batched evaluation (k_evals / k_closes): per-run record

@@ -153,6 +153,55 @@ __device__ __forceinline__ int cfx(const int k, const int j) {
 }
 static_assert((LQ_PPL & (LQ_PPL - 1)) == 0, "k_eval's piece-end transpose needs a power-of-two LQ_PPL");
 
+// ---- k_evals' staged form: wave LQ_EVALS_RW of every workgroup stages the NEXT run's piece table
+// while waves 0 .. LQ_EVALS_RW - 1 evaluate the current run from the other of two LDS tables, so no
+// workgroup stops its row stores to wait for table loads (a wave's loads wait for every store it
+// issued before them — vmcnt counts both, in order — and the stager issues no stores).  Its tables
+// are compact: only the set's used pieces, cell c's at slots pre[c] .. pre[c] + cnt[c] - 1 (cells past
+// the capacity left to the re-solve, as cells past the plain table's `cap` are).
+#ifndef LQ_EVALS_STAGER
+#define LQ_EVALS_STAGER 0  // 1: the wide form's evaluation through k_evals_st (diagnostic builds: measured slower,
+                           // 12.5 vs 11.8 us per run at config 3 — DESIGN.md section 10)
+#endif
+#ifndef LQ_EVALS_CAP
+#define LQ_EVALS_CAP 64                                 // compact table: pieces of a set staged at most
+#endif
+#ifndef LQ_STG_CHUNK
+#define LQ_STG_CHUNK 8                                  // the stager's pieces per load round
+#endif
+#define LQ_EVALS_RW 7                                   // row waves (the eighth stages)
+#define LQ_EVALS_MAXB (LQ_EVALS_RW * 64 * EVAL_PASSES)  // EVs per block at most (each wave's re-solve list)
+
+struct CTab {
+  double2* ab;  // [capc + 2][eval_row_stride(N)] piece rows (abx order); rows capc, capc + 1 all zero
+  double* cf;   // [capc][8] coefficient records (cfx)
+  double* ge;   // [capc + 8] piece ends (a lookup reads up to 8 past a cell's first slot)
+  double* lo;   // [G] coverage starts
+  int* cnt;     // [G] staged pieces per cell (0: none, or past the capacity)
+  int* pre;     // [G] the cell's first slot
+  int* meta;    // [0] the largest cnt, [1] the staged pieces
+};
+__host__ __device__ inline size_t ctab_bytes(int N, int G, int capc) {
+  const size_t b = (size_t)(capc + 2) * eval_row_stride(N) * 16 + (size_t)capc * 64 + (size_t)(capc + 8) * 8 +
+                   (size_t)G * 16 + 16;
+  return (b + 15) & ~(size_t)15;
+}
+__device__ __forceinline__ CTab ctab_at(char* base, int N, int G, int capc) {
+  CTab t;
+  t.ab = reinterpret_cast<double2*>(base);
+  t.cf = reinterpret_cast<double*>(base + (size_t)(capc + 2) * eval_row_stride(N) * 16);
+  t.ge = t.cf + (size_t)capc * 8;
+  t.lo = t.ge + capc + 8;
+  t.cnt = reinterpret_cast<int*>(t.lo + G);
+  t.pre = t.cnt + G;
+  t.meta = t.pre + G;
+  return t;
+}
+// k_evals_st dynamic LDS: two tables | row sums [2][EVAL_WAVES][N] | wave records [2][EVAL_WAVES][8]
+inline size_t evals_st_lds(int N, int G, int capc) {
+  return 2 * ctab_bytes(N, G, capc) + (size_t)2 * EVAL_WAVES * (N + 8) * sizeof(double);
+}
+
 __device__ __forceinline__ double clampw(double x, double wmax) { return fmin(fmax(x, 0.0), wmax); }
 
 // ---------------------------------------------------------------- plan kernel
@@ -932,11 +981,83 @@ struct RunOff {
   bool launder = false;
   bool gamma_lds = false;  // the block's gamma from the previous run's s_g (k_evals: the same EVs every run)
   bool nostage = false;  // (diagnostic builds, LQ_EVALS_NOSTAGE: keep the previous run's staged table)
+  int buf = 0;           // (k_evals_st) the compact table and the record scratch of this run: parity
 };
 
-template <int NT = 0, bool CLOSE = false>
+// k_evals_st's stager: set s's path table of ring offset `tab` into the compact table T, by ONE wave
+// (lane c: cell c, G <= 64).  The cells' counts and coverage starts in one memory round, their prefix
+// by a wave scan (cells from the first whose pieces pass `capc` on: none staged), then the pieces LQ_STG_CHUNK at
+// a time: one load per piece (lanes t < N its row, lanes N .. N + 3 its coefficient record in 16-B
+// quarters) and one for the 8 pieces' ends, each piece's cell from a ballot over the cells' ends.
+__device__ __forceinline__ void stage_compact(const EvalArgs& a, const int s, const int64_t tab, const CTab T,
+                                           const int N, const int G, const int capc, const int lane) {
+  const int64_t cb = tab + (int64_t)s * G;
+  int cn = 0;
+  double cl = 0.0;
+  if (lane < G) {
+    cn = min(max(ld_t<false>(a.t_cnt + cb + lane), 0), LQ_PPL);
+    cl = ld_t<false>(a.t_lo + cb + lane);
+  }
+  int incl = cn;  // inclusive prefix of the counts over the cells
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  const bool fit = incl <= capc;
+  const int ends = fit ? incl : 0x7fffffff;  // (an unstaged cell ends past every staged piece)
+  const int pre = incl - cn;
+  int np = fit ? incl : 0, mx = fit ? cn : 0;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    np = max(np, __shfl_xor(np, d, 64));
+    mx = max(mx, __shfl_xor(mx, d, 64));
+  }
+  if (lane < G) {
+    T.cnt[lane] = fit ? cn : 0;
+    T.pre[lane] = pre;
+    T.lo[lane] = cl;
+  }
+  if (lane == 0) {
+    T.meta[0] = mx;
+    T.meta[1] = np;
+  }
+  const int NS = eval_row_stride(N);
+  const size_t sb = (size_t)cb * LQ_PPL;
+  for (int p0 = 0; p0 < np; p0 += LQ_STG_CHUNK) {
+    double2 v[LQ_STG_CHUNK];
+    int sl = 0;  // lane u < LQ_STG_CHUNK: the slot of piece p0 + u
+#pragma unroll
+    for (int u = 0; u < LQ_STG_CHUNK; ++u) {
+      const int p = p0 + u;
+      const int c = __popcll(__ballot(lane < G && ends <= p));  // cells wholly before piece p
+      const int slot = c * LQ_PPL + p - __builtin_amdgcn_readlane(pre, min(c, 63));
+      if (lane == u) sl = slot;
+      const double2* src = lane < N ? a.t_ab + (sb + slot) * N + lane
+                                    : reinterpret_cast<const double2*>(a.t_cf + (sb + slot) * 8) + (lane - N);
+      v[u] = p < np && lane < N + 4 ? ld_t<false>(src) : make_double2(0.0, 0.0);
+    }
+    const double vg = lane < LQ_STG_CHUNK && p0 + lane < np ? ld_t<false>(a.t_ge + sb + sl) : 0.0;
+#pragma unroll
+    for (int u = 0; u < LQ_STG_CHUNK; ++u) {
+      const int p = p0 + u;
+      if (p < np) {
+        if (lane < N) T.ab[p * NS + ((N & 1) ? lane : (lane & 1) * (N >> 1) + (lane >> 1))] = v[u];
+        else if (lane < N + 4) *reinterpret_cast<double2*>(T.cf + cfx(p, 2 * (lane - N))) = v[u];
+      }
+    }
+    if (lane < LQ_STG_CHUNK && p0 + lane < np) T.ge[p0 + lane] = vg;
+  }
+}
+
+// STG (k_evals_st): waves 0 .. LQ_EVALS_RW - 1 only, the table already staged (compact, LDS table
+// ro.buf), EVs in one contiguous segment per wave (its passes: 64 rows each), the row sums and wave
+// records into the run's scratch parity — no barrier inside: the caller's one barrier per run orders
+// the table, the rows and the record.
+template <int NT = 0, bool CLOSE = false, bool STG = false>
 __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, const FinalArgs* fr = nullptr,
                                            const RunOff ro = RunOff{}) {
+  static_assert(!(STG && CLOSE), "the staged form has no in-launch closing");
   // dynamic LDS: [cap + 2][NS] piece rows (rows cap, cap + 1: zero pieces) | [cap][8]
   // coefficients (cfx) | [LQ_PPL][Gs] piece ends | cells: coverage start | piece count | (CLOSE) per
   // piece: gamma sum, EV count.  Laid out for the banks (64 dwords for ds_read_b64 / b128): a
@@ -964,6 +1085,12 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   double* const aw0 = a.w0 ? a.w0 + ro.ev : nullptr;
   int8_t* const astatus = a.status ? a.status + ro.ev : nullptr;
   const int s = info.x, start = info.y, end = info.z;  // thread: EVs start + tid + EVAL_EVS h
+  // (STG: wave wv's EVs are block rows sg0 .. sg0 + sgn - 1, lane + 64 h in pass h)
+  const int sg_per = STG ? (end - start + LQ_EVALS_RW - 1) / LQ_EVALS_RW : 0;
+  const int sg0 = STG ? wv * sg_per : 0;
+  const int sgn = STG ? max(0, min(sg_per, end - start - sg0)) : 0;
+  auto brow = [&](const int h) { return STG ? sg0 + 64 * h + lane : tid + EVAL_EVS * h; };  // block row of pass h
+  auto bact = [&](const int h) { return STG ? 64 * h + lane < sgn : start + tid + EVAL_EVS * h < end; };
   LQ_STAMPW(6);  // (diagnostic build: the block map's load round)
   int G_ = a.G, cap_ = a.cap;
   if (ro.launder) asm volatile("" : "+s"(G_), "+s"(cap_));  // (k_evals: the LDS layout per run, as tid)
@@ -983,21 +1110,35 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   double* s_ge = s_cf + (size_t)cap * 8;
   double* s_lo = s_ge + cap;
   int* s_cnt = reinterpret_cast<int*>(s_lo + G);
+  int* s_pre = nullptr;  // (STG: a cell's first slot)
+  int stg_meta[2] = {0, 0};
+  if constexpr (STG) {
+    const CTab T = ctab_at(reinterpret_cast<char*>(s_dyn) + (size_t)ro.buf * ctab_bytes(N, G, cap), N, G, cap);
+    s_ab = T.ab;
+    s_cf = T.cf;
+    s_ge = T.ge;
+    s_lo = T.lo;
+    s_cnt = T.cnt;
+    s_pre = T.pre;
+    stg_meta[0] = T.meta[0];
+    stg_meta[1] = T.meta[1];
+  }
   unsigned long long* s_pf = reinterpret_cast<unsigned long long*>(s_cnt + ((G + 1) & ~1));
   int* s_pn = reinterpret_cast<int*>(s_pf + cap + 2);
-  const int np = min(G * LQ_PPL, cap);
-  const int Gs = np / LQ_PPL;  // cells with staged pieces (the rest are re-solved)
+  const int np = STG ? stg_meta[1] : min(G * LQ_PPL, cap);
+  const int Gs = STG ? G : np / LQ_PPL;  // cells with staged pieces (the rest are re-solved)
   // staged cells per wave (wv, wv + W, ...) and piece-row loads per lane and cell
   constexpr int CPW = (LQ_PIECE_CAP / LQ_PPL + EVAL_WAVES - 1) / EVAL_WAVES;
   constexpr int UA = ((NT ? NT : LOMPC_MAX_N) * LQ_PPL + 63) / 64;
   int wc = 0;  // lane j < CPW: piece count of cell wv + W j
-  if (lane < CPW && wv + EVAL_WAVES * lane < Gs) wc = ld_t<false>(a.t_cnt + ro.tab + (size_t)s * G + wv + EVAL_WAVES * lane);
+  if (!STG && lane < CPW && wv + EVAL_WAVES * lane < Gs)
+    wc = ld_t<false>(a.t_cnt + ro.tab + (size_t)s * G + wv + EVAL_WAVES * lane);
   // this thread's EVs (caller order)
   double gh[EVAL_PASSES];
 #pragma unroll
   for (int h = 0; h < EVAL_PASSES; ++h) {  // (k_evals after its first run: from LDS, no memory round
-    const int i = start + tid + EVAL_EVS * h;  //  queued behind the previous run's row stores)
-    gh[h] = ro.gamma_lds ? s_g[tid + EVAL_EVS * h] : i < end ? a.gamma[i] : 0.0;
+    const int i = start + brow(h);            //  queued behind the previous run's row stores)
+    gh[h] = ro.gamma_lds ? s_g[brow(h)] : bact(h) ? a.gamma[i] : 0.0;
   }
   const QPConst& q = set_consts(a.qd, a.ce, s);
   double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
@@ -1011,7 +1152,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   // (issued before the gamma loads, above), then only those cells' used rows, coefficient records
   // and piece ends — cells hold 1-2 pieces on average, so this moves a fraction of the 8 slots
   const size_t sb = (size_t)cb * LQ_PPL;
-  if (!ro.nostage) {
+  if constexpr (!STG) if (!ro.nostage) {  // (STG: staged by the stager wave)
     int vn = 0;
     double vl = 0.0;
     if (tid < G) {
@@ -1079,7 +1220,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       s_lo[c] = ld_t<false>(a.t_lo + cb + c);
     }
   }
-  __syncthreads();  // the staged table and the box table (lq_tab_fill) published
+  if constexpr (!STG) __syncthreads();  // the staged table and the box table (lq_tab_fill) published
   LQ_STAMPE(1);
   // ---- lane = EV: piece, scalar outputs; EVs no certified piece covers listed for the
   //      individual re-solve (counted as pending failures until then)
@@ -1090,19 +1231,19 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   double acc_cost = 0.0, acc_p0 = 0.0, acc_err = 0.0;
   int n_ok = 0, n_fail = 0, n_inv = 0, nlist = 0;
   bool inv_rows = false;  // (wave-uniform) some row of this wave has an invalid gamma
-  const int mxc = s_mx;  // (block-uniform) the set's largest cell piece count: no piece end past it is read
+  const int mxc = STG ? stg_meta[0] : s_mx;  // (block-uniform) the set's largest cell piece count: no piece end past it is read
   // one pass of the lookup: this thread's EV h
   auto lookup = [&](const int h) {
-    const int i = start + tid + EVAL_EVS * h;
-    const bool act = i < end;
+    const int i = start + brow(h);
+    const bool act = bact(h);
     const double g = gh[h];
     const bool valid = act && g >= 0.0 && g <= ym;
     const int c = valid ? cell_of(g, wlo, cscale, G) : 0;
     const int nc = s_cnt[c];
-    const int kb = c * LQ_PPL, ke = kb + nc;  // the cell's pieces [kb, ke), ascending gamma
+    const int kb = STG ? s_pre[c] : c * LQ_PPL, ke = kb + nc;  // the cell's pieces [kb, ke), ascending gamma
     double ge[LQ_PPL];
 #pragma unroll
-    for (int k = 0; k < LQ_PPL; ++k) ge[k] = k < mxc ? s_ge[k * Gs + min(c, Gs - 1)] : 0.0;
+    for (int k = 0; k < LQ_PPL; ++k) ge[k] = k < mxc ? s_ge[STG ? kb + k : k * Gs + min(c, Gs - 1)] : 0.0;
     const double glo_c = s_lo[c];
     int key = kb;  // piece = number of piece ends below g (every end read at once, no loop)
     double gend = ge[0];
@@ -1110,7 +1251,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     for (int k = 0; k + 1 < LQ_PPL; ++k) key += (k + 1 < nc && g > ge[k]) ? 1 : 0;
 #pragma unroll
     for (int k = 1; k < LQ_PPL; ++k) gend = nc == k + 1 ? ge[k] : gend;  // the last piece's end
-    const bool cov = valid && ke > kb && ke <= np && g >= glo_c && g <= gend;
+    const bool cov = valid && ke > kb && (STG || ke <= np) && g >= glo_c && g <= gend;  // (STG: unstaged cells count 0)
     if (act && !valid) {
       ++n_inv;
       if (acost) st_ev8(acost + i, NAN);
@@ -1140,8 +1281,10 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
         atomicAdd(s_pf + key, (unsigned long long)rint(fmax(g - wlo, 0.0) * fxs));
       }
     }
-    s_g[tid + EVAL_EVS * h] = g;
-    s_k[tid + EVAL_EVS * h] = cov ? key : ((CLOSE && valid) ? ZD : ZK);
+    if (!STG || act) {  // (STG: a pass's lanes past the wave's segment are the next wave's rows)
+      s_g[brow(h)] = g;
+      s_k[brow(h)] = cov ? key : ((CLOSE && valid) ? ZD : ZK);
+    }
     inv_rows |= __ballot(act && !valid) != 0ull;
     const unsigned long long need = __ballot(valid && !cov);
     if (valid && !cov) {
@@ -1152,13 +1295,29 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     nlist += __popcll(need);
   };
   // a wave without EVs in a pass skips it (wave-uniform; its rows are never read)
-  auto pass_live = [&](const int h) { return h == 0 || start + EVAL_EVS * h + 64 * wv < end; };
+  auto pass_live = [&](const int h) { return STG ? 64 * h < sgn : h == 0 || start + EVAL_EVS * h + 64 * wv < end; };
   if constexpr (CLOSE) {  // (the record is built before the rows: every lookup first)
 #pragma unroll
     for (int h = 0; h < EVAL_PASSES; ++h)
       if (pass_live(h)) lookup(h);
   }
   LQ_STAMPE(7);
+  // this wave's record and row sums (STG: in the run's parity of the scratch after the two tables)
+  double* accw_all;  // [EVAL_WAVES][astr] row sums
+  double* red_all;   // [EVAL_WAVES][8] wave records
+  int astr;
+  if constexpr (STG) {
+    double* scr = reinterpret_cast<double*>(reinterpret_cast<char*>(s_dyn) + 2 * ctab_bytes(N, G, cap));
+    accw_all = scr + (size_t)ro.buf * EVAL_WAVES * N;
+    red_all = scr + (size_t)2 * EVAL_WAVES * N + (size_t)ro.buf * EVAL_WAVES * 8;
+    astr = N;
+  } else {
+    accw_all = &s_accw[0][0];
+    red_all = &s_red[0][0];
+    astr = LOMPC_MAX_N;
+  }
+  double* const red_w = red_all + wv * 8;
+  double* const accw_w = accw_all + wv * astr;
   // per-wave totals of the scalar outputs
   auto wave_record = [&]() {
     double tot[4] = {acc_cost, acc_p0, (double)n_ok, 0.0};
@@ -1167,13 +1326,13 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     double cnt[2] = {(double)n_fail, (double)n_inv};
     lqw::wave_totals(cnt, 64);
     if (lane == 0) {
-      s_red[wv][PX_COST] = tot[0];
-      s_red[wv][PX_PRICE0] = tot[1];
-      s_red[wv][PX_MAX_ERR] = mx;
-      s_red[wv][PX_N_OK] = tot[2];
-      s_red[wv][PX_N_REPAIRED] = tot[3];
-      s_red[wv][PX_N_FAILED] = cnt[0];
-      s_red[wv][PX_N_INVALID] = cnt[1];
+      red_w[PX_COST] = tot[0];
+      red_w[PX_PRICE0] = tot[1];
+      red_w[PX_MAX_ERR] = mx;
+      red_w[PX_N_OK] = tot[2];
+      red_w[PX_N_REPAIRED] = tot[3];
+      red_w[PX_N_FAILED] = cnt[0];
+      red_w[PX_N_INVALID] = cnt[1];
     }
   };
   // the workgroup record (fixed-order combination of the waves'), by the threads of `lanes`
@@ -1182,10 +1341,10 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     for (int c = t; c < N + NPX; c += nthreads) {
       double v = 0.0;
       if (c < N) {
-        for (int k = 0; k < EVAL_WAVES; ++k) v += s_accw[k][c];
+        for (int k = 0; k < EVAL_WAVES; ++k) v += accw_all[k * astr + c];
       } else {
         const int x = c - N;
-        for (int k = 0; k < EVAL_WAVES; ++k) v = x == PX_MAX_ERR ? fmax(v, s_red[k][x]) : v + s_red[k][x];
+        for (int k = 0; k < EVAL_WAVES; ++k) v = x == PX_MAX_ERR ? fmax(v, red_all[k * 8 + x]) : v + red_all[k * 8 + x];
       }
       st_wt8(part + c, v);
     }
@@ -1354,8 +1513,8 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       lookup(h);
       __builtin_amdgcn_wave_barrier();  // this wave's own rows in LDS: in order
       any_inv = inv_rows;
-      const int r0b = EVAL_EVS * h + 64 * wv;
-      const int nh = max(0, min(64, end - start - r0b));  // wave-uniform
+      const int r0b = STG ? sg0 + 64 * h : EVAL_EVS * h + 64 * wv;
+      const int nh = STG ? min(64, sgn - 64 * h) : max(0, min(64, end - start - r0b));  // wave-uniform
       if (nh > 0) row_segment(r0b, nh);
     }
     if (lane == 0) st_wt4(a.fail_cnt + (size_t)rb * EVAL_WAVES + wv, nlist);
@@ -1378,12 +1537,14 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
         s1 += __shfl(acc1, lane + k * Lr, 64);
       }
       if (lane < Lr) {
-        s_accw[wv][V * lane] = s0;
-        if (V == 2) s_accw[wv][V * lane + 1] = s1;
+        accw_w[V * lane] = s0;
+        if (V == 2) accw_w[V * lane + 1] = s1;
       }
     }
-    __syncthreads();
-    if (tid < 64) store_record(tid, 64);
+    if constexpr (!STG) {
+      __syncthreads();
+      if (tid < 64) store_record(tid, 64);
+    }
   }
   LQ_STAMPE(5);
 }
@@ -1572,7 +1733,85 @@ __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_evals(EvalArgs a, 
   }
 }
 
+// k_evals with the stager (LQ_EVALS_STAGER; compact tables, a.cap = their capacity, a.G <= 64, N + 4
+// <= 64, blocks of <= LQ_EVALS_MAXB EVs): wave LQ_EVALS_RW stages run 0's table, then during run r the
+// table of run r + 1 into the other LDS table while waves 0 .. LQ_EVALS_RW - 1 evaluate run r (eval_block
+// STG); ONE barrier per run, after which wave 0 stores run r's workgroup record from the run's scratch
+// parity (the stager's row sums and record are zero) while the other waves start run r + 1.
+template <int NT>
+__global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_evals_st(EvalArgs a, EvalsArgs x) {
+  extern __shared__ __attribute__((aligned(16))) double2 s_dyn[];
+  const int b = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: the roles' branches are scalar)
+  const int N = NT ? NT : a.N, G = a.G, capc = a.cap;
+  const size_t tb = ctab_bytes(N, G, capc);
+  char* const base = reinterpret_cast<char*>(s_dyn);
+  double* const accw = reinterpret_cast<double*>(base + 2 * tb);  // [2][EVAL_WAVES][N]
+  double* const red = accw + (size_t)2 * EVAL_WAVES * N;         // [2][EVAL_WAVES][8]
+  const int s = a.blk[b].x;
+  if (wv == LQ_EVALS_RW) {
+    const int NS = eval_row_stride(N);
+    for (int k = 0; k < 2; ++k) {
+      const CTab T = ctab_at(base + k * tb, N, G, capc);
+      for (int i = lane; i < 2 * NS; i += 64) T.ab[(size_t)capc * NS + i] = make_double2(0.0, 0.0);  // zero pieces
+      for (int i = lane; i < N; i += 64) accw[((size_t)k * EVAL_WAVES + LQ_EVALS_RW) * N + i] = 0.0;
+      if (lane < 8) red[((size_t)k * EVAL_WAVES + LQ_EVALS_RW) * 8 + lane] = 0.0;
+    }
+    stage_compact(a, s, (int64_t)(x.run0 % x.slots) * x.SG, ctab_at(base, N, G, capc), N, G, capc, lane);
+  }
+  __syncthreads();
+  for (int r = 0; r < x.nruns; ++r) {
+    const int j = x.run0 + r;
+    if (wv < LQ_EVALS_RW) {
+      RunOff ro;
+      ro.tab = (int64_t)(j % x.slots) * x.SG;
+      ro.rec = r * x.nblk;
+      ro.ev = (int64_t)j * x.ev_stride;
+      ro.lmbd = a.lmbd + (size_t)j * x.lm_stride;
+      ro.lmbd_r = a.lmbd_r + (size_t)j * x.lr_stride;
+      ro.launder = true;
+      ro.gamma_lds = r > 0;
+      ro.buf = r & 1;
+      int bl = b;
+      asm volatile("" : "+s"(bl));
+      eval_block<NT, false, true>(a, bl, nullptr, ro);
+    } else if (r + 1 < x.nruns) {
+      stage_compact(a, s, (int64_t)((j + 1) % x.slots) * x.SG, ctab_at(base + ((r + 1) & 1) * tb, N, G, capc), N, G,
+                    capc, lane);
+    }
+    __syncthreads();  // run r's rows, row sums and wave records done; run r + 1's table staged
+    if (wv == 0) {    // run r's workgroup record (the waves combined in a fixed order, as store_record)
+      const int rb = r * x.nblk + b;
+      const int par = r & 1;
+      double* part = a.partial + (size_t)rb * (N + NPX);
+      for (int c = lane; c < N + NPX; c += 64) {
+        double v = 0.0;
+        if (c < N) {
+          for (int k = 0; k < EVAL_WAVES; ++k) v += accw[((size_t)par * EVAL_WAVES + k) * N + c];
+        } else {
+          const int xx = c - N;
+          for (int k = 0; k < EVAL_WAVES; ++k) {
+            const double u = red[((size_t)par * EVAL_WAVES + k) * 8 + xx];
+            v = xx == PX_MAX_ERR ? fmax(v, u) : v + u;
+          }
+        }
+        st_wt8(part + c, v);
+      }
+      if (lane == 0) st_wt4(a.fail_cnt + (size_t)rb * EVAL_WAVES + LQ_EVALS_RW, 0);  // (the stager's list)
+    }
+  }
+}
+
 typedef void (*EvalsKernel)(EvalArgs, EvalsArgs);
+EvalsKernel evals_st_kernel(int N) {
+  switch (N) {
+    case 12: return k_evals_st<12>;
+    case 16: return k_evals_st<16>;
+    case 24: return k_evals_st<24>;
+    case 48: return k_evals_st<48>;
+    default: return k_evals_st<0>;
+  }
+}
 EvalsKernel evals_kernel(int N) {
   switch (N) {
     case 12: return k_evals<12>;
@@ -2545,20 +2784,29 @@ int lq_price_loop_host(lompc_plan* p, const lompc_price_loop_args* a, double* lm
 // The stepped form's block map, tables and records (once per prepare).  The path takes np_wg of the
 // k_step workgroup slots for the whole launch, so the evaluation blocks are sized to fill the rest once
 // (or a whole number of times for big batches).
+// the wide form's evaluation takes k_evals_st (the stager wave) when its compact table and lane maps fit
+bool evals_stg_ok(const lompc_plan* p) { return LQ_EVALS_STAGER && p->G <= 64 && p->N + 4 <= 64; }
+
 int stepped_setup(lompc_plan* p, hipStream_t st, bool wide) {
   auto& z = p->stp;
   const int N = p->N;
   const int64_t S = p->S, G = p->G, ncell = S * G, B = p->B;
-  const int cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
-  if (z.occ_N != N) {
-    HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&z.occ, step_kernel(N), EVAL_EVS, eval_lds(N, p->G, cap)));
+  const bool stg = wide && evals_stg_ok(p);
+  const int cap = std::min(stg ? LQ_EVALS_CAP : LQ_PIECE_CAP, p->G * LQ_PPL);
+  const int64_t okey = ((int64_t)N * 4096 + G) * 2 + (stg ? 1 : 0);
+  if (z.occ_key != okey) {
+    if (stg)
+      HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&z.occ, evals_st_kernel(N), EVAL_EVS, evals_st_lds(N, p->G, cap)));
+    else
+      HIPCHK(p, hipOccupancyMaxActiveBlocksPerMultiprocessor(&z.occ, step_kernel(N), EVAL_EVS, eval_lds(N, p->G, cap)));
     z.occ = std::max(z.occ, 1);
-    z.occ_N = N;
+    z.occ_key = okey;
   }
+  const int64_t maxb = stg ? LQ_EVALS_MAXB : EVAL_MAXB;  // EVs per block at most
   z.np_wg = wide ? 0 : (int)((ncell + LQ_STEP_CELLS - 1) / LQ_STEP_CELLS);  // (wide: the paths have their own launch)
   const int64_t slots = (int64_t)p->n_cu * z.occ;
   const int64_t free1 = std::max<int64_t>(slots - z.np_wg, slots / 2);  // the first round, beside the path
-  const int64_t rounds = std::max<int64_t>(1, (10 * B + 9ll * slots * EVAL_MAXB - 1) / (9ll * slots * EVAL_MAXB));
+  const int64_t rounds = std::max<int64_t>(1, (10 * B + 9ll * slots * maxb - 1) / (9ll * slots * maxb));
   const int64_t target = free1 + (rounds - 1) * slots;
   std::vector<int64_t> off(S + 1);
   {  // the set offsets from the prepared map (host copy kept in the pinned metadata)
@@ -2567,7 +2815,7 @@ int stepped_setup(lompc_plan* p, hipStream_t st, bool wide) {
   }
   auto blocks_of = [&](int64_t m) -> int64_t {
     if (m <= 0) return 0;
-    const int64_t lo = (m + EVAL_MAXB - 1) / EVAL_MAXB, hi = (m + 255) / 256;
+    const int64_t lo = (m + maxb - 1) / maxb, hi = (m + 255) / 256;
     return std::max<int64_t>(lo, std::min<int64_t>(hi, m * target / std::max<int64_t>(B, 1)));
   };
   int64_t nblk = 0;
@@ -2613,6 +2861,7 @@ int stepped_setup(lompc_plan* p, hipStream_t st, bool wide) {
   }
   z.ok = true;
   z.wide = wide;
+  z.stg = stg;
   return LOMPC_OK;
 }
 
@@ -2656,7 +2905,7 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   const int Kc = (int)std::min<int64_t>({(int64_t)K, LQ_WIDE_RUNS, fit});
   const bool wide = (p->flags & LOMPC_PLAN_WARM_START) == 0 && Kc >= 1;
   const int slots = Kc + 1;
-  if ((!z.ok || z.wide != wide) && (rc = stepped_setup(p, st, wide))) return rc;
+  if ((!z.ok || z.wide != wide || z.stg != (wide && evals_stg_ok(p))) && (rc = stepped_setup(p, st, wide))) return rc;
   const bool xr = p->comm != nullptr;
   if (xr && (rc = lq_xbufs(p, 2))) return rc;
   // (the ring sized for the largest group the plan allows, whatever this call's K: a later call with
@@ -2714,7 +2963,7 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   const int cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
   const size_t lds = eval_lds(N, p->G, cap);
   const StepKernel kern = step_kernel(N);
-  if (wide && !split) {
+  if (wide && (!split || z.stg)) {
     // batched: per path group of n <= Kc runs THREE launches — k_paths (the n paths), k_evals (the n
     // evaluations, each workgroup through its block of every run) and k_closes (the n x S closings);
     // the same kernels' arithmetic as the split form below, so the same bits
@@ -2740,8 +2989,13 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     ff.blk_prefix = reinterpret_cast<const int*>(z.d_map + (((size_t)z.nblk * sizeof(int4) + 15) & ~(size_t)15));
     ff.set_sum_w = xr ? p->d_xsend : set_sum_w;
     ff.set_stats = xr ? p->d_xsend + p->S * N : set_stats;
-    for (int g0 = 0; g0 < K; g0 += Kc) {
-      const int n = std::min(Kc, K - g0);
+    // (k_evals_st's split form: the same three kernels, one run per group — its arithmetic is not
+    // k_step's: the stager leaves seven waves to the rows, so the row sums group differently)
+    const int grp = split ? 1 : Kc;
+    if (z.stg) ea.cap = std::min(LQ_EVALS_CAP, p->G * LQ_PPL);
+    const size_t lds_e = z.stg ? evals_st_lds(N, p->G, ea.cap) : lds;
+    for (int g0 = 0; g0 < K; g0 += grp) {
+      const int n = std::min(grp, K - g0);
       {
         PathArgs pw = path_args(p, lmbd, lmbd_r, z.wt);
         hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -2756,7 +3010,8 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
         const bool ev = !span_events || g0 == 0;
         if (ev && plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1)) return fail_arg(p, "profiling events");
         const EvalsArgs x{g0, n, slots, z.nblk, lmbd_stride, lmbd_r_stride, ev_stride, ncell};
-        hipExtLaunchKernelGGL(evals_kernel(N), dim3((unsigned)z.nblk), dim3(EVAL_EVS), lds, st, e0, e1, 0, ea, x);
+        hipExtLaunchKernelGGL(z.stg ? evals_st_kernel(N) : evals_kernel(N), dim3((unsigned)z.nblk), dim3(EVAL_EVS), lds_e, st,
+                              e0, e1, 0, ea, x);
         HIPCHK(p, hipGetLastError());
         if (ev) plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1, n);
       }
@@ -2977,7 +3232,7 @@ int lompc_plan_status(lompc_plan* p, void* stream, int64_t* n_repaired, int64_t*
 int lompc_plan_get_info(const lompc_plan* p, int64_t* B, int64_t* S, int* cells, int* eval_workgroups,
                         int* steps_group) {
   if (!p) return LOMPC_ERR_INVALID_ARG;
-  if (steps_group) *steps_group = p->stp.ok ? 1 : 0;
+  if (steps_group) *steps_group = p->stp.ok ? (p->stp.stg ? 2 : 1) : 0;
   if (B) *B = p->B;
   if (S) *S = p->S;
   if (cells) *cells = p->G;

@@ -463,14 +463,16 @@ class BatchPlan:
         return self
 
     def info(self) -> dict:
-        """Batch size, parameter sets, gamma cells per set, k_eval workgroups of the plan and the runs per
-        stepped run_steps launch (1 once the stepped form has run, else 0)."""
+        """Batch size, parameter sets, gamma cells per set, k_eval workgroups of the plan, the runs per
+        stepped run_steps launch (1 once the stepped form has run, else 0) and whether run_steps' wide
+        form evaluates through k_evals_st (the stager wave: set reductions grouped by seven row waves)."""
         if self.direct:
-            return {"B": self.B, "sets": self.S, "cells": 0, "workgroups": 0, "steps_group": 0}
+            return {"B": self.B, "sets": self.S, "cells": 0, "workgroups": 0, "steps_group": 0, "evals_staged": False}
         B, S, cells, wg, grp = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
         self._check_rc(self._lib.lompc_plan_get_info(self._plan, ctypes.byref(B), ctypes.byref(S), ctypes.byref(cells),
                                                      ctypes.byref(wg), ctypes.byref(grp)))
-        return {"B": B.value, "sets": S.value, "cells": cells.value, "workgroups": wg.value, "steps_group": grp.value}
+        return {"B": B.value, "sets": S.value, "cells": cells.value, "workgroups": wg.value,
+                "steps_group": min(grp.value, 1), "evals_staged": grp.value == 2}
 
     def update(self, gamma, set_offsets, w_ref=None, validate=True) -> "BatchPlan":
         """Re-target the plan at a new batch with the same contexts and set counts (e.g. the

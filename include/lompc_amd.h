@@ -287,8 +287,10 @@ int lompc_plan_status(lompc_plan* plan, void* stream, int64_t* n_repaired,
                       int64_t* n_failed, int64_t* n_invalid);
 
 /* Batch size, total parameter sets, gamma cells per set and k_eval workgroups of the plan, and the
- * runs per stepped launch of its lompc_plan_run_steps calls (1 once the stepped form has run, else 0);
- * any pointer may be null. */
+ * runs per stepped launch of its lompc_plan_run_steps calls (0 before any; 1 once they have run; 2: in
+ * the wide form with the staged evaluation k_evals_st, whose row sums group by seven row waves — its
+ * set reductions equal single runs' to rounding, its per-EV outputs bit for bit); any pointer may be
+ * null. */
 int lompc_plan_get_info(const lompc_plan* plan, int64_t* B, int64_t* S, int* cells, int* eval_workgroups,
                         int* steps_group);
 

@@ -66,7 +66,7 @@ for libname in args.libs:
             walls.append((time.perf_counter() - t0) / K * 1e6)
             ms, n = plan.profile(read=True)
             ks.append(ms / max(n, 1) * 1e3)
-            plan.check()
+            rep = plan.check()[0]
         plan.profile(enable=("k_path", "k_eval", "k_finalize"))
         for k in ("k_path", "k_eval", "k_finalize"):
             plan.profile(read=True, reset=True, kernel=k)
@@ -86,5 +86,6 @@ for libname in args.libs:
         print(f"   run_steps call overhead (n_runs = 0, out given): {wrap_us:6.1f} us", flush=True)
         print(f"{libname} cells {plan.cells} {args.outputs}: per step {np.median(walls):6.2f} us (min {min(walls):6.2f})"
               f"  k_step {np.median(ks):6.2f} us  alone: " +
-              "  ".join(f"{k} {ms / max(n, 1) * 1e3:6.2f}" for k, (ms, n) in alone.items()), flush=True)
+              "  ".join(f"{k} {ms / max(n, 1) * 1e3:6.2f}" for k, (ms, n) in alone.items()) +
+              f"  repaired per step {rep / K:.0f}", flush=True)
         del plan

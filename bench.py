@@ -465,8 +465,9 @@ def collective_cost(runs, args, world, dev, torch, dist, comm, batched, dt):
     """The per-step cost of the cross-rank exchange, so a scaling run is attributable: the same K
     timed steps again WITHOUT the exchange (RCCL: the plan's communicator detached, so no all-gather /
     combine kernel; gloo: no torch.distributed combine), max over ranks; collective_us_per_step =
-    timed step - that step.  Also the exchange alone (RCCL: K all-gathers of the packed set records
-    through torch.distributed on the same communicator size; gloo: K combine_set_results calls)."""
+    timed step - that step.  Also the exchange alone (RCCL: ceil(K / 32) all-gathers of a group's packed
+    set records through torch.distributed on the same communicator size; gloo: K combine_set_results
+    calls)."""
     from lompc_amd.dist import combine_set_results
 
     K = args.steps
@@ -497,16 +498,18 @@ def collective_cost(runs, args, world, dev, torch, dist, comm, batched, dt):
         finally:
             plan.set_comm(comm)
         S, N = plan.S, plan.N
-        rec = torch.zeros(S * (N + 8), dtype=torch.float64, device=dev)
+        G32 = 32  # (the wide form's group: one all-gather of its runs' contiguous records)
+        rec = torch.zeros(min(K, G32) * S * (N + 8), dtype=torch.float64, device=dev)
         recv = torch.empty(world * rec.numel(), dtype=torch.float64, device=dev)
 
         def gathers():
-            for _ in range(K):
+            for _ in range((K + G32 - 1) // G32):
                 dist.all_gather_into_tensor(recv, rec)
 
         gathers()
         t_ag = timed(gathers)
-        how = "RCCL all-gather of the packed set records + the k_combine kernel, inside each step's run"
+        how = ("RCCL: ONE all-gather of a group's (up to 32 steps') packed set records + the k_combine_runs kernel "
+               "after the group's closings, inside the run_steps call")
     else:
         outs = [(x["plan"].out["set_sum_w"], x["plan"].out["set_stats"]) for x in runs]
 
@@ -1016,10 +1019,11 @@ def cpu_same_algorithm(eng, N, P, args, ref):
     B = int(off[-1])
 
     def timed(nt, budget):
-        oracle_c.path_run(N, cs, [P, P], lms[0], lr, g, off, w_ref=wr, nthreads=nt)  # warm-up (threads, pages)
+        # (one output buffer set every run rewrites, as the GPU line's steps do: warm-up touches its pages)
+        o = oracle_c.path_run(N, cs, [P, P], lms[0], lr, g, off, w_ref=wr, nthreads=nt)
         done, t0, k = 0, time.perf_counter(), 0
         while True:
-            o = oracle_c.path_run(N, cs, [P, P], lms[k % len(lms)], lr, g, off, w_ref=wr, nthreads=nt)
+            o = oracle_c.path_run(N, cs, [P, P], lms[k % len(lms)], lr, g, off, w_ref=wr, nthreads=nt, out=o)
             assert o["info"][3] == 0
             done += B
             k += 1

@@ -85,11 +85,12 @@ def load_path():
 
 
 def path_run(N, consts, sets_per_ctx, lmbd, lmbd_r, gamma, set_off, w_ref=None, cells=0, nthreads=0, want_w=True,
-             want_cost=True):
+             want_cost=True, out=None):
     """The path engine's algorithm on the host (oracle/path_cpu.cpp): B QPs grouped by set (the sets of
     consts[0] first), lmbd (S, 3N), lmbd_r (S,), gamma (B,), set_off (S+1,).  Returns a dict of w (B, N),
     cost (B,), set_sum_w (S, N), set_stats (S, 8) and info (pieces, certified cells, EVs solved
-    individually, EVs failed)."""
+    individually, EVs failed).  ``out``: a previous call's dict, whose buffers are rewritten (a fresh
+    50 MB w per call spends its time in first-touch page faults, which serialise the threads)."""
     lib = load_path()
     cs = np.ascontiguousarray(np.array([[c.delta, c.theta, c.y_max, c.w_max, 1.0 if c.ev_type == "small" else 0.0]
                                         for c in consts], dtype=np.float64))
@@ -100,8 +101,9 @@ def path_run(N, consts, sets_per_ctx, lmbd, lmbd_r, gamma, set_off, w_ref=None, 
     off = np.ascontiguousarray(np.asarray(set_off, dtype=np.int64))
     wr = None if w_ref is None else np.ascontiguousarray(np.asarray(w_ref, dtype=np.float64))
     S, B = off.shape[0] - 1, g.shape[0]
-    out = {"w": np.empty((B, N)) if want_w else None, "cost": np.empty(B) if want_cost else None,
-           "set_sum_w": np.empty((S, N)), "set_stats": np.empty((S, 8))}
+    if out is None or out["set_sum_w"].shape != (S, N) or (want_w and (out["w"] is None or out["w"].shape != (B, N))):
+        out = {"w": np.empty((B, N)) if want_w else None, "cost": np.empty(B) if want_cost else None,
+               "set_sum_w": np.empty((S, N)), "set_stats": np.empty((S, 8))}
     info = np.zeros(4, dtype=np.int64)
     ptr = lambda a: None if a is None else a.ctypes.data
     rc = lib.path_cpu_run(int(N), len(consts), cs.ctypes.data, spc.ctypes.data, lm.ctypes.data, lr.ctypes.data,

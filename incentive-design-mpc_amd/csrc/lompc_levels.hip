@@ -15,9 +15,12 @@
 //       levels' overall max / min beside rng[0] / rng[P] (the caller's range check: outside it, EVs
 //       keep their previous partition and the runs are not the partitions — the caller then takes
 //       the index-based path).
-// Deterministic: the same levels give the same bits.
+// Deterministic: the same levels give the same bits.  lompc_levels_gamma then lays out every
+// partition's loop-plan batch (gamma = y_max - y ascending, then its central QP) in one launch.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -94,6 +97,27 @@ __global__ __launch_bounds__(256) void k_lv_stats(const double* __restrict__ ys,
   }
 }
 
+// gam[i + k central] = y_max - ys[i] for element i of storage run k (runs[k] <= i < runs[k + 1]), and with
+// `central` each run's central QP gsc[k] right after it, at runs[k + 1] + k
+__global__ __launch_bounds__(256) void k_lv_gamma(const double* __restrict__ ys, int64_t n,
+                                                  const int64_t* __restrict__ runs, int P, double y_max, int central,
+                                                  const double* __restrict__ gsc, double* __restrict__ gam) {
+  __shared__ int64_t e[LV_MAXP + 1];
+  for (int k = (int)threadIdx.x; k <= P; k += 256) e[k] = runs[k];
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    int lo = 0, hi = P;  // the last run with e[lo] <= i (empty runs skipped): e[lo] <= i < e[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (e[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    gam[i + (central ? lo : 0)] = y_max - ys[i];
+  }
+  if (central && blockIdx.x == 0)
+    for (int k = (int)threadIdx.x; k < P; k += 256) gam[e[k + 1] + k] = gsc[k];
+}
+
 size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
@@ -121,5 +145,14 @@ extern "C" int lompc_levels_layout(const double* y, int64_t n, const double* bou
   if (P > 1) hipLaunchKernelGGL(k_lv_bounds, dim3((unsigned)(P - 1)), dim3(64), 0, st, ys, n, bounds, cge);
   hipLaunchKernelGGL(k_lv_partials, dim3(LV_CHUNKS, (unsigned)P), dim3(256), 0, st, ys, n, P, cge, part);
   hipLaunchKernelGGL(k_lv_stats, dim3(1), dim3(256), 0, st, ys, n, P, bounds, cge, part, stats);
+  return hipGetLastError() == hipSuccess ? LOMPC_OK : LOMPC_ERR_HIP;
+}
+
+extern "C" int lompc_levels_gamma(const double* ys, int64_t n, const int64_t* runs, int P, double y_max, int central,
+                                  const double* gsc, double* gam, void* stream) {
+  if (n < 0 || P < 1 || P > LV_MAXP || !runs || !gam || (n > 0 && !ys) || (central && !gsc)) return LOMPC_ERR_INVALID_ARG;
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 2048);
+  hipLaunchKernelGGL(k_lv_gamma, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ys, n, runs, P, y_max,
+                     central, gsc, gam);
   return hipGetLastError() == hipSuccess ? LOMPC_OK : LOMPC_ERR_HIP;
 }

@@ -153,9 +153,12 @@ class ChargingStation:
         # every partition's loop plan of a step prepared beside the BiMPC solve (False: each partition's
         # plan prepared when its loop starts — for A/B timing)
         self.stage_partitions = True
+        # the partitions' loop-plan batches laid out in one launch per type (False: per partition — A/B timing)
+        self.gamma_layout = True
         self.phase_ms = {}
         self.last_step_ms = {}  # host time of the last step's phases (_tick)
         self.chain_ms = {}  # the last step's price chain per EV type (host time of its native call)
+        self._gl_host, self._gl_keep = {}, {}  # _gamma_layout's pinned run bounds per price solver
         self.device = torch.cuda.current_device() if device is None else int(device)
         self._dev = f"cuda:{self.device}"
         # Set constants, initialize PriceSolvers and BiMPC.
@@ -519,11 +522,13 @@ class ChargingStation:
             with torch.cuda.device(self.device), torch.cuda.stream(solver._stream):
                 # the type's partition layout too (its sorts and one host sync: on this thread, beside
                 # the interior point, not before it); its tensors are read on the main stream later
-                self._partition_layout(kind, y, idx, main)
+                _, ys, seg = self._partition_layout(kind, y, idx, main)
+                gam, at = self._gamma_layout(solver, ys, seg, st) if self.gamma_layout else (None, None)
                 for p in range(self.P):
                     if st[p, 0] > 0:
-                        ys, (a, b) = self._part_slice(kind, y, idx, p)
-                        solver.stage_partition(p, ys[a:b], st[p, 0], st[p, 1], st[p, 2], st[p, 3], descending=True)
+                        a, b = seg[p]
+                        solver.stage_partition(p, ys[a:b], st[p, 0], st[p, 1], st[p, 2], st[p, 3], descending=True,
+                                               gamma_view=None if gam is None else gam[at[p][0]:at[p][1]])
 
         if self.group is not None:
             for job in jobs:
@@ -532,6 +537,40 @@ class ChargingStation:
         if self._stage_pool is None:
             self._stage_pool = concurrent.futures.ThreadPoolExecutor(max_workers=2)
         return [self._stage_pool.submit(stage, job) for job in jobs]
+
+    def _gamma_layout(self, solver: PriceSolver, ys, seg, st):
+        """Every partition's loop-plan batch of one EV type in ONE launch (lompc_levels_gamma, for
+        PriceSolver._build_plans' ``prebuilt``): gamma = y_max - y0 of the layout's levels (ascending
+        within each partition's run, whose levels descend), and on rank 0 each partition's central QP
+        (gamma_sc = y_max - (y_hi + y_lo) / 2, price_solver.py:73-76) right after its run.  The runs'
+        bounds and central gammas go up in one copy from pinned memory.  Returns (the buffer,
+        {p: (start, end)} of its views)."""
+        torch = _torch()
+        P, ym = self.P, float(solver.consts.y_max)
+        central = 1 if solver._rank() == 0 else 0
+        order = sorted(range(P), key=lambda p: seg[p])  # the runs in storage order
+        n = int(ys.numel())
+        hb = self._gl_host.get(solver)
+        if hb is None:  # (per solver: the two types' staging threads run at once)
+            hb = self._gl_host[solver] = torch.empty(2 * P + 1, dtype=torch.float64).pin_memory()
+        h = hb.numpy()
+        runs = h[: P + 1].view(np.int64)
+        runs[0] = seg[order[0]][0]
+        for k, p in enumerate(order):
+            runs[k + 1] = seg[p][1]
+            h[P + 1 + k] = ym - (float(st[p, 1]) + float(st[p, 2])) / 2 if st[p, 0] > 0 else 0.0
+        if runs[0] != 0 or runs[P] != n:
+            raise RuntimeError("partition layout: the runs do not tile the levels")
+        dev = hb.to(ys.device, non_blocking=True)
+        gam = torch.empty(n + central * P, dtype=torch.float64, device=ys.device)
+        lib = _lib.load()
+        rc = lib.lompc_levels_gamma(ys.data_ptr(), n, dev.data_ptr(), P, ym, central, dev.data_ptr() + 8 * (P + 1),
+                                    gam.data_ptr(), torch.cuda.current_stream(ys.device).cuda_stream)
+        if rc != _lib.LOMPC_OK:
+            raise RuntimeError(_lib.status_text(lib, None, rc))
+        at = {p: (seg[p][0] + k * central, seg[p][1] + (k + 1) * central) for k, p in enumerate(order)}
+        self._gl_keep[solver] = (hb, dev)  # (the copy's source stays alive until it has run)
+        return gam, at
 
     def _sorted_layouts(self):
         """Both EV types' partition layouts and statistics from ONE sort per type and rank, by the

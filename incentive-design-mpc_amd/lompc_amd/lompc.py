@@ -422,10 +422,13 @@ class BatchPlan:
                 raise ValueError("Parameter value must be nonnegative.")
         self.gamma, self.off = gamma, off
         self.w_ref = None if w_ref is None else lo._dev(w_ref).reshape(S, N)
-        if getattr(self, "B", None) != B or getattr(self, "S", None) != S:
+        wt = self._want
+        per_ev = wt["w"] or wt["cost"] or wt["w0"] or wt["status"]
+        # (re)allocate what the new shape changes: per-EV outputs with B, set outputs with S (a price loop's
+        # plan, re-targeted at a partition of another size every step, has only set outputs)
+        if getattr(self, "S", None) != S or (per_ev and getattr(self, "B", None) != B):
             dev = f"cuda:{lo.device}"
             e = lambda shape, dt=torch.float64: torch.empty(shape, dtype=dt, device=dev)
-            wt = self._want
             self.out = {
                 "w": e((B, N)) if wt["w"] else None,
                 "cost": e((B,)) if wt["cost"] else None,

@@ -194,11 +194,12 @@ class PriceSolver:
 
     @_solver_stream
     def set_charge_levels_stats(self, y0d, n: int, y_hi: float, y_lo: float, y_sum: float,
-                                descending: bool = False) -> None:
+                                descending: bool = False, gamma_view=None) -> None:
         """set_charge_levels for a device slice of charge levels whose (global) count / max /
         min / sum the caller already has (ChargingStation computes every partition's in one pass
         per step, charging_station.py:187-266): no host sync, no collective.  ``descending``: y0d
-        is already in descending order (gamma ascending), so the loop plan needs no sort."""
+        is already in descending order (gamma ascending), so the loop plan needs no sort.
+        ``gamma_view``: the plan's batch prebuilt by the caller (_build_plans' ``prebuilt``)."""
         if not (n > 0 and 0.0 <= y_lo <= y_hi <= self.consts.y_max):
             raise AssertionError("0 <= y0 <= y_max required (price_solver.py:71)")
         self.y0 = y0d
@@ -207,7 +208,10 @@ class PriceSolver:
         self.y0_rng = (y_hi - y_lo) / 2  # = \bar{\Gamma}
         self.gamma_sc = self.consts.y_max - (y_hi + y_lo) / 2
         self.gamma_sm = self.consts.y_max - y_sum / n
-        self._build_plans(self.consts.y_max - y0d, presorted=descending)
+        if gamma_view is not None:
+            self._build_plans(None, presorted=True, prebuilt=gamma_view)
+        else:
+            self._build_plans(self.consts.y_max - y0d, presorted=descending)
 
     def _device_comm(self):
         """The extension's RCCL communicator of the group (None: single rank, gloo, DIRECT mode)."""
@@ -237,7 +241,7 @@ class PriceSolver:
 
     @_solver_stream
     def stage_partition(self, p: int, y0d, n: int, y_hi: float, y_lo: float, y_sum: float,
-                        descending: bool = False) -> None:
+                        descending: bool = False, gamma_view=None) -> None:
         """set_charge_levels_stats for partition p ahead of its price loop: the partition's own
         loop plan is (re)prepared now, on the solver's stream, and kept with its levels until
         use_partition(p).  ChargingStation stages every partition of a step before the BiMPC
@@ -251,7 +255,7 @@ class PriceSolver:
         else:
             self._plan = None
         try:
-            self.set_charge_levels_stats(y0d, n, y_hi, y_lo, y_sum, descending=descending)
+            self.set_charge_levels_stats(y0d, n, y_hi, y_lo, y_sum, descending=descending, gamma_view=gamma_view)
             self._staged[p] = {k: getattr(self, k) for k in self._PART_STATE}
         finally:
             for k in self._PART_STATE:
@@ -263,22 +267,30 @@ class PriceSolver:
             setattr(self, k, v)
         self._w0_live = False
 
-    def _build_plans(self, gamma, presorted: bool = False) -> None:
+    def _build_plans(self, gamma, presorted: bool = False, prebuilt=None) -> None:
         """Batch layout of one price iteration: set 0 = this rank's EVs, set 1 = the central QP.
         The loop plan holds set 0's gamma in ascending order (LOMPC_PLAN_SORTED_GAMMA: its runs
         aggregate per certified piece, O(pieces) per iteration; only the per-set sums leave the
         loop, price_solver.py:196-214, so the EV order does not matter there); the w0 plan keeps
-        the caller's order (get_w0_price0 returns w0 per EV)."""
+        the caller's order (get_w0_price0 returns w0 per EV).  ``prebuilt``: that batch already
+        laid out by the caller — a contiguous device view [gamma ascending | gamma_sc (rank 0)]
+        (ChargingStation builds every partition's in one pass per type and step)."""
         torch = _torch()
-        B = int(gamma.numel())
         central = 1 if self._rank() == 0 else 0
-        gamma = gamma.reshape(-1).to(dtype=torch.float64).contiguous()
-        self._gam = torch.empty(B + central, dtype=torch.float64, device=self._dev)
-        self._gam[:B] = gamma if presorted else torch.sort(gamma).values
-        self._gam_w0 = gamma
-        self._gcentral = None if not central else self._gam[B:]
-        if central:
-            self._gam[B] = float(self.gamma_sc)
+        if prebuilt is not None:
+            B = int(prebuilt.numel()) - central
+            self._gam = prebuilt
+            self._gam_w0 = prebuilt[:B]
+            self._gcentral = None if not central else prebuilt[B:]
+        else:
+            B = int(gamma.numel())
+            gamma = gamma.reshape(-1).to(dtype=torch.float64).contiguous()
+            self._gam = torch.empty(B + central, dtype=torch.float64, device=self._dev)
+            self._gam[:B] = gamma if presorted else torch.sort(gamma).values
+            self._gam_w0 = gamma
+            self._gcentral = None if not central else self._gam[B:]
+            if central:
+                self._gam[B] = float(self.gamma_sc)
         off = np.array([0, B, B + central], dtype=np.int64)
         # gamma = y_max - y0 with 0 <= y0 <= y_max asserted in set_charge_levels.  The price
         # iterations change the prices a little at a time: each gamma cell's exact solve starts

@@ -279,6 +279,16 @@ int lompc_plan_run_chain(lompc_plan* plan, const double* lmbd0, const double* lm
 int lompc_levels_layout(const double* y, int64_t n, const double* bounds, int P, double* ys, int64_t* perm,
                         double* stats, void* work, size_t* work_bytes, void* stream);
 
+/* Every partition's price-loop batch of one EV type in one launch (PriceSolver.set_charge_levels'
+ * gamma = y_max - y0, price_solver.py:66-77, for each partition of charging_station.py:275-307, and
+ * the central QP's gamma_sc = y_max - (max + min) / 2, price_solver.py:73-76, the plans' last set):
+ * ys dev [n] the levels in storage order (e.g. lompc_levels_layout's), runs dev [P+1] the storage
+ * runs' bounds (runs[0] = 0, runs[P] = n, non-decreasing), gsc dev [P] per run (read only with
+ * central != 0).  gam dev [n + P central]: run k's gammas at runs[k] + k central .. runs[k+1] + k
+ * central - 1 (ascending when ys is descending), its gsc at runs[k+1] + k when central.  Asynchronous. */
+int lompc_levels_gamma(const double* ys, int64_t n, const int64_t* runs, int P, double y_max, int central,
+                       const double* gsc, double* gam, void* stream);
+
 /* Synchronise ``stream``; EVs repaired / failed / invalid summed over EVERY run since the previous
  * lompc_plan_status call (sticky device tallies, zeroed here), so a failure in any of the runs of a
  * lompc_plan_run_steps call or of a price loop is seen.  These count this rank's EVs only; with a

@@ -32,25 +32,34 @@ torch.cuda.synchronize()
 sol = st.price_solver_l
 _, ys, seg = st._partition_layout("Large", st.y_l, st.idx_l)
 stl = st._pstats[1]
-t_tot = []
-for rep in range(3):
-    for p in range(P):
-        if stl[p, 0] <= 0:
-            continue
+for form in ("per partition", "one layout per type"):
+    t_tot, t_lay = [], []
+    for rep in range(3):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        with torch.cuda.stream(sol._stream):
-            sol.stage_partition(p, ys[seg[p][0]:seg[p][1]], stl[p, 0], stl[p, 1], stl[p, 2], stl[p, 3], descending=True)
-        t1 = time.perf_counter()
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        t_tot.append(((t1 - t0) * 1e6, (t2 - t0) * 1e6))
-a = np.array(t_tot)
-print(f"stage_partition: host {a[:, 0].mean():7.1f} us (median {np.median(a[:, 0]):7.1f}), "
-      f"with the GPU work {a[:, 1].mean():7.1f} us, over {len(a)} calls")
+        gam, at = st._gamma_layout(sol, ys, seg, stl) if form != "per partition" else (None, None)
+        t_lay.append((time.perf_counter() - t0) * 1e6)
+        for p in range(P):
+            if stl[p, 0] <= 0:
+                continue
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            with torch.cuda.stream(sol._stream):
+                gv = None if gam is None else gam[at[p][0]:at[p][1]]
+                sol.stage_partition(p, ys[seg[p][0]:seg[p][1]], stl[p, 0], stl[p, 1], stl[p, 2], stl[p, 3], descending=True,
+                                    gamma_view=gv)
+            t1 = time.perf_counter()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            t_tot.append(((t1 - t0) * 1e6, (t2 - t0) * 1e6))
+    a = np.array(t_tot)
+    print(f"{form}: stage_partition host {a[:, 0].mean():7.1f} us (median {np.median(a[:, 0]):7.1f}), "
+          f"with the GPU work {a[:, 1].mean():7.1f} us, over {len(a)} calls; the type's layout {np.mean(t_lay):6.1f} us",
+          flush=True)
+off = [seg[p][0] for p in range(P)] + [0]
 # the parts of one call, host time each (no sync between them)
 p = int(np.argmax(stl[:, 0]))
-y0 = ys[off[p]:off[p + 1]]
+y0 = ys[seg[p][0]:seg[p][1]]
 parts = {}
 for rep in range(20):
     torch.cuda.synchronize()

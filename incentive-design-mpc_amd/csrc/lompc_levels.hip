@@ -118,6 +118,105 @@ __global__ __launch_bounds__(256) void k_lv_gamma(const double* __restrict__ ys,
     for (int k = (int)threadIdx.x; k < P; k += 256) gam[e[k + 1] + k] = gsc[k];
 }
 
+// The statistics alone, without the sort (lompc_levels_stats, P <= LV_HP): EV i belongs to partition
+// p = #{k in 1 .. P-1 : bounds[k] <= y_i} (the sorted runs' rule).  Workgroup b sums its contiguous
+// chunk: each thread its strided EVs in registers (one predicated update per partition: no dynamic
+// register indexing), then fixed-order wave butterflies and a fixed-order combine of the 4 waves; the
+// workgroups' records are then combined in workgroup order by k_lvh_final.  Deterministic.
+constexpr int LV_HP = 16;
+constexpr int LV_HBLK = 512;  // workgroups at most
+
+__global__ __launch_bounds__(256) void k_lvh_partial(const double* __restrict__ y, int64_t n,
+                                                     const double* __restrict__ bounds, int P, int nblk,
+                                                     double* __restrict__ part) {
+  const int b = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
+  __shared__ double sb[LV_HP];
+  if (t < LV_HP) sb[t] = t >= 1 && t < P ? bounds[t] : INFINITY;
+  __syncthreads();
+  double bd[LV_HP];
+#pragma unroll
+  for (int k = 0; k < LV_HP; ++k) bd[k] = sb[k];
+  double cnt[LV_HP], sum[LV_HP], mx[LV_HP], mn[LV_HP];
+#pragma unroll
+  for (int k = 0; k < LV_HP; ++k) {
+    cnt[k] = 0.0;
+    sum[k] = 0.0;
+    mx[k] = -INFINITY;
+    mn[k] = INFINITY;
+  }
+  double ymx = -INFINITY, ymn = INFINITY;
+  const int64_t c0 = n * b / nblk, c1 = n * (b + 1) / nblk;
+  for (int64_t i = c0 + t; i < c1; i += 256) {
+    const double v = y[i];
+    int p = 0;
+#pragma unroll
+    for (int k = 1; k < LV_HP; ++k) p += bd[k] <= v ? 1 : 0;
+#pragma unroll
+    for (int k = 0; k < LV_HP; ++k) {
+      const bool m = k == p;
+      cnt[k] += m ? 1.0 : 0.0;
+      sum[k] += m ? v : 0.0;
+      mx[k] = m ? fmax(mx[k], v) : mx[k];
+      mn[k] = m ? fmin(mn[k], v) : mn[k];
+    }
+    ymx = fmax(ymx, v);
+    ymn = fmin(ymn, v);
+  }
+  __shared__ double sw[4][4 * LV_HP + 2];
+#pragma unroll
+  for (int k = 0; k < LV_HP; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      cnt[k] += __shfl_xor(cnt[k], o);
+      sum[k] += __shfl_xor(sum[k], o);
+      mx[k] = fmax(mx[k], __shfl_xor(mx[k], o));
+      mn[k] = fmin(mn[k], __shfl_xor(mn[k], o));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ymx = fmax(ymx, __shfl_xor(ymx, o));
+    ymn = fmin(ymn, __shfl_xor(ymn, o));
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < LV_HP; ++k) {
+      sw[wv][4 * k + 0] = cnt[k];
+      sw[wv][4 * k + 1] = mx[k];
+      sw[wv][4 * k + 2] = mn[k];
+      sw[wv][4 * k + 3] = sum[k];
+    }
+    sw[wv][4 * LV_HP] = ymx;
+    sw[wv][4 * LV_HP + 1] = ymn;
+  }
+  __syncthreads();
+  if (t < 4 * LV_HP + 2) {
+    const int f = t < 4 * LV_HP ? (t & 3) : (t == 4 * LV_HP ? 1 : 2);  // 0 count / 3 sum: add; 1 max; 2 min
+    double v = sw[0][t];
+    for (int w = 1; w < 4; ++w) v = f == 1 ? fmax(v, sw[w][t]) : f == 2 ? fmin(v, sw[w][t]) : v + sw[w][t];
+    part[(size_t)b * (4 * LV_HP + 2) + t] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lvh_final(const double* __restrict__ part, int nblk, int P,
+                                                   const double* __restrict__ bounds, double* __restrict__ stats) {
+  const int t = (int)threadIdx.x;
+  if (t < 4 * LV_HP + 2) {
+    const int f = t < 4 * LV_HP ? (t & 3) : (t == 4 * LV_HP ? 1 : 2);
+    double v = part[t];
+    for (int b = 1; b < nblk; ++b) {
+      const double u = part[(size_t)b * (4 * LV_HP + 2) + t];
+      v = f == 1 ? fmax(v, u) : f == 2 ? fmin(v, u) : v + u;
+    }
+    if (t < 4 * P) stats[t] = v;                 // per partition (count, max, min, sum)
+    else if (t >= 4 * LV_HP) stats[4 * P + (t - 4 * LV_HP)] = v;  // max y, min y
+  }
+  if (t == 0) {
+    stats[4 * P + 2] = bounds[0];
+    stats[4 * P + 3] = bounds[P];
+  }
+}
+
 size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
@@ -154,5 +253,24 @@ extern "C" int lompc_levels_gamma(const double* ys, int64_t n, const int64_t* ru
   const int64_t blocks = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 2048);
   hipLaunchKernelGGL(k_lv_gamma, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ys, n, runs, P, y_max,
                      central, gsc, gam);
+  return hipGetLastError() == hipSuccess ? LOMPC_OK : LOMPC_ERR_HIP;
+}
+
+// The partition statistics of lompc_levels_layout without its sort (P <= 16; more: LOMPC_ERR_UNSUPPORTED).
+extern "C" int lompc_levels_stats(const double* y, int64_t n, const double* bounds, int P, double* stats, void* work,
+                                  size_t* work_bytes, void* stream) {
+  if (!work_bytes || n < 1 || P < 1) return LOMPC_ERR_INVALID_ARG;
+  if (P > LV_HP) return LOMPC_ERR_UNSUPPORTED;
+  const int nblk = (int)std::min<int64_t>(LV_HBLK, std::max<int64_t>(1, (n + 4095) / 4096));
+  const size_t need = (size_t)LV_HBLK * (4 * LV_HP + 2) * sizeof(double);
+  if (!work) {
+    *work_bytes = need;
+    return LOMPC_OK;
+  }
+  if (*work_bytes < need || !y || !bounds || !stats) return LOMPC_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  double* part = static_cast<double*>(work);
+  hipLaunchKernelGGL(k_lvh_partial, dim3((unsigned)nblk), dim3(256), 0, st, y, n, bounds, P, nblk, part);
+  hipLaunchKernelGGL(k_lvh_final, dim3(1), dim3(256), 0, st, part, nblk, P, bounds, stats);
   return hipGetLastError() == hipSuccess ? LOMPC_OK : LOMPC_ERR_HIP;
 }

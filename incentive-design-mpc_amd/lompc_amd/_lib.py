@@ -95,6 +95,7 @@ SIGNATURES = [
     ("lompc_plan_run_chain", _I, [_P, _P, _P, _P, _D, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_levels_layout", _I, [_P, _L, _P, _I, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lompc_levels_gamma", _I, [_P, _L, _P, _I, _D, _I, _P, _P, _P]),
+    ("lompc_levels_stats", _I, [_P, _L, _P, _I, _P, _P, ctypes.POINTER(ctypes.c_size_t), _P]),
     ("lompc_plan_status", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_get_info", _I, [_P, _P, _P, _P, _P, _P]),
     ("lompc_plan_update", _I, [_P, _L, _P, _P, _P, _P]),

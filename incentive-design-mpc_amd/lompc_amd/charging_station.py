@@ -239,6 +239,7 @@ class ChargingStation:
             p = (torch.searchsorted(b, y, right=True) - 1).clamp_(0, self.P - 1)
             idx.copy_(torch.where((y >= b[0]) & (y <= b[-1]), p, idx))
         self._layout = {}
+        self._pending = {}  # (types whose statistics came without the sort: _partition_layout sorts them)
 
     def _init_logs(self, consts: ChargingStationConstants) -> None:
         # charging_station.py:118-149
@@ -601,21 +602,32 @@ class ChargingStation:
                 continue
             lv = self._lv.get(kind)
             if lv is None or lv["n"] != n:  # (buffers per type, reused from step to step)
-                wb = ctypes.c_size_t(0)
+                wb, hb = ctypes.c_size_t(0), ctypes.c_size_t(0)
                 rc = lib.lompc_levels_layout(None, n, None, P, None, None, None, None, ctypes.byref(wb), None)
                 if rc != _lib.LOMPC_OK:
                     raise ValueError(_lib.status_text(lib, None, rc))
+                rc = lib.lompc_levels_stats(None, n, None, P, None, None, ctypes.byref(hb), None)
                 e = lambda m, dt: torch.empty(m, dtype=dt, device=y.device)
                 lv = self._lv[kind] = {"n": n, "ys": e(n, torch.float64), "perm": e(n, torch.int64),
-                                       "stats": e(4 * P + 4, torch.float64), "work": e(wb.value, torch.uint8),
-                                       "wb": wb.value}
-            wb = ctypes.c_size_t(lv["wb"])
-            rc = lib.lompc_levels_layout(y.data_ptr(), n, b.data_ptr(), P, lv["ys"].data_ptr(), lv["perm"].data_ptr(),
-                                         lv["stats"].data_ptr(), lv["work"].data_ptr(), ctypes.byref(wb), stream)
-            if rc != _lib.LOMPC_OK:
-                raise RuntimeError(_lib.status_text(lib, None, rc))
+                                       "stats": e(4 * P + 4, torch.float64), "stats_sort": e(4 * P + 4, torch.float64),
+                                       "work": e(max(wb.value, hb.value), torch.uint8), "wb": wb.value,
+                                       "hb": hb.value if rc == _lib.LOMPC_OK else 0}
+            if lv["hb"]:  # the statistics alone now; the sort when the layout is first needed (beside the IPM)
+                hb = ctypes.c_size_t(lv["hb"])
+                rc = lib.lompc_levels_stats(y.data_ptr(), n, b.data_ptr(), P, lv["stats"].data_ptr(),
+                                            lv["work"].data_ptr(), ctypes.byref(hb), stream)
+                if rc != _lib.LOMPC_OK:
+                    raise RuntimeError(_lib.status_text(lib, None, rc))
+                parts.append((kind, None, None))
+            else:
+                wb = ctypes.c_size_t(lv["wb"])
+                rc = lib.lompc_levels_layout(y.data_ptr(), n, b.data_ptr(), P, lv["ys"].data_ptr(),
+                                             lv["perm"].data_ptr(), lv["stats"].data_ptr(), lv["work"].data_ptr(),
+                                             ctypes.byref(wb), stream)
+                if rc != _lib.LOMPC_OK:
+                    raise RuntimeError(_lib.status_text(lib, None, rc))
+                parts.append((kind, lv["ys"], lv["perm"]))
             recs.append(lv["stats"])
-            parts.append((kind, lv["ys"], lv["perm"]))
         rec = torch.stack(recs)  # (2, 4P + 4)
         if self.group is None:
             h = rec.cpu().numpy()[None]  # the one host sync
@@ -644,8 +656,11 @@ class ChargingStation:
             mine = dist.get_rank(self.group) if self.group is not None else 0
             cnt = rows[mine, : 4 * P].reshape(P, 4)[:, 0].astype(np.int64)  # this rank's runs
             ends = np.cumsum(cnt[::-1])  # runs in storage order, partition P-1 first
-            self._layout[kind] = (perm, ys, {p: (int(ends[k] - cnt[p]), int(ends[k]))
-                                             for k, p in enumerate(range(P - 1, -1, -1))})
+            seg = {p: (int(ends[k] - cnt[p]), int(ends[k])) for k, p in enumerate(range(P - 1, -1, -1))}
+            if ys is None:
+                self._pending[kind] = seg  # (sorted by _partition_layout)
+            else:
+                self._layout[kind] = (perm, ys, seg)
             out[kind] = st
         return out
 
@@ -657,6 +672,19 @@ class ChargingStation:
         type and step instead of one per partition).  Made by _sorted_layouts on one rank; otherwise
         here from the partition indices."""
         torch = _torch()
+        if kind not in self._layout and kind in self._pending:
+            # the sort the statistics pass deferred: this rank's levels descending (lompc_levels_layout, on
+            # the current stream), the runs from the statistics' counts
+            seg = self._pending.pop(kind)
+            lv, lib = self._lv[kind], _lib.load()
+            b = self._bounds[id(self.y0_s_rng if kind == "Small" else self.y0_l_rng)]
+            wb = ctypes.c_size_t(lv["wb"])
+            rc = lib.lompc_levels_layout(y.data_ptr(), int(y.numel()), b.data_ptr(), self.P, lv["ys"].data_ptr(),
+                                         lv["perm"].data_ptr(), lv["stats_sort"].data_ptr(), lv["work"].data_ptr(),
+                                         ctypes.byref(wb), torch.cuda.current_stream(self.device).cuda_stream)
+            if rc != _lib.LOMPC_OK:
+                raise RuntimeError(_lib.status_text(lib, None, rc))
+            self._layout[kind] = (lv["perm"], lv["ys"], seg)
         if kind not in self._layout:
             # (partition, -y) order exactly: a stable sort by descending y, then a stable sort by
             # partition (a composite float key would round near-equal charge levels out of order)

@@ -289,6 +289,14 @@ int lompc_levels_layout(const double* y, int64_t n, const double* bounds, int P,
 int lompc_levels_gamma(const double* ys, int64_t n, const int64_t* runs, int P, double y_max, int central,
                        const double* gsc, double* gam, void* stream);
 
+/* lompc_levels_layout's stats [4P + 4] without its sort (the BiMPC's inputs need only these, so the
+ * sort can run later, beside the host interior point): EV i in partition #{k in 1..P-1 : bounds[k] <=
+ * y_i}; per partition (count, max, min, sum) — sums in a fixed order of their own, not the sorted
+ * runs' —, then (max y, min y, bounds[0], bounds[P]).  P <= 16 (else LOMPC_ERR_UNSUPPORTED).  work /
+ * work_bytes as lompc_levels_layout.  Asynchronous, deterministic. */
+int lompc_levels_stats(const double* y, int64_t n, const double* bounds, int P, double* stats, void* work,
+                       size_t* work_bytes, void* stream);
+
 /* Synchronise ``stream``; EVs repaired / failed / invalid summed over EVERY run since the previous
  * lompc_plan_status call (sticky device tallies, zeroed here), so a failure in any of the runs of a
  * lompc_plan_run_steps call or of a price loop is seen.  These count this rank's EVs only; with a

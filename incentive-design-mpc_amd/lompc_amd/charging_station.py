@@ -159,6 +159,9 @@ class ChargingStation:
         self.last_step_ms = {}  # host time of the last step's phases (_tick)
         self.chain_ms = {}  # the last step's price chain per EV type (host time of its native call)
         self._gl_host, self._gl_keep = {}, {}  # _gamma_layout's pinned run bounds per price solver
+        # the w0 / price0 pass of both types in one engine run (False: one per type — A/B timing)
+        self.w0_one_call = True
+        self._w0plan, self._w0_host, self._w0_keep = None, None, None
         self.device = torch.cuda.current_device() if device is None else int(device)
         self._dev = f"cuda:{self.device}"
         # Set constants, initialize PriceSolvers and BiMPC.
@@ -743,11 +746,71 @@ class ChargingStation:
             raise SolverError("LoMPC QPs without a certified optimum")
         return red[:, :3]
 
+    def _w0_both(self, prices_s, prices_l, lmbd_r):
+        """Both EV types' w0 / price0 pass (price_solver.py:272-285 for every partition) in ONE engine
+        run of one plan over both contexts (kept across steps, re-targeted by lompc_plan_update): the
+        sets are the partitions in layout order, small type first.  Returns (w0_s, w0_l in EV order,
+        the device rows per (type, partition) (sum w0, sum price0, count, failed, invalid) combined over
+        ranks, partition order, small type's P rows first)."""
+        torch = _torch()
+        from .lompc import BatchPlan
+
+        N, P = self.N_lo, self.P
+        gams, offs, lm, per = [], [0], np.zeros((2 * P, 3 * N)), []
+        for t, (kind, solver, y, idx, prices) in enumerate(
+                (("Small", self.price_solver_s, self.y_s, self.idx_s, prices_s),
+                 ("Large", self.price_solver_l, self.y_l, self.idx_l, prices_l))):
+            perm, ys, seg = self._partition_layout(kind, y, idx)
+            order = sorted(range(P), key=lambda p: seg[p])  # set t P + k = partition order[k]
+            gams.append(solver.consts.y_max - ys)
+            offs += [offs[-1] - seg[order[0]][0] + seg[p][1] for p in order]
+            lm[t * P:(t + 1) * P, : self.r] = prices[order]
+            per.append((perm, order, int(ys.numel())))
+        gamma = torch.cat(gams)
+        off = np.asarray(offs, dtype=np.int64)
+        plan = self._w0plan
+        if plan is None:
+            plan = self._w0plan = BatchPlan([self.price_solver_s.lompc, self.price_solver_l.lompc], gamma, off,
+                                            sets_per_ctx=[P, P], want_w=False, want_cost=False, want_w0=True,
+                                            want_set=True, validate=False)
+        else:
+            plan.update(gamma, off, validate=False)
+        hb = self._w0_host
+        if hb is None:
+            hb = self._w0_host = torch.empty(2 * P * (3 * N + 1), dtype=torch.float64).pin_memory()
+        h = hb.numpy()
+        h[: 2 * P * 3 * N] = lm.reshape(-1)
+        h[2 * P * 3 * N:] = float(lmbd_r)
+        dev = hb.to(gamma.device, non_blocking=True)
+        res = plan.run(dev[: 2 * P * 3 * N], dev[2 * P * 3 * N:])
+        st = res["set_stats"]
+        back = np.concatenate([t * P + np.argsort(per[t][1]) for t in range(2)])  # partition p of type t: its set
+        red = torch.stack([st[:, _lib.LOMPC_STAT_SUM_W0], st[:, _lib.LOMPC_STAT_SUM_PRICE0],
+                           st[:, _lib.LOMPC_STAT_COUNT], st[:, _lib.LOMPC_STAT_N_FAILED],
+                           st[:, _lib.LOMPC_STAT_N_INVALID]], dim=1)[torch.as_tensor(back, device=st.device)]
+        if self.group is not None:
+            import torch.distributed as dist
+
+            dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
+        w0s, o = [], 0
+        for (perm, _, n), y in zip(per, (self.y_s, self.y_l)):
+            w0 = torch.empty_like(y)
+            w0[perm] = res["w0"][o:o + n]
+            w0s.append(w0)
+            o += n
+        self._w0_keep = dev  # (the prices' copy source stays alive until it has run)
+        return w0s[0], w0s[1], red
+
     def _get_w0_price0(self, prices_s, prices_l, lmbd_r: float):
         # charging_station.py:310-329
-        w0_s, red_s = self._w0_batched("Small", self.price_solver_s, self.y_s, self.idx_s, prices_s, lmbd_r)
-        w0_l, red_l = self._w0_batched("Large", self.price_solver_l, self.y_l, self.idx_l, prices_l, lmbd_r)
-        red_s, red_l = self._w0_checked(red_s), self._w0_checked(red_l)
+        if self.w0_one_call and self.price_solver_s.lompc.mode != "direct":  # (DIRECT plans: one context each)
+            w0_s, w0_l, red = self._w0_both(prices_s, prices_l, lmbd_r)
+            red = self._w0_checked(red)
+            red_s, red_l = red[: self.P], red[self.P:]
+        else:
+            w0_s, red_s = self._w0_batched("Small", self.price_solver_s, self.y_s, self.idx_s, prices_s, lmbd_r)
+            w0_l, red_l = self._w0_batched("Large", self.price_solver_l, self.y_l, self.idx_l, prices_l, lmbd_r)
+            red_s, red_l = self._w0_checked(red_s), self._w0_checked(red_l)
         price0_s, price0_l = np.zeros((self.P,)), np.zeros((self.P,))
         for p in range(self.P):
             if red_s[p, 2] > 0:

@@ -1681,6 +1681,9 @@ struct EvalsArgs {
   int64_t lm_stride, lr_stride, ev_stride, SG;
 };
 
+#ifndef LQ_EVALS_RUN_BARRIER
+#define LQ_EVALS_RUN_BARRIER 0  // 1: k_evals' former barrier at the end of every run (diagnostic builds)
+#endif
 #ifndef LQ_EVALS_SKEW
 #define LQ_EVALS_SKEW 0  // k_evals: start delay (100 MHz ticks) of the grid's second half (diagnostic builds)
 #endif
@@ -1715,7 +1718,13 @@ __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_evals(EvalArgs a, 
     const long long t0__ = __builtin_amdgcn_s_memtime();
 #endif
     eval_block<NT, false>(a, bl, nullptr, ro);
-    __syncthreads();  // (the staged table and the record scratch are the next run's)
+    // (no barrier here: every wave has passed the block's record barrier, so every row of the run is
+    // written and its table no longer read; wave 0 reads only the row sums while the others stage the
+    // next run, and no wave writes row sums again before the next run's staging barrier, which wave 0
+    // reaches after its record)
+#if LQ_EVALS_RUN_BARRIER
+    __syncthreads();
+#endif
 #ifdef LOMPC_STAMPS
     if (threadIdx.x == 0 && r < 32 && b < 512) {  // start, block map, scalars, counts, pieces, staged, rows, end
       long long* q = g_stamps + ((size_t)b * 32 + r) * 8;

@@ -981,6 +981,8 @@ struct RunOff {
   bool launder = false;
   bool gamma_lds = false;  // the block's gamma from the previous run's s_g (k_evals: the same EVs every run)
   bool nostage = false;  // (diagnostic builds, LQ_EVALS_NOSTAGE: keep the previous run's staged table)
+  bool pipelined = false;  // (k_evals) staging loads before a barrier, the record by the block's last wave
+  bool first = false;      // (k_evals) the launch's first run
   int buf = 0;           // (k_evals_st) the compact table and the record scratch of this run: parity
 };
 
@@ -1073,6 +1075,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   __shared__ int s_fc[EVAL_WAVES];  // (CLOSE) re-solve list lengths
   __shared__ int s_last;            // (CLOSE) this workgroup closes the set
   __shared__ int s_mx;              // the set's largest piece count of a cell
+  __shared__ int s_done;            // (pipelined) waves past their rows, this run
   int tid_ = (int)threadIdx.x;
   if (ro.launder) asm volatile("" : "+v"(tid_));  // (k_evals: lane-derived indices recomputed every run, not
                                                   // hoisted out of its loop and spilled)
@@ -1152,6 +1155,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   // (issued before the gamma loads, above), then only those cells' used rows, coefficient records
   // and piece ends — cells hold 1-2 pieces on average, so this moves a fraction of the 8 slots
   const size_t sb = (size_t)cb * LQ_PPL;
+  if (ro.pipelined && ro.first && tid == 0) s_done = 0;  // (published by the staging barriers)
   if constexpr (!STG) if (!ro.nostage) {  // (STG: staged by the stager wave)
     int vn = 0;
     double vl = 0.0;
@@ -1188,6 +1192,9 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       vg[j] = lane < nc[j] ? ld_t<false>(a.t_ge + so + lane) : 0.0;
     }
     LQ_STAMPW(3);  // (diagnostic build: the pieces' load round)
+    // (k_evals: the loads above were issued while other waves may still write the previous run's rows
+    // from the table; the LDS writes below wait until every wave is past them)
+    if (ro.pipelined) __syncthreads();
 #pragma unroll
     for (int j = 0; j < CPW; ++j) {
       const int c = wv + EVAL_WAVES * j;
@@ -1542,8 +1549,20 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       }
     }
     if constexpr (!STG) {
-      __syncthreads();
-      if (tid < 64) store_record(tid, 64);
+      if (ro.pipelined) {
+        // the block's last wave to finish its rows writes the record (the others go on to the next run's
+        // staging loads); the acquire-release LDS counter orders every wave's row sums before its read
+        int old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(&s_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        old = __shfl(old, 0, 64);
+        if (old == EVAL_WAVES - 1) {
+          store_record(lane, 64);
+          if (lane == 0) __hip_atomic_store(&s_done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      } else {
+        __syncthreads();
+        if (tid < 64) store_record(tid, 64);
+      }
     }
   }
   LQ_STAMPE(5);
@@ -1681,6 +1700,9 @@ struct EvalsArgs {
   int64_t lm_stride, lr_stride, ev_stride, SG;
 };
 
+#ifndef LQ_EVALS_PIPELINED
+#define LQ_EVALS_PIPELINED 1  // k_evals: staging loads issued before the table's barrier, records by the last wave
+#endif
 #ifndef LQ_EVALS_RUN_BARRIER
 #define LQ_EVALS_RUN_BARRIER 0  // 1: k_evals' former barrier at the end of every run (diagnostic builds)
 #endif
@@ -1705,6 +1727,8 @@ __global__ __launch_bounds__(EVAL_EVS, EVAL_MIN_WAVES) void k_evals(EvalArgs a, 
     ro.lmbd_r = a.lmbd_r + (size_t)j * x.lr_stride;
     ro.launder = true;
     ro.gamma_lds = r > 0;
+    ro.pipelined = LQ_EVALS_PIPELINED;
+    ro.first = r == 0;
 #ifdef LQ_EVALS_NOSTAGE
     ro.nostage = r > 0;  // (timing only: every run after the first evaluates run 0's table)
 #endif

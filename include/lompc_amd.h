@@ -226,9 +226,12 @@ int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, d
  * 0 = every run writes the same rows and the last run's remain; ev_stride > 0 requires
  * ev_stride >= B), so every run of the call can be observable.  With profile_every > 0 only every
  * E-th launch carries the enabled profiling events.
- * One C-ABI call for a sequence of independent batches (a benchmark's timed steps).  Plans whose
- * cells fill whole path workgroups take the STEPPED form: one launch carries the
- * path of run k + 1, the evaluation of run k and the closing of run k - 1.  In that form every
+ * One C-ABI call for a sequence of independent batches (a benchmark's timed steps).  Plans without
+ * warm starts take the WIDE form: per group of up to 32 runs three launches — the
+ * group's paths, its evaluations (each workgroup through its block of every run) and its closings —
+ * and, with a communicator, ONE all-gather + combine per group.  Warm-started plans take the STEPPED
+ * form: one launch carries the path of run k + 1, the evaluation of run k and the closing of run
+ * k - 1.  In both forms every
  * set is closed by summing its evaluated rows (k_finalize's order), also for runs without w
  * output; lompc_plan_run on a plan without w output closes from the pieces' aggregates inside the
  * evaluation instead: the two agree to the certification tolerance (~1e-12 relative), bit for bit
@@ -236,9 +239,10 @@ int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, d
  *   LOMPC_STEPS_PER_KERNEL  the same runs issued one part per launch (paths / evaluations /
  *                           closings), with the same evaluation block map, so bit for bit the same
  *                           outputs (verification / A-B)
- *   LOMPC_STEPS_SPAN_EVENTS the enabled K_EVAL timing as ONE event pair from the start of the first
- *                           full stepped launch to the end of the last, read back as that many
- *                           launches (no per-launch event boundaries inside the timed steps) */
+ *   LOMPC_STEPS_SPAN_EVENTS the enabled K_EVAL timing as ONE event pair (wide form: around the first
+ *                           group's evaluation launch, read back as its runs; stepped form: from the
+ *                           start of the first full stepped launch to the end of the last, read back
+ *                           as that many launches) — no per-launch event boundaries inside the steps */
 #define LOMPC_STEPS_PER_KERNEL 1
 #define LOMPC_STEPS_SPAN_EVENTS 2
 int lompc_plan_run_steps(lompc_plan* plan, const double* lmbd, int64_t lmbd_stride,

@@ -70,12 +70,14 @@ if mode == "station":
     torch.cuda.synchronize()
     assert lib.lompc_debug_loopstamps(buf.ctypes.data, 0) == 0
     tot += buf.reshape(64, 16).astype(np.float64)
-    G = st.price_solver_l._plan.cells
+    ps_l = st.price_solver_l
+    last = max(ps_l._staged)  # (the chains run the staged plans: take the large type's last partition)
+    ps_l.use_partition(last)
+    G = ps_l._plan.cells
     # one more price loop of the large type's last partition, warm (its plan and prices as left):
     # the per-wave path phases of its last k_loop_iter launch (path_cell's stamps)
     lib.lompc_debug_stamps.restype = ctypes.c_int
     lib.lompc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    ps_l = st.price_solver_l
     ps_l.compute_optimal_prices(0.5 * ps_l.consts.w_max * np.ones(N), 0.0)
     torch.cuda.synchronize()
     sb = np.zeros(65536 * 8, dtype=np.int64)

@@ -172,3 +172,38 @@ def test_regularizer_rejects_bad_shapes():
     np.testing.assert_allclose(np.ones((2, 3)) @ x, np.ones(2))
     with pytest.raises(ValueError):
         reg.solve_price_regularization(np.ones((3, 3)), np.ones(2), np.ones(3))
+
+
+@pytest.mark.parametrize("price", ["linear-convex", "linear"])
+@pytest.mark.parametrize("ev", ["small", "large"])
+def test_price_regularize_matches_regularizer(ev, price):
+    """lompc_price_regularize (the regularisation step of price_solver.py:142-147 with :248-255, shared
+    by the price chain and PriceSolver's per-partition loop): lmbd[:r] the regularizer LP's solution
+    for A = Dphi(w)', b = A lmbd, c = phi(w) (the same vertex as PriceRegularizer), lmbd[r:] untouched,
+    and phi(w)' lmbd before / after within rounding of the numpy products."""
+    rng = np.random.default_rng(31 + (ev == "large") + 2 * (price == "linear"))
+    c = O.small_consts() if ev == "small" else O.large_consts()
+    lib = _lib.load()
+    for N in (12, 24, 48):
+        r = 3 * N if price == "linear-convex" else 2 * N
+        reg = PriceRegularizer(N, r)
+        for _ in range(5):
+            w = c.w_max * rng.random(N)
+            w[rng.random(N) < 0.25] = 0.0
+            lm = np.zeros(3 * N)
+            lm[:r] = c.theta * rng.random(r) * (rng.random(r) < 0.7)
+            ph = PO.phi(N, c.theta, c.w_max, w)
+            D = PO.Dphi(N, c.theta, c.w_max, w)[:r, :]
+            x = reg.solve_price_regularization(D.T, D.T @ lm[:r], ph[:r])
+            out = lm.copy()
+            pre, post = ctypes.c_double(0.0), ctypes.c_double(0.0)
+            assert lib.lompc_price_regularize(N, r, float(c.theta), float(c.w_max), w.ctypes.data, out.ctypes.data,
+                                              ctypes.byref(pre), ctypes.byref(post)) == _lib.LOMPC_OK
+            np.testing.assert_array_equal(out[:r], x)
+            np.testing.assert_array_equal(out[r:], lm[r:])
+            assert abs(pre.value - ph @ lm) <= 1e-12 * max(1.0, abs(ph @ lm))
+            assert abs(post.value - ph @ out) <= 1e-12 * max(1.0, abs(ph @ out))
+    w = np.zeros(12)
+    assert lib.lompc_price_regularize(12, 30, 1.0, 1.0, w.ctypes.data, np.zeros(36).ctypes.data,
+                                      ctypes.byref(ctypes.c_double()), ctypes.byref(ctypes.c_double())) \
+        == _lib.LOMPC_ERR_INVALID_ARG

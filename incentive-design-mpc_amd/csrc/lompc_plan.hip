@@ -96,6 +96,12 @@ __device__ unsigned long long g_lstamps[64 * 16];  // k_loop_iter's phase sums (
 #define LQ_PIECE_CAP 128                   // k_eval: piece slots of one set staged in LDS (more: re-solved)
 #endif
 #define LQ_GMAX 1024                       // max cells per set
+#ifndef LQ_DIAG_NOLOOKUP
+#define LQ_DIAG_NOLOOKUP 0  // diagnostic timing builds: every valid EV takes its cell's first piece (wrong results)
+#endif
+#ifndef LQ_DIAG_NOROWLDS
+#define LQ_DIAG_NOROWLDS 0  // diagnostic timing builds: the rows' values without their LDS reads (wrong results)
+#endif
 #ifndef LQ_STEP_CELLS
 #define LQ_STEP_CELLS 4                    // k_step: path cells per workgroup, one per wave (<= EVAL_WAVES; 4: one per
                                            // SIMD — 19.2 us per step vs 22.4 with 8, 19.9 with 2, profiles/r03_v5)
@@ -1250,7 +1256,8 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     const int kb = STG ? s_pre[c] : c * LQ_PPL, ke = kb + nc;  // the cell's pieces [kb, ke), ascending gamma
     double ge[LQ_PPL];
 #pragma unroll
-    for (int k = 0; k < LQ_PPL; ++k) ge[k] = k < mxc ? s_ge[STG ? kb + k : k * Gs + min(c, Gs - 1)] : 0.0;
+    for (int k = 0; k < LQ_PPL; ++k)
+      ge[k] = (k < mxc && !LQ_DIAG_NOLOOKUP) ? s_ge[STG ? kb + k : k * Gs + min(c, Gs - 1)] : 0.0;
     const double glo_c = s_lo[c];
     int key = kb;  // piece = number of piece ends below g (every end read at once, no loop)
     double gend = ge[0];
@@ -1258,7 +1265,8 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     for (int k = 0; k + 1 < LQ_PPL; ++k) key += (k + 1 < nc && g > ge[k]) ? 1 : 0;
 #pragma unroll
     for (int k = 1; k < LQ_PPL; ++k) gend = nc == k + 1 ? ge[k] : gend;  // the last piece's end
-    const bool cov = valid && ke > kb && (STG || ke <= np) && g >= glo_c && g <= gend;  // (STG: unstaged cells count 0)
+    const bool cov = LQ_DIAG_NOLOOKUP ? valid && ke > kb  // (diagnostic timing builds: the cell's first piece)
+                                      : valid && ke > kb && (STG || ke <= np) && g >= glo_c && g <= gend;
     if (act && !valid) {
       ++n_inv;
       if (acost) st_ev8(acost + i, NAN);
@@ -1437,8 +1445,13 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       double2 u0[RU], u1[RU];
 #pragma unroll
       for (int j = 0; j < RU; ++j) {
-        u0[j] = s_ab[kk[j] * NS + col];  // stages t0, t0 + 1 (abx)
-        u1[j] = V == 2 ? s_ab[kk[j] * NS + (N >> 1) + col] : make_double2(0.0, 0.0);
+        if (LQ_DIAG_NOROWLDS) {  // (diagnostic timing builds: no LDS reads in the rows)
+          u0[j] = make_double2(1e-3 * kk[j], 1e-3);
+          u1[j] = make_double2(2e-3 * kk[j], 1e-3);
+        } else {
+          u0[j] = s_ab[kk[j] * NS + col];  // stages t0, t0 + 1 (abx)
+          u1[j] = V == 2 ? s_ab[kk[j] * NS + (N >> 1) + col] : make_double2(0.0, 0.0);
+        }
       }
       int kn[RU];  // the next batch's keys and gammas (software pipeline: one LDS round per batch)
       double gn[RU];

@@ -122,7 +122,8 @@ __global__ __launch_bounds__(256) void k_lv_gamma(const double* __restrict__ ys,
 // p = #{k in 1 .. P-1 : bounds[k] <= y_i} (the sorted runs' rule).  Workgroup b sums its contiguous
 // chunk: each thread its strided EVs in registers (one predicated update per partition: no dynamic
 // register indexing), then fixed-order wave butterflies and a fixed-order combine of the 4 waves; the
-// workgroups' records are then combined in workgroup order by k_lvh_final.  Deterministic.
+// workgroups' records are then combined by k_lvh_final (one wave per statistic, lane-strided, a fixed
+// butterfly).  Deterministic.
 constexpr int LV_HP = 16;
 constexpr int LV_HBLK = 512;  // workgroups at most
 
@@ -146,21 +147,29 @@ __global__ __launch_bounds__(256) void k_lvh_partial(const double* __restrict__ 
   }
   double ymx = -INFINITY, ymn = INFINITY;
   const int64_t c0 = n * b / nblk, c1 = n * (b + 1) / nblk;
-  for (int64_t i = c0 + t; i < c1; i += 256) {
-    const double v = y[i];
-    int p = 0;
+  constexpr int U = 4;  // loads in flight per thread: the chunk's memory rounds, not one per element
+  for (int64_t i0 = c0 + t; i0 < c1; i0 += 256 * U) {
+    double vv[U];
 #pragma unroll
-    for (int k = 1; k < LV_HP; ++k) p += bd[k] <= v ? 1 : 0;
+    for (int u = 0; u < U; ++u) vv[u] = i0 + 256 * u < c1 ? y[i0 + 256 * u] : NAN;
 #pragma unroll
-    for (int k = 0; k < LV_HP; ++k) {
-      const bool m = k == p;
-      cnt[k] += m ? 1.0 : 0.0;
-      sum[k] += m ? v : 0.0;
-      mx[k] = m ? fmax(mx[k], v) : mx[k];
-      mn[k] = m ? fmin(mn[k], v) : mn[k];
+    for (int u = 0; u < U; ++u) {
+      if (!(i0 + 256 * u < c1)) break;
+      const double v = vv[u];
+      int p = 0;
+#pragma unroll
+      for (int k = 1; k < LV_HP; ++k) p += bd[k] <= v ? 1 : 0;
+#pragma unroll
+      for (int k = 0; k < LV_HP; ++k) {
+        const bool m = k == p;
+        cnt[k] += m ? 1.0 : 0.0;
+        sum[k] += m ? v : 0.0;
+        mx[k] = m ? fmax(mx[k], v) : mx[k];
+        mn[k] = m ? fmin(mn[k], v) : mn[k];
+      }
+      ymx = fmax(ymx, v);
+      ymn = fmin(ymn, v);
     }
-    ymx = fmax(ymx, v);
-    ymn = fmin(ymn, v);
   }
   __shared__ double sw[4][4 * LV_HP + 2];
 #pragma unroll
@@ -198,22 +207,30 @@ __global__ __launch_bounds__(256) void k_lvh_partial(const double* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(256) void k_lvh_final(const double* __restrict__ part, int nblk, int P,
-                                                   const double* __restrict__ bounds, double* __restrict__ stats) {
-  const int t = (int)threadIdx.x;
-  if (t < 4 * LV_HP + 2) {
-    const int f = t < 4 * LV_HP ? (t & 3) : (t == 4 * LV_HP ? 1 : 2);
-    double v = part[t];
-    for (int b = 1; b < nblk; ++b) {
-      const double u = part[(size_t)b * (4 * LV_HP + 2) + t];
-      v = f == 1 ? fmax(v, u) : f == 2 ? fmin(v, u) : v + u;
-    }
-    if (t < 4 * P) stats[t] = v;                 // per partition (count, max, min, sum)
-    else if (t >= 4 * LV_HP) stats[4 * P + (t - 4 * LV_HP)] = v;  // max y, min y
+// one wave per statistic t: lane l combines the workgroups' records l, l + 64, ... in order, then a
+// fixed butterfly over the lanes (deterministic)
+__global__ __launch_bounds__(64) void k_lvh_final(const double* __restrict__ part, int nblk, int P,
+                                                  const double* __restrict__ bounds, double* __restrict__ stats) {
+  const int t = (int)blockIdx.x, lane = (int)threadIdx.x;
+  const int f = t < 4 * LV_HP ? (t & 3) : (t == 4 * LV_HP ? 1 : 2);  // 0 count / 3 sum: add; 1 max; 2 min
+  const double id = f == 1 ? -INFINITY : f == 2 ? INFINITY : 0.0;
+  double v = id;
+  for (int b = lane; b < nblk; b += 64) {
+    const double u = part[(size_t)b * (4 * LV_HP + 2) + t];
+    v = f == 1 ? fmax(v, u) : f == 2 ? fmin(v, u) : v + u;
   }
-  if (t == 0) {
-    stats[4 * P + 2] = bounds[0];
-    stats[4 * P + 3] = bounds[P];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double u = __shfl_xor(v, o);
+    v = f == 1 ? fmax(v, u) : f == 2 ? fmin(v, u) : v + u;
+  }
+  if (lane == 0) {
+    if (t < 4 * P) stats[t] = v;                                      // per partition (count, max, min, sum)
+    else if (t >= 4 * LV_HP) stats[4 * P + (t - 4 * LV_HP)] = v;       // max y, min y
+    if (t == 0) {
+      stats[4 * P + 2] = bounds[0];
+      stats[4 * P + 3] = bounds[P];
+    }
   }
 }
 
@@ -271,6 +288,6 @@ extern "C" int lompc_levels_stats(const double* y, int64_t n, const double* boun
   hipStream_t st = (hipStream_t)stream;
   double* part = static_cast<double*>(work);
   hipLaunchKernelGGL(k_lvh_partial, dim3((unsigned)nblk), dim3(256), 0, st, y, n, bounds, P, nblk, part);
-  hipLaunchKernelGGL(k_lvh_final, dim3(1), dim3(256), 0, st, part, nblk, P, bounds, stats);
+  hipLaunchKernelGGL(k_lvh_final, dim3(4 * LV_HP + 2), dim3(64), 0, st, part, nblk, P, bounds, stats);
   return hipGetLastError() == hipSuccess ? LOMPC_OK : LOMPC_ERR_HIP;
 }

@@ -96,6 +96,9 @@ __device__ unsigned long long g_lstamps[64 * 16];  // k_loop_iter's phase sums (
 #define LQ_PIECE_CAP 128                   // k_eval: piece slots of one set staged in LDS (more: re-solved)
 #endif
 #define LQ_GMAX 1024                       // max cells per set
+#ifndef LQ_EVAL_OUT_AFTER_ROWS
+#define LQ_EVAL_OUT_AFTER_ROWS 1  // k_eval / k_step / k_evals: a pass's scalar outputs after its rows
+#endif
 #ifndef LQ_DIAG_NOLOOKUP
 #define LQ_DIAG_NOLOOKUP 0  // diagnostic timing builds: every valid EV takes its cell's first piece (wrong results)
 #endif
@@ -1246,7 +1249,12 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
   bool inv_rows = false;  // (wave-uniform) some row of this wave has an invalid gamma
   const int mxc = STG ? stg_meta[0] : s_mx;  // (block-uniform) the set's largest cell piece count: no piece end past it is read
   // one pass of the lookup: this thread's EV h
-  auto lookup = [&](const int h) {
+  // the lookup in two halves: lookup_key (the piece: the rows need only it) and lookup_out (the piece's
+  // coefficients -> the scalar outputs), which the row passes run after their rows (its LDS round and
+  // stores then follow the row stores instead of holding them back); per pass the piece and flags
+  int pk[EVAL_PASSES];
+  unsigned pf[EVAL_PASSES];  // bit 0: cov, bit 1: act && !valid
+  auto lookup_key = [&](const int h) {
     const int i = start + brow(h);
     const bool act = bact(h);
     const double g = gh[h];
@@ -1267,7 +1275,27 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
     for (int k = 1; k < LQ_PPL; ++k) gend = nc == k + 1 ? ge[k] : gend;  // the last piece's end
     const bool cov = LQ_DIAG_NOLOOKUP ? valid && ke > kb  // (diagnostic timing builds: the cell's first piece)
                                       : valid && ke > kb && (STG || ke <= np) && g >= glo_c && g <= gend;
-    if (act && !valid) {
+    pk[h] = key;
+    pf[h] = (cov ? 1u : 0u) | ((act && !valid) ? 2u : 0u);
+    if (!STG || act) {  // (STG: a pass's lanes past the wave's segment are the next wave's rows)
+      s_g[brow(h)] = g;
+      s_k[brow(h)] = cov ? key : ((CLOSE && valid) ? ZD : ZK);
+    }
+    inv_rows |= __ballot(act && !valid) != 0ull;
+    const unsigned long long need = __ballot(valid && !cov);
+    if (valid && !cov) {
+      st_wt4(a.fail_idx + (size_t)rb * EVAL_MAXB + 64 * EVAL_PASSES * wv + nlist +
+                 __popcll(need & ((1ull << lane) - 1ull)), i);
+      ++n_fail;
+    }
+    nlist += __popcll(need);
+  };
+  auto lookup_out = [&](const int h) {
+    const int i = start + brow(h);
+    const double g = gh[h];
+    const int key = pk[h];
+    const bool cov = (pf[h] & 1u) != 0u;
+    if ((pf[h] & 2u) != 0u) {
       ++n_inv;
       if (acost) st_ev8(acost + i, NAN);
       if (aw0) st_ev8(aw0 + i, NAN);
@@ -1296,18 +1324,10 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
         atomicAdd(s_pf + key, (unsigned long long)rint(fmax(g - wlo, 0.0) * fxs));
       }
     }
-    if (!STG || act) {  // (STG: a pass's lanes past the wave's segment are the next wave's rows)
-      s_g[brow(h)] = g;
-      s_k[brow(h)] = cov ? key : ((CLOSE && valid) ? ZD : ZK);
-    }
-    inv_rows |= __ballot(act && !valid) != 0ull;
-    const unsigned long long need = __ballot(valid && !cov);
-    if (valid && !cov) {
-      st_wt4(a.fail_idx + (size_t)rb * EVAL_MAXB + 64 * EVAL_PASSES * wv + nlist +
-                 __popcll(need & ((1ull << lane) - 1ull)), i);
-      ++n_fail;
-    }
-    nlist += __popcll(need);
+  };
+  auto lookup = [&](const int h) {
+    lookup_key(h);
+    lookup_out(h);
   };
   // a wave without EVs in a pass skips it (wave-uniform; its rows are never read)
   auto pass_live = [&](const int h) { return STG ? 64 * h < sgn : h == 0 || start + EVAL_EVS * h + 64 * wv < end; };
@@ -1530,12 +1550,14 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
 #pragma unroll
     for (int h = 0; h < EVAL_PASSES; ++h) {
       if (!pass_live(h)) break;
-      lookup(h);
+      if (LQ_EVAL_OUT_AFTER_ROWS) lookup_key(h);
+      else lookup(h);
       __builtin_amdgcn_wave_barrier();  // this wave's own rows in LDS: in order
       any_inv = inv_rows;
       const int r0b = STG ? sg0 + 64 * h : EVAL_EVS * h + 64 * wv;
       const int nh = STG ? min(64, sgn - 64 * h) : max(0, min(64, end - start - r0b));  // wave-uniform
       if (nh > 0) row_segment(r0b, nh);
+      if (LQ_EVAL_OUT_AFTER_ROWS) lookup_out(h);
     }
     if (lane == 0) st_wt4(a.fail_cnt + (size_t)rb * EVAL_WAVES + wv, nlist);
     wave_record();

@@ -323,7 +323,7 @@ def main():
     # the stepped form (lompc_plan_run_steps, full outputs, no communicator): the timed region's
     # events sit on its k_step launches
     stepped = batched and args.mode == "path" and runs[0]["plan"].info()["cells"] % 4 == 0
-    # wide form (no warm start): per group of <= 32 steps k_paths (the paths), k_evals (every step's
+    # wide form (no warm start): per group of <= 64 steps k_paths (the paths), k_evals (every step's
     # evaluation, each workgroup through its block of every step) and k_closes (the closings); its events
     # sit on k_evals and read as one launch per step
     wide = stepped and not args.warm
@@ -365,7 +365,7 @@ def main():
                                                       if sharded else "dp1")),
             "sharded_code_path": bool(sharded),
             "dist_backend": (args.dist_backend if sharded else None),
-            "launches_per_step": (("3 per group of up to 32 steps (k_paths, k_evals, k_closes)" if wide else
+            "launches_per_step": (("3 per group of up to 64 steps (k_paths, k_evals, k_closes)" if wide else
                                    "1 (k_step) + 2 for the K steps' pipeline fill and drain")
                                   + ("; + per step the all-gather and the combine kernel" if comm is not None else "")
                                   if stepped else sum(r["plan"].launches_per_run() for r in runs)),
@@ -465,7 +465,7 @@ def collective_cost(runs, args, world, dev, torch, dist, comm, batched, dt):
     """The per-step cost of the cross-rank exchange, so a scaling run is attributable: the same K
     timed steps again WITHOUT the exchange (RCCL: the plan's communicator detached, so no all-gather /
     combine kernel; gloo: no torch.distributed combine), max over ranks; collective_us_per_step =
-    timed step - that step.  Also the exchange alone (RCCL: ceil(K / 32) all-gathers of a group's packed
+    timed step - that step.  Also the exchange alone (RCCL: ceil(K / 64) all-gathers of a group's packed
     set records through torch.distributed on the same communicator size; gloo: K combine_set_results
     calls)."""
     from lompc_amd.dist import combine_set_results
@@ -498,17 +498,17 @@ def collective_cost(runs, args, world, dev, torch, dist, comm, batched, dt):
         finally:
             plan.set_comm(comm)
         S, N = plan.S, plan.N
-        G32 = 32  # (the wide form's group: one all-gather of its runs' contiguous records)
-        rec = torch.zeros(min(K, G32) * S * (N + 8), dtype=torch.float64, device=dev)
+        G = 64  # (the wide form's group: one all-gather of its runs' contiguous records)
+        rec = torch.zeros(min(K, G) * S * (N + 8), dtype=torch.float64, device=dev)
         recv = torch.empty(world * rec.numel(), dtype=torch.float64, device=dev)
 
         def gathers():
-            for _ in range((K + G32 - 1) // G32):
+            for _ in range((K + G - 1) // G):
                 dist.all_gather_into_tensor(recv, rec)
 
         gathers()
         t_ag = timed(gathers)
-        how = ("RCCL: ONE all-gather of a group's (up to 32 steps') packed set records + the k_combine_runs kernel "
+        how = ("RCCL: ONE all-gather of a group's (up to 64 steps') packed set records + the k_combine_runs kernel "
                "after the group's closings, inside the run_steps call")
     else:
         outs = [(x["plan"].out["set_sum_w"], x["plan"].out["set_stats"]) for x in runs]

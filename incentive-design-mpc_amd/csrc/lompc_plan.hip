@@ -2933,7 +2933,10 @@ int stepped_setup(lompc_plan* p, hipStream_t st, bool wide) {
   return LOMPC_OK;
 }
 
-#define LQ_WIDE_RUNS 32                 // wide form: runs per path launch (its table ring holds one more)
+#ifndef LQ_WIDE_RUNS
+#define LQ_WIDE_RUNS 64                 // wide form: runs per path launch (its table ring holds one more; 64: 13.96
+                                        // vs 14.32 us per step over 64 steps with 32 — the paths' launch tail amortised)
+#endif
 #define LQ_WIDE_BYTES (1ll << 30)        // wide form: the table ring's memory at most
 
 // K >= 1 independent runs.  Two schedules, one per plan kind:

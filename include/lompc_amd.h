@@ -227,7 +227,7 @@ int lompc_plan_run(lompc_plan* plan, const double* lmbd, const double* lmbd_r, d
  * ev_stride >= B), so every run of the call can be observable.  With profile_every > 0 only every
  * E-th launch carries the enabled profiling events.
  * One C-ABI call for a sequence of independent batches (a benchmark's timed steps).  Plans without
- * warm starts take the WIDE form: per group of up to 32 runs three launches — the
+ * warm starts take the WIDE form: per group of up to 64 runs three launches — the
  * group's paths, its evaluations (each workgroup through its block of every run) and its closings —
  * and, with a communicator, ONE all-gather + combine per group.  Warm-started plans take the STEPPED
  * form: one launch carries the path of run k + 1, the evaluation of run k and the closing of run

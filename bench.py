@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--mode", choices=["path", "direct"], default="path")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cells", type=int, default=12,
+                    help="gamma cells per parameter set of the benchmark's plan (0: the plan's default, 16 at these "
+                         "set sizes); 12 measured best for the wide run_steps form (12.89 vs 13.42 us per step over "
+                         "64 steps, scripts/step_probe.py), at +0.5 us for one run's path alone")
     ap.add_argument("--warm", action="store_true",
                     help="plan warm start: every gamma cell's exact solve starts from the working set the "
                          "previous step ended with there (as a price loop's plan does)")
@@ -204,7 +208,7 @@ def main():
         lr = torch.zeros(2 * P, dtype=torch.float64, device=dev)
         runs = [dict(plan=BatchPlan([e["lompc"] for e in eng], gamma, off, sets_per_ctx=[P, P], w_ref=wr,
                                     want_w=args.outputs == "full", want_cost=args.outputs != "set", want_set=True,
-                                    stream=main, warm_start=args.warm), stream=main, lm_ptr=[lm[k].data_ptr() for k in range(nsteps)], lr_ptr=lr.data_ptr(),
+                                    stream=main, warm_start=args.warm, cells=args.cells or None), stream=main, lm_ptr=[lm[k].data_ptr() for k in range(nsteps)], lr_ptr=lr.data_ptr(),
                      lm_stride=int(lm[0].numel()),
                      qps=B, keep=(gamma, lm, wr, lr))]
     else:
@@ -359,8 +363,9 @@ def main():
             "mode": args.mode,
             "outputs": args.outputs,
             "warm_start": bool(args.warm),
-            "parallelism": (f"dp{world} (EV shards; per step ONE RCCL all-gather of both types' per-set "
-                            "reductions + a rank-ordered combine kernel, issued inside the C-ABI run)"
+            "cells_per_set": (runs[0]["plan"].info()["cells"] if args.mode == "path" else None),
+            "parallelism": (f"dp{world} (EV shards; ONE RCCL all-gather of both types' per-set reductions per "
+                            "group of up to 64 steps + a rank-ordered combine kernel, issued inside the C-ABI call)"
                             if comm is not None else (f"dp{world} (EV shards, torch.distributed all-gather per step)"
                                                       if sharded else "dp1")),
             "sharded_code_path": bool(sharded),
@@ -642,7 +647,8 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
     for name, kw, bpq in (("reductions", dict(want_w=False, want_cost=False), 8),
                           ("w0", dict(want_w=False, want_cost=False, want_w0=True), 16)):
         plan = BatchPlan(base.lompcs, base.gamma, base.off, sets_per_ctx=base.sets_per_ctx, w_ref=base.w_ref,
-                         want_set=True, stream=torch.cuda.current_stream(), warm_start=args.warm, **kw)
+                         want_set=True, stream=torch.cuda.current_stream(), warm_start=args.warm,
+                         cells=base.info()["cells"], **kw)
         if comm is not None:
             plan.set_comm(comm)
         plan.run_steps(lm_ptr[0], lr_ptr, max(args.warmup, 1), stride, 0)
@@ -723,7 +729,8 @@ def sequential_leg(run, eng, N, P, args, torch):
     wt = base.w_ref
     step = 0.5
     warm = BatchPlan(base.lompcs, base.gamma, base.off, sets_per_ctx=base.sets_per_ctx, w_ref=base.w_ref,
-                     want_w=True, want_cost=True, want_set=True, stream=torch.cuda.current_stream(), warm_start=True)
+                     want_w=True, want_cost=True, want_set=True, stream=torch.cuda.current_stream(), warm_start=True,
+                     cells=base.info()["cells"])
 
     def timed(plan):
         out = {k: torch.empty(s, dtype=torch.float64, device=dev) for k, s in
@@ -1020,10 +1027,11 @@ def cpu_same_algorithm(eng, N, P, args, ref):
 
     def timed(nt, budget):
         # (one output buffer set every run rewrites, as the GPU line's steps do: warm-up touches its pages)
-        o = oracle_c.path_run(N, cs, [P, P], lms[0], lr, g, off, w_ref=wr, nthreads=nt)
+        o = oracle_c.path_run(N, cs, [P, P], lms[0], lr, g, off, w_ref=wr, nthreads=nt, cells=args.cells)
         done, t0, k = 0, time.perf_counter(), 0
         while True:
-            o = oracle_c.path_run(N, cs, [P, P], lms[k % len(lms)], lr, g, off, w_ref=wr, nthreads=nt, out=o)
+            o = oracle_c.path_run(N, cs, [P, P], lms[k % len(lms)], lr, g, off, w_ref=wr, nthreads=nt, out=o,
+                                  cells=args.cells)
             assert o["info"][3] == 0
             done += B
             k += 1
@@ -1035,10 +1043,10 @@ def cpu_same_algorithm(eng, N, P, args, ref):
     v1, runs1, dt1 = timed(1, args.cpu_seconds / 4)
     out = {"value": v, "unit": "QP/s", "cores": threads, "kind": "port (same algorithm as the GPU path engine)",
            "sample": f"{runs} runs x {B} EVs (horizon {N}, 24 sets, full outputs, the timed steps' prices) in {dt:.1f} s, "
-                     f"OpenMP {threads} threads (oracle/path_cpu.cpp)",
+                     f"OpenMP {threads} threads (oracle/path_cpu.cpp, {args.cells or 'default'} cells per set as the GPU plan)",
            "single_thread": {"value": v1, "sample": f"{runs1} runs x {B} EVs in {dt1:.1f} s, 1 thread"}}
     if ref is not None:
-        o = oracle_c.path_run(N, cs, [P, P], lms[-1], lr, g, off, w_ref=wr, nthreads=threads)
+        o = oracle_c.path_run(N, cs, [P, P], lms[-1], lr, g, off, w_ref=wr, nthreads=threads, cells=args.cells)
         out["parity"] = {"step": "the last timed step (all EVs)",
                          "max_abs_dw": float(np.abs(o["w"] - ref["w"]).max()),
                          "max_rel_dcost": float((np.abs(o["cost"] - ref["cost"]) / np.maximum(1.0, np.abs(ref["cost"]))).max()),

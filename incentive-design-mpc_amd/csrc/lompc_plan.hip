@@ -82,7 +82,8 @@ __device__ unsigned long long g_lstamps[64 * 16];  // k_loop_iter's phase sums (
 #define EVAL_WAVES 8  // k_eval: waves per workgroup (16: 16.1 us, 8: 14.8 us, 4: 16.2 us at config 3)
 #endif
 #ifndef EVAL_RU
-#define EVAL_RU 4  // k_eval: row store instructions per software-pipelined batch
+#define EVAL_RU 2  // k_eval: row store instructions per software-pipelined batch (2: k_evals 11.17 vs 11.70 us
+                   // per run with 4, 11.68 with 3 — the same rows in the same order, so the same bits)
 #endif
 #ifndef EVAL_MIN_WAVES
 #define EVAL_MIN_WAVES ((2 * EVAL_WAVES + 3) / 4)  // k_eval: waves per SIMD for two workgroups per CU

@@ -215,7 +215,12 @@ int lompc_price_regularize(int N, int r, double theta, double w_max, const doubl
     for (int i = 0; i < r; ++i) acc += A[(size_t)t * r + i] * lmbd[i];
     b[t] = acc;
   }
-  const int rc = lompc_lp_separable(N, r, A.data(), b.data(), phi.data(), x.data());
+  int rc = lompc_lp_separable(N, r, A.data(), b.data(), phi.data(), x.data());
+  // a cost entry below zero (theta w_t or theta (w_max - w_t) at ~-1e-17 when the loop's w_k, an
+  // unclamped piece aggregate, sits a rounding error outside [0, w_max]) leaves the closed form: the
+  // general LP then, as PriceRegularizer.solve_price_regularization does (the LP stays bounded:
+  // columns t and N + t together cost theta w_max > 0 per unit)
+  if (rc == LOMPC_ERR_UNSUPPORTED) rc = lompc_lp_solve(N, r, A.data(), b.data(), phi.data(), x.data(), nullptr);
   if (rc) return rc;
   for (int i = 0; i < r; ++i) lmbd[i] = x[i];
   s = 0.0;

@@ -302,6 +302,46 @@ int64_t oracle_lompc_solve_batch_warm(int N, int ev_small, double delta, double 
   return nfail;
 }
 
+/* As oracle_lompc_solve_batch, but every EV keeps its own working set between calls (state, B x N
+ * bytes, caller-owned; *fresh != 0: no stored sets yet, every solve starts cold and *fresh is
+ * cleared).  A price loop's consecutive iterations move the prices a little, so most EVs end on the
+ * working set they ended on before: one equality-constrained solve and the optimality check.  The
+ * same dense active set and termination test as every other entry (only the start differs). */
+int64_t oracle_lompc_solve_batch_state(int N, int ev_small, double delta, double theta, double y_max, double w_max,
+                                       const double* lmbd, double lmbd_r, int64_t B, const double* gamma, double* w,
+                                       double* cost, unsigned char* state, int* fresh, int nthreads) {
+  if (N < 1 || N > OMAXN) return -1;
+  int64_t nfail = 0;
+  const int warm0 = !*fresh;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel reduction(+ : nfail)
+#endif
+  {
+    ocfg c;
+    cfg_init(&c, N, ev_small, delta, theta, y_max, w_max);
+    double* H = (double*)malloc((size_t)N * N * sizeof(double));
+    double g[OMAXN], c0;
+    int st[OMAXN];
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 64)
+#endif
+    for (int64_t i = 0; i < B; ++i) {
+      unsigned char* s = state + i * N;
+      for (int j = 0; j < N; ++j) st[j] = warm0 ? s[j] : 0;
+      build_qp(&c, lmbd, lmbd_r, gamma[i], H, g, &c0);
+      int rc = solve_one(&c, H, g, w + i * N, st, NULL, warm0);
+      if (rc && warm0) rc = solve_one(&c, H, g, w + i * N, st, NULL, 0);
+      if (rc) nfail += 1;
+      for (int j = 0; j < N; ++j) s[j] = (unsigned char)st[j];
+      if (cost) cost[i] = objective(&c, w + i * N, lmbd, lmbd_r, gamma[i]);
+    }
+    free(H);
+  }
+  *fresh = 0;
+  return nfail;
+}
+
 int oracle_max_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

@@ -41,9 +41,29 @@ def load():
         lib.oracle_lompc_solve_batch.argtypes = [I, I, D, D, D, D, P, D, L, P, P, P, I]
         lib.oracle_lompc_solve_batch_warm.restype = L
         lib.oracle_lompc_solve_batch_warm.argtypes = [I, I, D, D, D, D, P, D, L, P, P, P, I]
+        lib.oracle_lompc_solve_batch_state.restype = L
+        lib.oracle_lompc_solve_batch_state.argtypes = [I, I, D, D, D, D, P, D, L, P, P, P, P, P, I]
         lib.oracle_max_threads.restype = I
         _lib = lib
     return _lib
+
+
+def solve_batch_state(N, consts, lmbd, lmbd_r, gamma, state, nthreads=0):
+    """solve_batch with a per-EV working set kept between calls: ``state`` is a dict owned by the
+    caller (empty at first); the same optima, each solve started from the EV's previous working set."""
+    lib = load()
+    lm = np.ascontiguousarray(np.asarray(lmbd, dtype=np.float64))
+    g = np.ascontiguousarray(np.asarray(gamma, dtype=np.float64))
+    B = g.shape[0]
+    if state.get("ws") is None or state["ws"].shape != (B, N):
+        state["ws"] = np.zeros((B, N), dtype=np.uint8)
+        state["fresh"] = ctypes.c_int(1)
+    w = np.empty((B, N))
+    nf = lib.oracle_lompc_solve_batch_state(int(N), int(consts.ev_type == "small"), consts.delta, consts.theta,
+                                            consts.y_max, consts.w_max, lm.ctypes.data, float(lmbd_r), B,
+                                            g.ctypes.data, w.ctypes.data, None, state["ws"].ctypes.data,
+                                            ctypes.byref(state["fresh"]), int(nthreads))
+    return w, int(nf)
 
 
 def solve_batch(N, consts, lmbd, lmbd_r, gamma, nthreads=0, warm=False):

@@ -122,25 +122,36 @@ class OraclePriceSolver:
         self.A = self.lompc.get_input_mat()
         self.m = self.lompc.get_sc_modulus()
         self.lp = lp  # optional LP solver override (A, b, c) -> x
-        self.warm = False  # oracle_c's warm-started batch (same optima; fast on sorted gamma)
+        # oracle_c's warm-started batch (same optima): True = each solve from the previous EV's working
+        # set (fast on sorted gamma); "state" = each EV from its own working set of the previous call
+        # (fast along a price loop, whose iterations move the prices a little)
+        self.warm = False
+        self._ws = {}
 
     def set_charge_levels(self, y0):
         self.nEVs, self.y0_rng, self.gamma_sc, self.gamma_sm = O.set_charge_levels(y0, self.consts.y_max)
         self.y0 = np.asarray(y0, dtype=np.float64)
+        self._ws = {}
 
     def _batch(self, lmbd, lmbd_r):
         import oracle_c
 
         g = self.consts.y_max - self.y0
-        w, _, nf = oracle_c.solve_batch(self.N, self.consts, lmbd, lmbd_r, g, warm=self.warm)
+        if self.warm == "state":
+            w, nf = oracle_c.solve_batch_state(self.N, self.consts, lmbd, lmbd_r, g, self._ws)
+        else:
+            w, _, nf = oracle_c.solve_batch(self.N, self.consts, lmbd, lmbd_r, g, warm=self.warm)
         assert nf == 0
         return w
 
-    def _get_w_err(self, lmbd, lmbd_r, w_ref, A_bar):
-        """price_solver.py:196-214 (vectorised over the oracle batch)."""
+    def _get_w_err(self, lmbd, lmbd_r, w_ref, A_bar, want_max=True):
+        """price_solver.py:196-214 (vectorised over the oracle batch; want_max=False: w_err_max is not
+        computed — the loop tests the average error, settings.py PRICE_SOLVER_TOL_TYPE "avg")."""
         W = self._batch(lmbd, lmbd_r)
-        dv = W - w_ref
-        w_err_max = float(np.max(np.sqrt(np.einsum("bi,bi->b", dv @ A_bar, dv))))
+        w_err_max = float("nan")
+        if want_max:
+            dv = W - w_ref
+            w_err_max = float(np.max(np.sqrt(np.einsum("bi,bi->b", dv @ A_bar, dv))))
         w_avg = W.sum(axis=0) / self.nEVs
         w_avg_err = np.sqrt((w_avg - w_ref) @ A_bar @ (w_avg - w_ref))
         return w_err_max, np.abs(w_avg[0] - w_ref[0]), w_avg_err
@@ -157,7 +168,7 @@ class OraclePriceSolver:
         w_k, dual_cost = self.lompc.solve_lompc(lmbd_k, lmbd_r, self.gamma_sc)
         ac, pred = [], []
         for it in range(MAX_ITERS):
-            _, _, w_avg_err = self._get_w_err(lmbd_k, lmbd_r, w_ref, A_bar)
+            _, _, w_avg_err = self._get_w_err(lmbd_k, lmbd_r, w_ref, A_bar, want_max=False)
             if w_avg_err <= tol:
                 break
             lmbd_k_new[:r], dec = price_step(N, r, th, wm, self.m, A_bar_inv, w_ref, w_k, lmbd_k[:r])

@@ -207,3 +207,35 @@ def test_price_regularize_matches_regularizer(ev, price):
     assert lib.lompc_price_regularize(12, 30, 1.0, 1.0, w.ctypes.data, np.zeros(36).ctypes.data,
                                       ctypes.byref(ctypes.c_double()), ctypes.byref(ctypes.c_double())) \
         == _lib.LOMPC_ERR_INVALID_ARG
+
+
+@pytest.mark.parametrize("edge", ["below_zero", "above_w_max"])
+def test_price_regularize_w_a_rounding_error_outside_the_box(edge):
+    """The loop's final w_k is an unclamped piece aggregate: a coordinate can sit a rounding error
+    outside [0, w_max] (w_t = -1e-17 or w_max + 1e-15), which makes one cost entry of phi(w) slightly
+    negative.  lompc_price_regularize then takes the general LP (lompc_lp_solve) as
+    PriceRegularizer.solve_price_regularization does, instead of failing: same x as the regularizer,
+    A x = b, and the optimal value of HiGHS."""
+    c = O.large_consts()
+    lib = _lib.load()
+    rng = np.random.default_rng(77 + (edge == "above_w_max"))
+    for N, r in ((12, 36), (48, 144), (24, 48)):
+        reg = PriceRegularizer(N, r)
+        w = c.w_max * rng.random(N)
+        w[3] = -1e-17 if edge == "below_zero" else c.w_max + 1e-15
+        lm = np.zeros(3 * N)
+        lm[:r] = c.theta * rng.random(r)
+        ph = PO.phi(N, c.theta, c.w_max, w)
+        assert np.min(ph[:r]) < 0  # (the case: a cost entry below zero)
+        D = PO.Dphi(N, c.theta, c.w_max, w)[:r, :]
+        x = reg.solve_price_regularization(D.T, D.T @ lm[:r], ph[:r])
+        out = lm.copy()
+        pre, post = ctypes.c_double(0.0), ctypes.c_double(0.0)
+        assert lib.lompc_price_regularize(N, r, float(c.theta), float(c.w_max), w.ctypes.data, out.ctypes.data,
+                                          ctypes.byref(pre), ctypes.byref(post)) == _lib.LOMPC_OK
+        np.testing.assert_array_equal(out[:r], x)
+        assert np.all(out[:r] >= 0)
+        np.testing.assert_allclose(D.T @ out[:r], D.T @ lm[:r], rtol=1e-9, atol=1e-9 * c.theta)
+        _, best = PO.lp_highs(D.T, D.T @ lm[:r], ph[:r])
+        assert abs(ph[:r] @ out[:r] - best) <= 1e-9 * max(1.0, abs(best))
+        assert abs(post.value - ph @ out) <= 1e-12 * max(1.0, abs(ph @ out))

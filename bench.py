@@ -9,27 +9,31 @@ partition price vectors (lambda ~ theta U[0,1]^{3N}, test_lompc.py:34) and
 solve every EV's LoMPC QP (gamma_i = y_max - y0_i, y0 ~ U[0.3, 0.5],
 settings.py:27-28) with full outputs (w, cost) plus the fused per-partition
 reductions of price_solver.py:203-214; with N > 1 ranks the per-partition
-reductions of both types are combined by ONE RCCL all-gather (lompc_amd.dist.
-combine_set_results, rank-ordered local sum / max).  Weak scaling:
+reductions of both types are exchanged by ONE RCCL all-gather per group of up to
+64 steps (the extension's communicator, inside the same C-ABI call) and combined
+in rank order on the device (k_combine_runs: local sum / max).  Weak scaling:
 262 144 EVs per GPU (config 3; at 8 GPUs this is config 4's 2 097 152).
 
-A plan run is three kernels: k_path (per (set, gamma cell) solution paths), k_eval (per-EV
+A single plan run is three kernels: k_path (per (set, gamma cell) solution paths), k_eval (per-EV
 evaluation + rows) and k_finalize (per-set reductions and any individual re-solve).  The K timed
 steps are independent runs (fresh prices each), issued by ONE lompc_plan_run_steps call in its
-wide form: the K steps' paths in one k_paths launch (thousands of independent latency-bound
-chains at once), then one k_step launch per step carrying step k's evaluation and step k-1's
-closing, plus one closing launch after the last step; every step's work is done in full inside
-the timed region, and the results equal the launch-per-kernel form bit for bit.
+WIDE form: per group of up to 64 steps three launches — k_paths (every step's paths at once:
+thousands of independent latency-bound chains), k_evals (each workgroup evaluates its block of EVs
+for every step of the group in turn, no kernel boundary between steps) and k_closes (one workgroup
+per (step, set): the closings).  Every step's work is done in full inside the timed region, and
+the results equal the launch-per-kernel form bit for bit (verified after the timed region).
 
-Rank 0 prints ONE JSON line.  ``roofline`` prices the launch that carries the per-EV work
-(k_step; k_eval when the stepped form does not apply) by the evaluation's algorithmic bytes
-per QP (gamma in 8 B, w out 8N B, cost out 8 B) over its duration from HIP events attached to
-its dispatch in the timed region; ``kernels`` gives each plan kernel's average duration as its
-own launch from a separate 20-step pass with events on all three (after the timed region) and
-k_path's latency roof (PMC figures from profiles/, when they match this configuration);
-``cpu_baseline`` times the C oracle (oracle/, dense active set) on a bounded sample of the same
-workload: all host threads, one thread, and the lmbd_r > 0 variant; ``direct_mode`` times the
-per-EV DIRECT mode on the same batch.
+Rank 0 prints ONE JSON line.  ``roofline`` prices k_evals — the kernel that carries the per-EV
+work — by the evaluation's algorithmic bytes per QP (gamma in 8 B, w out 8N B, cost out 8 B) over
+its duration per step: ONE HIP-event pair around the first group's k_evals launch in the timed
+region (hipExtLaunchKernel events on its own stream) divided by the group's steps; ``kernels``
+gives each plan kernel's average duration as its own launch from a separate 20-step pass (after
+the timed region) and PMC figures from profiles/ when they match this configuration;
+``contracts`` the reference's other per-iteration shapes (reductions only, w0 only, every step's
+rows to fresh HBM buffers, dependent steps); ``cpu_baseline`` the same path algorithm and the
+dense C oracle (oracle/) on the host's cores over a bounded sample of the same workload;
+``direct_mode`` the per-EV DIRECT mode on the same batch; ``bimpc`` the config-5 closed-loop
+station step (BiMPC steps/sec).
 """
 from __future__ import annotations
 
@@ -95,6 +99,8 @@ def parse():
                          "reductions all-gathered by the extension's RCCL communicator and combined on the device")
     ap.add_argument("--no-contracts", action="store_true",
                     help="skip the reductions-only / w0-only contract legs (the reference's _get_w_err / get_w0_price0)")
+    ap.add_argument("--station-pl1-steps", type=int, default=4,
+                    help="extra station steps at the reference's default PRINT_LEVEL = 1 (prints captured)")
     ap.add_argument("--station-prof-steps", type=int, default=4,
                     help="extra station steps with the price loops' per-part timing (after the timed steps)")
     return ap.parse_args()
@@ -251,6 +257,17 @@ def main():
     # when sharded — the HIP events on every E-th step's k_step), so host issue stays far below
     # the GPU time even on a slow host CPU; every step's set reductions are kept ([K][S][...])
     batched = len(runs) == 1 and "lm_stride" in runs[0] and not args.per_step_issue and not py_combine
+    # every timed step writes its own set reductions ([K][S][...]), so every step is observable afterwards
+    # (verify_steps); the per-EV outputs (w, cost) are one buffer that every step rewrites, as a price
+    # loop's iterations do (price_solver.py:203-209), the last step's remaining.  (Allocated before the
+    # warmup: no allocation between the warmup and the timed region.)
+    outs_t = outs_v = None
+    if batched:
+        pl = runs[0]["plan"]
+        K = args.steps
+        outs_t = {k: torch.empty((K,) + tuple(pl.out[k].shape), dtype=torch.float64, device=dev)
+                  for k in ("set_sum_w", "set_stats") if pl.out.get(k) is not None}
+        outs_v = {k: torch.empty_like(v) for k, v in outs_t.items()}
     # warmup (and correctness gate: every QP certified) — in the timed region's own form, so its
     # one-time setup (the stepped form's tables and block map) is not timed
     if batched:
@@ -265,27 +282,20 @@ def main():
     for r in runs:
         r["plan"].profile(enable=("k_eval",) if args.kernel_events != "none" else False)
         r["plan"].profile(read=True, reset=True)
-    # every timed step writes its own set reductions ([K][S][...]), so every step is observable afterwards
-    # (verify_steps); the per-EV outputs (w, cost) are one buffer that every step rewrites, as a price
-    # loop's iterations do (price_solver.py:203-209), the last step's remaining
-    outs_t = outs_v = None
-    if batched:
-        pl = runs[0]["plan"]
-        K = args.steps
-        outs_t = {k: torch.empty((K,) + tuple(pl.out[k].shape), dtype=torch.float64, device=dev)
-                  for k in ("set_sum_w", "set_stats") if pl.out.get(k) is not None}
-        outs_v = {k: torch.empty_like(v) for k, v in outs_t.items()}
+    ev_every = max(1, args.event_every)
+    no_events = args.kernel_events == "none"
+    go = None
+    if batched:  # the timed call prepared (its arguments converted) before the clock starts
+        r = runs[0]
+        go, _ = r["plan"].steps_call(r["lm_ptr"][args.warmup], r["lr_ptr"], args.steps, r["lm_stride"], 0,
+                                     profile_every=0 if no_events else ev_every, out=outs_t,
+                                     span_events=args.kernel_events == "span")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev_every = max(1, args.event_every)
-    no_events = args.kernel_events == "none"
     t0 = time.perf_counter()
     if batched:
-        r = runs[0]
-        r["plan"].run_steps(r["lm_ptr"][args.warmup], r["lr_ptr"], args.steps, r["lm_stride"], 0,
-                            profile_every=0 if no_events else ev_every, out=outs_t,
-                            span_events=args.kernel_events == "span")
+        go()
     else:
         for k in range(args.warmup, nsteps):
             sample = not no_events and (k - args.warmup) % ev_every == 0
@@ -822,7 +832,9 @@ def station_leg(args, world, dev, sharded=False):
     steps, warm = args.station_steps, args.station_warmup
     # storage rate / capacity 0.5 (x_max = 0.5 is one of the example's listed values, :47): at
     # horizon 48 the example's 0.3 / 0.3 makes the first BiMPC infeasible (example.station_consts)
-    consts = station_consts(steps + warm + max(args.station_prof_steps, 0), M_2, n_lo=N, n_bi=N, partitions=P, price_type="linear-convex",
+    pl1 = max(args.station_pl1_steps, 0)
+    consts = station_consts(steps + warm + max(args.station_prof_steps, 0) + pl1, M_2, n_lo=N, n_bi=N, partitions=P,
+                            price_type="linear-convex",
                             demand_scale=DEMAND_SCALE * M_2 / NUM_EVS_PER_EV_TYPE, u_b_max=0.5, x_max=0.5)
     group = dist.group.WORLD if sharded else None
     is_c5 = 2 * M_2 == 2097152 and N == 48 and P == 12
@@ -838,7 +850,12 @@ def station_leg(args, world, dev, sharded=False):
                                          "(real_time_price_control.py:46-47); at horizon 48 the first BiMPC from an "
                                          "empty battery needs u_b_max >= 2 d_e ~ 0.37 (beta = 0.183), so 0.3 is "
                                          "infeasible and u_b_max = 0.5 is used"},
-                      "sharded_code_path": bool(sharded)}}
+                      "sharded_code_path": bool(sharded),
+                      "print_level": 0,
+                      "print_level_note": ("timed at settings.PRINT_LEVEL = 0; the reference's default is 1 "
+                                           "(settings.py:4), which prints per partition and adds one more batched "
+                                           "solve (the batch error at the final prices, price_solver.py:150-152) per "
+                                           "partition — logging-only work; print_level_1 below times steps at 1")}}
     try:
         np.random.seed(args.seed)  # the reference's legacy global stream (charging_station.py:95-100)
         st = ChargingStation(consts, device=dev.index, group=group)
@@ -887,6 +904,7 @@ def station_leg(args, world, dev, sharded=False):
         spread["attribution"] = station_attribution(ms, parts, stats, warm, steps)
         info = st.bimpc.last_info or {}
         loop = price_loop_breakdown(st, args.station_prof_steps, consts, torch)
+        out["print_level_1"] = print_level_leg(st, pl1, consts, torch) if pl1 and world == 1 else None
         out.update({"value": steps / dt, "ms_per_step": dt / steps * 1e3,
                     "ms_per_step_median": float(np.median(ms)), "ms_per_step_min": float(ms.min()),
                     "ms_per_step_max": float(ms.max()),
@@ -986,6 +1004,45 @@ def price_loop_breakdown(st, n, consts, torch):
                                    "host_other": per(_lib.LOMPC_LOOP_PROF_HOST)}}
 
 
+def print_level_leg(st, n, consts, torch):
+    """``n`` more station steps at the reference's default settings.PRINT_LEVEL = 1 (settings.py:4): the
+    per-partition prints (captured here, never on stdout: the line stays the only output), the extra
+    batched solve per partition that feeds them (price_solver.py:150-152), and the two EV types' chains
+    in the reference's interleaved order on one thread (the printing order), so no chain overlap."""
+    import contextlib
+    import io
+
+    from lompc_amd import settings
+
+    stats = st.logs["statistics"]
+    t_first = st.t
+    buf = io.StringIO()
+    settings.PRINT_LEVEL = 1
+    ms = []
+    try:
+        with contextlib.redirect_stdout(buf):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                ts = time.perf_counter()
+                st._step()
+                torch.cuda.synchronize()
+                ms.append((time.perf_counter() - ts) * 1e3)
+                check_station_state(st, consts)
+            dt = time.perf_counter() - t0
+    finally:
+        settings.PRINT_LEVEL = 0
+    its = 0
+    for key in ("niter_s", "niter_l"):
+        a = np.asarray(stats[key][:, t_first:st.t])
+        its += int(a[a >= 0].sum())
+    return {"steps": n, "value": n / dt, "unit": "steps/s", "ms_per_step": dt / n * 1e3,
+            "ms_per_step_median": float(np.median(ms)), "price_iterations_per_step": its / n,
+            "printed_lines": buf.getvalue().count("\n"),
+            "note": "the steps after the timed and profiled ones (another part of the trajectory: compare per "
+                    "price iteration, not per step)"}
+
+
 def check_station_state(st, consts):
     """Invariants of a closed-loop step (raise -> the leg reports "error" and the run fails):
     storage state within [0, x_max] up to the BiMPC's robustness margin, the planner converged
@@ -1003,6 +1060,18 @@ def check_station_state(st, consts):
     for key in ("Mp_s", "Mp_l"):
         if int(st.logs["statistics"][key][:, t].sum()) != st.M_2:
             raise AssertionError(f"{key} does not count every EV once")
+
+
+def host_threads_note(threads: int) -> dict:
+    """Where the CPU baselines' thread count comes from: OpenMP's default is OMP_NUM_THREADS when set
+    (the GPU box exports 16, its CPU share per GPU), otherwise the process's CPU affinity."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"host_cpus": os.cpu_count(), "affinity_cpus": aff,
+            "threads_source": (f"OMP_NUM_THREADS={env} in the environment (the box's CPU share per GPU; "
+                               f"{aff} CPUs in this process's affinity, {os.cpu_count()} on the machine)"
+                               if env else f"OpenMP default: the {aff} CPUs of this process's affinity"),
+            "threads_used": threads}
 
 
 def cpu_same_algorithm(eng, N, P, args, ref):
@@ -1044,7 +1113,8 @@ def cpu_same_algorithm(eng, N, P, args, ref):
     out = {"value": v, "unit": "QP/s", "cores": threads, "kind": "port (same algorithm as the GPU path engine)",
            "sample": f"{runs} runs x {B} EVs (horizon {N}, 24 sets, full outputs, the timed steps' prices) in {dt:.1f} s, "
                      f"OpenMP {threads} threads (oracle/path_cpu.cpp, {args.cells or 'default'} cells per set as the GPU plan)",
-           "single_thread": {"value": v1, "sample": f"{runs1} runs x {B} EVs in {dt1:.1f} s, 1 thread"}}
+           "single_thread": {"value": v1, "sample": f"{runs1} runs x {B} EVs in {dt1:.1f} s, 1 thread"},
+           **host_threads_note(threads)}
     if ref is not None:
         o = oracle_c.path_run(N, cs, [P, P], lms[-1], lr, g, off, w_ref=wr, nthreads=threads, cells=args.cells)
         out["parity"] = {"step": "the last timed step (all EVs)",
@@ -1103,7 +1173,7 @@ def cpu_baseline(eng, N, seconds, seed=0):
     return {"value": v, "unit": "QP/s", "cores": threads, "kind": "port",
             "sample": f"{done} QPs ({reps} passes over {n} small + {n} large EVs, horizon {N}, partition-0 "
                       f"prices, lmbd_r = 0) in {dt:.1f} s, C oracle dense active set, OpenMP {threads} threads",
-            "host_cpus": os.cpu_count(), "seed": seed,
+            **host_threads_note(threads), "seed": seed,
             "single_thread": {"value": v1, "sample": f"{done1} QPs in {dt1:.1f} s, 1 thread"},
             "lmbd_r_random": {"value": vr, "sample": f"{doner} QPs in {dtr:.1f} s, {threads} threads, "
                                                      "lmbd_r = 3 N delta U[0,1] per type"}}

@@ -127,6 +127,15 @@ __global__ __launch_bounds__(256) void k_lv_gamma(const double* __restrict__ ys,
 constexpr int LV_HP = 16;
 constexpr int LV_HBLK = 512;  // workgroups at most
 
+// max / min that propagate NaN (fmax / fmin drop it): the whole-type max y / min y of the statistics
+// pass carry a NaN level to the caller, whose range check [rng[0], rng[P]] then fails (a NaN counted
+// in partition 0 would otherwise leave the sorted runs and the statistics' counts out of step)
+__device__ __forceinline__ double lv_nmax(double a, double b) { return (a != a || b != b) ? NAN : fmax(a, b); }
+__device__ __forceinline__ double lv_nmin(double a, double b) { return (a != a || b != b) ? NAN : fmin(a, b); }
+__device__ __forceinline__ double lv_comb(int f, double a, double b) {
+  return f == 1 ? fmax(a, b) : f == 2 ? fmin(a, b) : f == 4 ? lv_nmax(a, b) : f == 5 ? lv_nmin(a, b) : a + b;
+}
+
 __global__ __launch_bounds__(256) void k_lvh_partial(const double* __restrict__ y, int64_t n,
                                                      const double* __restrict__ bounds, int P, int nblk,
                                                      double* __restrict__ part) {
@@ -167,8 +176,8 @@ __global__ __launch_bounds__(256) void k_lvh_partial(const double* __restrict__ 
         mx[k] = m ? fmax(mx[k], v) : mx[k];
         mn[k] = m ? fmin(mn[k], v) : mn[k];
       }
-      ymx = fmax(ymx, v);
-      ymn = fmin(ymn, v);
+      ymx = lv_nmax(ymx, v);
+      ymn = lv_nmin(ymn, v);
     }
   }
   __shared__ double sw[4][4 * LV_HP + 2];
@@ -184,8 +193,8 @@ __global__ __launch_bounds__(256) void k_lvh_partial(const double* __restrict__ 
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    ymx = fmax(ymx, __shfl_xor(ymx, o));
-    ymn = fmin(ymn, __shfl_xor(ymn, o));
+    ymx = lv_nmax(ymx, __shfl_xor(ymx, o));
+    ymn = lv_nmin(ymn, __shfl_xor(ymn, o));
   }
   if (lane == 0) {
 #pragma unroll
@@ -200,9 +209,10 @@ __global__ __launch_bounds__(256) void k_lvh_partial(const double* __restrict__ 
   }
   __syncthreads();
   if (t < 4 * LV_HP + 2) {
-    const int f = t < 4 * LV_HP ? (t & 3) : (t == 4 * LV_HP ? 1 : 2);  // 0 count / 3 sum: add; 1 max; 2 min
+    // 0 count / 3 sum: add; 1 max; 2 min; 4 / 5: the whole type's max / min (NaN propagated)
+    const int f = t < 4 * LV_HP ? (t & 3) : (t == 4 * LV_HP ? 4 : 5);
     double v = sw[0][t];
-    for (int w = 1; w < 4; ++w) v = f == 1 ? fmax(v, sw[w][t]) : f == 2 ? fmin(v, sw[w][t]) : v + sw[w][t];
+    for (int w = 1; w < 4; ++w) v = lv_comb(f, v, sw[w][t]);
     part[(size_t)b * (4 * LV_HP + 2) + t] = v;
   }
 }
@@ -212,18 +222,12 @@ __global__ __launch_bounds__(256) void k_lvh_partial(const double* __restrict__ 
 __global__ __launch_bounds__(64) void k_lvh_final(const double* __restrict__ part, int nblk, int P,
                                                   const double* __restrict__ bounds, double* __restrict__ stats) {
   const int t = (int)blockIdx.x, lane = (int)threadIdx.x;
-  const int f = t < 4 * LV_HP ? (t & 3) : (t == 4 * LV_HP ? 1 : 2);  // 0 count / 3 sum: add; 1 max; 2 min
-  const double id = f == 1 ? -INFINITY : f == 2 ? INFINITY : 0.0;
+  const int f = t < 4 * LV_HP ? (t & 3) : (t == 4 * LV_HP ? 4 : 5);  // as k_lvh_partial's combine
+  const double id = (f == 1 || f == 4) ? -INFINITY : (f == 2 || f == 5) ? INFINITY : 0.0;
   double v = id;
-  for (int b = lane; b < nblk; b += 64) {
-    const double u = part[(size_t)b * (4 * LV_HP + 2) + t];
-    v = f == 1 ? fmax(v, u) : f == 2 ? fmin(v, u) : v + u;
-  }
+  for (int b = lane; b < nblk; b += 64) v = lv_comb(f, v, part[(size_t)b * (4 * LV_HP + 2) + t]);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double u = __shfl_xor(v, o);
-    v = f == 1 ? fmax(v, u) : f == 2 ? fmin(v, u) : v + u;
-  }
+  for (int o = 32; o > 0; o >>= 1) v = lv_comb(f, v, __shfl_xor(v, o));
   if (lane == 0) {
     if (t < 4 * P) stats[t] = v;                                      // per partition (count, max, min, sum)
     else if (t >= 4 * LV_HP) stats[4 * P + (t - 4 * LV_HP)] = v;       // max y, min y

@@ -1588,9 +1588,15 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       if (ro.pipelined) {
         // the block's last wave to finish its rows writes the record (the others go on to the next run's
         // staging loads); the acquire-release LDS counter orders every wave's row sums before its read
+        // Every lane of the wave takes part in the ordering: a workgroup-scope release fence (LDS only:
+        // the row stores to HBM stay in flight) before lane 0's increment orders all lanes' row-sum
+        // writes, and the acquire fence after the broadcast orders the last wave's reads of every
+        // wave's sums, per the HIP memory model rather than per-wave LDS issue order
         int old = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         if (lane == 0) old = __hip_atomic_fetch_add(&s_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
         old = __shfl(old, 0, 64);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         if (old == EVAL_WAVES - 1) {
           store_record(lane, 64);
           if (lane == 0) __hip_atomic_store(&s_done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3039,7 +3045,13 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     // batched: per path group of n <= Kc runs THREE launches — k_paths (the n paths), k_evals (the n
     // evaluations, each workgroup through its block of every run) and k_closes (the n x S closings);
     // the same kernels' arithmetic as the split form below, so the same bits
-    const int64_t need = std::min<int64_t>(LQ_WIDE_RUNS, fit) * z.nblk;  // record slots x blocks
+    // record slots x blocks, bounded like the table ring: a run's slot holds every block's record, its
+    // re-solve counts and its re-solve list (EVAL_MAXB indices per block), so a batch of many blocks
+    // takes smaller groups instead of gigabytes of mostly empty lists (the runs are independent: the
+    // group size changes no bits)
+    const int64_t rec_run = (int64_t)z.nblk * ((N + NPX) * 8 + EVAL_WAVES * 4 + EVAL_MAXB * 4);
+    const int64_t kr = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(LQ_WIDE_RUNS, fit), LQ_WIDE_BYTES / rec_run));
+    const int64_t need = kr * z.nblk;
     if (need > z.cap_rrec) {
       if ((rc = grow(p, &z.rpart, need * (N + NPX))) || (rc = grow(p, &z.rfcnt, need * EVAL_WAVES)) ||
           (rc = grow(p, &z.rfidx, need * EVAL_MAXB)))
@@ -3063,7 +3075,7 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     ff.set_stats = xr ? p->d_xsend + p->S * N : set_stats;
     // (k_evals_st's split form: the same three kernels, one run per group — its arithmetic is not
     // k_step's: the stager leaves seven waves to the rows, so the row sums group differently)
-    const int grp = split ? 1 : Kc;
+    const int grp = split ? 1 : (int)std::min<int64_t>(Kc, kr);
     if (z.stg) ea.cap = std::min(LQ_EVALS_CAP, p->G * LQ_PPL);
     const size_t lds_e = z.stg ? evals_st_lds(N, p->G, ea.cap) : lds;
     for (int g0 = 0; g0 < K; g0 += grp) {

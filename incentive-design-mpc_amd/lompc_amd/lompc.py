@@ -548,6 +548,19 @@ class BatchPlan:
         flags say).  per_kernel: LOMPC_STEPS_PER_KERNEL (the same runs, one part per launch, bit for
         bit the same outputs); span_events: one event pair over the stepped launches
         (LOMPC_STEPS_SPAN_EVENTS)."""
+        call, res = self.steps_call(lmbd, lmbd_r, n_runs, lmbd_stride, lmbd_r_stride, profile_every=profile_every,
+                                    per_run_sets=per_run_sets, per_run=per_run, out=out, per_kernel=per_kernel,
+                                    span_events=span_events)
+        call()
+        return res
+
+    def steps_call(self, lmbd, lmbd_r, n_runs: int, lmbd_stride: int, lmbd_r_stride: int = 0,
+                   profile_every: int = 0, per_run_sets: bool = False, per_run: bool = False, out=None,
+                   per_kernel: bool = False, span_events: bool = False):
+        """run_steps prepared: (call, outputs) — ``call()`` issues the same lompc_plan_run_steps with
+        every argument already converted (no Python work between the caller's clock and the C-ABI
+        entry beyond one ctypes call); it may be called again for the same runs into the same
+        outputs."""
         if self.direct:
             raise ValueError("run_steps: PATH-mode plans only")
         self._usable()
@@ -584,12 +597,17 @@ class BatchPlan:
             raise ValueError("run_steps: set_sum_w and set_stats are both per run or both shared")
         flags = (_lib.LOMPC_STEPS_PER_KERNEL if per_kernel else 0) | (_lib.LOMPC_STEPS_SPAN_EVENTS if span_events else 0)
         ptrs = [_ptr(res[k]) for k in keys]
-        rc = self._lib.lompc_plan_run_steps(self._plan, pl, int(lmbd_stride), pr, int(lmbd_r_stride), K,
-                                            int(profile_every), *ptrs, sw_stride, st_stride, ev_stride, flags,
-                                            self._stream)
-        if rc:
-            self._check_rc(rc)
-        return res
+        fn = self._lib.lompc_plan_run_steps
+        args = (self._plan, pl, int(lmbd_stride), pr, int(lmbd_r_stride), K, int(profile_every), *ptrs, sw_stride,
+                st_stride, ev_stride, flags, self._stream)
+        check = self._check_rc
+
+        def call():
+            rc = fn(*args)
+            if rc:
+                check(rc)
+
+        return call, res
 
     def run_chain(self, lmbd0, lmbd_r, w_target, step: float, n_runs: int, out=None) -> dict:
         """n_runs DEPENDENT runs in one C-ABI call (lompc_plan_run_chain): run 0 at lmbd0 (S, 3N), run

@@ -26,6 +26,9 @@ ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--outputs", default="full")
 ap.add_argument("--horizon", type=int, default=24)
 ap.add_argument("--evs", type=int, default=262144)
+ap.add_argument("--warmup", type=int, default=0, help="warmup call's runs (0: --steps)")
+ap.add_argument("--gpu-span", action="store_true", help="torch events around each timed call")
+ap.add_argument("--idle-ms", type=float, default=0.0, help="host sleep before each timed call (GPU idle)")
 args = ap.parse_args()
 
 import torch  # noqa: E402
@@ -53,23 +56,39 @@ for libname in args.libs:
     for cells in args.cells:
         plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], w_ref=wr, want_w=args.outputs == "full",
                          want_cost=args.outputs != "set", cells=cells or None)
-        plan.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True)
+        plan.run_steps(lm, lr, args.warmup or K, lm[0].numel(), lr[0].numel(), per_run_sets=True)
         plan.check()
-        walls, ks = [], []
+        walls, ks, spans = [], [], []
+        go, _ = plan.steps_call(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, span_events=True)
+        ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(args.reps):
             plan.profile(enable=("k_eval",))
             plan.profile(read=True, reset=True)
             torch.cuda.synchronize()
+            if args.idle_ms:
+                time.sleep(args.idle_ms / 1e3)
             t0 = time.perf_counter()
-            plan.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, span_events=True)
+            if args.gpu_span:
+                ea.record()
+            go()
+            if args.gpu_span:
+                eb.record()
             torch.cuda.synchronize()
             walls.append((time.perf_counter() - t0) / K * 1e6)
+            if args.gpu_span:
+                spans.append(ea.elapsed_time(eb) * 1e3 / K)
             ms, n = plan.profile(read=True)
             ks.append(ms / max(n, 1) * 1e3)
             rep = plan.check()[0]
         plan.profile(enable=("k_path", "k_eval", "k_finalize"))
         for k in ("k_path", "k_eval", "k_finalize"):
             plan.profile(read=True, reset=True, kernel=k)
+        wide = []
+        for _ in range(3):  # the wide call's own kernels: k_paths per launch, k_evals / k_closes per run
+            plan.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True)
+            wide.append({k: plan.profile(read=True, reset=True, kernel=k) for k in ("k_path", "k_eval", "k_finalize")})
+        print("   wide call: " + " | ".join(
+            "  ".join(f"{k} {ms * 1e3:.1f} us / {n}" for k, (ms, n) in w.items()) for w in wide), flush=True)
         for j in range(20):
             plan.run(lm[j % K], lr[j % K])
         plan.check()
@@ -88,4 +107,7 @@ for libname in args.libs:
               f"  k_step {np.median(ks):6.2f} us  alone: " +
               "  ".join(f"{k} {ms / max(n, 1) * 1e3:6.2f}" for k, (ms, n) in alone.items()) +
               f"  repaired per step {rep / K:.0f}", flush=True)
+        print("   every call (us per step): " + " ".join(f"{v:.2f}" for v in walls), flush=True)
+        if spans:
+            print("   GPU span (us per step):   " + " ".join(f"{v:.2f}" for v in spans), flush=True)
         del plan

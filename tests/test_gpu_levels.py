@@ -112,3 +112,28 @@ def test_gamma_layout_matches_per_partition_batches(gpu, rank):
         assert np.all(np.diff(v[: b - a]) >= 0)
         if rank == 0 and st[p, 0] > 0:
             assert v[-1] == 0.9 - (float(st[p, 1]) + float(st[p, 2])) / 2
+
+
+@pytest.mark.parametrize("where", [0, 777, 39999])
+def test_levels_stats_nan_fails_the_range_check(gpu, where):
+    """A NaN charge level reaches the caller: lompc_levels_stats' whole-type max y / min y propagate it
+    (fmax / fmin would drop it), so _sorted_layouts' range check fails and the type takes the index
+    path — instead of a NaN counted in partition 0 while the deferred sort puts it elsewhere."""
+    rs = np.random.default_rng(95)
+    P = 12
+    rng_s = np.linspace(0.3, 0.9, P + 1)
+    y = 0.3 + 0.55 * rs.random(40000)
+    y[where] = np.nan
+    cs = object.__new__(ChargingStation)
+    cs.P, cs.group, cs.device = P, None, 0
+    cs.y_s, cs.y_l = torch.as_tensor(y, device="cuda:0"), torch.as_tensor(y[:5000].copy(), device="cuda:0")
+    cs.y_l[:] = 0.5  # (the large type: no NaN)
+    cs.y0_s_rng, cs.y0_l_rng = rng_s, rng_s
+    cs.idx_s = torch.zeros(len(y), dtype=torch.int64, device="cuda:0")
+    cs.idx_l = torch.zeros(5000, dtype=torch.int64, device="cuda:0")
+    cs._bounds, cs._lv = {}, {}
+    ChargingStation._update_indices(cs)
+    out = ChargingStation._sorted_layouts(cs)
+    assert set(out) == {"Large"}
+    rec = cs._lv["Small"]["stats"].cpu().numpy()
+    assert np.isnan(rec[4 * P]) and np.isnan(rec[4 * P + 1])

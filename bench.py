@@ -63,10 +63,11 @@ def parse():
     ap.add_argument("--mode", choices=["path", "direct"], default="path")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cells", type=int, default=12,
+    ap.add_argument("--cells", type=int, default=4,
                     help="gamma cells per parameter set of the benchmark's plan (0: the plan's default, 16 at these "
-                         "set sizes); 12 measured best for the wide run_steps form (12.89 vs 13.42 us per step over "
-                         "64 steps, scripts/step_probe.py), at +0.5 us for one run's path alone")
+                         "set sizes); 4 measured best for the wide run_steps form (scripts/step_probe.py, K = 20: "
+                         "13.4 vs 14.3 us per step at 12 cells — k_paths 28 vs 38 us per call, k_evals 10.7 vs 11.1 "
+                         "us per run; K = 100: 12.2 vs 12.5), at +2.6 us for one run's path alone (18.3 vs 15.7 us)")
     ap.add_argument("--warm", action="store_true",
                     help="plan warm start: every gamma cell's exact solve starts from the working set the "
                          "previous step ended with there (as a price loop's plan does)")
@@ -269,10 +270,17 @@ def main():
                   for k in ("set_sum_w", "set_stats") if pl.out.get(k) is not None}
         outs_v = {k: torch.empty_like(v) for k, v in outs_t.items()}
     # warmup (and correctness gate: every QP certified) — in the timed region's own form, so its
-    # one-time setup (the stepped form's tables and block map) is not timed
+    # one-time setup (the stepped form's tables and block map) is not timed; the warmup carries the
+    # timed call's HIP events too (the runtime's first timed dispatch on a queue costs host time), and
+    # its event readings are discarded
+    ev_every = max(1, args.event_every)
+    no_events = args.kernel_events == "none"
+    for r in runs:
+        r["plan"].profile(enable=("k_eval",) if not no_events else False)
     if batched:
         r = runs[0]
-        r["plan"].run_steps(r["lm_ptr"][0], r["lr_ptr"], max(args.warmup, 1), r["lm_stride"], 0)
+        r["plan"].run_steps(r["lm_ptr"][0], r["lr_ptr"], max(args.warmup, 1), r["lm_stride"], 0,
+                            profile_every=0 if no_events else ev_every, span_events=args.kernel_events == "span")
     else:
         for k in range(args.warmup):
             step(k)
@@ -280,10 +288,7 @@ def main():
         rep, fail, inv = r["plan"].check()  # (sticky tallies: every warmup step)
         assert fail == 0 and inv == 0, (fail, inv)
     for r in runs:
-        r["plan"].profile(enable=("k_eval",) if args.kernel_events != "none" else False)
         r["plan"].profile(read=True, reset=True)
-    ev_every = max(1, args.event_every)
-    no_events = args.kernel_events == "none"
     go = None
     if batched:  # the timed call prepared (its arguments converted) before the clock starts
         r = runs[0]

@@ -2995,6 +2995,12 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     if ((rc = grow(p, &t.cnt, c)) || (rc = grow(p, &t.lo, c)) || (rc = grow(p, &t.ge, c * LQ_PPL)) ||
         (rc = grow(p, &t.cf, c * LQ_PPL * 8)) || (rc = grow(p, &t.ab, c * LQ_PPL * N)) || (rc = grow(p, &t.sl, c * 64)))
       return rc;
+    // every slot written once now, in the call that sizes the ring (a plan's first wide call: the
+    // warmup), so a later call's first use of a slot meets no cold page translations
+    HIPCHK(p, hipMemsetAsync(t.ge, 0, (size_t)c * LQ_PPL * sizeof(*t.ge), st));
+    HIPCHK(p, hipMemsetAsync(t.cf, 0, (size_t)c * LQ_PPL * 8 * sizeof(*t.cf), st));
+    HIPCHK(p, hipMemsetAsync(t.ab, 0, (size_t)c * LQ_PPL * N * sizeof(*t.ab), st));
+    HIPCHK(p, hipMemsetAsync(t.sl, 0, (size_t)c * 64 * sizeof(*t.sl), st));
     z.cap_wt = c;
   }
   auto tab = [&](int j) {
@@ -3056,6 +3062,10 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
       if ((rc = grow(p, &z.rpart, need * (N + NPX))) || (rc = grow(p, &z.rfcnt, need * EVAL_WAVES)) ||
           (rc = grow(p, &z.rfidx, need * EVAL_MAXB)))
         return rc;
+      // (touched once here, as the table ring)
+      HIPCHK(p, hipMemsetAsync(z.rpart, 0, (size_t)need * (N + NPX) * sizeof(*z.rpart), st));
+      HIPCHK(p, hipMemsetAsync(z.rfcnt, 0, (size_t)need * EVAL_WAVES * sizeof(*z.rfcnt), st));
+      HIPCHK(p, hipMemsetAsync(z.rfidx, 0, (size_t)need * EVAL_MAXB * sizeof(*z.rfidx), st));
       z.cap_rrec = need;
     }
     if (xr && (rc = lq_xbufs(p, Kc, Kc))) return rc;

@@ -17,10 +17,20 @@ Same constants dataclass, constructor checks, ``simulate() -> logs`` and logs sc
 * ``_get_w0_price0`` (charging_station.py:310-329) is ONE batched engine call per EV
   type over all partitions (the prices are fixed by then), with fused price0 sums.
 
-Sharded mode (``group``): every rank holds a contiguous slice of each type's EVs;
-partition statistics, the price loops' reductions, price0 sums and the aggregate
-demand are combined with torch.distributed; the BiMPC and the price steps run
-redundantly on identical inputs; the re-draw replays the global random stream.
+Sharded mode (``group``): every rank holds a contiguous slice of each type's EVs (the per-EV
+state, the w0 / price0 pass and the state update are sharded).  Default ``sharded_loops =
+"replicated"``: ONE all-gather of both types' charge levels per step gives every rank the whole
+population, from which every rank builds the same partition statistics and layouts and runs every
+(type, partition) price loop itself (k_agg is O(pieces): a loop costs the same whatever the EV
+count, so replicating it costs nothing, and no collective runs inside a loop — ~600 per step with
+one per price iteration); the w0 / price0 pass runs on this rank's EVs, and its per-partition sums
+(the aggregate demand, charging_station.py:356-366) are combined by ONE all-reduce; the state
+update's residual sum and global redraw counts are the step's remaining exchanges.  The first
+step's prices, iterations and statistics are then bit for bit the single process's; later steps
+differ only through the w0 sums' order (and the per-rank plans' gamma windows) at rounding level.
+``sharded_loops = "exchange"``: every price iteration all-gathers the per-rank set reductions
+(the round-4/5 form, kept for A/B).  The BiMPC and the price steps run redundantly on identical
+inputs; the re-draw replays the global random stream.
 """
 from __future__ import annotations
 
@@ -137,7 +147,7 @@ def redraw_full(y, mask, lo_val: float, hi_val: float, rng_random, group=None) -
 
 class ChargingStation:
     def __init__(self, consts: ChargingStationConstants, device: int | None = None, mode: str | None = None,
-                 group=None) -> None:
+                 group=None, sharded_loops: str = "replicated") -> None:
         # charging_station.py:44-53
         assert consts.simulation_length >= 1
         assert (consts.horizon_bimpc >= consts.horizon_lompc) and (consts.horizon_lompc >= 1)
@@ -147,6 +157,15 @@ class ChargingStation:
             consts.demand.shape[0] >= consts.simulation_length + consts.horizon_bimpc + 1)
         torch = _torch()
         self.group = group
+        if sharded_loops not in ("replicated", "exchange"):
+            raise ValueError("sharded_loops: 'replicated' or 'exchange'")
+        # sharded with every price loop replicated on every rank (no collective inside a loop)
+        self.replicated = group is not None and sharded_loops == "replicated"
+        # sharded with one all-gather of the set reductions per price iteration
+        self._exchange = group is not None and not self.replicated
+        self._yfull = None  # replicated: this step's whole-population levels {kind: device tensor}
+        self._idxfull = {}  # replicated, index path only: the whole population's partition indices
+        self._layout_w0 = {}  # replicated: this rank's EVs in the loops' layout order, per type
         self._pool = None  # one worker thread: the large-EV price chain beside the small one
         self._stage_pool = None  # two worker threads: the partition plans staged beside the BiMPC solve
         self.profile_phases = False  # accumulate per-phase wall times of _step in phase_ms (synchronising)
@@ -167,10 +186,11 @@ class ChargingStation:
         # Set constants, initialize PriceSolvers and BiMPC.
         self._set_constants(consts)
         self.bimpc = BiMPC(self.N_bi, self.P, self.consts_bi, self.consts_s, self.consts_l)
+        lgroup = group if self._exchange else None  # (replicated: every rank's loops see the whole population)
         self.price_solver_s = PriceSolver(self.N_lo, self.consts_s, self.price_type, device=self.device, mode=mode,
-                                          group=group)
+                                          group=lgroup)
         self.price_solver_l = PriceSolver(self.N_lo, self.consts_l, self.price_type, device=self.device, mode=mode,
-                                          group=group)
+                                          group=lgroup)
         # Initialize state variables = (EV SoCs, charge stored).
         self._init_states()
         # Initialize logs.
@@ -211,6 +231,82 @@ class ChargingStation:
 
         return dist.get_rank(self.group) == 0
 
+    # ------------------------------------------------------------------ replicated sharding
+    def _gather_levels(self) -> None:
+        """Replicated sharding: both types' charge levels of every rank in ONE all-gather (each rank's
+        contiguous slice, padded to the largest shard), concatenated in rank order — the whole
+        population in EV-index order, exactly the single process's level vectors."""
+        torch = _torch()
+        import torch.distributed as dist
+
+        world = dist.get_world_size(self.group)
+        bounds = [shard_bounds(self.M_2, r, world) for r in range(world)]
+        pad = max(b - a for a, b in bounds)
+        n = self._hi - self._lo
+        send = torch.zeros((2, pad), dtype=torch.float64, device=self._dev)
+        send[0, :n] = self.y_s
+        send[1, :n] = self.y_l
+        recv = torch.empty(world * 2 * pad, dtype=torch.float64, device=self._dev)
+        dist.all_gather_into_tensor(recv, send.reshape(-1), group=self.group)
+        r = recv.view(world, 2, pad)
+        self._yfull = {kind: torch.cat([r[k, t, : b - a] for k, (a, b) in enumerate(bounds)])
+                       for t, kind in enumerate(("Small", "Large"))}
+
+    def _gather_idx(self, kind):
+        """Replicated sharding, index path only (a type whose levels left the partition range, so its
+        EVs keep their previous partition index, charging_station.py:111-116): the whole population's
+        partition indices of one type (every rank takes this path together: they all see the same
+        levels)."""
+        torch = _torch()
+        import torch.distributed as dist
+
+        world = dist.get_world_size(self.group)
+        bounds = [shard_bounds(self.M_2, r, world) for r in range(world)]
+        pad = max(b - a for a, b in bounds)
+        idx = self.idx_s if kind == "Small" else self.idx_l
+        send = torch.zeros(pad, dtype=torch.int64, device=self._dev)
+        send[: idx.numel()] = idx
+        recv = torch.empty(world * pad, dtype=torch.int64, device=self._dev)
+        dist.all_gather_into_tensor(recv, send, group=self.group)
+        r = recv.view(world, pad)
+        return torch.cat([r[k, : b - a] for k, (a, b) in enumerate(bounds)])
+
+    def _loop_levels(self, kind):
+        """(levels, partition indices) the price loops' layout is built from: this rank's EVs, or with
+        replicated sharding the whole population (indices None: gathered only if the index path is
+        taken)."""
+        if self.replicated:
+            return self._yfull[kind], None
+        return (self.y_s, self.idx_s) if kind == "Small" else (self.y_l, self.idx_l)
+
+    def _w0_layouts(self):
+        """Replicated sharding: this rank's EVs in the loops' layout order (each partition's run of the
+        whole population's layout restricted to global indices [lo, hi): still in descending charge
+        level), for the sharded w0 / price0 pass — {kind: (local permutation, levels, {p: (start,
+        end)})}, both types' run bounds in one host copy."""
+        torch = _torch()
+        if self._layout_w0:
+            return self._layout_w0
+        lo, hi, P = self._lo, self._hi, self.P
+        parts, ends = [], []
+        for kind in ("Small", "Large"):
+            perm, ys, seg = self._partition_layout(kind, *self._loop_levels(kind))
+            m = (perm >= lo) & (perm < hi)
+            order = sorted(range(P), key=lambda p: seg[p])
+            c = torch.cumsum(m.to(torch.int64), 0)
+            e = torch.as_tensor([seg[p][1] - 1 for p in order], dtype=torch.int64, device=m.device)
+            ends.append(torch.where(e >= 0, c[e.clamp(min=0)], 0))
+            nz = torch.nonzero_static(m, size=hi - lo).squeeze(1)
+            parts.append((kind, order, perm[nz] - lo, ys[nz]))
+        cnt = torch.stack(ends).cpu().numpy()  # the one host sync
+        for j, (kind, order, lperm, lys) in enumerate(parts):
+            seg_l, prev = {}, 0
+            for k, p in enumerate(order):
+                seg_l[p] = (prev, int(cnt[j, k]))
+                prev = int(cnt[j, k])
+            self._layout_w0[kind] = (lperm, lys, seg_l)
+        return self._layout_w0
+
     def _init_states(self) -> None:
         # charging_station.py:94-109 (global draws, this rank keeps its slice)
         torch = _torch()
@@ -243,6 +339,9 @@ class ChargingStation:
             idx.copy_(torch.where((y >= b[0]) & (y <= b[-1]), p, idx))
         self._layout = {}
         self._pending = {}  # (types whose statistics came without the sort: _partition_layout sorts them)
+        self._yfull = None
+        self._idxfull = {}
+        self._layout_w0 = {}
 
     def _init_logs(self, consts: ChargingStationConstants) -> None:
         # charging_station.py:118-149
@@ -350,9 +449,19 @@ class ChargingStation:
         gamma_sm, gamma_lm = np.zeros((self.P,)), np.zeros((self.P,))
         # one rank: each type's EVs sorted once by charge level, the partitions' statistics from that
         # order (both types in one host sync); the layout the price loops need comes with it
+        if self.replicated:
+            self._gather_levels()  # (the step's one exchange of levels: every rank then sees every EV)
         sl = self._sorted_layouts()
-        st_s = sl["Small"] if sl and "Small" in sl else partition_stats(self.y_s, self.idx_s, self.P, self.group)
-        st_l = sl["Large"] if sl and "Large" in sl else partition_stats(self.y_l, self.idx_l, self.P, self.group)
+
+        def index_stats(kind):  # a type the sorted layout left out: the index path
+            if self.replicated:
+                self._idxfull[kind] = self._gather_idx(kind)  # (for _partition_layout too)
+                return partition_stats(self._yfull[kind], self._idxfull[kind], self.P)
+            y, idx = self._loop_levels(kind)
+            return partition_stats(y, idx, self.P, self.group)
+
+        st_s = sl["Small"] if sl and "Small" in sl else index_stats("Small")
+        st_l = sl["Large"] if sl and "Large" in sl else index_stats("Large")
         for p in range(self.P):
             Mp_s[p] = int(st_s[p, 0])
             if Mp_s[p] > 0:
@@ -410,8 +519,8 @@ class ChargingStation:
         prices_s, prices_l = np.zeros((self.P, self.r)), np.zeros((self.P, self.r))
         stats_s, stats_l = [], []
         st_s, st_l = self._pstats
-        chains = (("Small", self.price_solver_s, self.y_s, self.idx_s, st_s, w_hat_s_opt, prices_s, stats_s),
-                  ("Large", self.price_solver_l, self.y_l, self.idx_l, st_l, w_hat_l_opt, prices_l, stats_l))
+        chains = (("Small", self.price_solver_s, *self._loop_levels("Small"), st_s, w_hat_s_opt, prices_s, stats_s),
+                  ("Large", self.price_solver_l, *self._loop_levels("Large"), st_l, w_hat_l_opt, prices_l, stats_l))
         for kind, _, y, idx, *_ in chains:  # (on this thread: the layouts' host sync)
             self._partition_layout(kind, y, idx)
 
@@ -444,7 +553,7 @@ class ChargingStation:
             else:
                 stats.append({})
 
-        if PRINT_LEVEL == 0 and self.group is None:
+        if PRINT_LEVEL == 0 and not self._exchange:
             torch = _torch()
             main = torch.cuda.current_stream(self.device)
 
@@ -516,10 +625,9 @@ class ChargingStation:
         st_s, st_l = self._pstats
         main = torch.cuda.current_stream(self.device)
         jobs = []
-        for kind, solver, y, idx, st in (("Small", self.price_solver_s, self.y_s, self.idx_s, st_s),
-                                         ("Large", self.price_solver_l, self.y_l, self.idx_l, st_l)):
+        for kind, solver, st in (("Small", self.price_solver_s, st_s), ("Large", self.price_solver_l, st_l)):
             solver._stream.wait_stream(main)  # (the state the layout sorts is the main stream's)
-            jobs.append((kind, solver, y, idx, st))
+            jobs.append((kind, solver, *self._loop_levels(kind), st))
 
         def stage(job):
             kind, solver, y, idx, st = job
@@ -534,7 +642,7 @@ class ChargingStation:
                         solver.stage_partition(p, ys[a:b], st[p, 0], st[p, 1], st[p, 2], st[p, 3], descending=True,
                                                gamma_view=None if gam is None else gam[at[p][0]:at[p][1]])
 
-        if self.group is not None:
+        if self._exchange:  # (every rank creates its plans' device communicators in the same order)
             for job in jobs:
                 stage(job)
             return []
@@ -593,7 +701,9 @@ class ChargingStation:
         lib = _lib.load()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         parts, recs = [], []
-        for kind, y, rng in (("Small", self.y_s, self.y0_s_rng), ("Large", self.y_l, self.y0_l_rng)):
+        group = None if self.replicated else self.group  # (replicated: the whole population is here)
+        for kind, rng in (("Small", self.y0_s_rng), ("Large", self.y0_l_rng)):
+            y = self._loop_levels(kind)[0]
             n = int(y.numel())
             b = self._bounds.get(id(rng))
             if b is None:
@@ -632,15 +742,15 @@ class ChargingStation:
                 parts.append((kind, lv["ys"], lv["perm"]))
             recs.append(lv["stats"])
         rec = torch.stack(recs)  # (2, 4P + 4)
-        if self.group is None:
+        if group is None:
             h = rec.cpu().numpy()[None]  # the one host sync
         else:
             import torch.distributed as dist
 
-            world = dist.get_world_size(self.group)
+            world = dist.get_world_size(group)
             # (the concatenated output form: gloo rejects the stacked (world, ...) one)
             allr = torch.empty((world * rec.shape[0], rec.shape[1]), dtype=rec.dtype, device=rec.device)
-            dist.all_gather_into_tensor(allr, rec.contiguous(), group=self.group)
+            dist.all_gather_into_tensor(allr, rec.contiguous(), group=group)
             h = allr.view(world, *rec.shape).cpu().numpy()  # the one host sync
         out = {}
         for j, (kind, ys, perm) in enumerate(parts):
@@ -656,7 +766,7 @@ class ChargingStation:
             lo, hi = rows[0, 4 * P + 2], rows[0, 4 * P + 3]
             if not (ymin >= lo and ymax <= hi):  # (NaN fails too; every rank decides the same)
                 continue
-            mine = dist.get_rank(self.group) if self.group is not None else 0
+            mine = dist.get_rank(group) if group is not None else 0
             cnt = rows[mine, : 4 * P].reshape(P, 4)[:, 0].astype(np.int64)  # this rank's runs
             ends = np.cumsum(cnt[::-1])  # runs in storage order, partition P-1 first
             seg = {p: (int(ends[k] - cnt[p]), int(ends[k])) for k, p in enumerate(range(P - 1, -1, -1))}
@@ -689,6 +799,8 @@ class ChargingStation:
                 raise RuntimeError(_lib.status_text(lib, None, rc))
             self._layout[kind] = (lv["perm"], lv["ys"], seg)
         if kind not in self._layout:
+            if idx is None:  # (replicated: the whole population's indices, gathered by index_stats)
+                idx = self._idxfull[kind]
             # (partition, -y) order exactly: a stable sort by descending y, then a stable sort by
             # partition (a composite float key would round near-equal charge levels out of order)
             by_y = torch.argsort(y, descending=True, stable=True)
@@ -713,7 +825,7 @@ class ChargingStation:
         invalid) combined over ranks — `_w0_checked` reads and checks them)."""
         torch = _torch()
         N, P = self.N_lo, self.P
-        perm, ys, seg = self._partition_layout(kind, y, idx)
+        perm, ys, seg = self._w0_layouts()[kind] if self.replicated else self._partition_layout(kind, y, idx)
         # the sets in layout order (each partition's run of EVs; _sorted_layouts stores partition P-1
         # first): set k = partition order[k]
         order = sorted(range(P), key=lambda p: seg[p])
@@ -760,7 +872,7 @@ class ChargingStation:
         for t, (kind, solver, y, idx, prices) in enumerate(
                 (("Small", self.price_solver_s, self.y_s, self.idx_s, prices_s),
                  ("Large", self.price_solver_l, self.y_l, self.idx_l, prices_l))):
-            perm, ys, seg = self._partition_layout(kind, y, idx)
+            perm, ys, seg = self._w0_layouts()[kind] if self.replicated else self._partition_layout(kind, y, idx)
             order = sorted(range(P), key=lambda p: seg[p])  # set t P + k = partition order[k]
             gams.append(solver.consts.y_max - ys)
             offs += [offs[-1] - seg[order[0]][0] + seg[p][1] for p in order]

@@ -51,6 +51,14 @@ for s in $STEPS; do
     r5new) run r5new 600 $PYT tests/test_gpu_chain.py tests/test_gpu_price_loop_c5.py tests/test_gpu_levels.py -m gpu ;;
     stationt) run stationt 600 $PYT tests/test_gpu_station.py tests/test_gpu_example.py -m gpu ;;
     benchq) run benchq 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-station --no-direct ;;
+    # round 6
+    syncmodes) P="python -u scripts/step_probe.py --cells 4 --steps 20 --reps 8 --warmup 5 --gpu-span"
+               run sync_default 200 $P; run sync_spin 200 $P --spin
+               run sync_active 200 env ROC_ACTIVE_WAIT_TIMEOUT=100000 $P ;;
+    cells100) run cells100 300 python -u scripts/step_probe.py --cells 4 8 12 --steps 100 --reps 5 --warmup 10 ;;
+    stationt6) run stationt6 600 $PYT tests/test_gpu_station.py tests/test_gpu_levels.py -m gpu ;;
+    bdistst) run bdistst 600 python bench.py --force-dist --steps 20 --warmup 5 --no-cpu-baseline --no-direct --no-contracts ;;
+    bst) run bst 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-direct --no-contracts ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -29,7 +29,15 @@ ap.add_argument("--evs", type=int, default=262144)
 ap.add_argument("--warmup", type=int, default=0, help="warmup call's runs (0: --steps)")
 ap.add_argument("--gpu-span", action="store_true", help="torch events around each timed call")
 ap.add_argument("--idle-ms", type=float, default=0.0, help="host sleep before each timed call (GPU idle)")
+ap.add_argument("--warm-events", action="store_true", help="the warmup call carries the span events")
+ap.add_argument("--spin", action="store_true", help="hipSetDeviceFlags(hipDeviceScheduleSpin) before torch")
 args = ap.parse_args()
+
+if args.spin:
+    import ctypes
+
+    _hip = ctypes.CDLL("libamdhip64.so")
+    print("hipSetDeviceFlags(spin):", _hip.hipSetDeviceFlags(1), flush=True)
 
 import torch  # noqa: E402
 
@@ -56,7 +64,10 @@ for libname in args.libs:
     for cells in args.cells:
         plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], w_ref=wr, want_w=args.outputs == "full",
                          want_cost=args.outputs != "set", cells=cells or None)
-        plan.run_steps(lm, lr, args.warmup or K, lm[0].numel(), lr[0].numel(), per_run_sets=True)
+        if args.warm_events:
+            plan.profile(enable=("k_eval",))
+        plan.run_steps(lm, lr, args.warmup or K, lm[0].numel(), lr[0].numel(), per_run_sets=True,
+                       span_events=args.warm_events)
         plan.check()
         walls, ks, spans = [], [], []
         go, _ = plan.steps_call(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, span_events=True)

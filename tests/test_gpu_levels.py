@@ -33,6 +33,7 @@ def test_sorted_layouts_match_index_partitions(gpu, case):
         y_l[min(7, n_l - 1)] = 0.2  # below rng[0]: the large type takes the index path
     cs = object.__new__(ChargingStation)
     cs.P, cs.group, cs.device = P, None, 0
+    cs.replicated, cs._exchange = False, False
     cs.y_s, cs.y_l = torch.as_tensor(y_s, device="cuda:0"), torch.as_tensor(y_l, device="cuda:0")
     cs.y0_s_rng, cs.y0_l_rng = rng_s, rng_l
     cs.idx_s = torch.zeros(n_s, dtype=torch.int64, device="cuda:0")
@@ -91,6 +92,7 @@ def test_gamma_layout_matches_per_partition_batches(gpu, rank):
     y[:10] = rng_s[rs.integers(0, 7, 10)]
     cs = object.__new__(ChargingStation)
     cs.P, cs.group, cs.device = P, None, 0
+    cs.replicated, cs._exchange = False, False
     cs.y_s, cs.y_l = torch.as_tensor(y, device="cuda:0"), torch.as_tensor(y[:5000].copy(), device="cuda:0")
     cs.y0_s_rng, cs.y0_l_rng = rng_s, rng_s
     cs.idx_s = torch.zeros(len(y), dtype=torch.int64, device="cuda:0")
@@ -126,6 +128,7 @@ def test_levels_stats_nan_fails_the_range_check(gpu, where):
     y[where] = np.nan
     cs = object.__new__(ChargingStation)
     cs.P, cs.group, cs.device = P, None, 0
+    cs.replicated, cs._exchange = False, False
     cs.y_s, cs.y_l = torch.as_tensor(y, device="cuda:0"), torch.as_tensor(y[:5000].copy(), device="cuda:0")
     cs.y_l[:] = 0.5  # (the large type: no NaN)
     cs.y0_s_rng, cs.y0_l_rng = rng_s, rng_s

@@ -85,7 +85,7 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, M_2, q):
+def _rank(rank, world, port, M_2, q, mode):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -99,9 +99,12 @@ def _rank(rank, world, port, M_2, q):
         settings.PRINT_LEVEL = 0
         torch.cuda.set_device(0)
         np.random.seed(5)
-        cs = ChargingStation(consts(M_2, Tf=2), device=0, group=dist.group.WORLD)
+        cs = ChargingStation(consts(M_2, Tf=2), device=0, group=dist.group.WORLD, sharded_loops=mode)
+        assert cs.replicated == (mode == "replicated")
+        assert cs.price_solver_s.device_loop == (mode == "replicated")  # (no collective inside a loop)
         logs = cs.simulate()
-        q.put((rank, logs["inputs"], logs["prices"], logs["statistics"], logs["states"]["x"], cs.y_s.cpu().numpy()))
+        q.put((rank, logs["inputs"], logs["prices"], logs["statistics"], logs["states"]["x"], cs.y_s.cpu().numpy(),
+               logs["bounds"]))
         dist.barrier()
         dist.destroy_process_group()
     except BaseException:
@@ -109,10 +112,15 @@ def _rank(rank, world, port, M_2, q):
         raise
 
 
-def test_sharded_loop_matches_single_process(gpu, monkeypatch):
+@pytest.mark.parametrize("mode", ["replicated", "exchange"])
+def test_sharded_loop_matches_single_process(gpu, monkeypatch, mode):
     """Two EV shards (gloo over device tensors, both ranks on cuda:0) give the single-process
-    trajectory: partition statistics, fused reductions, price0 sums, aggregate demand and
-    the globally ordered full-charge re-draws are combined across ranks."""
+    trajectory: partition statistics, price0 sums, aggregate demand and the globally ordered
+    full-charge re-draws are combined across ranks.  ``replicated`` (the default): one all-gather of
+    the levels per step, every price loop on every rank (the device loop, no collective inside it):
+    the first step's statistics, BiMPC plan, iteration counts and price reductions equal the single
+    process's bit for bit (later steps: the w0 sums' order, to rounding).  ``exchange``: one
+    all-gather of the set reductions per price iteration."""
     import torch.multiprocessing as mp
 
     monkeypatch.setattr(settings, "PRINT_LEVEL", 0)
@@ -122,7 +130,7 @@ def test_sharded_loop_matches_single_process(gpu, monkeypatch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, M_2, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, M_2, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     outs = []
@@ -134,7 +142,13 @@ def test_sharded_loop_matches_single_process(gpu, monkeypatch):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    for _, inputs, prices, stats, x, _ in outs:
+    for _, inputs, prices, stats, x, _, bounds in outs:
+        if mode == "replicated":  # step 0 bit for bit: statistics, BiMPC plan, loops
+            for sec, k in (("inputs", "w_hat_s"), ("inputs", "w_hat_l"), ("inputs", "u_g"), ("prices", "price_red_s"),
+                           ("prices", "price_red_l"), ("statistics", "gamma_sm"), ("statistics", "gamma_lm"),
+                           ("bounds", "beta_s"), ("bounds", "beta_l")):
+                got = {"inputs": inputs, "prices": prices, "statistics": stats, "bounds": bounds}[sec][k]
+                np.testing.assert_array_equal(np.asarray(got)[..., 0], np.asarray(ref[sec][k])[..., 0], err_msg=k)
         for k in ("w_s", "w_l", "w_hat_s", "w_hat_l", "u_g"):
             np.testing.assert_allclose(inputs[k], ref["inputs"][k], rtol=0, atol=1e-9, err_msg=k)
         for k in ("avg_price_s", "avg_price_l"):

@@ -120,3 +120,69 @@ def test_update_indices_matches_reference_loop_on_edges():
         assert np.array_equal(cs.idx_s.numpy(), _ref_indices(y, rng, idx0)), rng
         assert np.array_equal(cs.idx_l.numpy(), _ref_indices(y[::-1], rng, idx0[::-1])), rng
 
+
+
+def _rank_rep(rank, world, port, ys_all, yl_all, P, q):
+    """Replicated sharding's host logic on CPU tensors: the levels' all-gather and this rank's EVs in
+    the whole population's layout order (ChargingStation._gather_levels / _w0_layouts)."""
+    from lompc_amd.charging_station import ChargingStation
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cs = object.__new__(ChargingStation)
+    cs.group, cs.M_2, cs.P, cs._dev = dist.group.WORLD, len(ys_all), P, "cpu"
+    cs._lo, cs._hi = shard_bounds(cs.M_2, rank, world)
+    cs.y_s = torch.as_tensor(ys_all[cs._lo:cs._hi].copy())
+    cs.y_l = torch.as_tensor(yl_all[cs._lo:cs._hi].copy())
+    cs.replicated, cs._exchange = True, False
+    cs._layout, cs._pending, cs._layout_w0 = {}, {}, {}
+    ChargingStation._gather_levels(cs)
+    full = {k: v.numpy().copy() for k, v in cs._yfull.items()}
+    rng = np.linspace(0.3, 0.9, P + 1)
+    cs._idxfull = {k: (torch.searchsorted(torch.as_tensor(rng), cs._yfull[k], right=True) - 1).clamp_(0, P - 1)
+                   for k in ("Small", "Large")}
+    lay = ChargingStation._w0_layouts(cs)
+    q.put((rank, full, {k: (v[0].numpy(), v[1].numpy(), v[2]) for k, v in lay.items()},
+           {k: cs._layout[k][2] for k in cs._layout}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_replicated_levels_and_local_layout_world2():
+    """world 2 (unequal shards): every rank holds the whole population's levels in EV order after the
+    one all-gather, and its w0 layout is exactly its own EVs in the loops' layout order (partition runs
+    in descending charge level), each run bounded by this rank's count in that partition."""
+    rng = np.random.default_rng(7)
+    n, P = 53, 6
+    ys_all, yl_all = 0.3 + 0.6 * rng.random(n), 0.3 + 0.6 * rng.random(n)
+    ys_all[5] = ys_all[9]  # (a tie)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_rank_rep, args=(r, 2, port, ys_all, yl_all, P, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=120) for _ in range(2)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    edges = np.linspace(0.3, 0.9, P + 1)
+    for rank, full, lay, seg_full in outs:
+        np.testing.assert_array_equal(full["Small"], ys_all)
+        np.testing.assert_array_equal(full["Large"], yl_all)
+        lo, hi = shard_bounds(n, rank, 2)
+        for kind, y_all in (("Small", ys_all), ("Large", yl_all)):
+            lperm, lys, seg = lay[kind]
+            assert sorted(lperm.tolist()) == list(range(hi - lo))
+            np.testing.assert_array_equal(lys, y_all[lo:hi][lperm])
+            part = np.clip(np.searchsorted(edges, y_all, side="right") - 1, 0, P - 1)
+            for p in range(P):
+                a, b = seg[p]
+                got = lperm[a:b] + lo
+                want = np.nonzero(part[lo:hi] == p)[0] + lo
+                assert sorted(got.tolist()) == want.tolist(), (kind, p)
+                assert np.all(np.diff(lys[a:b]) <= 0)
+                # the same EVs in the same order as the whole layout's run, restricted to this rank
+                fa, fb = seg_full[kind][p]
+                assert fb - fa == (part == p).sum()

@@ -203,45 +203,78 @@ class BlockPool {
   std::atomic<bool> stop_{false};
 };
 
-// In-place lower Cholesky of the 2N x 2N coupling matrix W (row-major; the upper triangle is
-// not read), right-looking: column j is scaled, copied to a contiguous vector, and every row
-// below takes one contiguous axpy (AVX2 / FMA vectorised), n^3 / 6 FMAs.  ~10x faster at
-// n = 96 than the blocked dot-product form with the worker pool, whose short dots and
-// parallel regions cost more than the arithmetic at these sizes.
-static bool chol_rl(double* a, int m, double* col) {
-  for (int j = 0; j < m; ++j) {
-    double* aj = a + (size_t)j * m;
-    const double s = aj[j];
-    if (!(s > 0.0)) return false;
-    const double d = std::sqrt(s), inv = 1.0 / d;
-    aj[j] = d;
-    for (int i = j + 1; i < m; ++i) {
-      const double l = a[(size_t)i * m + j] * inv;
-      a[(size_t)i * m + j] = l;
-      col[i] = l;
+// In-place Cholesky W = U'U of the 2N x 2N coupling matrix (row-major; U in the upper triangle,
+// the lower one not read), right-looking in panels of 4 rows: row j of U is contiguous, so the
+// panel's rows are scaled and updated along rows, and every trailing row then takes ONE rank-4
+// update from the panel — four FMAs per element loaded and stored instead of one, every loop
+// contiguous (AVX2 / FMA along the row), n^3 / 6 FMAs in all.
+static bool chol_upper(double* a, int m) {
+  for (int j0 = 0; j0 < m; j0 += 4) {
+    const int je = std::min(m, j0 + 4);
+    for (int j = j0; j < je; ++j) {  // the panel's rows: U_j = a_j / sqrt(a_jj); later panel rows updated
+      double* aj = a + (size_t)j * m;
+      const double s = aj[j];
+      if (!(s > 0.0)) return false;
+      const double d = std::sqrt(s), inv = 1.0 / d;
+      aj[j] = d;
+      for (int k = j + 1; k < m; ++k) aj[k] *= inv;
+      for (int i = j + 1; i < je; ++i) {
+        double* ai = a + (size_t)i * m;
+        const double u = aj[i];
+        for (int k = i; k < m; ++k) ai[k] -= u * aj[k];
+      }
     }
-    for (int i = j + 1; i < m; ++i) {
+    const int jb = je - j0;
+    if (je >= m) break;
+    const double* p0 = a + (size_t)j0 * m;  // the panel's rows of U
+    for (int i = je; i < m; ++i) {  // trailing rows: a_ik -= sum_q U_qi U_qk, k >= i
       double* ai = a + (size_t)i * m;
-      const double li = col[i];
-      for (int k = j + 1; k <= i; ++k) ai[k] -= li * col[k];
+      if (jb == 4) {
+        const double* p1 = p0 + m;
+        const double* p2 = p1 + m;
+        const double* p3 = p2 + m;
+        const double u0 = p0[i], u1 = p1[i], u2 = p2[i], u3 = p3[i];
+        for (int k = i; k < m; ++k) ai[k] -= (u0 * p0[k] + u1 * p1[k]) + (u2 * p2[k] + u3 * p3[k]);
+      } else {
+        for (int q = 0; q < jb; ++q) {
+          const double* pq = p0 + (size_t)q * m;
+          const double u = pq[i];
+          for (int k = i; k < m; ++k) ai[k] -= u * pq[k];
+        }
+      }
     }
   }
   return true;
+}
+
+// U'U x = b in place with the factor of chol_upper: U'y = b by row updates (row k of U scatters
+// y_k into the later entries), then U x = y by row dots — every access contiguous
+static void chol_upper_solve(const double* U, int m, double* b) {
+  for (int k = 0; k < m; ++k) {
+    const double* uk = U + (size_t)k * m;
+    const double y = b[k] / uk[k];
+    b[k] = y;
+    for (int i = k + 1; i < m; ++i) b[i] -= uk[i] * y;
+  }
+  for (int i = m - 1; i >= 0; --i) {
+    const double* ui = U + (size_t)i * m;
+    b[i] = (b[i] - lqd::dot(ui + i + 1, b + i + 1, m - i - 1)) / ui[i];
+  }
 }
 
 struct Newton {
   int N = 0, nb = 0, n = 0;
   std::vector<double> Du;   // [N]
   std::vector<double> Q;    // [N*N]
-  std::vector<double> W;    // [2N*2N] Cholesky of D2^-1 + F T F'
+  std::vector<double> W;    // [2N*2N] D2^-1 + F T F' = U'U (U upper, row-major)
   std::vector<double> ck;
-  std::vector<double> Xk;   // [nb][N*N] T_k^-1 (H_k^-1 = A^-1 T_k^-1 A^-T)
-  std::vector<double> Lf, Df;  // [N][nb] LDL' factors of the T_k, stage-major (hb_solve)
+  std::vector<double> S;    // [N*N] sum_k c_k^2 T_k^-1 (H_k^-1 = A^-1 T_k^-1 A^-T)
+  std::vector<double> Lf, Df, Di;  // [N][nb] LDL' factors of the T_k (Di = 1 / Df), stage-major (hb_solve)
+  std::vector<double> row, dd, ll;  // factor() scratch
   mutable std::vector<double> hb_tmp;
   mutable std::vector<double> sv_r, sv_c, sv_trial;                                  // solve()
   mutable std::vector<double> sr_t1, sr_y, sr_fy, sr_g, sr_tmp;                      // solve_reg()
   mutable std::vector<double> ap_r, ap_Lx, ap_Qy, ap_tmp;                            // apply()
-  std::vector<double> chol_col;
 
   // factor M for the current iterate; dbox: [n] box barrier diagonal, dg: [4N] coupling D_g.
   //
@@ -255,18 +288,25 @@ struct Newton {
   // is W = D_2^-1 + F T F' (2N x 2N) — the same Newton step as the 4N form at 1/8 of its
   // Cholesky.  An active row (D_g -> inf) keeps F T F'; inactive rows become a large diagonal.
   bool factor(const Bimpc& B, const double* z, const double* dbox, const double* dg) {
+#ifdef LQ_BIMPC_PROF
+    const double tf_start = nowus();
+#endif
     N = B.N;
     nb = B.nb;
     n = B.n;
     ck = B.ck;
-    Xk.resize((size_t)nb * N * N);
     Lf.resize((size_t)nb * N);
     Df.resize((size_t)nb * N);
-    std::vector<double> T((size_t)N * N, 0.0);
-    std::vector<char> okk(nb, 1);
-    BlockPool::get().run(nb, [&](int k) {
-      double* X = &Xk[(size_t)k * N * N];
-      std::vector<double> dd(N), l(N);
+    Di.resize((size_t)nb * N);
+    S.assign((size_t)N * N, 0.0);
+    row.resize(N);
+    dd.resize(N);
+    ll.resize(N);
+    // S = sum_k c_k^2 T_k^-1 (upper triangle), block by block in block order; T_k^-1 row by row from
+    // the LDL' factors: X_jj = 1/d_j + l_j^2 X_{j+1,j+1} and, right of the diagonal, row i = -l_i x
+    // row i+1 (L'X = D^-1 L^-1 is lower triangular) — ONE row buffer per block, scaled in place and
+    // added into S (no N x N inverse per block is stored)
+    for (int k = 0; k < nb; ++k) {
       // static regularisation (the EXP weights 5^(t-N+1) leave early steps with almost no
       // curvature); iterative refinement against the exact matrix removes its bias
       double s = 0.0;
@@ -279,87 +319,101 @@ struct Newton {
         const double Dn = t + 1 < N ? dbox[k * N + t + 1] + rho : 0.0;
         double a = 2.0 * B.delta * B.omega[k * N + t] + Dt + Dn;
         if (t > 0) a -= prev_l * prev_l * prev_d;
-        if (!(a > 0.0)) {
-          okk[k] = 0;
-          return;
-        }
-        dd[t] = a;
-        l[t] = t + 1 < N ? -Dn / a : 0.0;  // L_{t+1,t}
+        if (!(a > 0.0)) return false;
+        const double ia = 1.0 / a;  // (one division per stage)
+        dd[t] = ia;
+        ll[t] = t + 1 < N ? -Dn * ia : 0.0;  // L_{t+1,t}
         Df[(size_t)t * nb + k] = a;
-        Lf[(size_t)t * nb + k] = l[t];
-        prev_l = l[t];
+        Di[(size_t)t * nb + k] = ia;
+        Lf[(size_t)t * nb + k] = ll[t];
+        prev_l = ll[t];
         prev_d = a;
       }
-      // X = T_k^-1 from the LDL' factors: X_jj = 1/d_j + l_j^2 X_{j+1,j+1} and, above the
-      // diagonal, row i = -l_i x row i+1 (L'X = D^-1 L^-1 is lower triangular); rows are
-      // independent vector operations, no per-column substitution chains.  Upper triangle only:
-      // the sum below mirrors it once.
-      X[(size_t)(N - 1) * N + N - 1] = 1.0 / dd[N - 1];
-      for (int i = N - 2; i >= 0; --i) {
-        double* xi = X + (size_t)i * N;
-        const double* x1 = xi + N;
-        const double li = l[i];
-        for (int j = i + 1; j < N; ++j) xi[j] = -li * x1[j];
-        xi[i] = 1.0 / dd[i] + li * li * x1[i + 1];
-      }
-    });
-    for (int k = 0; k < nb; ++k) {
-      if (!okk[k]) return false;
       if (ck[k] == 0.0) continue;
-      const double c2 = ck[k] * ck[k];  // sum c_k^2 T_k^-1, in block order
-      const double* X = &Xk[(size_t)k * N * N];
-      for (int i = 0; i < N; ++i)
-        for (int j = i; j < N; ++j) T[(size_t)i * N + j] += c2 * X[(size_t)i * N + j];
+      const double c2 = ck[k] * ck[k];
+      double* r = row.data();
+      r[N - 1] = dd[N - 1];
+      S[(size_t)(N - 1) * N + N - 1] += c2 * r[N - 1];
+      for (int i = N - 2; i >= 0; --i) {
+        const double li = ll[i];
+        const double diag = dd[i] + li * li * r[i + 1];  // (dd: 1 / d)
+        for (int j = i + 1; j < N; ++j) r[j] *= -li;
+        r[i] = diag;
+        double* si = &S[(size_t)i * N];
+        for (int j = i; j < N; ++j) si[j] += c2 * r[j];
+      }
     }
+#ifdef LQ_BIMPC_PROF
+    double tq = nowus();
+    t_fx += tq - tf_start;
+#endif
     for (int i = 1; i < N; ++i)  // lower triangle by symmetry
-      for (int j = 0; j < i; ++j) T[(size_t)i * N + j] = T[(size_t)j * N + i];
-    // T = A^-1 (sum c_k^2 T_k^-1) A^-T: differences along the columns, then along the rows
-    for (int i = N - 1; i > 0; --i)
-      for (int j = 0; j < N; ++j) T[(size_t)i * N + j] -= T[(size_t)(i - 1) * N + j];
-    for (int i = 0; i < N; ++i)
-      for (int j = N - 1; j > 0; --j) T[(size_t)i * N + j] -= T[(size_t)i * N + j - 1];
+      for (int j = 0; j < i; ++j) S[(size_t)i * N + j] = S[(size_t)j * N + i];
     Du.assign(N, 0.0);
     for (int t = 0; t < N; ++t) {
       const double u = z[nb * N + t];
       Du[t] = 1.19 * B.c_g * std::pow(u, -0.3) + dbox[nb * N + t];  // f'' of c_g u^1.7
       if (!(Du[t] > 0.0)) return false;
-      T[t * N + t] += 1.0 / Du[t];
     }
     // Q = E' D_g E = diag(d0 + d1) + A' diag(d2 + d3) A  (apply() uses the exact matrix)
     Q.assign((size_t)N * N, 0.0);
     {
       double s = 0.0;
-      std::vector<double> suf(N);
+      std::vector<double>& suf = row;
       for (int t = N - 1; t >= 0; --t) {
         s += dg[2 * N + t] + dg[3 * N + t];
         suf[t] = s;
       }
-      for (int i = 0; i < N; ++i)
-        for (int j = 0; j < N; ++j) Q[i * N + j] = suf[std::max(i, j)];
-      for (int i = 0; i < N; ++i) Q[i * N + i] += dg[i] + dg[N + i];
-    }
-    // W = D_2^-1 + F T F' with F = [I; A]: blocks T, T A', A T, A T A'
-    const int m = 2 * N;
-    std::vector<double> AT((size_t)N * N);  // (A T)_ij = sum_{u <= i} T_uj
-    for (int i = 0; i < N; ++i)
-      for (int j = 0; j < N; ++j) AT[(size_t)i * N + j] = T[(size_t)i * N + j] + (i ? AT[(size_t)(i - 1) * N + j] : 0.0);
-    W.assign((size_t)m * m, 0.0);
-    for (int i = 0; i < N; ++i) {
-      double acc = 0.0;
-      for (int j = 0; j < N; ++j) {
-        W[(size_t)i * m + j] = T[(size_t)i * N + j];
-        W[(size_t)i * m + N + j] = AT[(size_t)j * N + i];          // (T A')_ij = (A T)_ji
-        W[(size_t)(N + i) * m + j] = AT[(size_t)i * N + j];
-        acc += AT[(size_t)i * N + j];                              // (A T A')_ij = sum_{u<=j} (A T)_iu
-        W[(size_t)(N + i) * m + N + j] = acc;
+      for (int i = 0; i < N; ++i) {
+        double* qi = &Q[(size_t)i * N];
+        for (int j = 0; j < i; ++j) qi[j] = suf[i];
+        for (int j = i; j < N; ++j) qi[j] = suf[j];
+        qi[i] += dg[i] + dg[N + i];
       }
     }
+    // W = D_2^-1 + F T F' with F = [I; A] and T = A^-1 S A^-T + D^-1 (D = Du, the u_g block):
+    //   T A'   = A^-1 S + D^-1 A'     (A^-1: differences down the columns; (D^-1 A')_ij = 1/Du_i, j >= i)
+    //   A T A' = S + A D^-1 A'       ((A D^-1 A')_ij = sum_{u <= min(i, j)} 1/Du_u)
+    // straight from S: no prefix sums of differences (the same matrix, fewer roundings)
+    const int m = 2 * N;
+    W.assign((size_t)m * m, 0.0);
+    std::vector<double>& cum = dd;  // cumulative 1/Du
+    {
+      double c = 0.0;
+      for (int t = 0; t < N; ++t) cum[t] = (c += 1.0 / Du[t]);
+    }
+    for (int i = 0; i < N; ++i) {
+      const double* si = &S[(size_t)i * N];
+      const double* sp = i ? si - N : nullptr;
+      double* w1 = &W[(size_t)i * m];       // row i:     [T | T A']
+      double* w2 = &W[(size_t)(N + i) * m];  // row N + i: [A T | A T A']
+      const double du = 1.0 / Du[i];
+      for (int j = 0; j < N; ++j) {
+        const double m0 = si[j] - (sp ? sp[j] : 0.0);  // (A^-1 S)_ij
+        w1[N + j] = m0 + (j >= i ? du : 0.0);
+        w2[N + j] = si[j] + cum[std::min(i, j)];
+      }
+      for (int j = 0; j < N; ++j) {  // T_ij = (A^-1 S)_ij - (A^-1 S)_i(j-1), + 1/Du on the diagonal
+        const double m0 = si[j] - (sp ? sp[j] : 0.0);
+        const double m1 = j ? si[j - 1] - (sp ? sp[j - 1] : 0.0) : 0.0;
+        w1[j] = m0 - m1 + (j == i ? du : 0.0);
+      }
+    }
+    for (int i = 0; i < N; ++i)  // A T = (T A')'
+      for (int j = 0; j < N; ++j) W[(size_t)(N + i) * m + j] = W[(size_t)j * m + N + i];
     for (int t = 0; t < N; ++t) {
       W[(size_t)t * m + t] += 1.0 / (dg[t] + dg[N + t]);
       W[(size_t)(N + t) * m + N + t] += 1.0 / (dg[2 * N + t] + dg[3 * N + t]);
     }
-    chol_col.resize(m);
-    return chol_rl(W.data(), m, chol_col.data());
+#ifdef LQ_BIMPC_PROF
+    const double tc = nowus();
+    t_fasm += tc - tq;
+    const bool okc = chol_upper(W.data(), m);
+    t_fch += nowus() - tc;
+    return okc;
+#else
+    return chol_upper(W.data(), m);
+#endif
   }
 
   void hb_solve(double* x) const {  // Hb^-1 in place
@@ -378,7 +432,7 @@ struct Newton {
       const double* lp = &Lf[(size_t)(t - 1) * nb];
       for (int k = 0; k < nb; ++k) vt[k] -= lp[k] * vp[k];
     }
-    for (size_t e = 0; e < (size_t)N * nb; ++e) v[e] /= Df[e];
+    for (size_t e = 0; e < (size_t)N * nb; ++e) v[e] *= Di[e];
     for (int t = N - 2; t >= 0; --t) {  // L' u = D^-1 w
       double* vt = v + (size_t)t * nb;
       const double* vn = vt + nb;
@@ -421,6 +475,13 @@ struct Newton {
     for (int i = 0; i < n; ++i) y[i] += tmp[i];
   }
 
+#ifdef LQ_BIMPC_PROF
+  mutable int n_solve = 0, n_reg = 0, n_apply = 0;
+  mutable double t_hb = 0, t_chs = 0, t_app = 0, t_fx = 0, t_fasm = 0, t_fch = 0;
+  static double nowus() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+#endif
   // M dz = rhs: regularised Schur solve + iterative refinement against apply()
   void solve(const Bimpc& B, const double* dbox, const double* rhs, double* dz) const {
     // refinement stops as soon as it stops reducing the residual: in the nearly flat directions
@@ -432,8 +493,20 @@ struct Newton {
     r.resize(n);
     c.resize(n);
     trial.resize(n);
+#ifdef LQ_BIMPC_PROF
+    ++n_solve;
+#endif
     auto resid = [&](const double* x) {
+#ifdef LQ_BIMPC_PROF
+      ++n_apply;
+#endif
+#ifdef LQ_BIMPC_PROF
+      const double ta = nowus();
+#endif
       apply(B, dbox, x, r.data());
+#ifdef LQ_BIMPC_PROF
+      t_app += nowus() - ta;
+#endif
       double nr = 0.0;
       for (int i = 0; i < n; ++i) {
         r[i] = rhs[i] - r[i];
@@ -444,11 +517,19 @@ struct Newton {
     double rn = 0.0;
     for (int i = 0; i < n; ++i) rn = std::max(rn, std::fabs(rhs[i]));
     double best = resid(dz);
-    // a residual at the rounding floor of the right-hand side cannot be halved: no pass then
-    for (int pass = 0; pass < 4 && best > 1e-14 * rn; ++pass) {
+#ifdef LQ_BIMPC_PROF
+    if (getenv("LQ_BIMPC_RES")) fprintf(stderr, "solve %d: initial residual %.2e of rhs\n", n_solve, best / rn);
+#endif
+    // a residual 1e-12 of the right-hand side is far below what a Newton direction needs (the
+    // early iterations' regularised solves land there: no pass then); the passes matter late, where
+    // the exp weights' flat directions leave the regularised solve 1e-9 .. 1e-2 off
+    for (int pass = 0; pass < 4 && best > 1e-12 * rn; ++pass) {
       solve_reg(B, r.data(), c.data());
       for (int i = 0; i < n; ++i) trial[i] = dz[i] + c[i];
       const double nr = resid(trial.data());
+#ifdef LQ_BIMPC_PROF
+      if (getenv("LQ_BIMPC_RES")) fprintf(stderr, "   pass %d: %.2e\n", pass, nr / rn);
+#endif
       if (!(nr < 0.5 * best)) break;
       best = nr;
       std::copy(trial.begin(), trial.end(), dz);
@@ -456,27 +537,46 @@ struct Newton {
   }
 
   void solve_reg(const Bimpc& B, const double* rhs, double* dz) const {
+#ifdef LQ_BIMPC_PROF
+    ++n_reg;
+#endif
     sr_t1.assign(rhs, rhs + n);
     sr_y.resize(N);
     sr_fy.resize(2 * N);
     sr_g.resize(N);
     sr_tmp.resize(n);
     std::vector<double>&t1 = sr_t1, &y = sr_y, &fy = sr_fy, &g = sr_g, &tmp = sr_tmp;
+#ifdef LQ_BIMPC_PROF
+    double t0 = nowus();
+#endif
     hb_solve(t1.data());
+#ifdef LQ_BIMPC_PROF
+    t_hb += nowus() - t0;
+    t0 = nowus();
+#endif
     mulL(B, t1.data(), y.data());
     double acc = 0.0;
     for (int t = 0; t < N; ++t) {  // F y = [y; A y]
       fy[t] = y[t];
       fy[N + t] = (acc += y[t]);
     }
-    lqd::chol_solve(W.data(), 2 * N, fy.data());
+    chol_upper_solve(W.data(), 2 * N, fy.data());
+#ifdef LQ_BIMPC_PROF
+    t_chs += nowus() - t0;
+#endif
     acc = 0.0;
     for (int t = N - 1; t >= 0; --t) {  // F' v = v_0 + A' v_1
       acc += fy[N + t];
       g[t] = fy[t] + acc;
     }
     mulLt(B, g.data(), tmp.data());
+#ifdef LQ_BIMPC_PROF
+    t0 = nowus();
+#endif
     hb_solve(tmp.data());
+#ifdef LQ_BIMPC_PROF
+    t_hb += nowus() - t0;
+#endif
     for (int i = 0; i < n; ++i) dz[i] = t1[i] - tmp[i];
   }
 };
@@ -844,6 +944,7 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
   std::vector<double> dbox(n), dgv(mg), rhs(n), dz(n), dsg(mg), dlg(mg), dllo(n), dlhi(n);
   std::vector<double> dz_a(n), dsg_a(mg), dlg_a(mg), dllo_a(n), dlhi_a(n);
   std::vector<double> rclo(n), rchi(n), rcg(mg);
+  std::vector<double> iz(n), iu(n), isg(mg);  // 1 / z, 1 / (ub - z), 1 / sg at the current iterate
   int it = 0, status = LOMPC_ERR_NOT_CONVERGED;
   // diagnostic builds only (-DLQ_BIMPC_TRACE / -DLQ_BIMPC_PROF): the iterations / the phases' wall
   // times on stderr
@@ -890,20 +991,20 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
                        std::vector<double>& dzo, std::vector<double>& dsgo, std::vector<double>& dlgo,
                        std::vector<double>& dlloo, std::vector<double>& dlhio) {
     // rhs = -rd + rlo/s_lo - rhi/s_hi - L'E'[(rgc + lg rg)/sg]
-    for (int i = 0; i < mg; ++i) tmpm[i] = (rgc[i] + lg[i] * rg[i]) / sg[i];
+    for (int i = 0; i < mg; ++i) tmpm[i] = (rgc[i] + lg[i] * rg[i]) * isg[i];
     mulEt(N, tmpm.data(), tmpN.data());
     mulLt(B, tmpN.data(), tmpn.data());
-    for (int i = 0; i < n; ++i) rhs[i] = -rd[i] + rlo[i] / z[i] - rhi[i] / (B.ub[i] - z[i]) - tmpn[i];
+    for (int i = 0; i < n; ++i) rhs[i] = -rd[i] + rlo[i] * iz[i] - rhi[i] * iu[i] - tmpn[i];
     NW.solve(B, dbox.data(), rhs.data(), dzo.data());
     mulL(B, dzo.data(), tmpN.data());
     mulE(N, tmpN.data(), tmpm.data());
     for (int i = 0; i < mg; ++i) {
       dsgo[i] = -rg[i] - tmpm[i];
-      dlgo[i] = (rgc[i] - lg[i] * dsgo[i]) / sg[i];
+      dlgo[i] = (rgc[i] - lg[i] * dsgo[i]) * isg[i];
     }
     for (int i = 0; i < n; ++i) {
-      dlloo[i] = (rlo[i] - llo[i] * dzo[i]) / z[i];
-      dlhio[i] = (rhi[i] + lhi[i] * dzo[i]) / (B.ub[i] - z[i]);
+      dlloo[i] = (rlo[i] - llo[i] * dzo[i]) * iz[i];
+      dlhio[i] = (rhi[i] + lhi[i] * dzo[i]) * iu[i];
     }
   };
   // largest steps keeping the primal (z in the boxes, coupling slacks) and the dual variables
@@ -922,7 +1023,7 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
   // reference accepts Clarabel's "optimal_inaccurate" silently, lompc.py / bimpc.py never check status)
   std::vector<double> zb(n), llob(n), lhib(n), lgb(mg), sgb(mg);
   double best_merit = INFINITY, bpres = 0, bdres = 0, bgap = 0, bf = 0;
-  int since_best = 0, spikes = 0;
+  int since_best = 0;
   for (it = 0; it < max_iter; ++it) {
     const double tr0 = tprof ? now() : 0.0;
     const double mu = residuals();
@@ -943,24 +1044,32 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
       bgap = gap;
       bf = fval;
       since_best = 0;
-      spikes = 0;
     } else if (++since_best >= 15) {
       break;
-    } else if (best_merit < 1e-6 && merit > 1e3 * best_merit) {
-      // breakdown next to the optimum (the exp weights' flat directions: the Newton steps lose
-      // accuracy, the step length collapses and the residuals blow up): once it persists for 3
-      // iterations the iterates do not come back, the best one is returned as below (a single
-      // transient spike keeps iterating)
-      if (++spikes >= 3) break;
-    } else {
-      spikes = 0;
+    } else if (best_merit <= 1e-6) {
+      // the merit rose from a best iterate that is already accurate: with the exp weights' flat
+      // directions this is where the Newton steps start to break down (the following iterations
+      // collapse the step length and blow the residuals up) — the best iterate is
+      // returned (and polished when the active set allows), as after a breakdown below
+      break;
     }
-    if (pres <= 1e-10 * (1.0 + hmax) && dres <= 1e-9 * (1.0 + gmax) && gap <= 1e-10 * (1.0 + std::fabs(fval))) {
+    // Clarabel's default stopping tolerances (the reference's BIMPC_SOLVER, settings.py:24, called with
+    // no settings, bimpc.py:287: tol_feas = tol_gap_rel = 1e-8); the polish below then makes the
+    // point exact when the active set is identified.  (1e-10 / 1e-9 here before round 6: the extra
+    // iterations sit where the exp weights' flat directions break the Newton steps down.)
+    if (pres <= 1e-8 * (1.0 + hmax) && dres <= 1e-8 * (1.0 + gmax) && gap <= 1e-8 * (1.0 + std::fabs(fval))) {
       status = LOMPC_OK;
       break;
     }
-    for (int i = 0; i < n; ++i) dbox[i] = llo[i] / z[i] + lhi[i] / (B.ub[i] - z[i]);
-    for (int i = 0; i < mg; ++i) dgv[i] = lg[i] / sg[i];
+    for (int i = 0; i < n; ++i) {
+      iz[i] = 1.0 / z[i];
+      iu[i] = 1.0 / (B.ub[i] - z[i]);
+      dbox[i] = llo[i] * iz[i] + lhi[i] * iu[i];
+    }
+    for (int i = 0; i < mg; ++i) {
+      isg[i] = 1.0 / sg[i];
+      dgv[i] = lg[i] * isg[i];
+    }
     const double tf0 = tprof ? now() : 0.0;
     if (!NW.factor(B, z.data(), dbox.data(), dgv.data())) break;
     const double tf1 = tprof ? now() : 0.0;
@@ -994,8 +1103,8 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
     const double tau = std::max(0.99, 1.0 - mu);  // fraction to the boundary
     ap = ad = std::min(1.0, tau * std::min(ap, ad));  // one step: the objective is nonlinear
     if (trace)
-      fprintf(stderr, "it %3d mu %.3e pres %.3e dres %.3e gap %.3e f %.12g sigma %.3e alpha %.3e\n", it, mu, pres, dres,
-              gap, fval, sigma, ap);
+      fprintf(stderr, "it %3d mu %.3e pres %.3e dres %.3e gap %.3e f %.12g sigma %.3e alpha %.3e merit %.3e gmax %.3e\n", it,
+              mu, pres, dres, gap, fval, sigma, ap, merit, gmax);
     if (!std::isfinite(ap) || !std::isfinite(ad) || !std::isfinite(sigma)) break;
     for (int i = 0; i < n; ++i) {
       z[i] += ap * dz[i];
@@ -1042,6 +1151,11 @@ int lompc_bimpc_solve(int N, int P, int charging_cost_type, double delta, double
   if (tprof)
     fprintf(stderr, "bimpc prof: %d it, total %.0f us: factor %.0f, directions %.0f, residuals %.0f, polish %.0f\n", it,
             now() - t_all, t_fac, t_dir, t_res, t_pol);
+#ifdef LQ_BIMPC_PROF
+  fprintf(stderr, "bimpc prof: solves %d, regularised solves %d, applies %d; hb_solve %.0f us, mulL+chol_solve %.0f us, apply %.0f us\n",
+          NW.n_solve, NW.n_reg, NW.n_apply, NW.t_hb, NW.t_chs, NW.t_app);
+  fprintf(stderr, "bimpc prof: factor: blocks %.0f us, assembly %.0f us, Cholesky %.0f us\n", NW.t_fx, NW.t_fasm, NW.t_fch);
+#endif
   if (duals) {  // [lower-bound duals (n) | upper-bound duals (n) | coupling duals (4N)]
     memcpy(duals, llo.data(), n * sizeof(double));
     memcpy(duals + n, lhi.data(), n * sizeof(double));

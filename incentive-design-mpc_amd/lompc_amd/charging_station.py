@@ -279,33 +279,37 @@ class ChargingStation:
             return self._yfull[kind], None
         return (self.y_s, self.idx_s) if kind == "Small" else (self.y_l, self.idx_l)
 
-    def _w0_layouts(self):
-        """Replicated sharding: this rank's EVs in the loops' layout order (each partition's run of the
-        whole population's layout restricted to global indices [lo, hi): still in descending charge
-        level), for the sharded w0 / price0 pass — {kind: (local permutation, levels, {p: (start,
-        end)})}, both types' run bounds in one host copy."""
+    def _w0_layout(self, kind, reader=None):
+        """Replicated sharding: this rank's EVs of one type in the loops' layout order (each partition's
+        run of the whole population's layout restricted to global indices [lo, hi): still in descending
+        charge level), for the sharded w0 / price0 pass — (local permutation, levels, {p: (start, end)}),
+        the run bounds in one host copy.  Made by the type's staging thread (beside the interior point)
+        or on first use."""
         torch = _torch()
-        if self._layout_w0:
-            return self._layout_w0
+        got = self._layout_w0.get(kind)
+        if got is not None:
+            return got
         lo, hi, P = self._lo, self._hi, self.P
-        parts, ends = [], []
-        for kind in ("Small", "Large"):
-            perm, ys, seg = self._partition_layout(kind, *self._loop_levels(kind))
-            m = (perm >= lo) & (perm < hi)
-            order = sorted(range(P), key=lambda p: seg[p])
-            c = torch.cumsum(m.to(torch.int64), 0)
-            e = torch.as_tensor([seg[p][1] - 1 for p in order], dtype=torch.int64, device=m.device)
-            ends.append(torch.where(e >= 0, c[e.clamp(min=0)], 0))
-            nz = torch.nonzero_static(m, size=hi - lo).squeeze(1)
-            parts.append((kind, order, perm[nz] - lo, ys[nz]))
-        cnt = torch.stack(ends).cpu().numpy()  # the one host sync
-        for j, (kind, order, lperm, lys) in enumerate(parts):
-            seg_l, prev = {}, 0
-            for k, p in enumerate(order):
-                seg_l[p] = (prev, int(cnt[j, k]))
-                prev = int(cnt[j, k])
-            self._layout_w0[kind] = (lperm, lys, seg_l)
-        return self._layout_w0
+        perm, ys, seg = self._partition_layout(kind, *self._loop_levels(kind))
+        m = (perm >= lo) & (perm < hi)
+        order = sorted(range(P), key=lambda p: seg[p])
+        c = torch.cumsum(m.to(torch.int64), 0)
+        e = torch.as_tensor([seg[p][1] - 1 for p in order], dtype=torch.int64, device=m.device)
+        nz = torch.nonzero_static(m, size=hi - lo).squeeze(1)
+        lperm, lys = perm[nz] - lo, ys[nz]
+        if reader is not None:  # (made on a staging stream, read on `reader`: the allocator keeps them)
+            lperm.record_stream(reader)
+            lys.record_stream(reader)
+        cnt = torch.where(e >= 0, c[e.clamp(min=0)], 0).cpu().numpy()  # the one host sync
+        seg_l, prev = {}, 0
+        for k, p in enumerate(order):
+            seg_l[p] = (prev, int(cnt[k]))
+            prev = int(cnt[k])
+        self._layout_w0[kind] = (lperm, lys, seg_l)
+        return self._layout_w0[kind]
+
+    def _w0_layouts(self):
+        return {kind: self._w0_layout(kind) for kind in ("Small", "Large")}
 
     def _init_states(self) -> None:
         # charging_station.py:94-109 (global draws, this rank keeps its slice)
@@ -636,6 +640,8 @@ class ChargingStation:
                 # the interior point, not before it); its tensors are read on the main stream later
                 _, ys, seg = self._partition_layout(kind, y, idx, main)
                 gam, at = self._gamma_layout(solver, ys, seg, st) if self.gamma_layout else (None, None)
+                if self.replicated:  # (this rank's EVs in that layout, for the w0 pass: made here, off the step's path)
+                    self._w0_layout(kind, main)
                 for p in range(self.P):
                     if st[p, 0] > 0:
                         a, b = seg[p]
@@ -955,14 +961,37 @@ class ChargingStation:
             self.ncharged_l += int(h[3])
             residual_charge += self.consts_l.theta * float(h[1])
         else:
+            # sharded: both types' local residual sums and full counts in ONE all-gather (one host sync);
+            # the residual sums combined in rank order, the redraws in global EV order (every rank draws
+            # the global vector from the replicated stream and keeps its slice)
+            import torch.distributed as dist
+
             self.y_s += w0_s
-            mask_s = self.y_s > thr_s
-            residual_charge += self.consts_s.theta * self._global_sum(torch.where(mask_s, self.y_s - thr_s, 0.0))
-            self.ncharged_s += redraw_full(self.y_s, mask_s, self.y0_min, self.y0_max, np.random.random, self.group)
             self.y_l += w0_l
-            mask_l = self.y_l > thr_l
-            residual_charge += self.consts_l.theta * self._global_sum(torch.where(mask_l, self.y_l - thr_l, 0.0))
-            self.ncharged_l += redraw_full(self.y_l, mask_l, self.y0_min, self.y0_max, np.random.random, self.group)
+            mask_s, mask_l = self.y_s > thr_s, self.y_l > thr_l
+            rec = torch.stack([torch.where(mask_s, self.y_s - thr_s, 0.0).sum(), torch.where(mask_l, self.y_l - thr_l, 0.0).sum(),
+                               mask_s.sum().to(torch.float64), mask_l.sum().to(torch.float64)])
+            world = dist.get_world_size(self.group)
+            allr = torch.empty(4 * world, dtype=torch.float64, device=rec.device)
+            dist.all_gather_into_tensor(allr, rec, group=self.group)
+            h = allr.view(world, 4).cpu().numpy()  # the one host sync
+            me = dist.get_rank(self.group)
+            res = h[0, :2].copy()
+            for r in range(1, world):  # fixed rank order
+                res += h[r, :2]
+            residual_charge += self.consts_s.theta * float(res[0]) + self.consts_l.theta * float(res[1])
+            for j, (y, mask) in enumerate(((self.y_s, mask_s), (self.y_l, mask_l))):
+                cnt = h[:, 2 + j].astype(np.int64)
+                total, before, local = int(cnt.sum()), int(cnt[:me].sum()), int(cnt[me])
+                if total:
+                    draws = self.y0_min + (self.y0_max - self.y0_min) * np.random.random((total,))
+                    if local:
+                        y.masked_scatter_(mask, torch.as_tensor(draws[before:before + local], dtype=torch.float64,
+                                                                 device=y.device))
+                if j == 0:
+                    self.ncharged_s += total
+                else:
+                    self.ncharged_l += total
         self._update_indices()
         if not ADD_RESIDUAL_CHARGE_TO_BATTERY:
             residual_charge = 0
@@ -975,15 +1004,6 @@ class ChargingStation:
             print(f"# small EVs charged    : {self.ncharged_s:5d}")
             print(f"# large EVs charged    : {self.ncharged_l:5d}")
             print("")
-
-    def _global_sum(self, v) -> float:
-        s = v.sum()
-        if self.group is not None:
-            import torch.distributed as dist
-
-            s = s.reshape(1).clone()
-            dist.all_reduce(s, group=self.group)
-        return float(s.item())
 
     def _update_logs(self, lmbd_r: float, nu: tuple, stats: tuple, price0: tuple, w0_stats) -> None:
         # charging_station.py:372-433

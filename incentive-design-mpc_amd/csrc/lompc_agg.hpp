@@ -324,7 +324,7 @@ struct AggSet {
   double lr, l1, l2, l3, tt, wm;
 };
 
-template <int NT>
+template <int NT, bool COH = false>  // (COH: the prices re-read with sc1 loads, as load_set<COH>)
 __device__ __forceinline__ AggSet agg_set_init(const AggArgs& r, const int s) {
   AggSet z;
   z.N = NT ? NT : r.N;
@@ -346,9 +346,9 @@ __device__ __forceinline__ AggSet agg_set_init(const AggArgs& r, const int s) {
   z.fs = (double)r.F / W;
   z.L = r.lmbd + (size_t)s * 3 * z.N;
   z.lr = r.lmbd_r[s];
-  z.l1 = z.L[0];
-  z.l2 = z.L[z.N];
-  z.l3 = z.L[2 * z.N];
+  z.l1 = ld_price<COH>(z.L);
+  z.l2 = ld_price<COH>(z.L + z.N);
+  z.l3 = ld_price<COH>(z.L + 2 * z.N);
   z.tt = z.q->theta * z.q->theta;
   z.wm = z.q->w_max;
   return z;
@@ -368,7 +368,7 @@ __device__ __forceinline__ int2 agg_cell_range(const AggSet& z, const int c) {
   return make_int2(z.ps[c * z.KF], z.ps[(c + 1) * z.KF]);
 }
 
-template <int NT, bool COH>
+template <int NT, bool COH, bool PCOH = false>  // (PCOH: the prices with sc1 loads, k_loop_run)
 __device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, const int s, const int c, const int2 rng,
                                          const int lane, AggPart& a) {
   const int N = NT ? NT : z.N, G = z.G, KF = z.KF;
@@ -479,7 +479,7 @@ __device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, cons
     lqw::WaveSet ws;
     double l2w;
     bool bad;
-    load_set(q, z.L, lr, N, lane, ws, l2w, bad);
+    load_set<PCOH>(q, z.L, lr, N, lane, ws, l2w, bad);
     const double c0 = q.theta * q.w_max * lqw::wave_sum(l2w, N);
     const double kappa = lr / q.delta;
     const double l0[3] = {l1, l2, l3};

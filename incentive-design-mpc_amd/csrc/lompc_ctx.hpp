@@ -259,5 +259,9 @@ struct StepArgs;
 bool lq_loop_fusable(const lompc_plan* p);
 int lq_launch_loop_iter(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,
                         const StepArgs& sa, int m, hipStream_t st);
+int lq_launch_loop_run(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,
+                       const StepArgs& sa, hipStream_t st);
+int lq_launch_loop(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,
+                   const StepArgs& sa, int m, hipStream_t st, bool persistent);
 int lq_price_loop_host(lompc_plan* p, const lompc_price_loop_args* a, double* lmbd, double* w_k, double* dual_cost,
                        double* dec_actual, double* dec_pred, int* iterations, double* errs, hipStream_t st);

@@ -28,6 +28,10 @@
 #include "lompc_ctx.hpp"
 #include "lompc_loopstep.hpp"
 
+#ifndef LQ_LOOP_PERSIST
+#define LQ_LOOP_PERSIST 1  // fused plans: the whole loop as ONE persistent launch (k_loop_run); 0: k_loop_iter per call
+#endif
+
 namespace {
 
 // Engine call m of the loop has run: the loop step (lompc_loopstep.hpp) on one wave
@@ -102,6 +106,27 @@ int lq_price_loop_device(lompc_plan* p, const lompc_price_loop_args* a, double* 
   };
   p->skip = p->d_loop;
   rc = LOMPC_OK;
+  if (fused && LQ_LOOP_PERSIST) {
+    // ONE launch runs every call of the loop (k_loop_run); the host waits for `done` — or for the
+    // launch to end without it (a wave's bounded spin expired: ctl[3])
+    const double t0 = prof ? now_us() : 0.0;
+    rc = lq_launch_loop_run(p, a->dev_in, a->dev_in + 2 * N3, const_cast<double*>(a->dev_sw),
+                            const_cast<double*>(a->dev_st), sa, st);
+    if (prof) t_issue += now_us() - t0;
+    p->skip = nullptr;
+    if (rc) return rc;
+    bool ended = false;
+    rc = wait_for([&]() {
+      if (done()) return true;
+      ended = hipStreamQuery(st) == hipSuccess;  // (the launch is over: `done` was set before it ended, or never)
+      return ended && !done();
+    });
+    if (rc) return rc;
+    if (!done()) {
+      p->err = "device price loop: a persistent wave timed out waiting for the next call";
+      return LOMPC_ERR_HIP;
+    }
+  } else {
   for (int j = 0; j <= MI; ++j) {
     // enqueue call j once calls 0 .. j - ahead - 1 have run; never past the finishing call + ahead
     if ((rc = wait_for([&]() { return progress() >= j - ahead || done(); }))) break;
@@ -127,6 +152,7 @@ int lq_price_loop_device(lompc_plan* p, const lompc_price_loop_args* a, double* 
   p->skip = nullptr;
   if (rc) return rc;
   if ((rc = wait_for(done))) return rc;
+  }
   const long long err = h->err;
   const int it = (int)h->conv_at;
   if (prof) {

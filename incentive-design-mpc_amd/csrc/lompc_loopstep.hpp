@@ -55,6 +55,13 @@ __device__ __forceinline__ void lq_publish(long long* p, long long v) {
   sys_release(p, v);
 }
 
+// the step's writes the next call reads (prices, loop state, the A_bar factor): write-through (sc1),
+// so a persistent loop's waves on other XCDs read them with sc1 loads after the generation flag
+__device__ __forceinline__ void lq_st_wt(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // loads of the engine call's set outputs: plain after a kernel boundary (k_loop_step),
 // device-coherent when workgroups of the same launch wrote them (k_loop_iter)
 template <bool COH>
@@ -78,19 +85,21 @@ struct StepIn {
 };
 
 // the step's inputs that do not depend on the engine call's outputs (the prices it ran at, w_ref,
-// the loop state): k_loop_iter loads them at its start, before its path
+// the loop state): k_loop_iter loads them at its start, before its path.  COH: with sc1 loads (the
+// persistent loop, k_loop_run: the previous call's step wrote them in the same launch)
+template <bool COH = false>
 __device__ __forceinline__ void step_prices(const StepArgs& a, const int lane, StepIn& in) {
   const int N = a.N, N3 = 3 * N;
   const bool act = lane < N;
-  in.wr = act ? a.dev_in[2 * N3 + 2 + lane] : 0.0;
+  in.wr = act ? a.dev_in[2 * N3 + 2 + lane] : 0.0;  // (w_ref: constant over the loop)
 #pragma unroll
-  for (int k = 0; k < 3; ++k) in.lm[k] = act ? a.dev_in[k * N + lane] : 0.0;
-  in.dc = a.state[0];
-  in.dterm = a.state[1];
-  in.ab.Q = a.tri[lane];
-  in.ab.iv = a.tri[64 + lane];
-  in.ab.d = a.tri[128 + lane];
-  in.ab.K = a.tri[192 + lane];
+  for (int k = 0; k < 3; ++k) in.lm[k] = act ? lq_ld_set<COH>(a.dev_in + k * N + lane) : 0.0;
+  in.dc = lq_ld_set<COH>(a.state);
+  in.dterm = lq_ld_set<COH>(a.state + 1);
+  in.ab.Q = lq_ld_set<COH>(a.tri + lane);
+  in.ab.iv = lq_ld_set<COH>(a.tri + 64 + lane);
+  in.ab.d = lq_ld_set<COH>(a.tri + 128 + lane);
+  in.ab.K = lq_ld_set<COH>(a.tri + 192 + lane);
 }
 
 // Engine call m of the loop has run (its set sums / stats in `in`, at the prices in a.dev_in);
@@ -98,12 +107,17 @@ __device__ __forceinline__ void step_prices(const StepArgs& a, const int lane, S
 struct NoStamp {
   __device__ __forceinline__ void operator()(int) const {}
 };
+struct NoRelease {  // (k_loop_iter / k_loop_step: the kernel's end releases the next call)
+  __device__ __forceinline__ void operator()() const {}
+};
 
 // (ST: a diagnostic build's phase stamp, called with 8 after the inputs and the error metric, 9
 // after the price QP)
-template <class ST = NoStamp>
+// (REL: called once the next call's prices and loop state are written, before the host-memory writes
+// of this step — k_loop_run releases its waiting waves there, so the PCIe writes overlap the next call)
+template <class ST = NoStamp, class REL = NoRelease>
 __device__ __forceinline__ void loop_step_core(const StepArgs& a, const int m, const int lane, const StepIn& in,
-                                               const ST& stamp = ST{}) {
+                                               const ST& stamp = ST{}, const REL& release = REL{}) {
   const int N = a.N, N3 = 3 * N;
   const bool act = lane < N;
   const double s0 = act ? in.s0 : 0.0, wk = act ? in.wk : 0.0;
@@ -121,7 +135,7 @@ __device__ __forceinline__ void loop_step_core(const StepArgs& a, const int m, c
   const double e0 = emax, e1 = fabs(lqw::readlane_d(d, 0)), e2 = sqrt(qf);
   // dual cost decrease of the previous step (price_solver.py:133-138; the reference's lmbd_k /
   // lmbd_k_new aliasing keeps the price term only for the first step)
-  if (m > 0 && lane == 0) sys_st(a.h_dec + (m - 1), cost_c - dc + dterm);
+  const double dec_prev = cost_c - dc + dterm;  // (stored to the host below, after the release)
   const bool conv = (a.tol_avg ? e2 : e0) <= a.tol;
   stamp(8);
   double x[3] = {0.0, 0.0, 0.0};
@@ -131,10 +145,10 @@ __device__ __forceinline__ void loop_step_core(const StepArgs& a, const int m, c
     lqp::PriceQPW P;
     P.init(N, a.r, a.theta, a.w_max, a.m, a.kappa, a.eps_reg, wk, m > 0 ? &in.ab : nullptr);
     if (m == 0) {  // the loop's A_bar factor for its later steps
-      a.tri[lane] = P.Ab.Q;
-      a.tri[64 + lane] = P.Ab.iv;
-      a.tri[128 + lane] = P.Ab.d;
-      a.tri[192 + lane] = P.Ab.K;
+      lq_st_wt(a.tri + lane, P.Ab.Q);
+      lq_st_wt(a.tri + 64 + lane, P.Ab.iv);
+      lq_st_wt(a.tri + 128 + lane, P.Ab.d);
+      lq_st_wt(a.tri + 192 + lane, P.Ab.K);
     }
     const double q_s = 3.0 * a.theta / (4.0 * a.w_max);
     double Ql[3], q[3];
@@ -162,6 +176,7 @@ __device__ __forceinline__ void loop_step_core(const StepArgs& a, const int m, c
   }
   stamp(9);
   if (err || conv || m >= a.max_iter) {  // finished: the results to the host, then the flags
+    if (m > 0 && lane == 0) sys_st(a.h_dec + (m - 1), dec_prev);
     if (act) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) sys_st(&a.h->lmbd[k * N + lane], lm[k]);
@@ -189,15 +204,19 @@ __device__ __forceinline__ void loop_step_core(const StepArgs& a, const int m, c
     for (int k = 0; k < 3; ++k) {
       const double v = k * N < a.r ? x[k] : 0.0;
       dt = fma(lm[k] - v, phr[k], dt);
-      a.dev_in[k * N + lane] = v;
-      a.dev_in[N3 + k * N + lane] = v;
+      lq_st_wt(a.dev_in + k * N + lane, v);
+      lq_st_wt(a.dev_in + N3 + k * N + lane, v);
     }
   }
   dt = lqw::wave_sum(dt, N);
   if (lane == 0) {
+    lq_st_wt(a.state, cost_c);
+    lq_st_wt(a.state + 1, m == 0 ? dt : 0.0);
+  }
+  release();
+  if (lane == 0) {
+    if (m > 0) sys_st(a.h_dec + (m - 1), dec_prev);
     sys_st(a.h_dec + a.max_iter + m, dec);
-    a.state[0] = cost_c;
-    a.state[1] = m == 0 ? dt : 0.0;
     // (an unfinished step's progress orders nothing for the host — it only paces the enqueueing;
     // h_dec is read after `done`, which the finishing step publishes behind every earlier store)
     sys_st(&a.h->progress, (long long)m + 1);

@@ -378,8 +378,17 @@ struct PathArgs {
   const int* skip;       // device-resident price loop: nonzero = the loop has finished, run nothing
 };
 
+// price loads: plain, or (COH) device-coherent sc1 loads past this CU's L1 — the persistent price
+// loop (k_loop_run) re-reads prices that another workgroup of the same launch wrote through (sc1)
+template <bool COH>
+__device__ __forceinline__ double ld_price(const double* p) {
+  if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+
 // per-stage data of set s from its prices (lompc.py:92-135 in standard form)
 // (bad: a negative or NaN price on this lane's stage)
+template <bool COH = false>
 __device__ __forceinline__ void load_set(const QPConst& q, const double* __restrict__ L, double lr, int N,
                                          int lane, lqw::WaveSet& ws, double& l2, bool& bad) {
   const double tt = q.theta * q.theta;
@@ -388,8 +397,8 @@ __device__ __forceinline__ void load_set(const QPConst& q, const double* __restr
   l2 = 0.0;
   bad = false;
   if (lane < N) {
-    const double l1 = L[lane], l3 = L[2 * N + lane];
-    l2 = L[N + lane];
+    const double l1 = ld_price<COH>(L + lane), l3 = ld_price<COH>(L + 2 * N + lane);
+    l2 = ld_price<COH>(L + N + lane);
     bad = !(l1 >= 0.0 && l2 >= 0.0 && l3 >= 0.0);
     ws.d_nat = 2.0 * lr * tt + 2.0 * q.q_scale * l3 + q.dsmall;
     ws.e_nat = q.theta * (l1 - l2);
@@ -403,7 +412,7 @@ __device__ __forceinline__ void load_set(const QPConst& q, const double* __restr
 // to the cell's fixed slots with write-through stores (visible to any XCD once they complete).
 // NT: the horizon as a compile-time constant (0: a.N at run time) — the scans' row / bank steps
 // become straight-line code, so independent chains can be interleaved
-template <int NT = 0, bool INIT_TAB = false>
+template <int NT = 0, bool INIT_TAB = false, bool COH = false>
 __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
   const int G = a.G;
   const int s = __builtin_amdgcn_readfirstlane(blk / G);
@@ -419,7 +428,7 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
   lqw::WaveSet ws;
   double l2;
   bool bad;
-  load_set(q, L, lr, N, lane, ws, l2, bad);
+  load_set<COH>(q, L, lr, N, lane, ws, l2, bad);
   if (INIT_TAB) lq_tab_init(q);  // (after the price loads are issued: the barrier overlaps them)
   if (bad || (lane == 0 && !(lr >= 0.0))) atomicOr(a.errflag, 1);
   const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);  // lompc.py:128
@@ -2057,6 +2066,134 @@ __global__ __launch_bounds__(64) void k_loop_iter(PathArgs pa, AggArgs ga, StepA
   LQ_LSTAMP(4);
 }
 
+// ---------------------------------------------------------------- k_loop_run
+// The WHOLE device-resident price loop as ONE launch (persistent): the S * G waves of k_loop_iter
+// run call after call.  Call m is k_loop_iter's body; the last arriver's step writes the next prices,
+// the loop state and (m = 0) the A_bar factor write-through (sc1), drains them, and publishes the
+// generation word ctl[2] = m + 1; every other wave polls ctl[2] (lane 0, sc1 loads, s_sleep backoff)
+// and then re-reads everything the step wrote with sc1 loads (prices in the path, the aggregation and
+// the step; the loop state and factor in step_prices) — MI355X_MICROARCH.md's valid hand-off form:
+// sc1 payload drained before an sc1 flag, sc1 polls, sc1 payload loads.  The finishing step sets
+// ctl[0] before its generation, so every wave leaves at the next call's top.  No launch boundary and
+// no per-launch setup between calls (k_loop_iter: one launch per call, 1.5-1.7 us apart).  Bounded
+// spins: a wave that waits LQ_RUN_SPINS polls without a new generation sets ctl[3] and ctl[0] and
+// leaves (the host reports the timeout).  Same arithmetic as k_loop_iter: the same bits.
+#ifndef LQ_RUN_SPINS
+#define LQ_RUN_SPINS (1 << 22)  // ~ seconds of polls (a call takes ~15 us)
+#endif
+template <int NT>
+__global__ __launch_bounds__(64) void k_loop_run(PathArgs pa, AggArgs ga, StepArgs sa, double* rec) {
+  constexpr int S = 2;  // (lq_loop_fusable: the loop's two sets)
+  const int blk = (int)blockIdx.x, lane = (int)threadIdx.x, G = pa.G;
+  const int s = blk / G, c = blk - s * G;
+  int cl_n[S], cl_v[S], cl_ok[S];  // (the sets' sizes and order flags: constant over the loop)
+#pragma unroll
+  for (int t = 0; t < S; ++t) {
+    const int4 si = ga.sinfo[t];
+    cl_n[t] = (int)(ga.set_off[t + 1] - ga.set_off[t]);
+    cl_v[t] = si.x;
+    cl_ok[t] = si.y;
+    asm volatile("" : "+v"(cl_n[t]), "+v"(cl_v[t]), "+v"(cl_ok[t]));
+  }
+  for (int m = 0; m <= sa.max_iter; ++m) {
+    if (m > 0) {  // call m - 1's step has published the prices of call m
+      int ok = 1;
+      if (lane == 0) {
+        int spins = 0;
+        while (__hip_atomic_load(sa.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < m) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins >= LQ_RUN_SPINS) {
+            ok = 0;
+            break;
+          }
+        }
+        if (!ok) {
+          __hip_atomic_store(sa.ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(sa.ctl + 0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      if (!lqw::readlane_i(ok, 0)) return;
+    }
+    if (__hip_atomic_load(sa.ctl + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // finished
+    StepIn in;
+    step_prices<true>(sa, lane, in);
+    path_cell<NT, true, true>(pa, blk);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the cell's tables have reached L2
+    {
+      const AggSet z = agg_set_init<NT, true>(ga, s);
+      AggPart ap;
+      if (z.order_ok) agg_cell<NT, true, true>(ga, z, s, c, agg_cell_range(z, c), lane, ap);
+      const AggRec x = agg_wave_record(ap);
+      double* rc = rec + (size_t)blk * LQ_AGG_REC;
+      if (lane < z.N) st_wt8(rc + lane, ap.accw);
+      if (lane < 5) st_wt8(rc + LOMPC_MAX_N + lane, x.pick(lane));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old = 0;
+    if (lane == 0) {
+      old = __hip_atomic_fetch_add(sa.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == S * G - 1) __hip_atomic_store(sa.ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lqw::readlane_i(old, 0) != S * G - 1) continue;
+    // the last arriver: both sets closed from the records (one memory round), then the loop step
+    AggSet zs[S];
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+      zs[t].N = NT ? NT : ga.N;
+      zs[t].n_s = cl_n[t];
+      zs[t].si = make_int4(cl_v[t], cl_ok[t], 0, 0);
+      zs[t].order_ok = cl_ok[t] != 0;
+    }
+    const int N = zs[0].N;
+    double rw[S][LQ_LOOP_G], rx[S][LQ_LOOP_G];
+    const int tl = min(lane, N - 1), xl = min(lane, 4);
+#pragma unroll
+    for (int t = 0; t < S; ++t)
+#pragma unroll
+      for (int k = 0; k < LQ_LOOP_G; ++k) {
+        const double* rk = rec + (size_t)(k < G ? t * G + k : S * G) * LQ_AGG_REC;
+        rw[t][k] = ld_t<true>(rk + tl);
+        rx[t][k] = ld_t<true>(rk + LOMPC_MAX_N + xl);
+      }
+    AggSetOut o[S];
+#pragma unroll
+    for (int t = 0; t < S; ++t)
+      o[t] = agg_finish<false, true, LQ_LOOP_G>(ga, zs[t], t, lane, G, [&](int k) { return rw[t][k]; },
+                                               [&](int k) { return rx[t][k]; });
+    in.s0 = o[0].sumw;
+    in.wk = o[1].sumw;
+    in.emax = lqw::readlane_d(o[0].stat, LOMPC_STAT_MAX_ERR);
+    in.cost_c = lqw::readlane_d(o[1].stat, LOMPC_STAT_SUM_COST);
+    in.n_inv = lqw::readlane_d(o[0].stat, LOMPC_STAT_N_INVALID) + lqw::readlane_d(o[1].stat, LOMPC_STAT_N_INVALID);
+    in.n_fail = lqw::readlane_d(o[0].stat, LOMPC_STAT_N_FAILED) + lqw::readlane_d(o[1].stat, LOMPC_STAT_N_FAILED);
+    // the step releases call m + 1 as soon as its prices and loop state (sc1) have left this wave —
+    // before its host-memory writes, which then overlap call m + 1 (a finishing step releases nothing:
+    // its ctl[0] and `done` end the loop, and the waves leave at the next call's top)
+    bool released = false;
+    const auto release = [&]() {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(sa.ctl + 2, m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      released = true;
+    };
+    loop_step_core(sa, m, lane, in, NoStamp{}, release);
+    if (!released) {  // (finished: the waiting waves find ctl[0] behind this generation)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(sa.ctl + 2, m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+typedef void (*LoopRunKernel)(PathArgs, AggArgs, StepArgs, double*);
+LoopRunKernel loop_run_kernel(int N) {
+  switch (N) {
+    case 12: return k_loop_run<12>;
+    case 16: return k_loop_run<16>;
+    case 24: return k_loop_run<24>;
+    case 48: return k_loop_run<48>;
+    default: return k_loop_run<0>;
+  }
+}
+
 typedef void (*LoopIterKernel)(PathArgs, AggArgs, StepArgs, double*, int);
 LoopIterKernel loop_iter_kernel(int N) {
   switch (N) {
@@ -2594,6 +2731,17 @@ bool lq_loop_fusable(const lompc_plan* p) {  // (S = 2: the loop's sets; ctl hol
 
 int lq_launch_loop_iter(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,
                         const StepArgs& sa, int m, hipStream_t st) {
+  return lq_launch_loop(p, lmbd, lmbd_r, set_sum_w, set_stats, sa, m, st, false);
+}
+
+// the whole loop as one persistent launch (k_loop_run)
+int lq_launch_loop_run(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,
+                       const StepArgs& sa, hipStream_t st) {
+  return lq_launch_loop(p, lmbd, lmbd_r, set_sum_w, set_stats, sa, 0, st, true);
+}
+
+int lq_launch_loop(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,
+                   const StepArgs& sa, int m, hipStream_t st, bool persistent) {
   if (!lq_loop_fusable(p)) return fail_arg(p, "k_loop_iter: plan not fusable");
   const int N = p->N;
   const int64_t nrec = (p->S * p->G + 1) * (int64_t)LQ_AGG_REC;  // + the zero record (k_loop_iter's padding)
@@ -2614,8 +2762,12 @@ int lq_launch_loop_iter(lompc_plan* p, const double* lmbd, const double* lmbd_r,
              p->d_sinfo, set_sum_w, set_stats, p->d_stats, p->d_tally, p->skip};
   hipEvent_t e0 = nullptr, e1 = nullptr;  // (timed as k_path)
   if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
-  hipExtLaunchKernelGGL(loop_iter_kernel(N), dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa, ga, sa,
-                        p->d_aggrec, m);
+  if (persistent)  // (S * G one-wave workgroups: all resident at once, whatever else runs)
+    hipExtLaunchKernelGGL(loop_run_kernel(N), dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa, ga, sa,
+                          p->d_aggrec);
+  else
+    hipExtLaunchKernelGGL(loop_iter_kernel(N), dim3((unsigned)(p->S * p->G)), dim3(64), 0, st, e0, e1, 0, pa, ga, sa,
+                          p->d_aggrec, m);
   HIPCHK(p, hipGetLastError());
   plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
   return LOMPC_OK;

@@ -59,6 +59,8 @@ for s in $STEPS; do
     stationt6) run stationt6 600 $PYT tests/test_gpu_station.py tests/test_gpu_levels.py -m gpu ;;
     bdistst) run bdistst 600 python bench.py --force-dist --steps 20 --warmup 5 --no-cpu-baseline --no-direct --no-contracts ;;
     bst) run bst 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-direct --no-contracts ;;
+    bprofh) run bprofh 300 python scripts/bimpc_prof.py ;;
+    looptests) run looptests 600 $PYT tests/test_gpu_price_loop_c5.py tests/test_gpu_price_loop_long.py tests/test_gpu_price_solver.py tests/test_gpu_chain.py tests/test_gpu_comm.py tests/test_gpu_station.py -m gpu ;;
     *) echo "unknown step $s" ;;
   esac
 done

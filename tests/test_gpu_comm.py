@@ -169,10 +169,12 @@ def test_sharded_price_loop_runs_native(nccl1, monkeypatch):
             assert np.array_equal(s0[k], s1[k]), k
 
 
-def test_station_world1_nccl_equals_single(nccl1, monkeypatch):
-    """The closed loop on a world-1 RCCL group (sharded code path: device-combined price loops,
-    torch.distributed partition statistics / price0 sums / re-draw counts / residual charge)
-    gives bitwise the single-process trajectory."""
+@pytest.mark.parametrize("mode", ["replicated", "exchange"])
+def test_station_world1_nccl_equals_single(nccl1, monkeypatch, mode):
+    """The closed loop on a world-1 RCCL group gives bitwise the single-process trajectory in both
+    sharded forms — replicated (the default: the levels all-gathered once per step, every price loop
+    on every rank as one persistent launch, the w0 sums / re-draw counts / residual charge combined
+    through torch.distributed) and exchange (device-combined set reductions per price iteration)."""
     from lompc_amd.charging_station import ChargingStation
     from test_gpu_station import consts
 
@@ -182,9 +184,12 @@ def test_station_world1_nccl_equals_single(nccl1, monkeypatch):
     ref = ChargingStation(consts(M_2, Tf=3), device=0)
     rl = ref.simulate()
     np.random.seed(5)
-    sh = ChargingStation(consts(M_2, Tf=3), device=0, group=nccl1)
+    sh = ChargingStation(consts(M_2, Tf=3), device=0, group=nccl1, sharded_loops=mode)
     sl = sh.simulate()
-    assert sh.price_solver_s._plan.comm is not None and sh.price_solver_l._plan.comm is not None
+    if mode == "exchange":
+        assert sh.price_solver_s._plan.comm is not None and sh.price_solver_l._plan.comm is not None
+    else:  # (the loops see the whole population: no communicator, the device loop)
+        assert sh.price_solver_s.group is None and sh.price_solver_s.device_loop and sh.replicated
     for sec in ("inputs", "bounds", "prices", "states", "statistics"):
         for k, v in rl[sec].items():
             a, b = np.asarray(v), np.asarray(sl[sec][k])

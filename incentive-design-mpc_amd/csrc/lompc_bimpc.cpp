@@ -270,11 +270,11 @@ struct Newton {
   std::vector<double> ck;
   std::vector<double> S;    // [N*N] sum_k c_k^2 T_k^-1 (H_k^-1 = A^-1 T_k^-1 A^-T)
   std::vector<double> Lf, Df, Di;  // [N][nb] LDL' factors of the T_k (Di = 1 / Df), stage-major (hb_solve)
-  std::vector<double> row, dd, ll;  // factor() scratch
+  std::vector<double> row, dd, rho, pl, pd;  // factor() scratch
   mutable std::vector<double> hb_tmp;
   mutable std::vector<double> sv_r, sv_c, sv_trial;                                  // solve()
   mutable std::vector<double> sr_t1, sr_y, sr_fy, sr_g, sr_tmp;                      // solve_reg()
-  mutable std::vector<double> ap_r, ap_Lx, ap_Qy, ap_tmp;                            // apply()
+  mutable std::vector<double> ap_Lx, ap_Qy, ap_tmp, ap_acc, ap_rk;                  // apply()
 
   // factor M for the current iterate; dbox: [n] box barrier diagonal, dg: [4N] coupling D_g.
   //
@@ -301,42 +301,52 @@ struct Newton {
     S.assign((size_t)N * N, 0.0);
     row.resize(N);
     dd.resize(N);
-    ll.resize(N);
+    // LDL' of every block's tridiagonal T_k at once, stage-major (stage t of all blocks is one
+    // vector operation: the blocks' independent recurrences overlap instead of 2P latency chains):
+    // diag a_t, sub-diagonal c_t = -D_{t+1} (rows t+1, t).  Static regularisation rho_k (the EXP
+    // weights 5^(t-N+1) leave early steps with almost no curvature; iterative refinement against the
+    // exact matrix removes its bias)
+    rho.resize(nb);
+    pl.assign(nb, 0.0);
+    pd.assign(nb, 0.0);
+    for (int k = 0; k < nb; ++k) {
+      double s = 0.0;
+      for (int t = 0; t < N; ++t) s += B.omega[k * N + t];
+      rho[k] = 1e-11 * (1.0 + 2.0 * B.delta * s);  // relative to the charging curvature
+    }
+    bool okk = true;
+    for (int t = 0; t < N; ++t) {
+      double* dft = &Df[(size_t)t * nb];
+      double* dit = &Di[(size_t)t * nb];
+      double* lft = &Lf[(size_t)t * nb];
+      for (int k = 0; k < nb; ++k) {
+        const double Dt = dbox[k * N + t] + rho[k];
+        const double Dn = t + 1 < N ? dbox[k * N + t + 1] + rho[k] : 0.0;
+        const double a = 2.0 * B.delta * B.omega[k * N + t] + Dt + Dn - pl[k] * pl[k] * pd[k];  // (t = 0: pl = 0)
+        okk = okk && a > 0.0;
+        const double ia = 1.0 / a;  // (one division per stage)
+        const double l = t + 1 < N ? -Dn * ia : 0.0;  // L_{t+1,t}
+        dft[k] = a;
+        dit[k] = ia;
+        lft[k] = l;
+        pl[k] = l;
+        pd[k] = a;
+      }
+    }
+    if (!okk) return false;
     // S = sum_k c_k^2 T_k^-1 (upper triangle), block by block in block order; T_k^-1 row by row from
     // the LDL' factors: X_jj = 1/d_j + l_j^2 X_{j+1,j+1} and, right of the diagonal, row i = -l_i x
     // row i+1 (L'X = D^-1 L^-1 is lower triangular) — ONE row buffer per block, scaled in place and
     // added into S (no N x N inverse per block is stored)
     for (int k = 0; k < nb; ++k) {
-      // static regularisation (the EXP weights 5^(t-N+1) leave early steps with almost no
-      // curvature); iterative refinement against the exact matrix removes its bias
-      double s = 0.0;
-      for (int t = 0; t < N; ++t) s += B.omega[k * N + t];
-      const double rho = 1e-11 * (1.0 + 2.0 * B.delta * s);  // relative to the charging curvature
-      // LDL' of the tridiagonal T_k: diag a_t, sub-diagonal c_t = -D_{t+1} (rows t+1, t)
-      double prev_l = 0.0, prev_d = 0.0;
-      for (int t = 0; t < N; ++t) {
-        const double Dt = dbox[k * N + t] + rho;
-        const double Dn = t + 1 < N ? dbox[k * N + t + 1] + rho : 0.0;
-        double a = 2.0 * B.delta * B.omega[k * N + t] + Dt + Dn;
-        if (t > 0) a -= prev_l * prev_l * prev_d;
-        if (!(a > 0.0)) return false;
-        const double ia = 1.0 / a;  // (one division per stage)
-        dd[t] = ia;
-        ll[t] = t + 1 < N ? -Dn * ia : 0.0;  // L_{t+1,t}
-        Df[(size_t)t * nb + k] = a;
-        Di[(size_t)t * nb + k] = ia;
-        Lf[(size_t)t * nb + k] = ll[t];
-        prev_l = ll[t];
-        prev_d = a;
-      }
       if (ck[k] == 0.0) continue;
       const double c2 = ck[k] * ck[k];
       double* r = row.data();
-      r[N - 1] = dd[N - 1];
+      r[N - 1] = Di[(size_t)(N - 1) * nb + k];
       S[(size_t)(N - 1) * N + N - 1] += c2 * r[N - 1];
       for (int i = N - 2; i >= 0; --i) {
-        const double li = ll[i];
-        const double diag = dd[i] + li * li * r[i + 1];  // (dd: 1 / d)
+        const double li = Lf[(size_t)i * nb + k];
+        const double diag = Di[(size_t)i * nb + k] + li * li * r[i + 1];  // (Di: 1 / d)
         for (int j = i + 1; j < N; ++j) r[j] *= -li;
         r[i] = diag;
         double* si = &S[(size_t)i * N];
@@ -448,26 +458,30 @@ struct Newton {
 
   // y = M x with the exact (unregularised) Newton matrix
   void apply(const Bimpc& B, const double* dbox, const double* x, double* y) const {
-    ap_r.resize(N);
     ap_Lx.resize(N);
     ap_Qy.resize(N);
     ap_tmp.resize(n);
-    double* r = ap_r.data();
     double* Lx = ap_Lx.data();
     double* Qy = ap_Qy.data();
     double* tmp = ap_tmp.data();
-    for (int k = 0; k < nb; ++k) {
-      double s = 0.0, acc = 0.0;
-      // 2 delta A'Omega A x_k: prefix sums then suffix sums
-      for (int t = 0; t < N; ++t) {
-        acc += x[k * N + t];
-        r[t] = 2.0 * B.delta * B.omega[k * N + t] * acc;
+    // 2 delta A'Omega A x_k for every block: prefix sums then suffix sums, stage-major (stage t of all
+    // blocks together: the blocks' independent recurrences overlap instead of 2P latency chains)
+    ap_acc.assign(nb, 0.0);
+    ap_rk.resize((size_t)N * nb);
+    double* acc = ap_acc.data();
+    double* rk = ap_rk.data();  // [t][k]
+    const double d2 = 2.0 * B.delta;
+    for (int t = 0; t < N; ++t)
+      for (int k = 0; k < nb; ++k) {
+        acc[k] += x[k * N + t];
+        rk[(size_t)t * nb + k] = d2 * B.omega[k * N + t] * acc[k];
       }
-      for (int t = N - 1; t >= 0; --t) {
-        s += r[t];
-        y[k * N + t] = s + dbox[k * N + t] * x[k * N + t];
+    std::fill(acc, acc + nb, 0.0);
+    for (int t = N - 1; t >= 0; --t)
+      for (int k = 0; k < nb; ++k) {
+        acc[k] += rk[(size_t)t * nb + k];
+        y[k * N + t] = acc[k] + dbox[k * N + t] * x[k * N + t];
       }
-    }
     for (int t = 0; t < N; ++t) y[nb * N + t] = Du[t] * x[nb * N + t];
     mulL(B, x, Lx);
     for (int i = 0; i < N; ++i) Qy[i] = lqd::dot(&Q[(size_t)i * N], Lx, N);

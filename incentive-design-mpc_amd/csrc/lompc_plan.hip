@@ -650,6 +650,7 @@ struct EvalArgs {
   int cap;                // pieces staged in LDS (a set with more re-solves the rest individually)
   int nblk;               // workgroups of EVs (close mode: workgroup nblk closes the empty sets)
   const int* skip;        // device-resident price loop: nonzero = the loop has finished, run nothing
+  int piece_sums;         // (k_evals, no w output) per-stage sums from per-piece aggregates, no rows
 };
 
 // cost / A_bar error / price0 of a QP solved by the whole wave (lane t = w_t), valid on every lane
@@ -1122,6 +1123,10 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
                            // re-solved) EVs, which then add exactly 0 to the row sums and need no
                            // branch in the row loop
   const int ZD = cap + 1;  // (CLOSE) zero piece whose row is not written: re-solved EVs
+  // (k_evals of a run with no w output: the set's per-stage sums from per-piece EV counts and
+  // fixed-point gamma sums — sum_p n_p a_p + Gamma_p b_p, unclamped, as the close mode and k_agg —
+  // instead of evaluating and summing every EV's N rows that are never stored)
+  const bool psum = !CLOSE && !STG && ro.pipelined && a.piece_sums && !aw;
   LQ_STAMPE(0);
   LQ_WSTART();
   const int NS = eval_row_stride(N);
@@ -1237,7 +1242,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       if (lane == 0) s_mx = G <= 64 ? (int)m : LQ_PPL;
     }
     if (tid < 2 * NS) s_ab[ZK * NS + tid] = make_double2(0.0, 0.0);  // both zero pieces
-    if (CLOSE && tid < cap + 2) {
+    if ((CLOSE || psum) && tid < cap + 2) {
       s_pf[tid] = 0ull;
       s_pn[tid] = 0;
     }
@@ -1329,7 +1334,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       if (acost) st_ev8(acost + i, cst);
       if (aw0) st_ev8(aw0 + i, w0v);
       if (astatus) astatus[i] = LOMPC_QP_OK;
-      if (CLOSE) {
+      if (CLOSE || psum) {
         atomicAdd(s_pn + key, 1);
         atomicAdd(s_pf + key, (unsigned long long)rint(fmax(g - wlo, 0.0) * fxs));
       }
@@ -1566,7 +1571,7 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
       any_inv = inv_rows;
       const int r0b = STG ? sg0 + 64 * h : EVAL_EVS * h + 64 * wv;
       const int nh = STG ? min(64, sgn - 64 * h) : max(0, min(64, end - start - r0b));  // wave-uniform
-      if (nh > 0) row_segment(r0b, nh);
+      if (nh > 0 && !psum) row_segment(r0b, nh);
       if (LQ_EVAL_OUT_AFTER_ROWS) lookup_out(h);
     }
     if (lane == 0) st_wt4(a.fail_cnt + (size_t)rb * EVAL_WAVES + wv, nlist);
@@ -1607,6 +1612,23 @@ __device__ __forceinline__ void eval_block(const EvalArgs& a, const int blk, con
         old = __shfl(old, 0, 64);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         if (old == EVAL_WAVES - 1) {
+          if (psum) {
+            // every wave's lookups (and their LDS piece aggregates) are complete: the per-stage sums
+            // over the set's piece slots in slot order (lane = stage) into this wave's row sums (the
+            // other waves' are zero: they evaluated no rows)
+            const double fxi = (whi - wlo) * 0x1p-40;
+            double accs = 0.0;
+            for (int p = 0; p < np; ++p) {
+              const int n = s_pn[p];
+              if (n == 0) continue;  // (block-uniform)
+              const double2 ab = s_ab[abx(p, min(lane, N - 1))];
+              const double gsum = fma((double)s_pf[p], fxi, (double)n * wlo);
+              accs = fma((double)n, ab.x, accs);
+              accs = fma(gsum, ab.y, accs);
+            }
+            if (lane < N) accw_w[lane] = accs;  // (its own row: zero, no rows were evaluated)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          }
           store_record(lane, 64);
           if (lane == 0) __hip_atomic_store(&s_done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -3224,6 +3246,7 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
     EvalArgs ea;
     FinalArgs ff;
     eval_args(p, lmbd, lmbd_r, w, cost, w0, status, tab(0), ea, ff);
+    ea.piece_sums = w ? 0 : 1;  // (no rows to store: the per-stage sums from the piece aggregates)
     ea.blk = reinterpret_cast<const int4*>(z.d_map);
     ea.nblk = z.nblk;
     ea.partial = z.rpart;

@@ -45,7 +45,10 @@ lm = torch.as_tensor(np.stack([np.concatenate([c.theta * rng.random((P, 3 * N)) 
                      device="cuda")
 lr = torch.zeros((K, 2 * P), dtype=torch.float64, device="cuda")
 wr = torch.as_tensor(np.concatenate([c.w_max * rng.random((P, N)) for c in cs]), device="cuda")
-plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], w_ref=wr)
+SET_ONLY = "--set" in sys.argv  # (the reductions-only contract: no per-EV outputs, the per-piece sums)
+CELLS = int(os.environ.get("ES_CELLS", "4"))
+plan = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], w_ref=wr, want_w=not SET_ONLY, want_cost=not SET_ONLY,
+                 cells=CELLS)
 for _ in range(3):
     plan.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True)
 plan.check()
@@ -58,7 +61,7 @@ t0 = st8[:, 0, 0].min()
 st8 -= t0
 st = st8[:, :, [0, 5, 6, 7]]  # start, staged, rows done, end
 span = st[:, :, 3].max()
-print(f"workgroups {nb}, runs {K}{' (nostage)' if NOSTAGE else ''}: launch span (first start .. last end) "
+print(f"workgroups {nb}, runs {K}, cells {CELLS}{' (nostage)' if NOSTAGE else ''}{' (set only)' if SET_ONLY else ''}: launch span (first start .. last end) "
       f"{span:.2f} us = {span / K:.2f} us per run")
 ph = {"blockmap": st8[:, :, 1] - st8[:, :, 0], "scalars": st8[:, :, 2] - st8[:, :, 1],
       "counts": st8[:, :, 3] - st8[:, :, 2], "pieces": st8[:, :, 4] - st8[:, :, 3],

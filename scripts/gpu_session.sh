@@ -60,6 +60,8 @@ for s in $STEPS; do
     bdistst) run bdistst 600 python bench.py --force-dist --steps 20 --warmup 5 --no-cpu-baseline --no-direct --no-contracts ;;
     bst) run bst 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-direct --no-contracts ;;
     bprofh) run bprofh 300 python scripts/bimpc_prof.py ;;
+    pipetests) run pipetests 600 $PYT tests/test_gpu_pipeline.py tests/test_gpu_parity.py -m gpu ;;
+    contracts) run contracts 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-station --no-direct ;;
     looptests) run looptests 600 $PYT tests/test_gpu_price_loop_c5.py tests/test_gpu_price_loop_long.py tests/test_gpu_price_solver.py tests/test_gpu_chain.py tests/test_gpu_comm.py tests/test_gpu_station.py -m gpu ;;
     *) echo "unknown step $s" ;;
   esac

@@ -453,7 +453,9 @@ def test_run_steps_matches_single_runs(gpu, want_w, K):
         for key in ("w", "cost", "status"):
             if out.get(key) is not None:
                 assert torch.equal(out[key], runs[-1][key]), key
-        staged = plan.info()["evals_staged"]
+        # (runs without w: the wide form's evaluation sums per-piece aggregates, n_p a_p + Gamma_p b_p
+        # unclamped, where the single runs sum the clamped rows — equal to 1e-12, as the staged form)
+        staged = plan.info()["evals_staged"] or (not want_w and cells is None)
         for k in range(K):
             for key in ("set_sum_w", "set_stats"):
                 same_sets(out[key][k], runs[k][key], staged, (cells, k, key))
@@ -467,7 +469,11 @@ def test_run_steps_matches_single_runs(gpu, want_w, K):
         assert seq.check()[1:] == (0, 0)
         for key in ("w", "cost", "status", "set_sum_w", "set_stats"):
             if out.get(key) is not None:
-                assert torch.equal(out[key], out_s[key]), key
+                if want_w or key not in ("set_sum_w", "set_stats"):
+                    assert torch.equal(out[key], out_s[key]), key
+                else:  # (no w: the wide form sums per-piece aggregates, the split form the clamped rows)
+                    for k in range(K):
+                        same_sets(out[key][k], out_s[key][k], True, (cells, k, key, "split"))
         # every output per run (per-EV outputs at a per-run stride, every closing writes its run's
         # re-solved rows): every run's outputs those of its single run; the span events count the
         # steady-state launches
@@ -488,7 +494,8 @@ def test_run_steps_matches_single_runs(gpu, want_w, K):
                 for key in ("w", "cost", "status", "set_sum_w", "set_stats"):
                     if o.get(key) is not None:
                         if key in ("set_sum_w", "set_stats"):
-                            same_sets(o[key][k], runs[k][key], pr.info()["evals_staged"], (cells, split, k, key))
+                            same_sets(o[key][k], runs[k][key], pr.info()["evals_staged"] or not want_w,
+                                      (cells, split, k, key))
                         else:
                             assert torch.equal(o[key][k], runs[k][key]), (cells, split, k, key)
     if K != 7 or not want_w:
@@ -626,3 +633,49 @@ def test_sorted_gamma_aggregation(gpu, N, diag_repair):
     with pytest.raises(Exception):
         uns.check()
     assert ou["set_stats"].cpu().numpy()[3, _lib.LOMPC_STAT_N_FAILED] == off[4] - off[3]
+
+
+@pytest.mark.parametrize("ev", ["small", "large"])
+def test_run_steps_piece_sums_match_oracle(gpu, ev):
+    """The reductions-only contract (price_solver.py:196-214: only the per-set sums of w, the max
+    A_bar error and the counts leave) through the wide run_steps: its evaluation sums each certified
+    piece's EVs from their count and fixed-point gamma sum (n_p a_p + Gamma_p b_p, unclamped) instead of
+    evaluating N rows per EV.  Every run's sums equal the oracle's per-EV sums (to the unclamped
+    aggregates' documented tolerance, DESIGN §10: rtol 1e-10, atol 1e-9), with EVs at and next to the
+    box bounds, a set of one EV and an empty set; the max error and the counts as the rows form."""
+    rng = np.random.default_rng(90 + (ev == "large"))
+    c = O.small_consts() if ev == "small" else O.large_consts()
+    N, K = 24, 5
+    parts = [np.concatenate([np.zeros(200), np.full(200, c.y_max), 1e-9 * rng.random(200),
+                             c.y_max - 1e-9 * rng.random(200), c.y_max * rng.random(3000)]),
+             c.y_max * rng.random(1), np.zeros(0), c.y_max - (0.3 + 0.2 * rng.random(9000))]
+    gn = np.concatenate(parts)
+    off = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.int64)
+    S = len(parts)
+    g = torch.as_tensor(gn, device="cuda:0")
+    lm = torch.as_tensor(c.theta * rng.random((K, S, 3 * N)), device="cuda:0")
+    lm[:, 0, :N] = 0.0  # (set 0: no charging price, the upper bound active)
+    lr = torch.as_tensor(0.1 * rng.random((K, S)), device="cuda:0")
+    wr = torch.as_tensor(c.w_max * rng.random((S, N)), device="cuda:0")
+    lompc = mk(c, N)
+    red = BatchPlan(lompc, g, off, w_ref=wr, want_w=False, want_cost=False, cells=4)
+    rows = BatchPlan(lompc, g, off, w_ref=wr, want_w=True, want_cost=False, cells=4)
+    o = red.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True)
+    orow = rows.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True)
+    assert red.check()[1:] == (0, 0) and rows.check()[1:] == (0, 0)
+    sw, st = o["set_sum_w"].cpu().numpy(), o["set_stats"].cpu().numpy()
+    stw = orow["set_stats"].cpu().numpy()
+    np.testing.assert_allclose(sw, orow["set_sum_w"].cpu().numpy(), rtol=1e-11, atol=1e-11)
+    np.testing.assert_array_equal(st[:, :, _lib.LOMPC_STAT_MAX_ERR], stw[:, :, _lib.LOMPC_STAT_MAX_ERR])
+    np.testing.assert_array_equal(st[:, :, _lib.LOMPC_STAT_COUNT], stw[:, :, _lib.LOMPC_STAT_COUNT])
+    lmn, lrn = lm.cpu().numpy(), lr.cpu().numpy()
+    for k in range(K):
+        for s in range(S):
+            a, b = off[s], off[s + 1]
+            assert st[k, s, _lib.LOMPC_STAT_COUNT] == b - a
+            if b == a:
+                assert np.all(sw[k, s] == 0.0)
+                continue
+            wo, _, nf = oracle_c.solve_batch(N, c, lmn[k, s], float(lrn[k, s]), gn[a:b])
+            assert nf == 0
+            np.testing.assert_allclose(sw[k, s], wo.sum(0), rtol=1e-10, atol=1e-9, err_msg=f"run {k} set {s}")

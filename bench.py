@@ -639,20 +639,84 @@ def direct_leg(eng, N, P, args, nsteps, dev, torch):
     return {"value": B * n / dt, "unit": "QP/s", "ms_per_step": dt / n * 1e3, "steps": n, "repaired_qps": rep}
 
 
+def sorted_reductions_leg(base, lm_ptr, lr_ptr, stride, args, torch, comm, red):
+    """``reductions`` over each set's gamma in ascending order (contract_legs); ``vs_reductions``: the
+    largest relative difference of its last step's per-set sums of w and costs from the unsorted
+    ``reductions`` leg's (the same EVs: only the summation order and the 2^-40 quantisation differ)."""
+    from lompc_amd import BatchPlan
+    from lompc_amd import _lib
+
+    K = args.steps
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gs = base.gamma.clone()
+    off = base.off
+    for s in range(len(off) - 1):
+        a, b = int(off[s]), int(off[s + 1])
+        gs[a:b] = torch.sort(base.gamma[a:b]).values
+    plan = BatchPlan(base.lompcs, gs, off, sets_per_ctx=base.sets_per_ctx, w_ref=base.w_ref, want_set=True,
+                     stream=torch.cuda.current_stream(), cells=base.info()["cells"], want_w=False, want_cost=False,
+                     sorted_gamma=True)
+    torch.cuda.synchronize()
+    prep_ms = (time.perf_counter() - t0) * 1e3
+    if comm is not None:
+        plan.set_comm(comm)
+    plan.run_steps(lm_ptr[0], lr_ptr, max(args.warmup, 1), stride, 0)
+    assert plan.check()[1:] == (0, 0)
+    plan.profile(enable=("k_eval", "k_path"))
+    call, res = plan.steps_call(lm_ptr[args.warmup], lr_ptr, K, stride, 0, span_events=True, per_run_sets=True)
+    call()  # (the same call once untimed: its outputs and events warm)
+    plan.check()
+    plan.profile(read=True, reset=True)
+    plan.profile(read=True, reset=True, kernel="k_path")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    call()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    rep, fail, inv = plan.check()
+    assert fail == 0 and inv == 0, ("reductions_sorted", fail, inv)
+    ms_a, n_a = plan.profile(read=True)
+    ms_p, n_p = plan.profile(read=True, kernel="k_path")
+    plan.profile(enable=False)
+    sw, ss = res["set_sum_w"][-1], res["set_stats"][-1]
+    rw, rs = red["set_sum_w"][-1], red["set_stats"][-1]
+    dw = float(((sw - rw).abs() / rw.abs().clamp_min(1e-300)).max())
+    c = _lib.LOMPC_STAT_SUM_COST
+    dc = float(((ss[:, c] - rs[:, c]).abs() / rs[:, c].abs().clamp_min(1e-300)).max())
+    B = plan.B
+    del plan
+    return {"value": B * K / dt, "unit": "QP/s", "ms_per_step": dt / K * 1e3, "steps": K,
+            "outputs": "every step's set reductions its own ([K][S][...])", "repaired_qps": rep,
+            "k_aggs_us_per_step": ms_a / max(n_a, 1) * 1e3, "k_paths_us_per_step": ms_p / K * 1e3 if n_p else None,
+            "launches": "per group of up to 64 steps: k_paths + k_aggs (one workgroup per (step, set))",
+            "prepare_ms": prep_ms,
+            "prepare": "once per population: per-set torch.sort of gamma + plan construction (fixed-point prefix "
+                       "sums and the fine bucket index of every set, allocation included)",
+            "vs_reductions": {"max_rel_set_sum_w": dw, "max_rel_sum_cost": dc},
+            "roofline": None,
+            "roofline_note": "O(pieces) per set: no per-EV bytes move per step; bound by the path and aggregation "
+                             "latency chains"}
+
+
 def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
     """The per-iteration contracts the reference actually runs on the same batch (both EV types,
     2P sets, fresh prices every step), each K steps in one lompc_plan_run_steps call (the wide
-    form: the K paths in one launch, then one k_step launch per step carrying step k's evaluation —
-    lookups and the per-stage row sums, no rows stored — and step k-1's closing):
+    form: per group of up to 64 steps one k_paths, one k_evals and one k_closes launch):
 
     * ``reductions`` — PriceSolver._get_w_err (price_solver.py:196-214): only the per-set sums of
       w, the max A_bar error and the counts leave the engine (the reference drops w0, :206);
-      algorithmic HBM bytes = gamma in = 8 B per QP;
-    * ``w0`` — get_w0_price0 (price_solver.py:272-285): w0 per EV out + price0 sums: 16 B per QP.
+      algorithmic HBM bytes = gamma in = 8 B per QP; k_evals sums each certified piece's EVs from
+      their count and fixed-point gamma sum (no rows evaluated);
+    * ``w0`` — get_w0_price0 (price_solver.py:272-285): w0 per EV out + price0 sums: 16 B per QP;
+    * ``reductions_sorted`` — ``reductions`` on the same sets with each set's gamma ascending (as the
+      station's partitions are: ranges of the sorted charge levels): per group one k_paths and one
+      k_aggs launch, O(pieces) per set, no per-EV bytes; the sort and the plan's prefix sums are
+      prepare work, once per population (``prepare_ms``), not per step.
 
-    Each reports QP/s, ms per step and the k_step launch time (one HIP-event pair over the steady-state
-    launches) with its HBM roofline at that contract's bytes (latency-bound: 8-16 B per QP is far below what
-    one launch can move; the path chain sets the launch time)."""
+    Each reports QP/s, ms per step and the evaluation launch's time per step (one HIP-event pair around
+    the launch, read as its steps) with its HBM roofline at that contract's bytes (latency-bound: 8-16 B
+    per QP is far below what one launch can move; staging and lookup rounds set the launch time)."""
     from lompc_amd import BatchPlan
 
     base = run["plan"]
@@ -672,9 +736,11 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
         plan.profile(read=True, reset=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        plan.run_steps(lm_ptr[args.warmup], lr_ptr, K, stride, 0, span_events=True, per_run_sets=True)
+        res = plan.run_steps(lm_ptr[args.warmup], lr_ptr, K, stride, 0, span_events=True, per_run_sets=True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        if name == "reductions":
+            red = {k: res[k].clone() for k in ("set_sum_w", "set_stats")}
         rep, fail, inv = plan.check()
         assert fail == 0 and inv == 0, (name, fail, inv)
         ms_e, n_e = plan.profile(read=True)
@@ -683,14 +749,16 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
         gbs = bpq * B / (ev_us * 1e-6) / 1e9 if n_e else 0.0
         out[name] = {"value": B * K / dt, "unit": "QP/s", "ms_per_step": dt / K * 1e3, "steps": K,
                      "outputs": "every step's set reductions its own ([K][S][...]); w0 one buffer every step rewrites",
-                     "repaired_qps": rep, "k_step_avg_us": ev_us, "k_step_launches_timed": n_e,
-                     "roofline": {"bound": "hbm", "kernel": "k_step", "bytes_per_qp": bpq,
+                     "repaired_qps": rep, "k_evals_avg_us": ev_us, "k_evals_steps_timed": n_e,
+                     "roofline": {"bound": "hbm", "kernel": "k_evals", "bytes_per_qp": bpq,
                                   "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-                                  "note": ("the evaluation + closing launch of the wide form (the K paths run in "
-                                           "one k_paths launch before, not in this duration): latency-bound, its "
-                                           "staging and lookup rounds, not 8-16 B per QP, set its time")}}
+                                  "note": ("the evaluation launch of the wide form per step (the K paths run in "
+                                           "one k_paths launch before, the closings in one k_closes launch after, "
+                                           "neither in this duration): latency-bound, its staging and lookup rounds, "
+                                           "not 8-16 B per QP, set its time")}}
         plan.profile(enable=False)
         del plan
+    out["reductions_sorted"] = sorted_reductions_leg(base, lm_ptr, lr_ptr, stride, args, torch, comm, red)
     # the headline's workload with every step's rows in their OWN buffer (w at a per-step stride: K x 50 MB
     # of fresh lines, which the 256 MB Infinity Cache cannot hold — the HBM-resident form of the roofline)
     base.profile(enable=("k_eval",))

@@ -573,7 +573,7 @@ __device__ __forceinline__ AggSetOut agg_finish(const AggArgs& r, const AggSet& 
       if (WT) st_wt8(r.set_stats + (size_t)s * LOMPC_SET_STATS + lane, x);
       else r.set_stats[(size_t)s * LOMPC_SET_STATS + lane] = x;
     }
-    r.stats[(size_t)s * LOMPC_SET_STATS + lane] = x;
+    if (r.stats) r.stats[(size_t)s * LOMPC_SET_STATS + lane] = x;
   }
   if (lane == 0 && r.tally) {
     if (rr > 0.0) __hip_atomic_fetch_add(r.tally + 0, (unsigned long long)rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -584,13 +584,10 @@ __device__ __forceinline__ AggSetOut agg_finish(const AggArgs& r, const AggSet& 
   return AggSetOut{v, x};
 }
 
-// one workgroup per set, wave wv: cells wv, wv + nw, ...; the waves' records combined in wave order
+// set s by one workgroup, wave wv: cells wv, wv + nw, ...; the waves' records combined in wave order
 template <int NT>
-__global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
-  __shared__ double s_w[LQ_AGG_W][LOMPC_MAX_N];
-  __shared__ double s_x[LQ_AGG_W][8];  // cost, price0, max err^2, repaired, failed
-  if (r.skip && *r.skip) return;
-  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+__device__ __forceinline__ void agg_set_block(const AggArgs& r, const int s, double (*s_w)[LOMPC_MAX_N], double (*s_x)[8]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
   const AggSet z = agg_set_init<NT>(r, s);
   lq_tab_init(*z.q);  // (the individual re-solves' box table)
   AggPart a;
@@ -603,6 +600,53 @@ __global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
     agg_finish<false, false, LQ_AGG_W>(r, z, s, lane, nw, [&](int k) { return s_w[k][lane]; }, [&](int k) { return s_x[k][min(lane, 7)]; });
 }
 
+// one workgroup per set
+template <int NT>
+__global__ __launch_bounds__(64 * LQ_AGG_W) void k_agg(AggArgs r) {
+  __shared__ double s_w[LQ_AGG_W][LOMPC_MAX_N];
+  __shared__ double s_x[LQ_AGG_W][8];  // cost, price0, max err^2, repaired, failed
+  if (r.skip && *r.skip) return;
+  agg_set_block<NT>(r, (int)blockIdx.x, s_w, s_x);
+}
+
+// The wide form over gamma-sorted sets (lompc_plan_run_steps without per-EV outputs): one workgroup
+// per (run, set) of a path group, after the group's k_paths launch — run j's prices at lmbd + j
+// lm_stride, its tables in ring slot j % slots, its set outputs at out_base + (rel ? j - run0 : j)
+// stride (rel: the group's contiguous send records).  k_agg's per-set work with the same cell-to-wave
+// map and record order, so the same bits as one k_agg launch per run.  Only the last run writes the
+// plan's stats scratch.
+struct AggsArgs {
+  int run0, slots, last, rel;
+  int64_t lm_stride, lr_stride, sw_stride, st_stride;
+};
+
+template <int NT>
+__global__ __launch_bounds__(64 * LQ_AGG_W) void k_aggs(AggArgs r0, AggsArgs x) {
+  __shared__ double s_w[LQ_AGG_W][LOMPC_MAX_N];
+  __shared__ double s_x[LQ_AGG_W][8];
+  const int rr = (int)blockIdx.x / r0.S, s = (int)blockIdx.x - rr * r0.S;
+  const int j = x.run0 + rr, jo = x.rel ? rr : j;
+  const int64_t o = (int64_t)(j % x.slots) * r0.S * r0.G;
+  const int N = NT ? NT : r0.N;
+  AggArgs r = r0;
+  r.lmbd = r0.lmbd + (size_t)j * x.lm_stride;
+  r.lmbd_r = r0.lmbd_r + (size_t)j * x.lr_stride;
+  r.t_cnt = r0.t_cnt + o;
+  r.t_lo = r0.t_lo + o;
+  r.t_sl = r0.t_sl + o * 64;
+  r.t_ge = r0.t_ge + o * LQ_PPL;
+  r.t_cf = r0.t_cf + o * LQ_PPL * 8;
+  r.t_ab = r0.t_ab + o * LQ_PPL * N;
+  r.set_sum_w = r0.set_sum_w ? r0.set_sum_w + (size_t)jo * x.sw_stride : nullptr;
+  r.set_stats = r0.set_stats ? r0.set_stats + (size_t)jo * x.st_stride : nullptr;
+  if (j != x.last) {  // (a zero stride: every run's outputs at one place, the last run's win)
+    r.stats = nullptr;
+    if (!x.rel && x.sw_stride == 0) r.set_sum_w = nullptr;
+    if (!x.rel && x.st_stride == 0) r.set_stats = nullptr;
+  }
+  agg_set_block<NT>(r, s, s_w, s_x);
+}
+
 typedef void (*AggKernel)(AggArgs);
 AggKernel agg_kernel(int N) {
   switch (N) {
@@ -611,5 +655,16 @@ AggKernel agg_kernel(int N) {
     case 24: return k_agg<24>;
     case 48: return k_agg<48>;
     default: return k_agg<0>;
+  }
+}
+
+typedef void (*AggsKernel)(AggArgs, AggsArgs);
+AggsKernel aggs_kernel(int N) {
+  switch (N) {
+    case 12: return k_aggs<12>;
+    case 16: return k_aggs<16>;
+    case 24: return k_aggs<24>;
+    case 48: return k_aggs<48>;
+    default: return k_aggs<0>;
   }
 }

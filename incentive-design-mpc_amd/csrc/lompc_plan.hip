@@ -3120,6 +3120,39 @@ int stepped_setup(lompc_plan* p, hipStream_t st, bool wide) {
 #endif
 #define LQ_WIDE_BYTES (1ll << 30)        // wide form: the table ring's memory at most
 
+// The wide form's runs per path launch for K runs: bounded by the table ring's memory
+// (LQ_WIDE_BYTES) and the grid (fit: the most the plan allows; < 1: the plan is too big for two slots)
+int64_t wide_fit(const lompc_plan* p) {
+  const int64_t ncell = p->S * p->G;
+  const int64_t cell_bytes = LQ_PPL * (16 * (int64_t)p->N + 8 * 8 + 8) + 4 + 8 + 64;
+  return std::min<int64_t>(LQ_WIDE_BYTES / (ncell * cell_bytes), INT32_MAX / 64 / ncell) - 1;
+}
+
+// the wide form's table ring, sized for the largest group the plan allows whatever this call's K (a
+// later call with more runs must not reallocate — hipMalloc / hipFree synchronise the device)
+int wide_ring(lompc_plan* p, hipStream_t st) {
+  auto& z = p->stp;
+  int rc;
+  const int N = p->N;
+  const int64_t ncell = p->S * p->G;
+  const int64_t ring = (std::min<int64_t>(LQ_WIDE_RUNS, wide_fit(p)) + 1) * ncell;
+  if (ring > z.cap_wt) {
+    auto& t = z.wt;
+    const int64_t c = ring;
+    if ((rc = grow(p, &t.cnt, c)) || (rc = grow(p, &t.lo, c)) || (rc = grow(p, &t.ge, c * LQ_PPL)) ||
+        (rc = grow(p, &t.cf, c * LQ_PPL * 8)) || (rc = grow(p, &t.ab, c * LQ_PPL * N)) || (rc = grow(p, &t.sl, c * 64)))
+      return rc;
+    // every slot written once now, in the call that sizes the ring (a plan's first wide call: the
+    // warmup), so a later call's first use of a slot meets no cold page translations
+    HIPCHK(p, hipMemsetAsync(t.ge, 0, (size_t)c * LQ_PPL * sizeof(*t.ge), st));
+    HIPCHK(p, hipMemsetAsync(t.cf, 0, (size_t)c * LQ_PPL * 8 * sizeof(*t.cf), st));
+    HIPCHK(p, hipMemsetAsync(t.ab, 0, (size_t)c * LQ_PPL * N * sizeof(*t.ab), st));
+    HIPCHK(p, hipMemsetAsync(t.sl, 0, (size_t)c * 64 * sizeof(*t.sl), st));
+    z.cap_wt = c;
+  }
+  return LOMPC_OK;
+}
+
 // K >= 1 independent runs.  Two schedules, one per plan kind:
 // * wide (no warm start — every run's path depends on its own prices only): the paths of up to
 //   LQ_WIDE_RUNS runs in ONE k_paths launch, then launch k (0 <= k <= K) = k_step(run k's evaluation
@@ -3150,33 +3183,15 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   const int N = p->N;
   const int64_t ncell = p->S * p->G, L = p->S * (N + LOMPC_SET_STATS);
   const int K = n_runs;
-  // wide: runs per path launch, bounded by the table ring's memory (LQ_WIDE_BYTES) and the grid; a
-  // plan too big for two table slots takes the stepped form
-  const int64_t cell_bytes = LQ_PPL * (16 * (int64_t)N + 8 * 8 + 8) + 4 + 8 + 64;
-  const int64_t fit = std::min<int64_t>(LQ_WIDE_BYTES / (ncell * cell_bytes), INT32_MAX / 64 / ncell) - 1;
+  // wide: runs per path launch (wide_fit); a plan too big for two table slots takes the stepped form
+  const int64_t fit = wide_fit(p);
   const int Kc = (int)std::min<int64_t>({(int64_t)K, LQ_WIDE_RUNS, fit});
   const bool wide = (p->flags & LOMPC_PLAN_WARM_START) == 0 && Kc >= 1;
   const int slots = Kc + 1;
   if ((!z.ok || z.wide != wide || z.stg != (wide && evals_stg_ok(p))) && (rc = stepped_setup(p, st, wide))) return rc;
   const bool xr = p->comm != nullptr;
   if (xr && (rc = lq_xbufs(p, 2))) return rc;
-  // (the ring sized for the largest group the plan allows, whatever this call's K: a later call with
-  // more runs must not reallocate — hipMalloc / hipFree synchronise the device)
-  const int64_t ring = (std::min<int64_t>(LQ_WIDE_RUNS, fit) + 1) * ncell;
-  if (wide && ring > z.cap_wt) {
-    auto& t = z.wt;
-    const int64_t c = ring;
-    if ((rc = grow(p, &t.cnt, c)) || (rc = grow(p, &t.lo, c)) || (rc = grow(p, &t.ge, c * LQ_PPL)) ||
-        (rc = grow(p, &t.cf, c * LQ_PPL * 8)) || (rc = grow(p, &t.ab, c * LQ_PPL * N)) || (rc = grow(p, &t.sl, c * 64)))
-      return rc;
-    // every slot written once now, in the call that sizes the ring (a plan's first wide call: the
-    // warmup), so a later call's first use of a slot meets no cold page translations
-    HIPCHK(p, hipMemsetAsync(t.ge, 0, (size_t)c * LQ_PPL * sizeof(*t.ge), st));
-    HIPCHK(p, hipMemsetAsync(t.cf, 0, (size_t)c * LQ_PPL * 8 * sizeof(*t.cf), st));
-    HIPCHK(p, hipMemsetAsync(t.ab, 0, (size_t)c * LQ_PPL * N * sizeof(*t.ab), st));
-    HIPCHK(p, hipMemsetAsync(t.sl, 0, (size_t)c * 64 * sizeof(*t.sl), st));
-    z.cap_wt = c;
-  }
+  if (wide && (rc = wide_ring(p, st))) return rc;
   auto tab = [&](int j) {
     if (wide) {  // ring slot j % slots
       const int64_t o = (int64_t)(j % slots) * ncell;
@@ -3397,6 +3412,67 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   return LOMPC_OK;
 }
 
+// Reductions-only runs over gamma-sorted sets (k_agg plans), wide: per group of up to Kc runs TWO
+// launches — k_paths (the group's paths into the table ring, as the wide form) and k_aggs (one
+// workgroup per (run, set): k_agg's per-piece aggregation on run j's tables).  The same kernels'
+// arithmetic as one k_path + k_agg per run (the sequential form, LOMPC_STEPS_PER_KERNEL), so the same
+// bits.  With a communicator the group's closings fill its contiguous send records: ONE all-gather and
+// one combine per group, as the wide form.  K_EVAL events: the k_aggs launch, as n runs.
+int lq_run_steps_aggs(lompc_plan* p, const double* lmbd, int64_t lmbd_stride, const double* lmbd_r,
+                      int64_t lmbd_r_stride, int K, bool span_events, double* set_sum_w, int64_t sw_stride,
+                      double* set_stats, int64_t st_stride, hipStream_t st) {
+  int rc;
+  const int N = p->N;
+  const int64_t ncell = p->S * p->G, L = p->S * (N + LOMPC_SET_STATS);
+  const int Kc = (int)std::min<int64_t>({(int64_t)K, LQ_WIDE_RUNS, wide_fit(p)});
+  const int slots = Kc + 1;
+  if ((rc = wide_ring(p, st))) return rc;
+  const bool xr = p->comm != nullptr;
+  if (xr && (rc = lq_xbufs(p, Kc, Kc))) return rc;
+  const PathTab& wt = p->stp.wt;
+  const PathArgs pw = path_args(p, lmbd, lmbd_r, wt);
+  const AggArgs ga{(int)p->S, p->G, N, p->aggF, p->d_q, p->ce, p->d_set_off, p->d_window, p->gamma, lmbd, lmbd_r,
+                   p->w_ref, wt.cnt, wt.lo, wt.sl, wt.ge, wt.cf, wt.ab, p->d_P, p->B + p->S, p->d_pos,
+                   p->d_sinfo, xr ? p->d_xsend : set_sum_w, xr ? p->d_xsend + p->S * N : set_stats, p->d_stats,
+                   p->d_tally, nullptr};
+  const int nw = std::min(p->G, (int)LQ_AGG_W);
+  for (int g0 = 0; g0 < K; g0 += Kc) {
+    const int n = std::min(Kc, K - g0);
+    {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      if (plan_prof_begin(p, LOMPC_PLAN_K_PATH, &e0, &e1)) return fail_arg(p, "profiling events");
+      hipExtLaunchKernelGGL(paths_kernel(N), dim3((unsigned)(n * ncell)), dim3(64), 0, st, e0, e1, 0, pw, lmbd_stride,
+                            lmbd_r_stride, g0, slots);
+      HIPCHK(p, hipGetLastError());
+      plan_prof_end(p, LOMPC_PLAN_K_PATH, e0, e1);
+    }
+    {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      const bool ev = !span_events || g0 == 0;
+      if (ev && plan_prof_begin(p, LOMPC_PLAN_K_EVAL, &e0, &e1)) return fail_arg(p, "profiling events");
+      const AggsArgs x{g0, slots, K - 1, xr ? 1 : 0, lmbd_stride, lmbd_r_stride, xr ? L : sw_stride, xr ? L : st_stride};
+      hipExtLaunchKernelGGL(aggs_kernel(N), dim3((unsigned)(n * p->S)), dim3(64 * nw), 0, st, e0, e1, 0, ga, x);
+      HIPCHK(p, hipGetLastError());
+      if (ev) plan_prof_end(p, LOMPC_PLAN_K_EVAL, e0, e1, n);
+    }
+    if (xr) {
+      if ((rc = lq_comm_allgather(p->comm, p->d_xsend, p->d_xrecv, (size_t)n * L, st))) {
+        p->err = p->comm->err;
+        return rc;
+      }
+      if (set_sum_w || set_stats) {
+        const CombineRunsArgs ca{p->d_xrecv, p->comm->nranks, n, (int)p->S, N, g0, K - 1, set_sum_w, set_stats,
+                                 sw_stride, st_stride};
+        const int64_t tot = (int64_t)n * L;
+        hipLaunchKernelGGL(k_combine_runs, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((tot + 255) / 256, 1024))),
+                           dim3(256), 0, st, ca);
+        HIPCHK(p, hipGetLastError());
+      }
+    }
+  }
+  return LOMPC_OK;
+}
+
 extern "C" {
 
 int lompc_plan_run(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* w, double* cost, double* w0,
@@ -3422,6 +3498,13 @@ int lompc_plan_run_steps(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   // sums the rows it does not store)
   const bool per_ev = w || cost || w0 || status;
   const bool agg = p->sorted && !per_ev;
+  // gamma-sorted sets without per-EV output: per group of runs one k_paths and one k_aggs launch
+  // (the sequential form below on request: LOMPC_STEPS_PER_KERNEL, the same bits)
+  if (n_runs >= 1 && !p->skip && agg && p->nblk > 0 && (p->flags & LOMPC_PLAN_WARM_START) == 0 &&
+      !(steps_flags & LOMPC_STEPS_PER_KERNEL) && wide_fit(p) >= 1)
+    return lq_run_steps_aggs(p, lmbd, lmbd_stride, lmbd_r, lmbd_r_stride, n_runs,
+                             (steps_flags & LOMPC_STEPS_SPAN_EVENTS) != 0, set_sum_w, set_sum_w_stride, set_stats,
+                             set_stats_stride, st);
   if (n_runs >= 1 && !p->skip && !agg && !p->close && p->nblk > 0 && p->G % LQ_STEP_CELLS == 0)
     return lq_run_steps_stepped(p, lmbd, lmbd_stride, lmbd_r, lmbd_r_stride, n_runs, profile_every,
                                 (steps_flags & LOMPC_STEPS_SPAN_EVENTS) != 0, w, cost, w0, status, ev_stride,

@@ -102,6 +102,30 @@ def test_plan_with_comm_equals_plain(nccl1, want_w):
                     assert torch.equal(v, o_s[key]), (per_kernel, per_run, key)
 
 
+def test_sorted_wide_with_comm_equals_plain(nccl1):
+    """run_steps over gamma-sorted sets without per-EV output (k_paths + k_aggs per group) with the
+    communicator: the group's per-set records go to its contiguous send records, ONE all-gather and one
+    combine per group — bitwise the plain plan's outputs, per run and shared, both issue forms."""
+    from lompc_amd.dist import device_comm
+
+    N, P, K = 24, 6, 9
+    lompcs, off, g, wr, lm, lr = _two_type_batch(np.random.default_rng(5), N, P, [20000, 17001], K)
+    gs = g.clone()
+    for s in range(2 * P):  # each set's gamma ascending
+        gs[off[s]:off[s + 1]] = torch.sort(g[off[s]:off[s + 1]]).values
+    kw = dict(sets_per_ctx=[P, P], w_ref=wr, want_w=False, want_cost=False, sorted_gamma=True)
+    plain = BatchPlan(lompcs, gs, off, **kw)
+    shard = BatchPlan(lompcs, gs, off, **kw).set_comm(device_comm(nccl1, 0))
+    st = (lm[0].numel(), lr[0].numel())
+    for per_kernel in (False, True):
+        for per_run_sets in (False, True):
+            o_s = shard.run_steps(lm, lr, K, *st, per_run_sets=per_run_sets, per_kernel=per_kernel)
+            o_p = plain.run_steps(lm, lr, K, *st, per_run_sets=per_run_sets)
+            assert shard.check()[1:] == (0, 0) and plain.check()[1:] == (0, 0)
+            for key in ("set_sum_w", "set_stats"):
+                assert torch.equal(o_p[key], o_s[key]), (per_kernel, per_run_sets, key)
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 @pytest.mark.parametrize("S,N", [(24, 24), (24, 48), (5000, 64)])
 def test_combine_records_matches_python_combine(gpu, nranks, S, N):

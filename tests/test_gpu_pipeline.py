@@ -635,6 +635,67 @@ def test_sorted_gamma_aggregation(gpu, N, diag_repair):
     assert ou["set_stats"].cpu().numpy()[3, _lib.LOMPC_STAT_N_FAILED] == off[4] - off[3]
 
 
+def test_run_steps_sorted_wide(gpu):
+    """run_steps over gamma-sorted sets without per-EV output (the reductions contract on the
+    station's sorted partitions): per group of up to 64 runs ONE k_paths and ONE k_aggs launch (one
+    workgroup per (run, set), k_agg's per-piece aggregation on the run's ring slot).  Every run's set
+    sums and stats equal, bitwise, the sequential form (LOMPC_STEPS_PER_KERNEL: k_path + k_agg per run)
+    and single runs; 70 runs take two groups (the ring wraps); shared outputs hold the last run's; the
+    sums match the oracle's per-EV sums (rtol 1e-10, atol 1e-9, test_sorted_gamma_aggregation's bar);
+    empty, one-EV, clustered and box-bound sets."""
+    rng = np.random.default_rng(71)
+    N, K = 24, 70
+    cs = [O.small_consts(), O.large_consts()]
+    lompcs = [mk(c, N) for c in cs]
+    sizes = [[0, 1, 64, 30000], [20000, 0, 1500, 7]]
+    parts = []
+    for k, c in enumerate(cs):
+        for m in sizes[k]:
+            g = c.y_max * rng.random(m)
+            if m == 1500:
+                g = np.repeat(c.y_max * rng.random(50), 30)
+            if m >= 20000:
+                g[:5] = 0.0
+                g[5:10] = c.y_max
+            parts.append(np.sort(g))
+    off = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.int64)
+    P = len(sizes[0])
+    gn = np.concatenate(parts)
+    g = torch.as_tensor(gn, device="cuda:0")
+    lm = torch.as_tensor(np.stack([np.concatenate([c.theta * rng.random((P, 3 * N)) for c in cs]) for _ in range(K)]),
+                         device="cuda:0")
+    lr = torch.as_tensor(0.2 * rng.random((K, 2 * P)), device="cuda:0")
+    wr = torch.as_tensor(np.concatenate([c.w_max * rng.random((P, N)) for c in cs]), device="cuda:0")
+    agg = BatchPlan(lompcs, g, off, sets_per_ctx=[P, P], w_ref=wr, want_w=False, want_cost=False, sorted_gamma=True)
+    st = (lm[0].numel(), lr[0].numel())
+    ow = {k: v.clone() for k, v in agg.run_steps(lm, lr, K, *st, per_run_sets=True).items() if v is not None}
+    rw, fw, iw = agg.check()
+    assert (fw, iw) == (0, 0)
+    osq = agg.run_steps(lm, lr, K, *st, per_run_sets=True, per_kernel=True)
+    assert agg.check() == (rw, 0, 0)
+    for key in ("set_sum_w", "set_stats"):
+        assert torch.equal(ow[key], osq[key]), key
+    for k in (0, 1, 63, 64, K - 1):
+        o1 = agg.run(lm[k], lr[k])
+        assert torch.equal(o1["set_sum_w"], ow["set_sum_w"][k]) and torch.equal(o1["set_stats"], ow["set_stats"][k]), k
+    agg.check()
+    osh = agg.run_steps(lm, lr, K, *st)  # shared outputs: the last run's
+    assert agg.check()[1:] == (0, 0)
+    assert torch.equal(osh["set_sum_w"], ow["set_sum_w"][-1]) and torch.equal(osh["set_stats"], ow["set_stats"][-1])
+    sa = ow["set_stats"].cpu().numpy()
+    np.testing.assert_array_equal(sa[:, :, _lib.LOMPC_STAT_COUNT], np.broadcast_to(np.diff(off), (K, 2 * P)))
+    for k in (0, 64, K - 1):
+        for s in range(2 * P):
+            a, b = off[s], off[s + 1]
+            if b == a:
+                continue
+            c = cs[s // P]
+            wo, co, nf = oracle_c.solve_batch(N, c, lm[k, s].cpu().numpy(), float(lr[k, s]), gn[a:b])
+            assert nf == 0
+            np.testing.assert_allclose(ow["set_sum_w"][k, s].cpu().numpy(), wo.sum(0), rtol=1e-10, atol=1e-9)
+            assert abs(sa[k, s, _lib.LOMPC_STAT_SUM_COST] - co.sum()) <= 1e-10 * max(1.0, abs(co.sum()))
+
+
 @pytest.mark.parametrize("ev", ["small", "large"])
 def test_run_steps_piece_sums_match_oracle(gpu, ev):
     """The reductions-only contract (price_solver.py:196-214: only the per-set sums of w, the max

@@ -949,7 +949,8 @@ def station_leg(args, world, dev, sharded=False):
             st._step()
             torch.cuda.synchronize()
             per_step.append(time.perf_counter() - ts)
-            parts.append((dict(st.last_step_ms), dict(st.chain_ms), (st.bimpc.last_info or {}).get("solve_ms", 0.0)))
+            parts.append((dict(st.last_step_ms), dict(st.chain_ms), (st.bimpc.last_info or {}).get("solve_ms", 0.0),
+                          dict(st.bimpc_split)))
             check_station_state(st, consts)
         if world > 1:
             dist.barrier()
@@ -1008,14 +1009,16 @@ def station_attribution(ms, parts, stats, warm, steps):
            (("Small", "niter_s"), ("Large", "niter_l"))}
     its = {k: np.where(v >= 0, v, 0).sum(axis=0) for k, v in its.items()}
     rows = []
-    for j, (marks, chains, ipm) in enumerate(parts):
+    for j, (marks, chains, ipm, split) in enumerate(parts):
         b = marks.get("bimpc", 0.0)
         slow = max(chains, key=chains.get) if chains else None
         rows.append({"ms": float(ms[j]), "bimpc_ipm": float(ipm), "bimpc_exposed_staging": float(b - ipm),
                      "prices": float(marks.get("prices", 0.0)),
                      "chain_small": float(chains.get("Small", 0.0)), "chain_large": float(chains.get("Large", 0.0)),
                      "slower_chain": slow, "slower_chain_iterations": int(its[slow][j]) if slow else None,
-                     "w0_price0": float(marks.get("w0_price0", 0.0)), "state": float(marks.get("state", 0.0))})
+                     "w0_price0": float(marks.get("w0_price0", 0.0)), "state": float(marks.get("state", 0.0)),
+                     "bimpc_split": {k: (round(v, 3) if isinstance(v, float) else {a: round(x, 3) for a, x in v.items()})
+                                     for k, v in split.items()}})
     out = {"per_step": rows}
     tot = np.array([r["bimpc_ipm"] + r["bimpc_exposed_staging"] + r["prices"] + r["w0_price0"] + r["state"]
                     for r in rows])

@@ -191,6 +191,7 @@ struct lompc_plan {
   // pinned staging of the host arrays
   char* h_buf = nullptr;
   int64_t cap_h = 0;
+  int64_t reserve_B = 0;  // lompc_plan_reserve: batch size the buffers are sized for when they first grow
   int64_t h_off_at = 0;           // byte offset of the set offsets in h_buf
   hipEvent_t ev_stage = nullptr;
   // HIP-event profiling, per kernel (LOMPC_PLAN_K_*): enabled mask, pairs since the last read

@@ -2229,10 +2229,12 @@ LoopIterKernel loop_iter_kernel(int N) {
 
 // ---------------------------------------------------------------- host helpers
 
-// capacities of the buffers a re-targeted plan (lompc_plan_update) may outgrow: 1/4 headroom, so a
-// batch that varies a little from call to call (a station's partitions, step to step) stops
-// reallocating (hipMalloc / hipHostMalloc synchronise the device and cost far more than a run)
-int64_t with_slack(int64_t n) { return n + n / 4 + 16; }
+// capacities of the buffers a re-targeted plan (lompc_plan_update) may outgrow: 1/4 headroom, and at
+// least double the previous capacity, so a batch whose size wanders from call to call (a station's
+// partitions, step to step: EVs move between charge-level partitions) reallocates O(log) times, not
+// at every new high (hipMalloc / hipHostMalloc took 50-470 us per re-targeted plan in the station's
+// staging, scripts/stage_profile.py)
+int64_t with_slack(int64_t n, int64_t cap) { return std::max(n + n / 4 + 16, 2 * cap); }
 
 int pick_cells(int64_t max_set, int flags) {
   const int g = (flags >> LOMPC_PLAN_CELLS_SHIFT) & 2047;  // the caller's choice (LOMPC_PLAN_CELLS)
@@ -2296,9 +2298,25 @@ void plan_prof_end(lompc_plan* p, int k, hipEvent_t e0, hipEvent_t e1, int launc
   p->prof_mult[k].push_back(launches);
 }
 
+#ifdef LQ_PREP_PROF  // diagnostic builds: lq_plan_prepare's phases on stderr (host microseconds)
+#define LQ_PREP_MARK(k) prep_t[k] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count()
+#else
+#define LQ_PREP_MARK(k)
+#endif
 int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64_t* sets_per_ctx, int64_t B,
                     const double* gamma, const int64_t* set_offsets, const double* w_ref, int flags,
                     hipStream_t st) {
+#ifdef LQ_PREP_PROF
+  double prep_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  struct PrepPrint {
+    double* t;
+    ~PrepPrint() {
+      fprintf(stderr, "prep us: checks %.1f occ %.1f grow %.1f evsync %.1f host %.1f copy %.1f kernels %.1f\n", t[1] - t[0],
+              t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t[6] - t[5], t[7] - t[6]);
+    }
+  } prep_print{prep_t};
+#endif
+  LQ_PREP_MARK(0);
   if (nctx < 1 || nctx > LQ_PLAN_MAX_CTX || !ctxs || !sets_per_ctx || !set_offsets)
     return fail_arg(p, "plan: 1 <= n_ctx <= LOMPC_PLAN_MAX_CTX contexts and their set counts required");
   int64_t S = 0;
@@ -2332,6 +2350,7 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     HIPCHK(p, hipDeviceGetAttribute(&p->n_cu, hipDeviceAttributeMultiprocessorCount, ctxs[0]->device));
     if (p->n_cu < 1) p->n_cu = 1;
   }
+  LQ_PREP_MARK(1);
   const int cap = std::min(LQ_PIECE_CAP, G * LQ_PPL);
   const int64_t occ_key = (int64_t)N * 4096 + cap;
   if (p->eval_occ_key != occ_key) {  // k_eval workgroups resident per CU (either variant may run)
@@ -2341,6 +2360,7 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     p->eval_occ = std::max(std::min(occ0, occ1), 1);
     p->eval_occ_key = occ_key;
   }
+  LQ_PREP_MARK(2);
   const int64_t slots = (int64_t)p->n_cu * p->eval_occ;
   const int64_t rounds = std::max<int64_t>(1, (10 * B + 9ll * slots * EVAL_MAXB - 1) / (9ll * slots * EVAL_MAXB));
   const int64_t target = rounds * slots;
@@ -2351,6 +2371,10 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   };
   int64_t nblk = 0;
   int64_t n_empty = 0;
+  // lompc_plan_reserve: a buffer that must grow is sized at once for the reserved batch size (upper
+  // bounds: blocks_of(m) <= ceil(m / 256), sorted blocks ceil(m / LQ_AGG_SB) per set)
+  const int64_t RB = std::max(B, p->reserve_B);
+  const int64_t nblk_r = p->reserve_B ? RB / 256 + S + 1 : 0, nsblk_r = p->reserve_B ? RB / LQ_AGG_SB + S + 1 : 0;
   for (int64_t s = 0; s < S; ++s) {
     const int64_t nb = blocks_of(set_offsets[s + 1] - set_offsets[s]);
     nblk += nb;
@@ -2378,7 +2402,7 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     p->cap_S = S;
   }
   if (nblk > p->cap_blk) {
-    const int64_t c = with_slack(nblk);
+    const int64_t c = std::max(with_slack(nblk, p->cap_blk), nblk_r);
     if ((rc = grow(p, &p->d_partial, (size_t)c * (N + NPX))) ||
         (rc = grow(p, &p->d_fail_cnt, (size_t)c * EVAL_WAVES)) || (rc = grow(p, &p->d_fail_idx, (size_t)c * EVAL_MAXB)))
       return rc;
@@ -2430,9 +2454,15 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   const size_t o_sblk = o_pre + up16((size_t)(S + 1) * sizeof(int));
   const size_t o_spre = o_sblk + up16((size_t)nsblk * sizeof(int4));
   const size_t need_h = sorted ? o_spre + up16((size_t)(S + 1) * sizeof(int)) : o_sblk;
+  const size_t need_h_r = p->reserve_B ? up16(LQ_PLAN_MAX_CTX * sizeof(QPConst)) + up16((size_t)nblk_r * sizeof(int4)) +
+                                             2 * up16((size_t)(S + 1) * sizeof(int64_t)) + up16((size_t)nsblk_r * sizeof(int4)) +
+                                             up16((size_t)(S + 1) * sizeof(int))
+                                       : 0;
+  LQ_PREP_MARK(3);
   HIPCHK(p, hipEventSynchronize(p->ev_stage));  // (the staging may still feed the previous copy)
+  LQ_PREP_MARK(4);
   if ((int64_t)need_h > p->cap_h) {
-    const int64_t c = with_slack((int64_t)need_h);
+    const int64_t c = std::max(with_slack((int64_t)need_h, p->cap_h), (int64_t)need_h_r);
     if (p->h_buf) HIPCHK(p, hipHostFree(p->h_buf));
     p->h_buf = nullptr;
     HIPCHK(p, hipHostMalloc((void**)&p->h_buf, (size_t)c, hipHostMallocDefault));
@@ -2478,12 +2508,12 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     p->aggF = G * LQ_AGG_KF;
     const int64_t nP = 3 * (B + S), npos = S * (int64_t)(p->aggF + 1);
     if (nsblk > p->cap_sblk) {
-      const int64_t c = with_slack(nsblk);
+      const int64_t c = std::max(with_slack(nsblk, p->cap_sblk), nsblk_r);
       if ((rc = grow(p, &p->d_bsum, (size_t)c * 4))) return rc;
       p->cap_sblk = c;
     }
     if (nP > p->cap_P) {
-      const int64_t c = with_slack(nP);
+      const int64_t c = std::max(with_slack(nP, p->cap_P), p->reserve_B ? 3 * (RB + S) : 0);
       if ((rc = grow(p, &p->d_P, c))) return rc;
       p->cap_P = c;
     }
@@ -2496,8 +2526,10 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
       p->cap_sinfo = S;
     }
   }
+  LQ_PREP_MARK(5);
   HIPCHK(p, hipMemcpyAsync(p->d_meta, p->h_buf, need_h, hipMemcpyHostToDevice, st));
   HIPCHK(p, hipEventRecord(p->ev_stage, st));
+  LQ_PREP_MARK(6);
   WindowArgs wa{p->d_q, p->ce, p->d_blk, p->d_blk_prefix, gamma, p->d_wacc, p->d_window, (int)S, (int)nblk};
   if (sorted) hipLaunchKernelGGL(k_plan_window_sorted, dim3((unsigned)S), dim3(64), 0, st, wa, p->d_set_off);
   else hipLaunchKernelGGL(k_plan_window, dim3((unsigned)nblk + 1), dim3(256), 0, st, wa);
@@ -2510,6 +2542,7 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
     if (nsblk > 0) hipLaunchKernelGGL(k_sorted_fill, dim3((unsigned)nsblk), dim3(256), 0, st, sa);
     HIPCHK(p, hipGetLastError());
   }
+  LQ_PREP_MARK(7);
   return LOMPC_OK;
 }
 
@@ -2883,6 +2916,12 @@ int lompc_plan_update(lompc_plan* p, int64_t B, const double* gamma, const int64
     prev = e;
   }
   return lq_plan_prepare(p, p->nctx, p->ctx, spc, B, gamma, set_offsets, w_ref, p->flags, (hipStream_t)stream);
+}
+
+int lompc_plan_reserve(lompc_plan* p, int64_t max_B) {
+  if (!p || max_B < 0 || max_B >= (1ll << 31) - EVAL_MAXB) return LOMPC_ERR_INVALID_ARG;
+  p->reserve_B = max_B;
+  return LOMPC_OK;
 }
 
 }  // extern "C"

@@ -99,6 +99,7 @@ SIGNATURES = [
     ("lompc_plan_status", _I, [_P, _P, _P, _P, _P]),
     ("lompc_plan_get_info", _I, [_P, _P, _P, _P, _P, _P]),
     ("lompc_plan_update", _I, [_P, _L, _P, _P, _P, _P]),
+    ("lompc_plan_reserve", _I, [_P, _L]),
     ("lompc_price_loop", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     ("lompc_price_chain", _I, [_I, _P, _P, _P, _P]),
     ("lompc_plan_profile_enable", _I, [_P, _I]),

@@ -177,6 +177,8 @@ class ChargingStation:
         self.phase_ms = {}
         self.last_step_ms = {}  # host time of the last step's phases (_tick)
         self.chain_ms = {}  # the last step's price chain per EV type (host time of its native call)
+        self.stage_ms = {}  # the last step's staging thread per EV type (host time)
+        self.bimpc_split = {}  # the last step's BiMPC phase split (_get_bimpc_solution)
         self._gl_host, self._gl_keep = {}, {}  # _gamma_layout's pinned run bounds per price solver
         # the w0 / price0 pass of both types in one engine run (False: one per type — A/B timing)
         self.w0_one_call = True
@@ -191,6 +193,10 @@ class ChargingStation:
                                           group=lgroup)
         self.price_solver_l = PriceSolver(self.N_lo, self.consts_l, self.price_type, device=self.device, mode=mode,
                                           group=lgroup)
+        # every partition's loop plan is sized for the whole population of its type at its first
+        # growth (partitions gain and lose EVs step to step: no reallocation inside the later steps)
+        for ps in (self.price_solver_s, self.price_solver_l):
+            ps.reserve_evs = self.M_2
         # Initialize state variables = (EV SoCs, charge stored).
         self._init_states()
         # Initialize logs.
@@ -448,6 +454,7 @@ class ChargingStation:
 
     def _get_bimpc_solution(self, lmbd_r: float):
         # charging_station.py:187-266
+        t_in = time.perf_counter()
         Mp_s, Mp_l = np.zeros((self.P,), dtype=int), np.zeros((self.P,), dtype=int)
         beta_s, beta_l = np.zeros((self.P,)), np.zeros((self.P,))
         gamma_sm, gamma_lm = np.zeros((self.P,)), np.zeros((self.P,))
@@ -477,16 +484,27 @@ class ChargingStation:
                 beta_l[p], gamma_lm[p] = self._robustness(self.price_solver_l, st_l[p], lmbd_r)
         self._pstats = (st_s, st_l)
         self._staged = self.stage_partitions
+        self.stage_ms = {}
+        t_stage = time.perf_counter()
         staging = self._stage_partitions() if self._staged else []
         Mp_s_ = Mp_s / self.B
         Mp_l_ = Mp_l / self.B
         demand = self.demand[self.t: self.t + self.N_bi] / self.B
         bimpc_params = BiMPCParameters(Mp_s_, Mp_l_, beta_s, beta_l, gamma_sm, gamma_lm, self.x, demand)
+        t_call = time.perf_counter()
         try:
             w_hat_s, w_hat_l, u_g = self.bimpc.solve_bimpc(bimpc_params)
         finally:
+            t_wait = time.perf_counter()
             for f in staging:  # (the partition plans were staged beside the host interior point)
                 f.result()
+        t_out = time.perf_counter()
+        # where the BiMPC phase's host time goes (bench.py's station attribution): the partition
+        # statistics before the staging starts, the staging threads' submit, the solve call, and the
+        # wait for staging the solve did not hide; stage_ms: each staging thread's own duration
+        self.bimpc_split = {"stats_ms": (t_stage - t_in) * 1e3, "submit_ms": (t_call - t_stage) * 1e3,
+                            "solve_call_ms": (t_wait - t_call) * 1e3, "stage_wait_ms": (t_out - t_wait) * 1e3,
+                            "stage_thread_ms": dict(self.stage_ms)}
         stats_bi = {"Mp_s": Mp_s, "Mp_l": Mp_l, "beta_s": beta_s, "beta_l": beta_l, "gamma_sm": gamma_sm,
                     "gamma_lm": gamma_lm}
         if _settings.PRINT_LEVEL >= 1 and self._rank0():
@@ -635,13 +653,25 @@ class ChargingStation:
 
         def stage(job):
             kind, solver, y, idx, st = job
+            t0 = time.perf_counter()
+            try:
+                stage_body(kind, solver, y, idx, st)
+            finally:
+                self.stage_ms[kind] = (time.perf_counter() - t0) * 1e3
+
+        def stage_body(kind, solver, y, idx, st):
             with torch.cuda.device(self.device), torch.cuda.stream(solver._stream):
                 # the type's partition layout too (its sorts and one host sync: on this thread, beside
                 # the interior point, not before it); its tensors are read on the main stream later
+                t0 = time.perf_counter()
                 _, ys, seg = self._partition_layout(kind, y, idx, main)
+                t1 = time.perf_counter()
                 gam, at = self._gamma_layout(solver, ys, seg, st) if self.gamma_layout else (None, None)
                 if self.replicated:  # (this rank's EVs in that layout, for the w0 pass: made here, off the step's path)
                     self._w0_layout(kind, main)
+                t2 = time.perf_counter()
+                self.stage_ms[kind + "/layout"] = (t1 - t0) * 1e3
+                self.stage_ms[kind + "/gamma"] = (t2 - t1) * 1e3
                 for p in range(self.P):
                     if st[p, 0] > 0:
                         a, b = seg[p]

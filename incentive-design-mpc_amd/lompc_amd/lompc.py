@@ -493,6 +493,13 @@ class BatchPlan:
                 self._check_rc(rc)
         return self
 
+    def reserve(self, max_B: int) -> "BatchPlan":
+        """Size hint (lompc_plan_reserve): a later ``update`` that must grow a workspace sizes it
+        for batches of up to max_B EVs at once (no allocation now)."""
+        if not self.direct:
+            self._check_rc(self._lib.lompc_plan_reserve(self._plan, int(max_B)))
+        return self
+
     def _usable(self) -> None:
         if getattr(self, "_broken", None):
             raise RuntimeError(f"BatchPlan unusable after a failed update: {self._broken[1]}")

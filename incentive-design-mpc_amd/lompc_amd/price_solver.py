@@ -101,6 +101,7 @@ class PriceSolver:
         self._h_st = torch.zeros((2, _lib.LOMPC_SET_STATS), dtype=torch.float64).pin_memory()
         self._plan = None
         self.loop_cells = None  # path cells per set of the loop plans (None: the engine's choice)
+        self.reserve_evs = 0  # > 0: the loop plans' workspaces sized for this many EVs (BatchPlan.reserve)
         self._plan_w0 = None
         self._w0_live = False
         self._staged = {}  # partition -> its loop plan and levels (stage_partition / use_partition)
@@ -300,6 +301,8 @@ class PriceSolver:
             self._plan = BatchPlan(self.lompc, self._gam, off, w_ref=self._wr2, want_w=False, want_cost=False,
                                    want_set=True, validate=False, warm_start=True,
                                    sorted_gamma=self.lompc.mode != "direct", cells=self.loop_cells)
+            if self.reserve_evs:  # (its later partitions' batches: no reallocation, lompc_plan_reserve)
+                self._plan.reserve(self.reserve_evs + central)
             comm = self._device_comm()
             if comm is not None:
                 self._plan.set_comm(comm)

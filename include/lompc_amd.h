@@ -208,6 +208,13 @@ int lompc_plan_create(int n_ctx, lompc_ctx* const* ctxs, const int64_t* sets_per
 int lompc_plan_update(lompc_plan* plan, int64_t B, const double* gamma, const int64_t* set_offsets,
                       const double* w_ref, void* stream);
 
+/* Size hint for a plan re-targeted at batches of varying size (a station's per-partition loop
+ * plans: EVs move between partitions from step to step): when a later lompc_plan_update must
+ * grow a workspace, it sizes it for batches of up to max_B EVs at once, so the plan stops
+ * reallocating (each hipMalloc / hipHostMalloc costs 50-470 us of host time and synchronises the
+ * device).  No allocation happens in this call; 0 clears the hint. */
+int lompc_plan_reserve(lompc_plan* plan, int64_t max_B);
+
 /* One price iteration of the whole batch: the exact LoMPC optimum of every EV at the
  * prices of its set plus the fused per-set reductions.  Outputs as lompc_solve_batch, in
  * the caller's EV order (each may be NULL):

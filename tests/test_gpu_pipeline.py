@@ -635,6 +635,40 @@ def test_sorted_gamma_aggregation(gpu, N, diag_repair):
     assert ou["set_stats"].cpu().numpy()[3, _lib.LOMPC_STAT_N_FAILED] == off[4] - off[3]
 
 
+@pytest.mark.parametrize("reserve", [0, 200000])
+def test_plan_update_matches_fresh_plan(gpu, reserve):
+    """lompc_plan_update re-targets one plan at batches of changing size (the station's partition
+    plans: EVs move between partitions) — growing and shrinking, with and without the
+    lompc_plan_reserve size hint — and every run equals, bitwise, a plan freshly created for that
+    batch (sorted sets without per-EV output, the loop plans' kind; and a plan with w rows)."""
+    rng = np.random.default_rng(33)
+    N = 24
+    c = O.large_consts()
+    lompc = mk(c, N)
+    for kw in (dict(want_w=False, want_cost=False, sorted_gamma=True), dict(want_w=True, want_cost=True)):
+        plan = None
+        for m in (1000, 50000, 300, 120000, 7, 90000):
+            g = np.sort(c.y_max * rng.random(m))
+            off = np.array([0, m // 3, m], dtype=np.int64)
+            gt = torch.as_tensor(g, device="cuda:0")
+            lm = torch.as_tensor(c.theta * rng.random((2, 3 * N)), device="cuda:0")
+            lr = torch.as_tensor([0.1, 0.0], device="cuda:0")
+            if plan is None:
+                plan = BatchPlan(lompc, gt, off, **kw)
+                if reserve:
+                    plan.reserve(reserve)
+            else:
+                plan.update(gt, off)
+            o1 = {k: v.clone() for k, v in plan.run(lm, lr).items() if v is not None}
+            assert plan.check()[1:] == (0, 0)
+            fresh = BatchPlan(lompc, gt, off, **kw)
+            o2 = fresh.run(lm, lr)
+            assert fresh.check()[1:] == (0, 0)
+            for k, v in o2.items():
+                if v is not None:
+                    assert torch.equal(o1[k], v), (m, k)
+
+
 def test_run_steps_sorted_wide(gpu):
     """run_steps over gamma-sorted sets without per-EV output (the reductions contract on the
     station's sorted partitions): per group of up to 64 runs ONE k_paths and ONE k_aggs launch (one

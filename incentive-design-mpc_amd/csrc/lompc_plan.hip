@@ -3275,7 +3275,9 @@ int lq_run_steps_stepped(lompc_plan* p, const double* lmbd, int64_t lmbd_stride,
   const int cap = std::min(LQ_PIECE_CAP, p->G * LQ_PPL);
   const size_t lds = eval_lds(N, p->G, cap);
   const StepKernel kern = step_kernel(N);
-  if (wide && (!split || z.stg)) {
+  // (split runs without w output take the batched launches one run per group too: their evaluation
+  // sums the certified pieces instead of rows, so only these kernels give the wide form's bits)
+  if (wide && (!split || z.stg || !w)) {
     // batched: per path group of n <= Kc runs THREE launches — k_paths (the n paths), k_evals (the n
     // evaluations, each workgroup through its block of every run) and k_closes (the n x S closings);
     // the same kernels' arithmetic as the split form below, so the same bits

@@ -494,10 +494,12 @@ class BatchPlan:
         return self
 
     def reserve(self, max_B: int) -> "BatchPlan":
-        """Size hint (lompc_plan_reserve): a later ``update`` that must grow a workspace sizes it
-        for batches of up to max_B EVs at once (no allocation now)."""
+        """Size hint (lompc_plan_reserve): every workspace that must grow is sized for batches of
+        up to max_B EVs at once.  The plan's current batch is re-prepared here, so the workspaces
+        are allocated now (at plan creation) rather than inside a later ``update``."""
         if not self.direct:
             self._check_rc(self._lib.lompc_plan_reserve(self._plan, int(max_B)))
+            self.update(self.gamma, self.off, self.w_ref, validate=False)
         return self
 
     def _usable(self) -> None:

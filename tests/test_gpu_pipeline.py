@@ -463,17 +463,14 @@ def test_run_steps_matches_single_runs(gpu, want_w, K):
         if cells is None:
             assert plan.info()["steps_group"] == 1  # (shared per-EV outputs: one run per launch)
             assert n >= (K - 1 + E - 1) // E and ms > 0.0
-        # the same runs, one kernel per launch: the same bits
+        # the same runs, one kernel per launch (without w: the batched kernels one run per group, whose
+        # evaluation sums the certified pieces as the wide form's does): the same bits
         seq = BatchPlan(lompcs, g, off, **kw)
         out_s = seq.run_steps(lm, lr, K, lm[0].numel(), lr[0].numel(), per_run_sets=True, per_kernel=True)
         assert seq.check()[1:] == (0, 0)
         for key in ("w", "cost", "status", "set_sum_w", "set_stats"):
             if out.get(key) is not None:
-                if want_w or key not in ("set_sum_w", "set_stats"):
-                    assert torch.equal(out[key], out_s[key]), key
-                else:  # (no w: the wide form sums per-piece aggregates, the split form the clamped rows)
-                    for k in range(K):
-                        same_sets(out[key][k], out_s[key][k], True, (cells, k, key, "split"))
+                assert torch.equal(out[key], out_s[key]), key
         # every output per run (per-EV outputs at a per-run stride, every closing writes its run's
         # re-solved rows): every run's outputs those of its single run; the span events count the
         # steady-state launches
@@ -488,7 +485,8 @@ def test_run_steps_matches_single_runs(gpu, want_w, K):
                 ms, n = pr.profile(read=True)
                 # (batched: one pair around the first group's k_evals, read as its runs; split: the steady launches)
                 # (the staged evaluation's split form: groups of one run, the pair around the first)
-                exp = (1 if pr.info()["evals_staged"] else min(K, 64) - 1) if split else min(K, 64)
+                one = pr.info()["evals_staged"] or not want_w  # (split: groups of one run, the pair around the first)
+                exp = (1 if one else min(K, 64) - 1) if split else min(K, 64)
                 assert n == exp and (ms > 0.0) == (n > 0)
             for k in range(K):
                 for key in ("w", "cost", "status", "set_sum_w", "set_stats"):

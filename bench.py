@@ -640,23 +640,19 @@ def direct_leg(eng, N, P, args, nsteps, dev, torch):
 
 
 def sorted_reductions_leg(base, lm_ptr, lr_ptr, stride, args, torch, comm, red):
-    """``reductions`` over each set's gamma in ascending order (contract_legs); ``vs_reductions``: the
-    largest relative difference of its last step's per-set sums of w and costs from the unsorted
-    ``reductions`` leg's (the same EVs: only the summation order and the 2^-40 quantisation differ)."""
+    """``reductions`` through a ``sort_sets`` plan over the headline's unsorted batch (contract_legs);
+    ``vs_caller_order``: the largest relative difference of its last step's per-set sums of w and
+    costs from the ``reductions_in_caller_order`` leg's (the same EVs: only the summation order and
+    the 2^-40 quantisation differ)."""
     from lompc_amd import BatchPlan
     from lompc_amd import _lib
 
     K = args.steps
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    gs = base.gamma.clone()
-    off = base.off
-    for s in range(len(off) - 1):
-        a, b = int(off[s]), int(off[s + 1])
-        gs[a:b] = torch.sort(base.gamma[a:b]).values
-    plan = BatchPlan(base.lompcs, gs, off, sets_per_ctx=base.sets_per_ctx, w_ref=base.w_ref, want_set=True,
-                     stream=torch.cuda.current_stream(), cells=base.info()["cells"], want_w=False, want_cost=False,
-                     sorted_gamma=True)
+    plan = BatchPlan(base.lompcs, base.gamma, base.off, sets_per_ctx=base.sets_per_ctx, w_ref=base.w_ref,
+                     want_set=True, stream=torch.cuda.current_stream(), cells=base.info()["cells"], want_w=False,
+                     want_cost=False, sort_sets=True, validate=False)
     torch.cuda.synchronize()
     prep_ms = (time.perf_counter() - t0) * 1e3
     if comm is not None:
@@ -675,7 +671,7 @@ def sorted_reductions_leg(base, lm_ptr, lr_ptr, stride, args, torch, comm, red):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     rep, fail, inv = plan.check()
-    assert fail == 0 and inv == 0, ("reductions_sorted", fail, inv)
+    assert fail == 0 and inv == 0, ("reductions", fail, inv)
     ms_a, n_a = plan.profile(read=True)
     ms_p, n_p = plan.profile(read=True, kernel="k_path")
     plan.profile(enable=False)
@@ -691,9 +687,9 @@ def sorted_reductions_leg(base, lm_ptr, lr_ptr, stride, args, torch, comm, red):
             "k_aggs_us_per_step": ms_a / max(n_a, 1) * 1e3, "k_paths_us_per_step": ms_p / K * 1e3 if n_p else None,
             "launches": "per group of up to 64 steps: k_paths + k_aggs (one workgroup per (step, set))",
             "prepare_ms": prep_ms,
-            "prepare": "once per population: per-set torch.sort of gamma + plan construction (fixed-point prefix "
-                       "sums and the fine bucket index of every set, allocation included)",
-            "vs_reductions": {"max_rel_set_sum_w": dw, "max_rel_sum_cost": dc},
+            "prepare": "once per population (BatchPlan(sort_sets=True) construction): each set's gamma sorted on the "
+                       "device, the fixed-point prefix sums and the fine bucket index of every set, allocation included",
+            "vs_caller_order": {"max_rel_set_sum_w": dw, "max_rel_sum_cost": dc},
             "roofline": None,
             "roofline_note": "O(pieces) per set: no per-EV bytes move per step; bound by the path and aggregation "
                              "latency chains"}
@@ -705,14 +701,14 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
     form: per group of up to 64 steps one k_paths, one k_evals and one k_closes launch):
 
     * ``reductions`` — PriceSolver._get_w_err (price_solver.py:196-214): only the per-set sums of
-      w, the max A_bar error and the counts leave the engine (the reference drops w0, :206);
-      algorithmic HBM bytes = gamma in = 8 B per QP; k_evals sums each certified piece's EVs from
-      their count and fixed-point gamma sum (no rows evaluated);
-    * ``w0`` — get_w0_price0 (price_solver.py:272-285): w0 per EV out + price0 sums: 16 B per QP;
-    * ``reductions_sorted`` — ``reductions`` on the same sets with each set's gamma ascending (as the
-      station's partitions are: ranges of the sorted charge levels): per group one k_paths and one
-      k_aggs launch, O(pieces) per set, no per-EV bytes; the sort and the plan's prefix sums are
-      prepare work, once per population (``prepare_ms``), not per step.
+      w, the max A_bar error and the counts leave the engine (the reference drops w0, :206), so the
+      EVs' order inside a set is free: the plan (``BatchPlan(sort_sets=True)``) snapshots the same
+      unsorted batch with each set sorted once at prepare (``prepare_ms``, not per step) and every
+      step is one k_paths + one k_aggs launch per group — O(pieces) per set, no per-EV bytes;
+    * ``reductions_in_caller_order`` — the same contract without the prepare-time sort: k_evals sums
+      each certified piece's EVs from their count and fixed-point gamma sum (no rows evaluated);
+      algorithmic HBM bytes = gamma in = 8 B per QP;
+    * ``w0`` — get_w0_price0 (price_solver.py:272-285): w0 per EV out + price0 sums: 16 B per QP.
 
     Each reports QP/s, ms per step and the evaluation launch's time per step (one HIP-event pair around
     the launch, read as its steps) with its HBM roofline at that contract's bytes (latency-bound: 8-16 B
@@ -723,7 +719,7 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
     out = {}
     lm_ptr, lr_ptr, stride = run["lm_ptr"], run["lr_ptr"], run["lm_stride"]
     K = args.steps
-    for name, kw, bpq in (("reductions", dict(want_w=False, want_cost=False), 8),
+    for name, kw, bpq in (("reductions_in_caller_order", dict(want_w=False, want_cost=False), 8),
                           ("w0", dict(want_w=False, want_cost=False, want_w0=True), 16)):
         plan = BatchPlan(base.lompcs, base.gamma, base.off, sets_per_ctx=base.sets_per_ctx, w_ref=base.w_ref,
                          want_set=True, stream=torch.cuda.current_stream(), warm_start=args.warm,
@@ -739,7 +735,7 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
         res = plan.run_steps(lm_ptr[args.warmup], lr_ptr, K, stride, 0, span_events=True, per_run_sets=True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        if name == "reductions":
+        if name == "reductions_in_caller_order":
             red = {k: res[k].clone() for k in ("set_sum_w", "set_stats")}
         rep, fail, inv = plan.check()
         assert fail == 0 and inv == 0, (name, fail, inv)
@@ -758,7 +754,7 @@ def contract_legs(eng, run, N, P, args, nsteps, dev, torch, comm, pmc):
                                            "not 8-16 B per QP, set its time")}}
         plan.profile(enable=False)
         del plan
-    out["reductions_sorted"] = sorted_reductions_leg(base, lm_ptr, lr_ptr, stride, args, torch, comm, red)
+    out["reductions"] = sorted_reductions_leg(base, lm_ptr, lr_ptr, stride, args, torch, comm, red)
     # the headline's workload with every step's rows in their OWN buffer (w at a per-step stride: K x 50 MB
     # of fresh lines, which the 256 MB Infinity Cache cannot hold — the HBM-resident form of the roofline)
     base.profile(enable=("k_eval",))

@@ -341,7 +341,12 @@ class BatchPlan:
     the k_finalize launch (measured slower with w rows: DESIGN.md §10).  ``sorted_gamma``: every
     set's gamma is ascending and stays unmodified until the next ``update`` — runs without per-EV
     outputs then aggregate per certified piece from prefix sums (k_agg, O(pieces) per run; a set
-    found unsorted reports all its EVs failed).  ``close_in_finalize``: runs without w output close
+    found unsorted reports all its EVs failed).  ``sort_sets``: for plans without per-EV outputs
+    (the price loop's reductions contract, price_solver.py:196-214: only per-set sums leave, so the
+    EVs' order within a set does not matter) — the plan takes a SNAPSHOT of gamma at construction /
+    ``update``, each set sorted ascending on the device (two stable sorts: by gamma, then by set), and
+    runs as ``sorted_gamma`` over it; later in-place changes of the caller's gamma are not seen.
+    ``close_in_finalize``: runs without w output close
     their sets in the k_finalize launch as well (A/B of the close mode).  ``cells``: gamma cells per
     set instead of the plan's choice (the answer does not depend on it).  ``set_comm(comm)``: a
     sharded batch — every run combines the set reductions of all ranks on the device (RCCL).
@@ -351,7 +356,7 @@ class BatchPlan:
     def __init__(self, lompc, gamma, set_offsets, *, sets_per_ctx=None, w_ref=None, gamma_ref=None, want_w=True,
                  want_cost=True, want_w0=False, want_status=False, want_set=True, stream=None, validate=True,
                  warm_start=False, diag_repair=False, close_in_eval=False, sorted_gamma=False,
-                 close_in_finalize=False, cells=None):
+                 close_in_finalize=False, cells=None, sort_sets=False):
         torch = _torch()
         lompcs = list(lompc) if isinstance(lompc, (list, tuple)) else [lompc]
         self.lompcs = lompcs
@@ -372,6 +377,10 @@ class BatchPlan:
             raise ValueError("sets_per_ctx must give one count per context, summing to S")
         self.N = N
         self._want = dict(w=want_w, cost=want_cost, w0=want_w0, status=want_status, set=want_set)
+        self.sort_sets = bool(sort_sets)
+        if self.sort_sets and (want_w or want_cost or want_w0 or want_status):
+            raise ValueError("sort_sets: plans without per-EV outputs only (the EVs are reordered)")
+        sorted_gamma = sorted_gamma or self.sort_sets
         self._stream = (stream if stream is not None else torch.cuda.current_stream(lo.device)).cuda_stream
         self._lib = lo._lib
         self._plan = None
@@ -420,6 +429,15 @@ class BatchPlan:
                 raise AssertionError("gamma <= y_max required")
             if bool(torch.logical_not(gamma >= 0).any()):
                 raise ValueError("Parameter value must be nonnegative.")
+        if getattr(self, "sort_sets", False) and B > 0:
+            # each set's gamma ascending (NaN after the values: torch's sort order), by two stable
+            # sorts — by gamma, then by set — on the device, once per batch
+            g = gamma.to(torch.float64)
+            o1 = torch.sort(g, stable=True).indices
+            sid = torch.repeat_interleave(torch.arange(S, device=g.device),
+                                          torch.as_tensor(np.diff(off), device=g.device))
+            o2 = torch.sort(sid[o1], stable=True).indices
+            gamma = g[o1[o2]].contiguous()
         self.gamma, self.off = gamma, off
         self.w_ref = None if w_ref is None else lo._dev(w_ref).reshape(S, N)
         wt = self._want

@@ -728,6 +728,51 @@ def test_run_steps_sorted_wide(gpu):
             assert abs(sa[k, s, _lib.LOMPC_STAT_SUM_COST] - co.sum()) <= 1e-10 * max(1.0, abs(co.sum()))
 
 
+def test_sort_sets_plan_on_unsorted_batch(gpu):
+    """BatchPlan(sort_sets=True) over an UNSORTED batch (the reductions contract: only per-set sums
+    leave, so the order inside a set is free): the plan snapshots gamma with each set sorted on the
+    device and runs as a sorted_gamma plan — its run_steps (k_paths + k_aggs) equal, bitwise, a
+    sorted_gamma plan over the host-sorted batch, and the oracle's per-EV sums (rtol 1e-10, atol 1e-9);
+    NaN / out-of-range gammas sort after the valid ones and are counted invalid; a plan asking for
+    per-EV outputs is refused."""
+    rng = np.random.default_rng(12)
+    N, K, P = 24, 5, 3
+    cs = [O.small_consts(), O.large_consts()]
+    lompcs = [mk(c, N) for c in cs]
+    sizes = [[5000, 1, 0], [20000, 64, 333]]
+    parts = [c.y_max * rng.random(m) for c, ms in zip(cs, sizes) for m in ms]
+    off = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.int64)
+    gn = np.concatenate(parts)
+    lm = torch.as_tensor(np.stack([np.concatenate([c.theta * rng.random((P, 3 * N)) for c in cs]) for _ in range(K)]),
+                         device="cuda:0")
+    lr = torch.as_tensor(0.1 * rng.random((K, 2 * P)), device="cuda:0")
+    kw = dict(sets_per_ctx=[P, P], want_w=False, want_cost=False)
+    st = (lm[0].numel(), lr[0].numel())
+    a = BatchPlan(lompcs, torch.as_tensor(gn, device="cuda:0"), off, sort_sets=True, **kw)
+    gs = np.concatenate([np.sort(gn[off[s]:off[s + 1]]) for s in range(2 * P)])
+    b = BatchPlan(lompcs, torch.as_tensor(gs, device="cuda:0"), off, sorted_gamma=True, **kw)
+    oa = {k: v.clone() for k, v in a.run_steps(lm, lr, K, *st, per_run_sets=True).items() if v is not None}
+    ob = b.run_steps(lm, lr, K, *st, per_run_sets=True)
+    assert a.check()[1:] == (0, 0) and b.check()[1:] == (0, 0)
+    for key in ("set_sum_w", "set_stats"):
+        assert torch.equal(oa[key], ob[key]), key
+    for s in range(2 * P):
+        if off[s + 1] == off[s]:
+            continue
+        wo, co, nf = oracle_c.solve_batch(N, cs[s // P], lm[K - 1, s].cpu().numpy(), float(lr[K - 1, s]), gn[off[s]:off[s + 1]])
+        assert nf == 0
+        np.testing.assert_allclose(oa["set_sum_w"][K - 1, s].cpu().numpy(), wo.sum(0), rtol=1e-10, atol=1e-9)
+    g2 = gn.copy()
+    g2[[3, 40, 4000]] = [np.nan, 2.0 * cs[0].y_max, np.nan]
+    c = BatchPlan(lompcs, torch.as_tensor(g2, device="cuda:0"), off, sort_sets=True, validate=False, **kw)
+    oc = c.run(lm[0], lr[0])
+    with pytest.raises(AssertionError):
+        c.check()
+    assert oc["set_stats"].cpu().numpy()[0, _lib.LOMPC_STAT_N_INVALID] == 3
+    with pytest.raises(ValueError):
+        BatchPlan(lompcs, torch.as_tensor(gn, device="cuda:0"), off, sets_per_ctx=[P, P], sort_sets=True)
+
+
 @pytest.mark.parametrize("ev", ["small", "large"])
 def test_run_steps_piece_sums_match_oracle(gpu, ev):
     """The reductions-only contract (price_solver.py:196-214: only the per-set sums of w, the max

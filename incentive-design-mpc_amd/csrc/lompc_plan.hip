@@ -2236,6 +2236,75 @@ LoopIterKernel loop_iter_kernel(int N) {
 // staging, scripts/stage_profile.py)
 int64_t with_slack(int64_t n, int64_t cap) { return std::max(n + n / 4 + 16, 2 * cap); }
 
+#ifndef LQ_WIDE_ALPHA
+#define LQ_WIDE_ALPHA 0.85  // EVs of a second-dispatch-round k_eval / k_evals block relative to a first-round one
+#endif
+// The k_eval block map of a batch: every set in near-equal blocks of <= maxb EVs (at least 256),
+// `target` blocks in all, set-major (blocks[b] = (set, first EV, end EV); pre[s] = set s's first block).
+// weighted (one dispatch round of persistent or single launches, more blocks than CUs): the blocks of
+// the later dispatch round (index >= n_cu) get LQ_WIDE_ALPHA of the EVs of the first round's — a CU's
+// second-dispatched workgroup runs ~13 % slower than its first (younger waves: the SIMDs' issue
+// arbitration favours the older workgroup; scripts/evals_stamps.py), and a launch ends
+// with its slowest workgroup.  Each set takes the blocks whose weights cover its share of the batch,
+// and inside a set the EVs split in proportion to the weights.  A map only: the same QPs and per-EV
+// arithmetic, the per-set sums combine per-block records in block order.
+void block_map(const int64_t* off, int64_t S, int64_t B, int64_t maxb, int64_t target, int n_cu, bool weighted,
+               std::vector<int4>& blks, std::vector<int>& pre) {
+  blks.clear();
+  pre.assign((size_t)S + 1, 0);
+  auto blocks_of = [&](int64_t m) -> int64_t {
+    if (m <= 0) return 0;
+    const int64_t lo = (m + maxb - 1) / maxb, hi = (m + 255) / 256;
+    return std::max<int64_t>(lo, std::min<int64_t>(hi, m * target / std::max<int64_t>(B, 1)));
+  };
+  int64_t nblk = 0;
+  for (int64_t s = 0; s < S; ++s) nblk += blocks_of(off[s + 1] - off[s]);
+  if (weighted && LQ_WIDE_ALPHA < 1.0 && nblk > (int64_t)n_cu && B > 0) {
+    std::vector<double> wc((size_t)nblk + 1, 0.0);
+    for (int64_t k = 0; k < nblk; ++k) wc[k + 1] = wc[k] + (k < (int64_t)n_cu ? 1.0 : LQ_WIDE_ALPHA);
+    std::vector<int64_t> lo_of((size_t)S);
+    int64_t need_after = 0;  // blocks the later non-empty sets need at least
+    for (int64_t t = 0; t < S; ++t) {
+      const int64_t m = off[t + 1] - off[t];
+      lo_of[t] = m > 0 ? (m + maxb - 1) / maxb : 0;
+      need_after += lo_of[t];
+    }
+    auto wt = [&](int64_t k) { return k < nblk ? wc[k] : wc[nblk] + (double)(k - nblk) * LQ_WIDE_ALPHA; };
+    int64_t b = 0;
+    for (int64_t s = 0; s < S; ++s) {
+      const int64_t o = off[s], m = off[s + 1] - o;
+      need_after -= lo_of[s];
+      int64_t nb = lo_of[s];
+      if (m > 0) {
+        const double tgt = wc[nblk] * (double)off[s + 1] / (double)B;  // the set's cumulative weight
+        const int64_t hi = std::min<int64_t>((m + 255) / 256, nblk - b - need_after);
+        while (nb < hi && b + nb < nblk && wc[b + nb] + 0.5 * (wc[b + nb + 1] - wc[b + nb]) < tgt) ++nb;
+      }
+      auto fits = [&](int64_t n) {  // every block of the set within maxb EVs (the kernels' LDS rows)
+        const double ws_ = wt(b + n) - wt(b);
+        for (int64_t k = 0; k < n; ++k)
+          if ((double)m * (wt(b + k + 1) - wt(b + k)) / ws_ > (double)(maxb - 2)) return false;
+        return true;
+      };
+      while (m > 0 && nb < m && !fits(nb)) ++nb;
+      const double w0 = wt(b), ws = wt(b + nb) - w0;
+      for (int64_t k = 0; k < nb; ++k) {
+        const int64_t e0 = o + (int64_t)((double)m * (wt(b + k) - w0) / ws);
+        const int64_t e1 = k + 1 == nb ? o + m : o + (int64_t)((double)m * (wt(b + k + 1) - w0) / ws);
+        blks.push_back(make_int4((int)s, (int)e0, (int)e1, 0));
+      }
+      b += nb;
+      pre[s + 1] = (int)b;
+    }
+    return;
+  }
+  for (int64_t s = 0; s < S; ++s) {
+    const int64_t o = off[s], m = off[s + 1] - o, nb = blocks_of(m);
+    for (int64_t k = 0; k < nb; ++k) blks.push_back(make_int4((int)s, (int)(o + m * k / nb), (int)(o + m * (k + 1) / nb), 0));
+    pre[s + 1] = (int)blks.size();
+  }
+}
+
 int pick_cells(int64_t max_set, int flags) {
   const int g = (flags >> LOMPC_PLAN_CELLS_SHIFT) & 2047;  // the caller's choice (LOMPC_PLAN_CELLS)
   if (g >= 1 && g <= LQ_GMAX) return g;
@@ -2364,22 +2433,17 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   const int64_t slots = (int64_t)p->n_cu * p->eval_occ;
   const int64_t rounds = std::max<int64_t>(1, (10 * B + 9ll * slots * EVAL_MAXB - 1) / (9ll * slots * EVAL_MAXB));
   const int64_t target = rounds * slots;
-  auto blocks_of = [&](int64_t m) -> int64_t {
-    if (m <= 0) return 0;
-    const int64_t lo = (m + EVAL_MAXB - 1) / EVAL_MAXB, hi = (m + 255) / 256;
-    return std::max<int64_t>(lo, std::min<int64_t>(hi, m * target / std::max<int64_t>(B, 1)));
-  };
-  int64_t nblk = 0;
+  // the k_eval block map (weighted by dispatch round when the blocks take one round: block_map)
+  std::vector<int4> bmap;
+  std::vector<int> bpre;
+  block_map(set_offsets, S, B, EVAL_MAXB, target, p->n_cu, rounds == 1, bmap, bpre);
+  const int64_t nblk = (int64_t)bmap.size();
   int64_t n_empty = 0;
   // lompc_plan_reserve: a buffer that must grow is sized at once for the reserved batch size (upper
   // bounds: blocks_of(m) <= ceil(m / 256), sorted blocks ceil(m / LQ_AGG_SB) per set)
   const int64_t RB = std::max(B, p->reserve_B);
   const int64_t nblk_r = p->reserve_B ? RB / 256 + S + 1 : 0, nsblk_r = p->reserve_B ? RB / LQ_AGG_SB + S + 1 : 0;
-  for (int64_t s = 0; s < S; ++s) {
-    const int64_t nb = blocks_of(set_offsets[s + 1] - set_offsets[s]);
-    nblk += nb;
-    n_empty += nb == 0 ? 1 : 0;
-  }
+  for (int64_t s = 0; s < S; ++s) n_empty += bpre[s + 1] == bpre[s] ? 1 : 0;
   p->device = ctxs[0]->device;
   p->N = N;
   p->nctx = nctx;
@@ -2476,13 +2540,8 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   p->h_off_at = (int64_t)o_off;
   int* hpre = reinterpret_cast<int*>(p->h_buf + o_pre);
   memcpy(hoff, set_offsets, (S + 1) * sizeof(int64_t));
-  int64_t b = 0;
-  hpre[0] = 0;
-  for (int64_t s = 0; s < S; ++s) {
-    const int64_t o = set_offsets[s], m = set_offsets[s + 1] - o, nb = blocks_of(m);
-    for (int64_t k = 0; k < nb; ++k) hblk[b++] = make_int4((int)s, (int)(o + m * k / nb), (int)(o + m * (k + 1) / nb), 0);
-    hpre[s + 1] = (int)b;
-  }
+  if (nblk > 0) memcpy(hblk, bmap.data(), (size_t)nblk * sizeof(int4));
+  memcpy(hpre, bpre.data(), (size_t)(S + 1) * sizeof(int));
   for (int k = 0, e = 0; k < LQ_PLAN_MAX_CTX; ++k) {
     e += k < nctx ? (int)sets_per_ctx[k] : 0;
     p->ce.end[k] = k + 1 < nctx ? e : (int)S;  // contexts past the last: never selected
@@ -3101,13 +3160,12 @@ int stepped_setup(lompc_plan* p, hipStream_t st, bool wide) {
     const int64_t* hoff = reinterpret_cast<const int64_t*>(p->h_buf + p->h_off_at);
     for (int64_t s = 0; s <= S; ++s) off[s] = hoff[s];
   }
-  auto blocks_of = [&](int64_t m) -> int64_t {
-    if (m <= 0) return 0;
-    const int64_t lo = (m + maxb - 1) / maxb, hi = (m + 255) / 256;
-    return std::max<int64_t>(lo, std::min<int64_t>(hi, m * target / std::max<int64_t>(B, 1)));
-  };
-  int64_t nblk = 0;
-  for (int64_t s = 0; s < S; ++s) nblk += blocks_of(off[s + 1] - off[s]);
+  // the block map: (set, first EV, end EV) per k_evals / k_step workgroup, and each set's first block
+  // (the wide form's: one dispatch round, weighted as lq_plan_prepare's — the same map, so the same bits)
+  std::vector<int4> blks;
+  std::vector<int> pre;
+  block_map(off.data(), S, B, maxb, target, p->n_cu, wide && rounds == 1, blks, pre);
+  int64_t nblk = (int64_t)blks.size();
   const size_t o_pre = ((size_t)nblk * sizeof(int4) + 15) & ~(size_t)15;
   const size_t bytes = o_pre + (size_t)(S + 1) * sizeof(int);
   int rc;
@@ -3119,15 +3177,8 @@ int stepped_setup(lompc_plan* p, hipStream_t st, bool wide) {
     z.cap_map = (int64_t)bytes;
   }
   HIPCHK(p, hipStreamSynchronize(st));  // (the pinned map may still feed an earlier copy)
-  int4* hb = reinterpret_cast<int4*>(z.h_map);
-  int* hp = reinterpret_cast<int*>(z.h_map + o_pre);
-  int64_t b = 0;
-  hp[0] = 0;
-  for (int64_t s = 0; s < S; ++s) {
-    const int64_t o = off[s], m = off[s + 1] - o, nb = blocks_of(m);
-    for (int64_t k = 0; k < nb; ++k) hb[b++] = make_int4((int)s, (int)(o + m * k / nb), (int)(o + m * (k + 1) / nb), 0);
-    hp[s + 1] = (int)b;
-  }
+  memcpy(z.h_map, blks.data(), (size_t)nblk * sizeof(int4));
+  memcpy(z.h_map + o_pre, pre.data(), (size_t)(S + 1) * sizeof(int));
   HIPCHK(p, hipMemcpyAsync(z.d_map, z.h_map, bytes, hipMemcpyHostToDevice, st));
   z.nblk = (int)nblk;
   if (ncell > z.cap_cells) {

@@ -83,3 +83,21 @@ rows = ((st[:, :, 1][..., None] <= mid) & (mid < st[:, :, 2][..., None])).sum(ax
 print("  timeline (bin, us, WGs staging, WGs in rows):")
 for i in range(0, len(mid), 2):
     print(f"   {mid[i]:7.2f}  {stag[i]:4d}  {rows[i]:4d}")
+# per-workgroup totals: the launch ends with its slowest workgroup (static block map)
+tot = st[:, -1, 3] - st[:, 0, 0]
+print(f"  per-workgroup total: min {tot.min():.1f} p10 {np.percentile(tot, 10):.1f} median {np.median(tot):.1f} "
+      f"p90 {np.percentile(tot, 90):.1f} max {tot.max():.1f} us (mean {tot.mean():.1f}); span {span:.1f}")
+per = nb // (2 * P)
+if per > 0:
+    ms = [float(np.mean(tot[s * per:(s + 1) * per])) for s in range(2 * P)]
+    print("  mean total by set (blocks in order):", " ".join(f"{m:.0f}" for m in ms))
+print("  mean total by b % 8 (dispatch XCD):", " ".join(f"{np.mean(tot[x::8]):.1f}" for x in range(8)))
+slow = np.argsort(tot)[-10:]
+print("  slowest workgroups (b, total):", [(int(b), round(float(tot[b]), 1)) for b in slow])
+half = (nb // (2 * P)) * P
+for nm, sl in (("small sets", slice(0, half)), ("large sets", slice(half, nb))):
+    print(f"  {nm}: " + "  ".join(f"{k} {np.median(v[sl, 1:]):.2f}" for k, v in ph.items()))
+cnt = np.zeros(2 * P * CELLS, dtype=np.int32)
+lib.lompc_debug_plan_tables.argtypes = [ctypes.c_void_p] * 7
+lib.lompc_debug_plan_tables(plan._plan, cnt.ctypes.data, None, None, None, None, None)
+print("  pieces per cell (last single-run table) small:", cnt[:P * CELLS].mean(), " large:", cnt[P * CELLS:].mean())

@@ -322,6 +322,8 @@ struct AggSet {
   double wlo, h1, fs;
   const double* L;
   double lr, l1, l2, l3, tt, wm;
+  bool preg = false;          // (k_loop_run redundant form) the prices in registers, lane t < N:
+  double p1 = 0, p2 = 0, p3 = 0;  // prices t, N + t, 2N + t
 };
 
 template <int NT, bool COH = false>  // (COH: the prices re-read with sc1 loads, as load_set<COH>)
@@ -479,7 +481,8 @@ __device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, cons
     lqw::WaveSet ws;
     double l2w;
     bool bad;
-    load_set<PCOH>(q, z.L, lr, N, lane, ws, l2w, bad);
+    if (z.preg) load_set_regs(q, z.p1, z.p2, z.p3, lr, N, lane, ws, l2w, bad);
+    else load_set<PCOH>(q, z.L, lr, N, lane, ws, l2w, bad);
     const double c0 = q.theta * q.w_max * lqw::wave_sum(l2w, N);
     const double kappa = lr / q.delta;
     const double l0[3] = {l1, l2, l3};

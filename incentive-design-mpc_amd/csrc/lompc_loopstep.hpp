@@ -111,13 +111,25 @@ struct NoRelease {  // (k_loop_iter / k_loop_step: the kernel's end releases the
   __device__ __forceinline__ void operator()() const {}
 };
 
+// what a step leaves for the next call when the caller keeps the loop in registers (k_loop_run's
+// redundant form: every wave runs the same step on the same closed outputs)
+struct StepOut {
+  bool fin = false;      // the loop ended at this call
+  double v[3] = {0, 0, 0};  // lane t < N: the next call's prices t, N + t, 2N + t (as stored)
+  double cost_c = 0.0, dterm = 0.0;  // the next call's state[0], state[1]
+  lqp::Tri ab{};         // the A_bar factor (computed by the first step)
+};
+
 // (ST: a diagnostic build's phase stamp, called with 8 after the inputs and the error metric, 9
 // after the price QP)
 // (REL: called once the next call's prices and loop state are written, before the host-memory writes
 // of this step — k_loop_run releases its waiting waves there, so the PCIe writes overlap the next call)
-template <class ST = NoStamp, class REL = NoRelease>
+// (WR = false: nothing is written — no prices, state or factor to memory, no host results; the
+// outputs only in `out`, for the waves of the redundant form that are not its writer)
+template <class ST = NoStamp, class REL = NoRelease, bool WR = true>
 __device__ __forceinline__ void loop_step_core(const StepArgs& a, const int m, const int lane, const StepIn& in,
-                                               const ST& stamp = ST{}, const REL& release = REL{}) {
+                                               const ST& stamp = ST{}, const REL& release = REL{},
+                                               StepOut* out = nullptr) {
   const int N = a.N, N3 = 3 * N;
   const bool act = lane < N;
   const double s0 = act ? in.s0 : 0.0, wk = act ? in.wk : 0.0;
@@ -144,7 +156,8 @@ __device__ __forceinline__ void loop_step_core(const StepArgs& a, const int m, c
     // the price-gradient step at (w_k, lmbd) (lompc_price_step)
     lqp::PriceQPW P;
     P.init(N, a.r, a.theta, a.w_max, a.m, a.kappa, a.eps_reg, wk, m > 0 ? &in.ab : nullptr);
-    if (m == 0) {  // the loop's A_bar factor for its later steps
+    if (out) out->ab = P.Ab;
+    if (WR && m == 0) {  // the loop's A_bar factor for its later steps
       lq_st_wt(a.tri + lane, P.Ab.Q);
       lq_st_wt(a.tri + 64 + lane, P.Ab.iv);
       lq_st_wt(a.tri + 128 + lane, P.Ab.d);
@@ -176,6 +189,8 @@ __device__ __forceinline__ void loop_step_core(const StepArgs& a, const int m, c
   }
   stamp(9);
   if (err || conv || m >= a.max_iter) {  // finished: the results to the host, then the flags
+    if (out) out->fin = true;
+    if (!WR) return;
     if (m > 0 && lane == 0) sys_st(a.h_dec + (m - 1), dec_prev);
     if (act) {
 #pragma unroll
@@ -204,11 +219,19 @@ __device__ __forceinline__ void loop_step_core(const StepArgs& a, const int m, c
     for (int k = 0; k < 3; ++k) {
       const double v = k * N < a.r ? x[k] : 0.0;
       dt = fma(lm[k] - v, phr[k], dt);
-      lq_st_wt(a.dev_in + k * N + lane, v);
-      lq_st_wt(a.dev_in + N3 + k * N + lane, v);
+      if (out) out->v[k] = v;
+      if (WR) {
+        lq_st_wt(a.dev_in + k * N + lane, v);
+        lq_st_wt(a.dev_in + N3 + k * N + lane, v);
+      }
     }
   }
   dt = lqw::wave_sum(dt, N);
+  if (out) {
+    out->cost_c = cost_c;
+    out->dterm = m == 0 ? dt : 0.0;
+  }
+  if (!WR) return;
   if (lane == 0) {
     lq_st_wt(a.state, cost_c);
     lq_st_wt(a.state + 1, m == 0 ? dt : 0.0);

@@ -407,13 +407,34 @@ __device__ __forceinline__ void load_set(const QPConst& q, const double* __restr
   }
 }
 
+// load_set with the set's prices already in registers (lane t < N: prices t, N + t, 2N + t)
+__device__ __forceinline__ void load_set_regs(const QPConst& q, double l1, double l2v, double l3, double lr, int N,
+                                              int lane, lqw::WaveSet& ws, double& l2, bool& bad) {
+  const double tt = q.theta * q.theta;
+  ws.N = N;
+  ws.lane = lane;
+  l2 = 0.0;
+  bad = false;
+  if (lane < N) {
+    l2 = l2v;
+    bad = !(l1 >= 0.0 && l2 >= 0.0 && l3 >= 0.0);
+    ws.d_nat = 2.0 * lr * tt + 2.0 * q.q_scale * l3 + q.dsmall;
+    ws.e_nat = q.theta * (l1 - l2);
+  } else {
+    ws.d_nat = ws.e_nat = 0.0;
+  }
+}
+
 // One (set, gamma cell) path by one wave (blk = s * G + cell); the wave's workgroup has
 // initialised the box table for the set's constants (lq_tab_init).  Every piece goes straight
 // to the cell's fixed slots with write-through stores (visible to any XCD once they complete).
 // NT: the horizon as a compile-time constant (0: a.N at run time) — the scans' row / bank steps
 // become straight-line code, so independent chains can be interleaved
-template <int NT = 0, bool INIT_TAB = false, bool COH = false>
-__device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
+template <int NT = 0, bool INIT_TAB = false, bool COH = false, bool PREG = false>
+__device__ __forceinline__ void path_cell(const PathArgs& a, const int blk, double p1 = 0.0, double p2 = 0.0,
+                                          double p3 = 0.0, double wr_in = 0.0, int* ws_io = nullptr) {
+  // (PREG: the set's prices p1..p3, the lane's w_ref wr_in and the cell's stored working set *ws_io
+  // in registers — k_loop_run2's later calls; the working set still stored for the next loop)
   const int G = a.G;
   const int s = __builtin_amdgcn_readfirstlane(blk / G);
   const int cell = blk - s * G;
@@ -421,14 +442,15 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
   const int N = NT ? NT : a.N;
   const double* __restrict__ L = a.lmbd + (size_t)s * 3 * N;
   const double lr = a.lmbd_r[s];
-  const double wr_nat = (a.w_ref && lane < N) ? a.w_ref[(size_t)s * N + lane] : 0.0;
+  const double wr_nat = PREG ? wr_in : (a.w_ref && lane < N) ? a.w_ref[(size_t)s * N + lane] : 0.0;
   const double wlo = a.window[2 * s], whi = a.window[2 * s + 1];
   const QPConst& q = set_consts(a.qd, a.ce, s);  // scalar loads, no register copy
   LQ_STAMP(0);
   lqw::WaveSet ws;
   double l2;
   bool bad;
-  load_set<COH>(q, L, lr, N, lane, ws, l2, bad);
+  if constexpr (PREG) load_set_regs(q, p1, p2, p3, lr, N, lane, ws, l2, bad);
+  else load_set<COH>(q, L, lr, N, lane, ws, l2, bad);
   if (INIT_TAB) lq_tab_init(q);  // (after the price loads are issued: the barrier overlaps them)
   if (bad || (lane == 0 && !(lr >= 0.0))) atomicOr(a.errflag, 1);
   const double c0 = q.theta * q.w_max * lqw::wave_sum(l2, N);  // lompc.py:128
@@ -450,7 +472,7 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
     int sl = sl0;
     bool warm = false;
     if (a.ws) {
-      const int v = a.ws[(size_t)blk * 64 + lane];
+      const int v = (PREG && ws_io) ? *ws_io : a.ws[(size_t)blk * 64 + lane];
       sl = (lane < N && v >= 0 && v <= 2 * q.m) ? v : sl0;
       warm = LQ_WARM_FP64 && __all(lane >= N || v <= 2 * q.m);  // (a stored set on every stage: wave-uniform)
     }
@@ -467,6 +489,7 @@ __device__ __forceinline__ void path_cell(const PathArgs& a, const int blk) {
     if (solved) {
       sl0 = sl;
       if (a.ws) a.ws[(size_t)blk * 64 + lane] = (uint8_t)sl;
+      if (ws_io) *ws_io = (int)(uint8_t)sl;
       const size_t sb = (size_t)blk * LQ_PPL;  // the cell's fixed piece slots
       // ---- parametric active-set tracking of w*(gamma) on [glo, ghi]
       double gcur = glo;
@@ -2205,8 +2228,149 @@ __global__ __launch_bounds__(64) void k_loop_run(PathArgs pa, AggArgs ga, StepAr
   }
 }
 
+// k_loop_run, redundant form (LQ_LOOP_REDUNDANT): no hand-off of the step's results.  Every wave
+// arrives on a monotonic counter (ctl[1]) after writing its cell record (write-through, drained),
+// waits until all S * G waves of the call have arrived, loads every record (sc1) and runs the SAME
+// closing and loop step as every other wave — the same instructions on the same records in the same
+// order, so the same bits in every wave — and goes straight on to the next call with the prices, the
+// loop state and the A_bar factor in its registers (the path and the aggregation take the prices from
+// registers: no memory round between the step and the next path).  Wave 0 alone writes: the set
+// outputs, the stats and tallies, the prices / state / factor to memory and the host results.  The
+// records alternate between two buffers by call parity (a wave may write call m + 1's record while a
+// slower wave still reads call m's: never call m + 2's, which needs every wave's call m + 1 arrival).
+// The same arithmetic as k_loop_run and k_loop_iter: the same bits.
+#ifndef LQ_LOOP_REDUNDANT
+#define LQ_LOOP_REDUNDANT 1
+#endif
+template <int NT>
+__global__ __launch_bounds__(64) void k_loop_run2(PathArgs pa, AggArgs ga, StepArgs sa, double* rec) {
+  constexpr int S = 2;
+  const int blk = (int)blockIdx.x, lane = (int)threadIdx.x, G = pa.G;
+  const int s = blk / G, c = blk - s * G;
+  const bool writer = blk == 0;
+  int cl_n[S], cl_v[S], cl_ok[S];
+#pragma unroll
+  for (int t = 0; t < S; ++t) {
+    const int4 si = ga.sinfo[t];
+    cl_n[t] = (int)(ga.set_off[t + 1] - ga.set_off[t]);
+    cl_v[t] = si.x;
+    cl_ok[t] = si.y;
+    asm volatile("" : "+v"(cl_n[t]), "+v"(cl_v[t]), "+v"(cl_ok[t]));
+  }
+  AggArgs gw = ga;  // (the closing's outputs: wave 0's only)
+  if (!writer) {
+    gw.set_sum_w = nullptr;
+    gw.set_stats = nullptr;
+    gw.stats = nullptr;
+    gw.tally = nullptr;
+  }
+  const int nsg = S * G;
+  StepIn in;
+  step_prices<false>(sa, lane, in);  // (the first call's prices, w_ref, the zeroed loop state)
+  double pv[3] = {in.lm[0], in.lm[1], in.lm[2]};
+  // the cell's stored working set, kept in a register from call to call (as each call stores it);
+  // w_ref from the price buffer (the plan's w_ref of both sets, constant over the loop)
+  const int N_ = NT ? NT : pa.N;
+  const double wr_c = (pa.w_ref && lane < N_) ? pa.w_ref[(size_t)s * N_ + lane] : 0.0;
+  int wsr = pa.ws ? (int)pa.ws[(size_t)blk * 64 + lane] : 0;
+  for (int m = 0; m <= sa.max_iter; ++m) {
+    // (the box table in LDS: written by the first call; the one-wave workgroup keeps its LDS)
+    if (m == 0) path_cell<NT, true, true, true>(pa, blk, pv[0], pv[1], pv[2], wr_c, &wsr);
+    else path_cell<NT, false, true, true>(pa, blk, pv[0], pv[1], pv[2], wr_c, &wsr);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the cell's tables have reached L2
+    double* rb = rec + (size_t)(m & 1) * (nsg + 1) * LQ_AGG_REC;  // this call's record buffer
+    {
+      AggSet z = agg_set_init<NT, true>(ga, s);
+      if (m > 0) {  // (the prices of this call: registers)
+        z.preg = true;
+        z.p1 = pv[0];
+        z.p2 = pv[1];
+        z.p3 = pv[2];
+        z.l1 = lqw::readlane_d(pv[0], 0);
+        z.l2 = lqw::readlane_d(pv[1], 0);
+        z.l3 = lqw::readlane_d(pv[2], 0);
+      }
+      AggPart ap;
+      if (z.order_ok) agg_cell<NT, true, true>(ga, z, s, c, agg_cell_range(z, c), lane, ap);
+      const AggRec x = agg_wave_record(ap);
+      double* rc = rb + (size_t)blk * LQ_AGG_REC;
+      if (lane < z.N) st_wt8(rc + lane, ap.accw);
+      if (lane < 5) st_wt8(rc + LOMPC_MAX_N + lane, x.pick(lane));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int ok = 1;
+    if (lane == 0) {
+      __hip_atomic_fetch_add(sa.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int target = (m + 1) * nsg;
+      int spins = 0;
+      while (__hip_atomic_load(sa.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins >= LQ_RUN_SPINS) {
+          ok = 0;
+          break;
+        }
+      }
+      if (!ok) {
+        __hip_atomic_store(sa.ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sa.ctl + 0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (!lqw::readlane_i(ok, 0)) return;
+    AggSet zs[S];
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+      zs[t].N = NT ? NT : ga.N;
+      zs[t].n_s = cl_n[t];
+      zs[t].si = make_int4(cl_v[t], cl_ok[t], 0, 0);
+      zs[t].order_ok = cl_ok[t] != 0;
+    }
+    const int N = zs[0].N;
+    double rw[S][LQ_LOOP_G], rx[S][LQ_LOOP_G];
+    const int tl = min(lane, N - 1), xl = min(lane, 4);
+#pragma unroll
+    for (int t = 0; t < S; ++t)
+#pragma unroll
+      for (int k = 0; k < LQ_LOOP_G; ++k) {  // (records k >= G: the zero record after buffer 0)
+        const double* rk = k < G ? rb + (size_t)(t * G + k) * LQ_AGG_REC : rec + (size_t)nsg * LQ_AGG_REC;
+        rw[t][k] = ld_t<true>(rk + tl);
+        rx[t][k] = ld_t<true>(rk + LOMPC_MAX_N + xl);
+      }
+    AggSetOut o[S];
+#pragma unroll
+    for (int t = 0; t < S; ++t)
+      o[t] = agg_finish<false, true, LQ_LOOP_G>(gw, zs[t], t, lane, G, [&](int k) { return rw[t][k]; },
+                                               [&](int k) { return rx[t][k]; });
+    in.s0 = o[0].sumw;
+    in.wk = o[1].sumw;
+    in.emax = lqw::readlane_d(o[0].stat, LOMPC_STAT_MAX_ERR);
+    in.cost_c = lqw::readlane_d(o[1].stat, LOMPC_STAT_SUM_COST);
+    in.n_inv = lqw::readlane_d(o[0].stat, LOMPC_STAT_N_INVALID) + lqw::readlane_d(o[1].stat, LOMPC_STAT_N_INVALID);
+    in.n_fail = lqw::readlane_d(o[0].stat, LOMPC_STAT_N_FAILED) + lqw::readlane_d(o[1].stat, LOMPC_STAT_N_FAILED);
+    StepOut so;
+    if (writer) loop_step_core<NoStamp, NoRelease, true>(sa, m, lane, in, NoStamp{}, NoRelease{}, &so);
+    else loop_step_core<NoStamp, NoRelease, false>(sa, m, lane, in, NoStamp{}, NoRelease{}, &so);
+    if (so.fin) return;
+    // the next call's inputs: what the step stored, kept in registers
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      pv[k] = so.v[k];
+      in.lm[k] = so.v[k];
+    }
+    in.dc = so.cost_c;
+    in.dterm = so.dterm;
+    in.ab = so.ab;
+  }
+}
+
 typedef void (*LoopRunKernel)(PathArgs, AggArgs, StepArgs, double*);
 LoopRunKernel loop_run_kernel(int N) {
+  if (LQ_LOOP_REDUNDANT) switch (N) {
+      case 12: return k_loop_run2<12>;
+      case 16: return k_loop_run2<16>;
+      case 24: return k_loop_run2<24>;
+      case 48: return k_loop_run2<48>;
+      default: return k_loop_run2<0>;
+    }
   switch (N) {
     case 12: return k_loop_run<12>;
     case 16: return k_loop_run<16>;
@@ -2858,16 +3022,18 @@ int lq_launch_loop(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
                    const StepArgs& sa, int m, hipStream_t st, bool persistent) {
   if (!lq_loop_fusable(p)) return fail_arg(p, "k_loop_iter: plan not fusable");
   const int N = p->N;
-  const int64_t nrec = (p->S * p->G + 1) * (int64_t)LQ_AGG_REC;  // + the zero record (k_loop_iter's padding)
+  // [cell records | the zero record (k_loop_iter's padding) | (k_loop_run2) the second record buffer]
+  const int64_t zoff = p->S * p->G * (int64_t)LQ_AGG_REC;
+  const int64_t nrec = (2 * p->S * p->G + 1) * (int64_t)LQ_AGG_REC;
   if (nrec > p->cap_aggrec) {
     const int rc = grow(p, &p->d_aggrec, nrec);
     if (rc) return rc;
     p->cap_aggrec = nrec;
     p->aggrec_zero = -1;
   }
-  if (p->aggrec_zero != nrec - LQ_AGG_REC) {  // (the cell records never reach it: zeroed once per layout)
-    HIPCHK(p, hipMemsetAsync(p->d_aggrec + (nrec - LQ_AGG_REC), 0, LQ_AGG_REC * sizeof(double), st));
-    p->aggrec_zero = nrec - LQ_AGG_REC;
+  if (p->aggrec_zero != zoff) {  // (the cell records never reach it: zeroed once per layout)
+    HIPCHK(p, hipMemsetAsync(p->d_aggrec + zoff, 0, LQ_AGG_REC * sizeof(double), st));
+    p->aggrec_zero = zoff;
   }
   const PathTab tb = own_tab(p);
   const PathArgs pa = path_args(p, lmbd, lmbd_r, tb);

@@ -150,7 +150,8 @@ def test_device_loop_matches_host_loop(gpu, monkeypatch, ev, price_type, N):
 @pytest.mark.parametrize("N", [12, 48])
 def test_device_loop_is_one_launch(gpu, monkeypatch, N):
     """Over a gamma-sorted loop plan the device loop runs the WHOLE loop as ONE persistent launch
-    (k_loop_run: per call path, aggregation and loop step, the calls chained by a generation word;
+    (k_loop_run2: per call path, aggregation and loop step, every wave running the same step after a
+    counter barrier;
     timed as k_path): no k_eval / k_agg launch, and the same iterations and prices as the host loop
     (which runs k_path + k_agg + the host step per iteration)."""
 

@@ -2399,6 +2399,7 @@ LoopIterKernel loop_iter_kernel(int N) {
 // at every new high (hipMalloc / hipHostMalloc took 50-470 us per re-targeted plan in the station's
 // staging, scripts/stage_profile.py)
 int64_t with_slack(int64_t n, int64_t cap) { return std::max(n + n / 4 + 16, 2 * cap); }
+constexpr int LQ_RESERVE_CELLS = 16;  // lompc_plan_reserve: cell-indexed buffers sized for this many cells per set (pick_cells' most)
 
 #ifndef LQ_WIDE_ALPHA
 #define LQ_WIDE_ALPHA 0.85  // EVs of a second-dispatch-round k_eval / k_evals block relative to a first-round one
@@ -2639,12 +2640,14 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
   const bool warm = (flags & LOMPC_PLAN_WARM_START) != 0;
   bool fresh_ws = false;
   if (ncell > p->cap_cells || (warm && !p->d_ws)) {
-    if ((rc = grow(p, &p->t_cnt, ncell)) || (rc = grow(p, &p->t_lo, ncell)) ||
-        (rc = grow(p, &p->t_ge, ncell * LQ_PPL)) || (rc = grow(p, &p->t_cf, ncell * LQ_PPL * 8)) ||
-        (rc = grow(p, &p->t_ab, ncell * LQ_PPL * N)) || (rc = grow(p, &p->t_sl, 2 * ncell * 64)))
+    // (a reserved plan: sized for the most cells the plan's choice gives a set, LQ_RESERVE_CELLS)
+    const int64_t cn = std::max(ncell, p->reserve_B ? S * (int64_t)std::max(G, LQ_RESERVE_CELLS) : 0);
+    if ((rc = grow(p, &p->t_cnt, cn)) || (rc = grow(p, &p->t_lo, cn)) ||
+        (rc = grow(p, &p->t_ge, cn * LQ_PPL)) || (rc = grow(p, &p->t_cf, cn * LQ_PPL * 8)) ||
+        (rc = grow(p, &p->t_ab, cn * LQ_PPL * N)) || (rc = grow(p, &p->t_sl, 2 * cn * 64)))
       return rc;
-    if (warm && (rc = grow(p, &p->d_ws, (size_t)ncell * 64))) return rc;
-    p->cap_cells = ncell;
+    if (warm && (rc = grow(p, &p->d_ws, (size_t)cn * 64))) return rc;
+    p->cap_cells = cn;
     fresh_ws = true;
   }
   // (0xff: no stored set — a cell's first run starts cold, from "all free", and its later runs warm)
@@ -2741,8 +2744,9 @@ int lq_plan_prepare(lompc_plan* p, int nctx, lompc_ctx* const* ctxs, const int64
       p->cap_P = c;
     }
     if (npos > p->cap_pos) {
-      if ((rc = grow(p, &p->d_pos, npos))) return rc;
-      p->cap_pos = npos;
+      const int64_t pr = std::max(npos, p->reserve_B ? S * (int64_t)(std::max(G, LQ_RESERVE_CELLS) * LQ_AGG_KF + 1) : 0);
+      if ((rc = grow(p, &p->d_pos, pr))) return rc;
+      p->cap_pos = pr;
     }
     if (S > p->cap_sinfo) {
       if ((rc = grow(p, &p->d_sinfo, S))) return rc;
@@ -3026,9 +3030,10 @@ int lq_launch_loop(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   const int64_t zoff = p->S * p->G * (int64_t)LQ_AGG_REC;
   const int64_t nrec = (2 * p->S * p->G + 1) * (int64_t)LQ_AGG_REC;
   if (nrec > p->cap_aggrec) {
-    const int rc = grow(p, &p->d_aggrec, nrec);
+    const int64_t c = std::max(nrec, p->reserve_B ? (2 * p->S * LQ_RESERVE_CELLS + 1) * (int64_t)LQ_AGG_REC : 0);
+    const int rc = grow(p, &p->d_aggrec, c);
     if (rc) return rc;
-    p->cap_aggrec = nrec;
+    p->cap_aggrec = c;
     p->aggrec_zero = -1;
   }
   if (p->aggrec_zero != zoff) {  // (the cell records never reach it: zeroed once per layout)

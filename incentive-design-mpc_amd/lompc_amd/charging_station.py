@@ -197,6 +197,8 @@ class ChargingStation:
         # growth (partitions gain and lose EVs step to step: no reallocation inside the later steps)
         for ps in (self.price_solver_s, self.price_solver_l):
             ps.reserve_evs = self.M_2
+            if not self._exchange and self.stage_partitions:  # (the plans made now: no allocation in a step)
+                ps.prewarm_partitions(range(self.P))
         # Initialize state variables = (EV SoCs, charge stored).
         self._init_states()
         # Initialize logs.

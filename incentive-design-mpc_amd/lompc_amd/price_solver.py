@@ -262,6 +262,19 @@ class PriceSolver:
             for k in self._PART_STATE:
                 setattr(self, k, cur[k])
 
+    def prewarm_partitions(self, parts) -> None:
+        """Create the loop plan of every partition in ``parts`` now (ChargingStation: at
+        construction), on a one-EV placeholder batch: with ``reserve_evs`` its workspaces are sized
+        for the whole population at once, so the steps' staging re-targets plans
+        (lompc_plan_update) and allocates nothing.  A placeholder plan has never run: its first
+        staging and loop are those of a fresh plan (``tests/test_gpu_pipeline.py``: update = fresh)."""
+        torch = _torch()
+        y = torch.full((1,), 0.5 * float(self.consts.y_max), dtype=torch.float64, device=self._dev)
+        v = 0.5 * float(self.consts.y_max)
+        for p in parts:
+            if p not in self._staged:
+                self.stage_partition(p, y, 1, v, v, v, descending=True)
+
     def use_partition(self, p: int) -> None:
         """Make the plan and levels staged for partition p current (set_charge_levels done)."""
         for k, v in self._staged[p].items():

@@ -14,6 +14,10 @@ run() {
   local rc=$?
   echo "$name rc=$rc" | tee -a gpurun_out/steps.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  # a failed step whose log shows a GPU fault ends the session too (no second faulting run)
+  if [ $rc -eq 1 ] && grep -q -e "illegal memory access" -e "hipErrorIllegalAddress" -e "Memory access fault" "gpurun_out/$name.log"; then
+    echo "stopping after $name (GPU fault in its log)"; exit 1
+  fi
   return 0
 }
 PYT="python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread"

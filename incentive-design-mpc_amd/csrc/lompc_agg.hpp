@@ -292,17 +292,15 @@ struct AggArgs {
 
 // sorted position of the first gamma >= v (lower) or > v (!lower) within [a, b) of set s,
 // b - a <= 64: one load per lane, one ballot; more: binary search (wave-uniform)
-// (g[j - go]: positions are the set's, g may hold them from position go on)
-__device__ __forceinline__ int agg_search(const double* __restrict__ g, int go, int a, int b, double v, bool lower,
-                                          int lane) {
+__device__ __forceinline__ int agg_search(const double* __restrict__ g, int a, int b, double v, bool lower, int lane) {
   if (b - a <= 64) {
-    const double x = a + lane < b ? g[a + lane - go] : INFINITY;
+    const double x = a + lane < b ? g[a + lane] : INFINITY;
     const bool before = lower ? (x < v) : (x <= v);
     return a + (int)__popcll(__ballot(before && a + lane < b));
   }
   while (a < b) {
     const int mid = (a + b) >> 1;
-    const double x = g[mid - go];
+    const double x = g[mid];
     if (lower ? (x < v) : (x <= v)) a = mid + 1;
     else b = mid;
   }
@@ -324,8 +322,6 @@ struct AggSet {
   double wlo, h1, fs;
   const double* L;
   double lr, l1, l2, l3, tt, wm;
-  int go = 0, pso = 0;        // g[j - go] is the set's gamma at sorted position j, ps[b - pso] its bucket b
-                              // (k_loop_run2: a cell's gammas and buckets mirrored in LDS)
   bool preg = false;          // (k_loop_run redundant form) the prices in registers, lane t < N:
   double p1 = 0, p2 = 0, p3 = 0;  // prices t, N + t, 2N + t
 };
@@ -371,7 +367,7 @@ struct AggPart {
 // hold no copy of them).
 // the cell's sorted positions [cs, ce)
 __device__ __forceinline__ int2 agg_cell_range(const AggSet& z, const int c) {
-  return make_int2(z.ps[c * z.KF - z.pso], z.ps[(c + 1) * z.KF - z.pso]);
+  return make_int2(z.ps[c * z.KF], z.ps[(c + 1) * z.KF]);
 }
 
 template <int NT, bool COH, bool PCOH = false>  // (PCOH: the prices with sc1 loads, k_loop_run)
@@ -418,8 +414,7 @@ __device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, cons
   const double gprev = __shfl(ge, max(lane - 1, 0), 64);  // (every lane: no read of an inactive lane)
   const double vb = lane == 0 ? lo : gprev;
   const int fb = min(max(agg_fine(vb, wlo, fs, r.F), c * KF), (c + 1) * KF - 1);
-  const int go = z.go, pso = z.pso;
-  int qa = lane <= cnt ? ps[fb - pso] : 0, qb = lane <= cnt ? ps[fb + 1 - pso] : 0;
+  int qa = lane <= cnt ? ps[fb] : 0, qb = lane <= cnt ? ps[fb + 1] : 0;
   qa = min(max(qa, cs), ce);
   qb = min(max(qb, cs), ce);
   int qpos = cs;
@@ -430,7 +425,7 @@ __device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, cons
 #pragma unroll
     for (int j = 0; j <= LQ_PPL; ++j) {
       const int a0 = lqw::readlane_i(qa, j), b0 = lqw::readlane_i(qb, j);  // (j wave-uniform)
-      xg[j] = (j <= cnt && b0 - a0 <= 64 && a0 + lane < b0) ? g[a0 + lane - go] : INFINITY;
+      xg[j] = (j <= cnt && b0 - a0 <= 64 && a0 + lane < b0) ? g[a0 + lane] : INFINITY;
     }
 #pragma unroll
     for (int j = 0; j <= LQ_PPL; ++j) {
@@ -442,7 +437,7 @@ __device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, cons
         const bool before = j == 0 ? (xg[j] < v) : (xg[j] <= v);
         pj = a0 + (int)__popcll(__ballot(before && a0 + lane < b0));
       } else {
-        pj = agg_search(g, go, a0, b0, v, j == 0, lane);
+        pj = agg_search(g, a0, b0, v, j == 0, lane);
       }
       if (lane == j) qpos = pj;
     }
@@ -459,8 +454,8 @@ __device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, cons
     d1 = z.P1[nb] - z.P1[na];
     dh = z.PH[nb] - z.PH[na];
     dl = z.PL[nb] - z.PL[na];
-    gf = g[na - go];
-    gl = g[nb - 1 - go];
+    gf = g[na];
+    gl = g[nb - 1];
   }
   const double X1 = (double)d1;
   const double X2 = fma((double)dh, 0x1p40, (double)dl);
@@ -495,7 +490,7 @@ __device__ __forceinline__ void agg_cell(const AggArgs& r, const AggSet& z, cons
     for (int part = 0; part < 2; ++part) {
       const int e0 = part ? v0 : u0, e1 = part ? v1 : u1;
       for (int j = e0; j < e1; ++j) {
-        const double gj = g[j - go];
+        const double gj = g[j];
         int sl = lane < N ? (int)r.t_sl[(size_t)cell * 64 + lane] : 0;  // (COH: this lane's own store)
         double wl = 0.0, rl = 0.0;
         const bool okk = lqw::wave_solve(q, ws, gj, sl, wl, rl);

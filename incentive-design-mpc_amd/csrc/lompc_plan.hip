@@ -2242,9 +2242,6 @@ __global__ __launch_bounds__(64) void k_loop_run(PathArgs pa, AggArgs ga, StepAr
 #ifndef LQ_LOOP_REDUNDANT
 #define LQ_LOOP_REDUNDANT 1
 #endif
-#ifndef LQ_LOOP_GCAP
-#define LQ_LOOP_GCAP 6144  // k_loop_run2: gammas of a cell kept in LDS (48 KB)
-#endif
 template <int NT>
 __global__ __launch_bounds__(64) void k_loop_run2(PathArgs pa, AggArgs ga, StepArgs sa, double* rec) {
   constexpr int S = 2;
@@ -2276,29 +2273,6 @@ __global__ __launch_bounds__(64) void k_loop_run2(PathArgs pa, AggArgs ga, StepA
   const int N_ = NT ? NT : pa.N;
   const double wr_c = (pa.w_ref && lane < N_) ? pa.w_ref[(size_t)s * N_ + lane] : 0.0;
   int wsr = pa.ws ? (int)pa.ws[(size_t)blk * 64 + lane] : 0;
-  // the aggregation's inputs that do not change over the loop — the sorted positions of this cell's
-  // fine buckets and the cell's gammas — copied to the workgroup's LDS once: two of agg_cell's
-  // dependent memory rounds per call (bucket bounds, candidate gammas) become LDS reads.  Addressed
-  // by relative indices (AggSet::go / pso), never by pointers offset below the arrays.  Cells of more
-  // than LQ_LOOP_GCAP EVs keep the global loads.
-  __shared__ int s_pos[LQ_AGG_KF + 1];
-  __shared__ double s_gam[LQ_LOOP_GCAP];
-  bool lds_agg = false;
-  int cs0 = 0;
-  {
-    const AggSet z0 = agg_set_init<NT, false>(ga, s);
-    if (z0.order_ok && z0.KF == LQ_AGG_KF) {
-      const int2 rg = agg_cell_range(z0, c);
-      const int n = rg.y - rg.x;
-      if (n >= 0 && n <= LQ_LOOP_GCAP) {
-        cs0 = rg.x;
-        for (int i = lane; i <= LQ_AGG_KF; i += 64) s_pos[i] = z0.ps[c * LQ_AGG_KF + i];
-        for (int i = lane; i < n; i += 64) s_gam[i] = z0.g[rg.x + i];
-        lds_agg = true;
-      }
-    }
-    __syncthreads();  // (one wave: the LDS copies complete and visible)
-  }
   for (int m = 0; m <= sa.max_iter; ++m) {
     // (the box table in LDS: written by the first call; the one-wave workgroup keeps its LDS)
     if (m == 0) path_cell<NT, true, true, true>(pa, blk, pv[0], pv[1], pv[2], wr_c, &wsr);
@@ -2307,12 +2281,6 @@ __global__ __launch_bounds__(64) void k_loop_run2(PathArgs pa, AggArgs ga, StepA
     double* rb = rec + (size_t)(m & 1) * (nsg + 1) * LQ_AGG_REC;  // this call's record buffer
     {
       AggSet z = agg_set_init<NT, true>(ga, s);
-      if (lds_agg) {  // (the same values from LDS: position j at s_gam[j - cs0], bucket b at s_pos[b - c KF])
-        z.g = s_gam;
-        z.go = cs0;
-        z.ps = s_pos;
-        z.pso = c * LQ_AGG_KF;
-      }
       if (m > 0) {  // (the prices of this call: registers)
         z.preg = true;
         z.p1 = pv[0];

@@ -533,10 +533,13 @@ struct AggSetOut {
 // one scalar over the records).  WT: set outputs written through to L2, complete when this returns.
 // PADDED: records nrec .. MAXREC - 1 exist and are zero (sums and maxima of nonnegative errors
 // unchanged: no per-record condition)
+template <bool WT>
+__device__ __forceinline__ AggSetOut agg_finish_tail(const AggArgs& r, const AggSet& z, const int s, const int lane,
+                                                const double v, const double xs, const double xm);
+
 template <bool WT, bool PADDED, int MAXREC, class FW, class FX>
 __device__ __forceinline__ AggSetOut agg_finish(const AggArgs& r, const AggSet& z, const int s, const int lane, const int nrec,
                                            FW wrec, FX xlane) {
-  const int N = z.N, n_s = z.n_s;
   // (nrec <= MAXREC: unrolled, so register-held records stay in registers; lanes >= N sum
   // whatever they hold, unread)
   double v = 0.0, xs = 0.0, xm = 0.0;  // lane j < 5: scalar j summed / maximised over the records in order
@@ -549,6 +552,15 @@ __device__ __forceinline__ AggSetOut agg_finish(const AggArgs& r, const AggSet& 
       xm = fmax(xm, xv);
     }
   }
+  return agg_finish_tail<WT>(r, z, s, lane, v, xs, xm);
+}
+
+// agg_finish's outputs from the records' sums already formed (v: lane t's stage sum; xs / xm: lane
+// j < 5's scalar summed / maximised over the records in order)
+template <bool WT>
+__device__ __forceinline__ AggSetOut agg_finish_tail(const AggArgs& r, const AggSet& z, const int s, const int lane,
+                                                const double v, const double xs, const double xm) {
+  const int N = z.N, n_s = z.n_s;
   const double xa = lane == 2 ? xm : xs;  // (scalar 2, the max error: a max)
   if (lane < N && r.set_sum_w) {
     if (WT) st_wt8(r.set_sum_w + (size_t)s * N + lane, v);

@@ -257,7 +257,7 @@ const char* lq_failed_text(lompc_plan* p, hipStream_t st);
 // one device-loop iteration as ONE launch (k_loop_iter: path + aggregation + the loop step) when
 // the plan allows it (gamma-sorted sets, no communicator, at most LQ_LOOP_G cells per set)
 struct StepArgs;
-bool lq_loop_fusable(const lompc_plan* p);
+bool lq_loop_fusable(const lompc_plan* p, bool persistent);
 int lq_launch_loop_iter(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,
                         const StepArgs& sa, int m, hipStream_t st);
 int lq_launch_loop_run(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,

@@ -87,7 +87,7 @@ int lq_price_loop_device(lompc_plan* p, const lompc_price_loop_args* a, double* 
               p->d_loop, reinterpret_cast<double*>(reinterpret_cast<char*>(p->d_loop) + 16),
               reinterpret_cast<double*>(reinterpret_cast<char*>(p->d_loop) + LQ_LOOP_TRI), d_h, d_dec};
   const int ahead = LOMPC_LOOP_AHEAD;
-  const bool fused = lq_loop_fusable(p);
+  const bool fused = lq_loop_fusable(p, LQ_LOOP_PERSIST);
   auto done = [&]() { return __atomic_load_n(const_cast<long long*>(&h->done), __ATOMIC_ACQUIRE) != 0; };
   auto progress = [&]() { return __atomic_load_n(const_cast<long long*>(&h->progress), __ATOMIC_ACQUIRE); };
   // spin until cond() (the device's progress lives in pinned memory); a generous guard against a hang

@@ -2002,6 +2002,7 @@ __global__ __launch_bounds__(256) void k_closes(FinalArgs f, ClosesArgs x) {
 // closed outputs in its registers.  The unfused form's three launches (k_path, k_agg, k_loop_step) and two kernel
 // boundaries become one launch and one arrival counter (ctl[1]).
 constexpr int LQ_LOOP_G = 16;  // k_loop_iter: at most this many cells per set (its closing's records in registers)
+constexpr int LQ_LOOP_G2 = 32;  // k_loop_run2: at most this many (its closing reads the records 16 at a time)
 
 #ifdef LOMPC_STAMPS
 // diagnostic build: per k_loop_iter wave (blk < 64) the phases' s_memrealtime ticks summed over the
@@ -2325,21 +2326,33 @@ __global__ __launch_bounds__(64) void k_loop_run2(PathArgs pa, AggArgs ga, StepA
       zs[t].order_ok = cl_ok[t] != 0;
     }
     const int N = zs[0].N;
-    double rw[S][LQ_LOOP_G], rx[S][LQ_LOOP_G];
     const int tl = min(lane, N - 1), xl = min(lane, 4);
+    // the records in cell order, 16 of each set per memory round (records k >= G: the zero record
+    // after buffer 0; with G <= 16 one round, the sums of k_loop_run's padded 16)
+    double v[S] = {0.0, 0.0}, xs[S] = {0.0, 0.0}, xm[S] = {0.0, 0.0};
+    for (int k0 = 0; k0 < G; k0 += LQ_LOOP_G) {  // (wave-uniform)
+      double rw[S][LQ_LOOP_G], rx[S][LQ_LOOP_G];
 #pragma unroll
-    for (int t = 0; t < S; ++t)
+      for (int t = 0; t < S; ++t)
 #pragma unroll
-      for (int k = 0; k < LQ_LOOP_G; ++k) {  // (records k >= G: the zero record after buffer 0)
-        const double* rk = k < G ? rb + (size_t)(t * G + k) * LQ_AGG_REC : rec + (size_t)nsg * LQ_AGG_REC;
-        rw[t][k] = ld_t<true>(rk + tl);
-        rx[t][k] = ld_t<true>(rk + LOMPC_MAX_N + xl);
-      }
+        for (int k = 0; k < LQ_LOOP_G; ++k) {
+          const double* rk =
+              k0 + k < G ? rb + (size_t)(t * G + k0 + k) * LQ_AGG_REC : rec + (size_t)nsg * LQ_AGG_REC;
+          rw[t][k] = ld_t<true>(rk + tl);
+          rx[t][k] = ld_t<true>(rk + LOMPC_MAX_N + xl);
+        }
+#pragma unroll
+      for (int t = 0; t < S; ++t)
+#pragma unroll
+        for (int k = 0; k < LQ_LOOP_G; ++k) {
+          v[t] += rw[t][k];
+          xs[t] += rx[t][k];
+          xm[t] = fmax(xm[t], rx[t][k]);
+        }
+    }
     AggSetOut o[S];
 #pragma unroll
-    for (int t = 0; t < S; ++t)
-      o[t] = agg_finish<false, true, LQ_LOOP_G>(gw, zs[t], t, lane, G, [&](int k) { return rw[t][k]; },
-                                               [&](int k) { return rx[t][k]; });
+    for (int t = 0; t < S; ++t) o[t] = agg_finish_tail<false>(gw, zs[t], t, lane, v[t], xs[t], xm[t]);
     in.s0 = o[0].sumw;
     in.wk = o[1].sumw;
     in.emax = lqw::readlane_d(o[0].stat, LOMPC_STAT_MAX_ERR);
@@ -3007,8 +3020,9 @@ int lq_plan_launch(lompc_plan* p, const double* lmbd, const double* lmbd_r, doub
   return lq_launch_eval(p, lmbd, lmbd_r, w, cost, w0, status, set_sum_w, set_stats, tb, st, prof_ctx);
 }
 
-bool lq_loop_fusable(const lompc_plan* p) {  // (S = 2: the loop's sets; ctl holds 2 set counters)
-  return p->sorted && !p->comm && p->nblk > 0 && p->S == 2 && p->G >= 1 && p->G <= LQ_LOOP_G;
+bool lq_loop_fusable(const lompc_plan* p, bool persistent) {  // (S = 2: the loop's sets; ctl holds 2 set counters)
+  const int gmax = (persistent && LQ_LOOP_REDUNDANT) ? LQ_LOOP_G2 : LQ_LOOP_G;  // (k_loop_run2: chunked closing)
+  return p->sorted && !p->comm && p->nblk > 0 && p->S == 2 && p->G >= 1 && p->G <= gmax;
 }
 
 int lq_launch_loop_iter(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,
@@ -3024,7 +3038,7 @@ int lq_launch_loop_run(lompc_plan* p, const double* lmbd, const double* lmbd_r, 
 
 int lq_launch_loop(lompc_plan* p, const double* lmbd, const double* lmbd_r, double* set_sum_w, double* set_stats,
                    const StepArgs& sa, int m, hipStream_t st, bool persistent) {
-  if (!lq_loop_fusable(p)) return fail_arg(p, "k_loop_iter: plan not fusable");
+  if (!lq_loop_fusable(p, persistent)) return fail_arg(p, "k_loop_iter: plan not fusable");
   const int N = p->N;
   // [cell records | the zero record (k_loop_iter's padding) | (k_loop_run2) the second record buffer]
   const int64_t zoff = p->S * p->G * (int64_t)LQ_AGG_REC;

@@ -100,7 +100,11 @@ class PriceSolver:
         self._h_sw = torch.zeros((2, N), dtype=torch.float64).pin_memory()
         self._h_st = torch.zeros((2, _lib.LOMPC_SET_STATS), dtype=torch.float64).pin_memory()
         self._plan = None
-        self.loop_cells = None  # path cells per set of the loop plans (None: the engine's choice)
+        # path cells per set of the loop plans (None: the engine's choice).  6: the device loop's
+        # iteration is a chain through the slowest of its S x G waves and their records — fewer, longer
+        # cells measured faster (scripts/loop_timing.py on the long-regime fixtures, us per iteration:
+        # 4 cells 13.64 / 15.60, 6: 13.66 / 15.10, 8: 13.86 / 15.25, 16: 14.43 / 15.49, 32: 16.06 / 17.37)
+        self.loop_cells = 6
         self.reserve_evs = 0  # > 0: the loop plans' workspaces sized for this many EVs (BatchPlan.reserve)
         self._plan_w0 = None
         self._w0_live = False

@@ -29,6 +29,8 @@ for cls in ("capped", "mid"):
     g = lambda k: arr[f"{cls}_{k}"]
     c = O.large_consts() if m["kind"] == "Large" else O.small_consts()
     ps = PriceSolver(48, LoMPCConstants(c.delta, c.theta, c.y_max, c.w_max, c.ev_type), "linear-convex", device=0)
+    if os.environ.get("LT_CELLS"):  # (the loop plans' path cells per set instead of the engine's choice)
+        ps.loop_cells = int(os.environ["LT_CELLS"])
     y0 = g("y0")
     n, ymax, ymin, ysum = g("pstats")
     best = None
@@ -45,5 +47,5 @@ for cls in ("capped", "mid"):
         if r > 0:
             best = dt if best is None else min(best, dt)
     it = st["iter"]
-    print(f"{cls}: {len(y0)} EVs, {it} iterations: best {best * 1e3:.2f} ms = {best / (it + 1) * 1e6:.2f} us per iteration",
+    print(f"{cls}: cells {ps._staged[0]['_plan'].info()['cells']}, {len(y0)} EVs, {it} iterations: best {best * 1e3:.2f} ms = {best / (it + 1) * 1e6:.2f} us per iteration",
           flush=True)
